@@ -1,0 +1,145 @@
+#!/usr/bin/env python
+"""Headline benchmark: ResNet-50 v1.5 sync-SGD training throughput (images/sec, whole job).
+
+BASELINE.json metric: "images/sec (whole node) ResNet-50 sync-SGD at 1/2/4/8
+MI355X; scaling efficiency".  One process per GPU (torchrun); each step is a
+full training step through the framework engine: forward + backward of
+ResNet-50 (bf16 compute, fp32 master weights) on a synthetic ImageNet-shaped
+batch (224x224x3, 1000 classes, random-init weights), bucketed RCCL
+gradient reduction overlapped with backward, fused momentum-SGD update.
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 5
+
+Timing: W untimed warmup steps, then barrier + device sync, K timed steps,
+barrier + device sync; the elapsed time is the MAX over ranks; rank 0 prints
+one JSON line.  ``value`` = N * per_gpu_batch * K / elapsed (weak scaling).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+# Comparator (stock PyTorch-ROCm: MIOpen conv/BN, torch DDP, torch SGD) images/sec measured on
+# MI355X with bench/stock_pytorch.py at the same config; None until measured (vs_baseline null).
+BASELINE_IMAGES_PER_SEC_PER_GPU = None
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    p.add_argument("--depth", type=int, default=50)
+    p.add_argument("--mode", default="allreduce", choices=["allreduce", "sharded"])
+    p.add_argument("--kernels", default=None, help="native|torch (MDTF_KERNELS)")
+    p.add_argument("--bucket_mb", type=int, default=None)
+    p.add_argument("--profile_dir", default=None)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    if args.kernels:
+        os.environ["MDTF_KERNELS"] = args.kernels
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import mdtf
+    from mdtf.cluster import Server
+    from mdtf.data.loaders import SyntheticDataLoader
+    from mdtf.models import ResNet, SoftmaxCrossEntropyLoss
+    from mdtf.runtime import Net, Tower
+    from mdtf.train import variables as V
+    from mdtf.train import step as S
+
+    distributed = "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if distributed:
+        server = Server.from_env()
+        world, rank = dist.get_world_size(), dist.get_rank()
+        dev = torch.device("cuda", server.local_rank) if torch.cuda.is_available() else torch.device("cpu")
+        pg = server.worker_group
+    else:
+        server, world, rank, pg = None, 1, 0, None
+        dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    store = V.get_store()
+    store.device = dev
+    store.compute_dtype = torch.bfloat16 if dev.type == "cuda" else None
+    store.generator.manual_seed(1234)
+
+    loader = SyntheticDataLoader(shape=(224, 224, 3), num_classes=1000, dtype=torch.bfloat16 if dev.type == "cuda"
+                                 else torch.float32, seed=rank)
+    loader.batch_size = args.batch
+    raw, gt = loader.load_train_batch()
+    base = mdtf.train.MomentumOptimizer(0.1 * args.batch * world / 256.0, momentum=0.9, weight_decay=5e-5)
+    gs = mdtf.train.get_or_create_global_step()
+    tower_grads = []
+    tower = Tower(Net(ResNet(args.depth)), "tower_0/", tower_grads, raw, gt, SoftmaxCrossEntropyLoss(), base,
+                  batch_size=args.batch)
+    _, loss, _ = tower.process()
+    opt = mdtf.train.SyncReplicasOptimizer(base, replicas_to_aggregate=world, total_num_replicas=world,
+                                           mode=args.mode,
+                                           bucket_bytes=(args.bucket_mb << 20) if args.bucket_mb else None)
+    train_op = opt.apply_gradients(Tower.average_gradients(tower_grads), global_step=gs)
+    sess = mdtf.train.MonitoredTrainingSession(is_chief=(rank == 0), checkpoint_dir=None, log_step_count_steps=0,
+                                               server=server)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier(group=pg)
+
+    for _ in range(args.warmup):
+        sess.run(train_op)
+    lv = sess.run(loss)
+    sync()
+    prof = None
+    if args.profile_dir and rank == 0:
+        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                  torch.profiler.ProfilerActivity.CUDA])
+        prof.__enter__()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sess.run(train_op)
+    sync()
+    elapsed = time.perf_counter() - t0
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(args.profile_dir, exist_ok=True)
+        with open(os.path.join(args.profile_dir, "torch_profile.txt"), "w") as f:
+            f.write(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=80))
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=pg)
+    elapsed = float(t.item())
+    final_loss = float(sess.run(loss))
+    if rank == 0:
+        ips = world * args.batch * args.steps / elapsed
+        base_ips = BASELINE_IMAGES_PER_SEC_PER_GPU
+        rec = {
+            "metric": "images/sec (whole node) ResNet-50 sync-SGD at 1/2/4/8 MI355X; scaling efficiency",
+            "value": round(ips, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(ips / (base_ips * world), 4) if base_ips else None,
+            "dtype": "bf16", "data": "synthetic (random 224x224x3 NHWC images, random labels; random-init weights)",
+            "config": {"model": "resnet%d_v1.5" % args.depth, "global_batch": args.batch * world, "seq_len": None,
+                       "per_gpu_batch": args.batch, "image_size": 224, "parallelism": "dp%d" % world,
+                       "grad_sync": args.mode, "optimizer": "momentum-sgd (fused)",
+                       "kernels": os.environ.get("MDTF_KERNELS", "native")},
+            "loss_first": float(lv), "loss_last": final_loss,
+        }
+        print(json.dumps(rec), flush=True)
+    sess.close()
+    if distributed:
+        server.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,137 @@
+"""Flat parameter space: every trainable variable re-homed into a few
+contiguous HBM buffers, pre-partitioned into gradient buckets.
+
+Why (MI355X-first): the reference updates each variable separately on PS CPUs
+(``distribute_train.py:151-158``) and averages tower gradients per variable
+(``distribute_tower.py:78-114``).  With contiguous buffers
+
+* the gradient reduction is a handful of large RCCL collectives over xGMI —
+  buckets are contiguous slices, so there are no pack/unpack copies;
+* the optimizer is ONE fused kernel launch per group (``mdtf/ops/optim.py``),
+  which also refreshes the bf16 compute shadow of the weights.
+
+Variables are grouped by (shadow dtype, weight-decay flag).  Inside a group the
+layout is *reverse creation order*, so the tail of the forward pass (the first
+gradients of backward) fills the first bucket.  Each bucket is padded to a
+multiple of ``pad_to`` (= world size in PS-shard mode) so that
+reduce-scatter/all-gather shards are equal and contiguous.
+"""
+import collections
+
+import torch
+
+_ALIGN = 64  # elements; 256-B aligned fp32 / 128-B aligned bf16 slices
+
+
+def _round_up(x, m):
+    return -(-x // m) * m
+
+
+class Bucket(object):
+    __slots__ = ("group", "index", "start", "end", "variables", "pending", "work", "launched",
+                 "shard_offset", "shard_len")
+
+    def __init__(self, group, index, start, end, variables):
+        self.group = group
+        self.index = index
+        self.start = start
+        self.end = end
+        self.variables = variables
+        self.pending = 0
+        self.work = None
+        self.launched = False
+        self.shard_offset = 0
+        self.shard_len = 0
+
+    @property
+    def numel(self):
+        return self.end - self.start
+
+
+class FlatGroup(object):
+    def __init__(self, variables, device, shadow_dtype, decay, bucket_elems=None, pad_to=1):
+        self.variables = list(variables)
+        self.device = device
+        self.shadow_dtype = shadow_dtype
+        self.decay = decay
+        self.pad_to = max(int(pad_to), 1)
+        bucket_elems = bucket_elems or (1 << 62)
+        self.offsets = []
+        self.buckets = []
+        off = 0
+        bstart, bvars = 0, []
+        for v in self.variables:
+            self.offsets.append(off)
+            bvars.append(v)
+            off += _round_up(v.numel(), _ALIGN)
+            if off - bstart >= bucket_elems:
+                off = bstart + _round_up(off - bstart, _ALIGN * self.pad_to)
+                self.buckets.append(Bucket(self, len(self.buckets), bstart, off, bvars))
+                bstart, bvars = off, []
+        if bvars:
+            off = bstart + _round_up(off - bstart, _ALIGN * self.pad_to)
+            self.buckets.append(Bucket(self, len(self.buckets), bstart, off, bvars))
+        self.numel = off
+        self.master = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        self.shadow = torch.zeros(self.numel, dtype=shadow_dtype, device=device) if shadow_dtype else None
+        self.state = {}
+        for b in self.buckets:
+            for v in b.variables:
+                v.bucket = b
+        for v, o in zip(self.variables, self.offsets):
+            n = v.numel()
+            mview = self.master[o:o + n].view(v.shape)
+            mview.copy_(v.master.detach().to(device))
+            v.master = mview
+            v.grad = self.grad[o:o + n].view(v.shape)
+            if self.shadow is not None:
+                sview = self.shadow[o:o + n].view(v.shape)
+                sview.copy_(mview)
+                v.shadow = sview
+            v.flat_group = self
+            v.flat_offset = o
+
+    def state_buffer(self, name, numel=None):
+        key = (name, numel or self.numel)
+        if key not in self.state:
+            self.state[key] = torch.zeros(numel or self.numel, dtype=torch.float32, device=self.device)
+        return self.state[key]
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def refresh_shadow(self):
+        if self.shadow is not None:
+            self.shadow.copy_(self.master)
+
+
+class FlatParamSpace(object):
+    """All trainable variables of the store, flattened into groups."""
+
+    def __init__(self, variables, device, compute_dtype=None, bucket_bytes=None, pad_to=1):
+        self.device = device
+        self.compute_dtype = compute_dtype
+        bucket_elems = (bucket_bytes // 4) if bucket_bytes else None
+        by_key = collections.OrderedDict()
+        for v in reversed(list(variables)):
+            shadow = compute_dtype if (compute_dtype is not None and not v.keep_fp32
+                                       and compute_dtype != torch.float32) else None
+            by_key.setdefault((shadow, bool(v.apply_weight_decay)), []).append(v)
+        self.groups = [FlatGroup(vs, device, sd, dec, bucket_elems, pad_to) for (sd, dec), vs in by_key.items()]
+        self.variables = list(variables)
+
+    @property
+    def buckets(self):
+        return [b for g in self.groups for b in g.buckets]
+
+    def zero_grad(self):
+        for g in self.groups:
+            g.zero_grad()
+
+    def refresh_shadows(self):
+        for g in self.groups:
+            g.refresh_shadow()
+
+    def numel(self):
+        return sum(g.numel for g in self.groups)

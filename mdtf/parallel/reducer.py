@@ -1,0 +1,252 @@
+"""Gradient aggregation across replicas over RCCL (xGMI) / gloo.
+
+Replaces three reference mechanisms with collectives on flat buckets:
+
+* ``Tower.average_gradients`` — in-graph mean of per-tower gradients
+  (``distribute_tower.py:78-114``);
+* ``SyncReplicasOptimizer`` — per-variable ConditionalAccumulators on the PS,
+  ``replicas_to_aggregate`` of ``total_num_replicas`` (``distribute_train.py:146-160``);
+* PS variable placement — variables round-robined over PS tasks, pulled by every
+  worker every step (``distribute_train.py:109-110``).
+
+Two modes:
+
+``allreduce``
+    every rank holds the full fp32 master and optimizer state; each bucket is
+    all-reduced as soon as its last gradient lands (overlapping backward), then
+    one fused optimizer launch per group.
+``sharded``  ("PS shards", ZeRO-1 layout)
+    each rank *is* the parameter server for ``1/N`` of every bucket: buckets
+    are reduce-scattered during backward, the fused optimizer updates only the
+    local shard of the fp32 master + state, and the refreshed compute weights
+    (bf16 shadow, or fp32 master for fp32 groups) are all-gathered.  Per rank
+    traffic ≈ the all-reduce's, the PS-CPU bottleneck and the separate
+    parameter pull are gone.
+
+Backup workers (``replicas_to_aggregate`` R < N): gradients of the first R
+replicas to finish backward are aggregated, the rest contribute zeros (TF
+drops them as stale); arrival order comes from an atomic counter in the
+cluster store.  Overlap is disabled in that mode because the mask is only
+known after backward.
+"""
+import torch
+import torch.distributed as dist
+
+
+class UpdateTarget(object):
+    """Tensors one fused optimizer launch operates on."""
+    __slots__ = ("group", "master", "grad", "shadow", "numel", "key", "decay")
+
+    def __init__(self, group, master, grad, shadow, key):
+        self.group = group
+        self.master = master
+        self.grad = grad
+        self.shadow = shadow
+        self.numel = master.numel()
+        self.key = key
+        self.decay = group.decay
+
+    def state(self, name):
+        return self.group.state_buffer("%s/%s" % (self.key, name), self.numel)
+
+
+class GradReducer(object):
+    def __init__(self, space, process_group=None, mode="allreduce", overlap=True,
+                 replicas_to_aggregate=None, store=None):
+        self.space = space
+        self.pg = process_group
+        self.mode = mode
+        self.distributed = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(process_group) if self.distributed else 1
+        self.rank = dist.get_rank(process_group) if self.distributed else 0
+        self.R = replicas_to_aggregate or self.world
+        if self.R > self.world or self.R < 1:
+            raise ValueError("replicas_to_aggregate=%d must be in [1, %d]" % (self.R, self.world))
+        self.store = store
+        self.overlap = overlap and self.world > 1 and self.R == self.world
+        self.contributed = True
+        self.num_contributors = self.world
+        self._shards = {}
+        if mode not in ("allreduce", "sharded"):
+            raise ValueError("mode must be 'allreduce' or 'sharded'")
+        if mode == "sharded":
+            self._init_shards()
+        for v in space.variables:
+            v.on_grad_ready = self._on_grad_ready if self.overlap else None
+
+    # ------------------------------------------------------------------
+    def _init_shards(self):
+        for g in self.space.groups:
+            off = 0
+            for b in g.buckets:
+                assert b.numel % self.world == 0, "bucket not padded to world size"
+                b.shard_len = b.numel // self.world
+                b.shard_offset = off
+                off += b.shard_len
+            n = off
+            self._shards[id(g)] = {
+                "master": torch.zeros(n, dtype=torch.float32, device=g.device),
+                "grad": torch.zeros(n, dtype=torch.float32, device=g.device),
+                "out": torch.zeros(n, dtype=g.shadow.dtype if g.shadow is not None else torch.float32,
+                                   device=g.device),
+            }
+        self.load_shards_from_master()
+
+    def load_shards_from_master(self):
+        """(Re)initialise the owned fp32 master shard from the full master."""
+        if self.mode != "sharded":
+            return
+        for g in self.space.groups:
+            sh = self._shards[id(g)]
+            for b in g.buckets:
+                s = b.start + self.rank * b.shard_len
+                sh["master"][b.shard_offset:b.shard_offset + b.shard_len].copy_(g.master[s:s + b.shard_len])
+
+    # -- step protocol ---------------------------------------------------
+    def begin_step(self):
+        self.space.zero_grad()
+        for v in self.space.variables:
+            v.uses = 0
+        for b in self.space.buckets:
+            b.pending = len(b.variables)
+            b.work = None
+            b.launched = False
+
+    def _on_grad_ready(self, var):
+        b = var.bucket
+        b.pending -= 1
+        if b.pending == 0:
+            self._launch(b)
+
+    def _launch(self, b):
+        if b.launched:
+            return
+        b.launched = True
+        if self.world == 1:
+            return
+        g = b.group
+        if self.mode == "allreduce":
+            b.work = dist.all_reduce(g.grad[b.start:b.end], group=self.pg, async_op=True)
+        else:
+            out = self._shards[id(g)]["grad"][b.shard_offset:b.shard_offset + b.shard_len]
+            b.work = dist.reduce_scatter_tensor(out, g.grad[b.start:b.end], group=self.pg, async_op=True)
+
+    def end_backward(self, step=0):
+        """Finish all reductions; returns the gradient scale (1/contributors)."""
+        if self.world > 1 and self.R < self.world:
+            order = self.store.add("mdtf/sync_replicas/%d" % step, 1)
+            self.contributed = order <= self.R
+            if not self.contributed:
+                self.space.zero_grad()     # a stale/backup replica: TF drops its gradients
+            if self.rank == 0 and step >= 2:
+                try:
+                    self.store.delete_key("mdtf/sync_replicas/%d" % (step - 2))
+                except Exception:
+                    pass
+            self.num_contributors = self.R
+        else:
+            self.num_contributors = self.world
+        for b in self.space.buckets:
+            if not b.launched:
+                self._launch(b)
+        for b in self.space.buckets:
+            if b.work is not None:
+                b.work.wait()
+                b.work = None
+        if self.world == 1 and self.mode == "sharded":
+            for g in self.space.groups:
+                self._shards[id(g)]["grad"].copy_(self._gather_index(g, g.grad))
+        return 1.0 / self.num_contributors
+
+    def _gather_index(self, g, full):
+        # world == 1: the shard is the whole bucket (minus nothing)
+        return torch.cat([full[b.start:b.end] for b in g.buckets])
+
+    def update_targets(self):
+        out = []
+        for g in self.space.groups:
+            if self.mode == "allreduce":
+                out.append(UpdateTarget(g, g.master, g.grad, g.shadow, "full"))
+            else:
+                sh = self._shards[id(g)]
+                out.append(UpdateTarget(g, sh["master"], sh["grad"], sh["out"] if g.shadow is not None else None,
+                                        "shard"))
+        return out
+
+    def after_update(self):
+        """Sharded mode: all-gather refreshed compute weights to every rank."""
+        if self.mode != "sharded":
+            return
+        works = []
+        for g in self.space.groups:
+            sh = self._shards[id(g)]
+            src = sh["out"] if g.shadow is not None else sh["master"]
+            dst_full = g.shadow if g.shadow is not None else g.master
+            for b in g.buckets:
+                part = src[b.shard_offset:b.shard_offset + b.shard_len]
+                dst = dst_full[b.start:b.end]
+                if self.world == 1:
+                    dst.copy_(part)
+                else:
+                    works.append(dist.all_gather_into_tensor(dst, part, group=self.pg, async_op=True))
+        for w in works:
+            w.wait()
+
+    # -- full-state helpers -------------------------------------------------
+    def gather_full_master(self):
+        """Make every rank's full fp32 master current (checkpointing, eval)."""
+        if self.mode != "sharded":
+            return
+        for g in self.space.groups:
+            if g.shadow is None:
+                continue  # fp32 groups are gathered every step
+            sh = self._shards[id(g)]
+            for b in g.buckets:
+                part = sh["master"][b.shard_offset:b.shard_offset + b.shard_len]
+                dst = g.master[b.start:b.end]
+                if self.world == 1:
+                    dst.copy_(part)
+                else:
+                    dist.all_gather_into_tensor(dst, part, group=self.pg)
+
+    def gather_full_state(self, target_key, name):
+        """Full-size optimizer state buffer for checkpointing (sharded → gathered)."""
+        out = []
+        for g in self.space.groups:
+            if self.mode == "allreduce":
+                out.append(g.state_buffer("full/%s" % name, g.numel))
+                continue
+            sh_state = g.state_buffer("shard/%s" % name, self._shards[id(g)]["master"].numel())
+            full = torch.zeros(g.numel, dtype=torch.float32, device=g.device)
+            for b in g.buckets:
+                part = sh_state[b.shard_offset:b.shard_offset + b.shard_len]
+                if self.world == 1:
+                    full[b.start:b.end].copy_(part)
+                else:
+                    dist.all_gather_into_tensor(full[b.start:b.end], part, group=self.pg)
+            out.append(full)
+        return out
+
+    def scatter_full_state(self, name, fulls):
+        """Inverse of :meth:`gather_full_state` (restore)."""
+        for g, full in zip(self.space.groups, fulls):
+            if self.mode == "allreduce":
+                g.state_buffer("full/%s" % name, g.numel).copy_(full)
+                continue
+            sh_state = g.state_buffer("shard/%s" % name, self._shards[id(g)]["master"].numel())
+            for b in g.buckets:
+                s = b.start + self.rank * b.shard_len
+                sh_state[b.shard_offset:b.shard_offset + b.shard_len].copy_(full[s:s + b.shard_len])
+
+    def broadcast_parameters(self, src=0):
+        """Chief → all: master weights and non-trainable variables (session init)."""
+        if self.world > 1:
+            for g in self.space.groups:
+                dist.broadcast(g.master, src=self._global_src(src), group=self.pg)
+        self.space.refresh_shadows()
+        self.load_shards_from_master()
+
+    def _global_src(self, src):
+        if self.pg is None or self.pg == dist.group.WORLD:
+            return src
+        return dist.get_global_rank(self.pg, src)

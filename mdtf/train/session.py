@@ -1,0 +1,282 @@
+"""Sessions: ``tf.Session`` / ``MonitoredTrainingSession`` semantics on eager kernels.
+
+Reference: ``distribute_train.py:169-206`` — ``MonitoredTrainingSession(master,
+is_chief, checkpoint_dir, scaffold=Scaffold(init_op, init_fn), hooks=[StopAtStep,
+SyncReplicas], save_checkpoint_secs=600, config, stop_grace_period_secs=60,
+log_step_count_steps=100)`` then ``while not sess.should_stop(): sess.run(...)``.
+
+Creation protocol (TF1 semantics):
+  1. every TrainOp is finalised — variables re-homed into flat buffers, the
+     gradient reducer bound to the worker process group (RCCL/gloo);
+  2. the chief restores the latest checkpoint of ``checkpoint_dir`` if one
+     exists, otherwise runs ``init_op`` / ``init_fn`` (warm start);
+  3. the chief's state (weights, non-trainable variables, optimizer slots,
+     global step) is broadcast to every replica — the "ready" barrier non-chief
+     workers wait on (fix for SURVEY Q7: one global step, owned by the chief);
+  4. hooks: ``begin`` → create → ``after_create_session``.
+``close`` runs ``end`` on every hook (the checkpoint hook saves a final
+checkpoint) and is safe to call twice.
+"""
+import os
+import time
+
+import torch
+
+from ..utils import log as logger
+from . import hooks as H
+from . import step as S
+from . import variables as V
+
+
+class Scaffold(object):
+    def __init__(self, init_op=None, init_feed_dict=None, init_fn=None, ready_op=None, local_init_op=None,
+                 summary_op=None, saver=None, copy_from_scaffold=None):
+        self.init_op = init_op
+        self.init_feed_dict = init_feed_dict
+        self.init_fn = init_fn
+        self.ready_op = ready_op
+        self.local_init_op = local_init_op
+        self.summary_op = summary_op
+        self.saver = saver
+
+    def finalize(self):
+        return self
+
+
+def global_variables_initializer():
+    """Variables are initialised at creation; kept for API parity (returns a no-op)."""
+    return None
+
+
+def _flatten(fetches):
+    """Return (flat list, rebuild fn)."""
+    if isinstance(fetches, (list, tuple)):
+        parts = [_flatten(f) for f in fetches]
+        flat = [x for p in parts for x in p[0]]
+
+        def rebuild(vals, parts=parts, typ=type(fetches)):
+            out, i = [], 0
+            for p in parts:
+                n = len(p[0])
+                out.append(p[1](vals[i:i + n]))
+                i += n
+            return typ(out) if typ is not list else out
+        return flat, rebuild
+    if isinstance(fetches, dict):
+        keys = list(fetches)
+        parts = [_flatten(fetches[k]) for k in keys]
+        flat = [x for p in parts for x in p[0]]
+
+        def rebuild(vals, parts=parts, keys=keys):
+            out, i = {}, 0
+            for k, p in zip(keys, parts):
+                n = len(p[0])
+                out[k] = p[1](vals[i:i + n])
+                i += n
+            return out
+        return flat, rebuild
+    return [fetches], lambda vals: vals[0]
+
+
+def _evaluate(f, ctx):
+    if f is None:
+        return None
+    if isinstance(f, V.GlobalStep):
+        return f.value()
+    if isinstance(f, V.Variable):
+        return S._host_value(f.master)
+    if isinstance(f, S.Fetchable):
+        return f.evaluate(ctx)
+    if isinstance(f, torch.Tensor):
+        return S._host_value(f)
+    raise TypeError("Cannot fetch %r" % (f,))
+
+
+class Session(object):
+    """Plain session: ``run(fetches, feed_dict)`` with graph-like semantics."""
+
+    def __init__(self, target="", graph=None, config=None):
+        self.target = target
+        self.config = config
+        self._closed = False
+
+    def run_raw(self, fetches, feed_dict=None):
+        flat, rebuild = _flatten(fetches)
+        ctx = S.RunContext(feed_dict, self)
+        # train ops first: StepTensors fetched alongside read the training forward
+        vals = [None] * len(flat)
+        order = sorted(range(len(flat)), key=lambda i: 0 if isinstance(flat[i], S.TrainOp) else 1)
+        for i in order:
+            vals[i] = _evaluate(flat[i], ctx)
+        return rebuild(vals)
+
+    run = run_raw
+
+    def close(self):
+        self._closed = True
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def should_stop(self):
+        return False
+
+
+class MonitoredSession(Session):
+    def __init__(self, hooks=None, is_chief=True, checkpoint_dir=None, scaffold=None, server=None,
+                 stop_grace_period_secs=120):
+        super(MonitoredSession, self).__init__()
+        self._hooks = list(hooks or [])
+        self.is_chief = is_chief
+        self.checkpoint_dir = checkpoint_dir
+        self.scaffold = scaffold or Scaffold()
+        self.server = server
+        self._stop = False
+        self.restored_from = None
+        for h in self._hooks:
+            h.begin()
+        self._create()
+        for h in self._hooks:
+            h.after_create_session(self, None)
+
+    # -- creation ----------------------------------------------------------
+    def _process_group(self):
+        srv = self.server
+        if srv is None:
+            from ..cluster import server as srv_mod
+            srv = srv_mod.current()
+        if srv is not None and srv.worker_group is not None:
+            return srv.worker_group, srv.store
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.group.WORLD, None
+        return None, None
+
+    def _create(self):
+        import torch.distributed as dist
+        pg, store = self._process_group()
+        ops = S.train_ops()
+        for op in ops:
+            op.finalize(pg, store)
+        V.get_store().frozen = True
+        if V.get_global_step() is None:
+            V.get_or_create_global_step()
+        from .saver import Saver, latest_checkpoint
+        restored = False
+        if self.is_chief:
+            ckpt = latest_checkpoint(self.checkpoint_dir) if self.checkpoint_dir else None
+            if ckpt:
+                saver = self.scaffold.saver or Saver()
+                saver.restore(self, ckpt)
+                self.restored_from = ckpt
+                restored = True
+                logger.info("Restored from checkpoint %s (global_step %d)" % (ckpt, V.get_global_step().value()))
+        distributed = dist.is_available() and dist.is_initialized() and pg is not None
+        if distributed and dist.get_world_size(pg) > 1:
+            self._broadcast_state(pg)
+        else:
+            for op in ops:
+                op.reducer.load_shards_from_master()
+        if self.is_chief and not restored and self.scaffold.init_fn is not None:
+            self.scaffold.init_fn(self.scaffold, self)
+            if distributed and dist.get_world_size(pg) > 1:
+                self._broadcast_state(pg)
+        for op in ops:
+            op.space.refresh_shadows()
+            op.reducer.load_shards_from_master()
+
+    def _broadcast_state(self, pg):
+        """Chief (group rank 0) → every replica."""
+        import torch.distributed as dist
+        src = dist.get_global_rank(pg, 0) if pg is not dist.group.WORLD else 0
+        store = V.get_store()
+        for op in S.train_ops():
+            for g in op.space.groups:
+                dist.broadcast(g.master, src=src, group=pg)
+                for buf in g.state.values():
+                    dist.broadcast(buf, src=src, group=pg)
+        for v in store.global_variables():
+            if not v.trainable:
+                dist.broadcast(v.master, src=src, group=pg)
+        gs = torch.tensor([V.get_global_step().value()], dtype=torch.int64,
+                          device=store.device if dist.get_backend(pg) == "nccl" else "cpu")
+        dist.broadcast(gs, src=src, group=pg)
+        V.get_global_step().assign(int(gs.item()))
+        for op in S.train_ops():
+            op.step_count = V.get_global_step().value()
+
+    # -- running -----------------------------------------------------------
+    def run(self, fetches, feed_dict=None, options=None, run_metadata=None):
+        if self._stop:
+            raise RuntimeError("Run called even after should_stop requested.")
+        args = H.SessionRunArgs(fetches, feed_dict)
+        rc = H.SessionRunContext(args, self)
+        extra = {}
+        feed = dict(feed_dict or {})
+        for h in self._hooks:
+            req = h.before_run(rc)
+            if req is not None:
+                extra[h] = req.fetches
+                if req.feed_dict:
+                    feed.update(req.feed_dict)
+        all_fetches = {"__user__": fetches}
+        for i, (h, f) in enumerate(extra.items()):
+            all_fetches["__hook%d__" % i] = f
+        results = self.run_raw(all_fetches, feed)
+        for i, h in enumerate(self._hooks):
+            key = None
+            if h in extra:
+                key = "__hook%d__" % list(extra).index(h)
+            h.after_run(rc, H.SessionRunValues(results.get(key) if key else None))
+        if rc.stop_requested:
+            self._stop = True
+        return results["__user__"]
+
+    def request_stop(self):
+        self._stop = True
+
+    def should_stop(self):
+        return self._stop
+
+    def close(self):
+        if self._closed:
+            return
+        self._closed = True
+        for h in self._hooks:
+            h.end(self)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    def __exit__(self, exc_type, exc, tb):
+        if exc_type is None:
+            self.close()
+        else:
+            self._closed = True
+        return False
+
+
+def MonitoredTrainingSession(master="", is_chief=True, checkpoint_dir=None, scaffold=None, hooks=None,
+                             chief_only_hooks=None, save_checkpoint_secs=600, save_summaries_steps=100,
+                             save_summaries_secs=None, config=None, stop_grace_period_secs=120,
+                             log_step_count_steps=100, max_wait_secs=7200, save_checkpoint_steps=None,
+                             summary_dir=None, server=None):
+    """TF1's MonitoredTrainingSession factory with the same default hooks."""
+    scaffold = scaffold or Scaffold()
+    all_hooks = list(hooks or [])
+    if is_chief:
+        all_hooks += list(chief_only_hooks or [])
+        summary_dir = summary_dir or checkpoint_dir
+        if log_step_count_steps and log_step_count_steps > 0:
+            all_hooks.append(H.StepCounterHook(every_n_steps=log_step_count_steps))
+        if summary_dir and (save_summaries_steps or save_summaries_secs):
+            all_hooks.append(H.SummarySaverHook(save_steps=save_summaries_steps if not save_summaries_secs else None,
+                                                save_secs=save_summaries_secs, output_dir=summary_dir))
+        if checkpoint_dir and (save_checkpoint_secs or save_checkpoint_steps):
+            all_hooks.append(H.CheckpointSaverHook(
+                checkpoint_dir, save_secs=save_checkpoint_secs if not save_checkpoint_steps else None,
+                save_steps=save_checkpoint_steps, scaffold=scaffold))
+    return MonitoredSession(all_hooks, is_chief, checkpoint_dir, scaffold, server, stop_grace_period_secs)
