@@ -1,0 +1,349 @@
+// Fused BatchNorm (+ residual add) (+ ReLU) for NHWC bf16 activations, fp32 statistics.
+//
+// Replaces the reference's tf.nn.moments + tf.nn.batch_normalization
+// (distribute_tools.py:168-180) with a standard per-channel training BN
+//  fused with what follows it in a ResNet block.
+//
+// Forward (training):
+//   1. bn_reduce_kernel<FWD>: per-channel partial Σx, Σx² over a row slice
+//      ([M = N·H·W rows] × [C channels], 16-byte bf16x8 loads, rows split over
+//      gridDim.x, channels over gridDim.y; fp32 in registers, LDS tree across
+//      the row groups of the block) -> partials[gx][C].
+//   2. bn_finalize_fwd: fp64 sum of partials -> mean, invstd, scale=γ·invstd,
+//      shift=β-mean·scale, moving-average update (unbiased variance).
+//   3. bn_apply_kernel: y = x·scale + shift (+ res) (ReLU), bf16x8 vectors.
+// Backward:
+//   1. bn_reduce_kernel<BWD>: Σdz, Σdz·x with dz = dy·[y>0] (ReLU mask from y).
+//   2. bn_finalize_bwd: dβ, dγ and dx = k1·dz + k2·x + k3 coefficients.
+//   3. bn_dx_kernel: dx (and d(residual) = dz) in one pass.
+// All passes are HBM-bound; workspaces are caller-allocated (graph-capture safe).
+#include "mdtf_common.h"
+
+using namespace mdtf;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+struct Geo {
+  int tpr;  // threads per row (channel vectors of 8 handled by one block row)
+  int rg;   // row groups per block
+  int gy;   // channel blocks
+  int gx;   // row blocks
+};
+
+Geo make_geo(long long M, int C) {
+  Geo g;
+  int cv = C / 8;
+  int t = 1;
+  while (t * 2 <= cv && t * 2 <= kThreads) t *= 2;
+  g.tpr = t;
+  g.rg = kThreads / t;
+  g.gy = static_cast<int>(ceil_div(cv, t));
+  long long gx = ceil_div(M, (long long)g.rg * 8);  // >= 8 rows per row-group
+  long long cap = 1024 / g.gy;
+  if (cap < 1) cap = 1;
+  if (gx > cap) gx = cap;
+  if (gx < 1) gx = 1;
+  g.gx = static_cast<int>(gx);
+  return g;
+}
+
+template <bool BWD, bool RELU>
+__global__ void __launch_bounds__(kThreads)
+    bn_reduce_kernel(const bf16_t* __restrict__ a,   // FWD: x      BWD: dy
+                     const bf16_t* __restrict__ b,   // FWD: unused BWD: x
+                     const bf16_t* __restrict__ y,   // BWD+RELU: output (mask)
+                     long long M, int C, int tpr, int rg, float* __restrict__ p0, float* __restrict__ p1) {
+  extern __shared__ float smem[];  // [2][rg][tpr*8]
+  const int t = threadIdx.x;
+  const int lane_c = t % tpr;
+  const int rgi = t / tpr;
+  const int cvec = blockIdx.y * tpr + lane_c;
+  const int c0 = cvec * 8;
+  float s0[8], s1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s0[i] = s1[i] = 0.f;
+  if (c0 < C) {
+    for (long long r = (long long)blockIdx.x * rg + rgi; r < M; r += (long long)gridDim.x * rg) {
+      const long long off = r * C + c0;
+      float va[8];
+      load_bf8(a + off, va);
+      if (!BWD) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s0[i] += va[i];
+          s1[i] += va[i] * va[i];
+        }
+      } else {
+        float vb[8];
+        load_bf8(b + off, vb);
+        if (RELU) {
+          float vy[8];
+          load_bf8(y + off, vy);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) va[i] = vy[i] > 0.f ? va[i] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s0[i] += va[i];
+          s1[i] += va[i] * vb[i];
+        }
+      }
+    }
+  }
+  const int W = tpr * 8;
+  float* L0 = smem;
+  float* L1 = smem + rg * W;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    L0[rgi * W + lane_c * 8 + i] = s0[i];
+    L1[rgi * W + lane_c * 8 + i] = s1[i];
+  }
+  __syncthreads();
+  // tree over row groups
+  for (int step = rg / 2; step > 0; step >>= 1) {
+    for (int e = t; e < step * W; e += kThreads) {
+      int g = e / W, k = e % W;
+      L0[g * W + k] += L0[(g + step) * W + k];
+      L1[g * W + k] += L1[(g + step) * W + k];
+    }
+    __syncthreads();
+  }
+  for (int k = t; k < W; k += kThreads) {
+    int c = blockIdx.y * W + k;
+    if (c < C) {
+      p0[(long long)blockIdx.x * C + c] = L0[k];
+      p1[(long long)blockIdx.x * C + c] = L1[k];
+    }
+  }
+}
+
+__global__ void bn_finalize_fwd(const float* __restrict__ p0, const float* __restrict__ p1, int gx, long long M, int C,
+                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                float* __restrict__ mmean, float* __restrict__ mvar, float decay, float eps,
+                                float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                float* __restrict__ scale, float* __restrict__ shift) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int i = 0; i < gx; ++i) {
+    s += p0[(long long)i * C + c];
+    q += p1[(long long)i * C + c];
+  }
+  double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  if (var < 0) var = 0;
+  float inv = rsqrtf((float)var + eps);
+  float g = gamma ? gamma[c] : 1.f;
+  float bt = beta ? beta[c] : 0.f;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = inv;
+  scale[c] = g * inv;
+  shift[c] = bt - (float)mean * g * inv;
+  if (mmean) {
+    double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    mmean[c] = decay * mmean[c] + (1.f - decay) * (float)mean;
+    mvar[c] = decay * mvar[c] + (1.f - decay) * (float)unbiased;
+  }
+}
+
+__global__ void bn_eval_coeffs(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+                               const float* __restrict__ mmean, const float* __restrict__ mvar, float eps,
+                               float* __restrict__ scale, float* __restrict__ shift) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float inv = rsqrtf(mvar[c] + eps);
+  float g = gamma ? gamma[c] : 1.f;
+  scale[c] = g * inv;
+  shift[c] = (beta ? beta[c] : 0.f) - mmean[c] * g * inv;
+}
+
+template <bool HAS_RES, bool RELU>
+__global__ void __launch_bounds__(kThreads)
+    bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
+                    long long n8, int C, const float* __restrict__ scale, const float* __restrict__ shift) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    long long off = i * 8;
+    int c = static_cast<int>(off % C);
+    float v[8];
+    load_bf8(x + off, v);
+    float4 s0 = *reinterpret_cast<const float4*>(scale + c);
+    float4 s1 = *reinterpret_cast<const float4*>(scale + c + 4);
+    float4 h0 = *reinterpret_cast<const float4*>(shift + c);
+    float4 h1 = *reinterpret_cast<const float4*>(shift + c + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    float r[8];
+    if (HAS_RES) load_bf8(res + off, r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float o = v[k] * sc[k] + sh[k];
+      if (HAS_RES) o += r[k];
+      if (RELU) o = fmaxf(o, 0.f);
+      v[k] = o;
+    }
+    store_bf8(y + off, v);
+  }
+}
+
+__global__ void bn_finalize_bwd(const float* __restrict__ p0, const float* __restrict__ p1, int gx, long long M, int C,
+                                const float* __restrict__ gamma, const float* __restrict__ mean,
+                                const float* __restrict__ invstd, float* __restrict__ dgamma,
+                                float* __restrict__ dbeta, float* __restrict__ k1, float* __restrict__ k2,
+                                float* __restrict__ k3) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sdz = 0.0, sdzx = 0.0;
+  for (int i = 0; i < gx; ++i) {
+    sdz += p0[(long long)i * C + c];
+    sdzx += p1[(long long)i * C + c];
+  }
+  float mu = mean[c], inv = invstd[c];
+  float g = gamma ? gamma[c] : 1.f;
+  float db = (float)sdz;
+  float dg = (float)((sdzx - (double)mu * sdz) * inv);
+  if (dgamma) dgamma[c] = dg;
+  if (dbeta) dbeta[c] = db;
+  float a = g * inv;
+  float invM = 1.f / (float)M;
+  // dx = a*(dz - db/M - xhat*dg/M), xhat = (x-mu)*inv
+  k1[c] = a;
+  k2[c] = -a * inv * dg * invM;
+  k3[c] = a * (-db * invM + mu * inv * dg * invM);
+}
+
+template <bool RELU, bool WRITE_DRES>
+__global__ void __launch_bounds__(kThreads)
+    bn_dx_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+                 bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long n8, int C, const float* __restrict__ k1,
+                 const float* __restrict__ k2, const float* __restrict__ k3) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    long long off = i * 8;
+    int c = static_cast<int>(off % C);
+    float g[8], xv[8];
+    load_bf8(dy + off, g);
+    load_bf8(x + off, xv);
+    if (RELU) {
+      float yv[8];
+      load_bf8(y + off, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    }
+    if (WRITE_DRES) store_bf8(dres + off, g);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = k1[c + k] * g[k] + k2[c + k] * xv[k] + k3[c + k];
+    store_bf8(dx + off, o);
+  }
+}
+
+inline int ew_grid(long long n8) {
+  long long b = ceil_div(n8, kThreads);
+  return static_cast<int>(b < 4096 ? (b > 0 ? b : 1) : 4096);
+}
+
+}  // namespace
+
+// Workspace floats needed by fwd/bwd: 2 * gx * C (partials) + 4 * C (coefficients).
+MDTF_EXPORT long long mdtf_bn_workspace_floats(long long M, int C) {
+  Geo g = make_geo(M, C);
+  return 2LL * g.gx * C + 4LL * C;
+}
+
+// Training forward. mean/invstd (fp32 [C]) are saved for backward.
+MDTF_EXPORT int mdtf_bn_fwd_train(const void* x, const void* res, void* y, long long M, int C, const float* gamma,
+                                  const float* beta, float* mmean, float* mvar, float decay, float eps, int relu,
+                                  float* mean, float* invstd, float* ws, hipStream_t st) {
+  if (C % 8) return MDTF_EINVAL;
+  Geo g = make_geo(M, C);
+  float* p0 = ws;
+  float* p1 = ws + (long long)g.gx * C;
+  float* scale = p1 + (long long)g.gx * C;
+  float* shift = scale + C;
+  size_t lds = 2 * sizeof(float) * g.rg * g.tpr * 8;
+  hipLaunchKernelGGL((bn_reduce_kernel<false, false>), dim3(g.gx, g.gy), dim3(kThreads), lds, st,
+                     (const bf16_t*)x, nullptr, nullptr, M, C, g.tpr, g.rg, p0, p1);
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, 256)), dim3(256), 0, st, p0, p1, g.gx, M, C, gamma, beta,
+                     mmean, mvar, decay, eps, mean, invstd, scale, shift);
+  long long n8 = M * C / 8;
+  const bf16_t* r = (const bf16_t*)res;
+  if (r && relu)
+    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x, r,
+                       (bf16_t*)y, n8, C, scale, shift);
+  else if (r)
+    hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x, r,
+                       (bf16_t*)y, n8, C, scale, shift);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
+                       nullptr, (bf16_t*)y, n8, C, scale, shift);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
+                       nullptr, (bf16_t*)y, n8, C, scale, shift);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// Inference forward with moving statistics.
+MDTF_EXPORT int mdtf_bn_fwd_eval(const void* x, const void* res, void* y, long long M, int C, const float* gamma,
+                                 const float* beta, const float* mmean, const float* mvar, float eps, int relu,
+                                 float* ws, hipStream_t st) {
+  if (C % 8) return MDTF_EINVAL;
+  float* scale = ws;
+  float* shift = ws + C;
+  hipLaunchKernelGGL(bn_eval_coeffs, dim3(ceil_div(C, 256)), dim3(256), 0, st, C, gamma, beta, mmean, mvar, eps,
+                     scale, shift);
+  long long n8 = M * C / 8;
+  const bf16_t* r = (const bf16_t*)res;
+  if (r && relu)
+    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x, r,
+                       (bf16_t*)y, n8, C, scale, shift);
+  else if (r)
+    hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x, r,
+                       (bf16_t*)y, n8, C, scale, shift);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
+                       nullptr, (bf16_t*)y, n8, C, scale, shift);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
+                       nullptr, (bf16_t*)y, n8, C, scale, shift);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// Backward. y is the forward output (ReLU mask); dres may be null.
+MDTF_EXPORT int mdtf_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* dres, long long M, int C,
+                            const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                            int relu, float* ws, hipStream_t st) {
+  if (C % 8) return MDTF_EINVAL;
+  Geo g = make_geo(M, C);
+  float* p0 = ws;
+  float* p1 = ws + (long long)g.gx * C;
+  float* k1 = p1 + (long long)g.gx * C;
+  float* k2 = k1 + C;
+  float* k3 = k2 + C;
+  size_t lds = 2 * sizeof(float) * g.rg * g.tpr * 8;
+  if (relu)
+    hipLaunchKernelGGL((bn_reduce_kernel<true, true>), dim3(g.gx, g.gy), dim3(kThreads), lds, st, (const bf16_t*)dy,
+                       (const bf16_t*)x, (const bf16_t*)y, M, C, g.tpr, g.rg, p0, p1);
+  else
+    hipLaunchKernelGGL((bn_reduce_kernel<true, false>), dim3(g.gx, g.gy), dim3(kThreads), lds, st, (const bf16_t*)dy,
+                       (const bf16_t*)x, nullptr, M, C, g.tpr, g.rg, p0, p1);
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, 256)), dim3(256), 0, st, p0, p1, g.gx, M, C, gamma, mean,
+                     invstd, dgamma, dbeta, k1, k2, k3);
+  long long n8 = M * C / 8;
+  if (relu && dres)
+    hipLaunchKernelGGL((bn_dx_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
+                       (const bf16_t*)x, (const bf16_t*)y, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3);
+  else if (relu)
+    hipLaunchKernelGGL((bn_dx_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
+                       (const bf16_t*)x, (const bf16_t*)y, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3);
+  else if (dres)
+    hipLaunchKernelGGL((bn_dx_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
+                       (const bf16_t*)x, nullptr, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3);
+  else
+    hipLaunchKernelGGL((bn_dx_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
+                       (const bf16_t*)x, nullptr, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,595 @@
+// Memory-bound NHWC kernels: activations, pooling, softmax-xent, layout, LRN, column sums.
+//
+// Reference ops (distribute_tools.py): tf.nn.relu (:78,127), bias_add (:77,206),
+// max_pool / avg_pool (:160-165), lrn (:185), sparse softmax cross entropy
+// (user Loss), plus the NCHW<->NHWC transform and ResNet's
+// global average pool.  All bf16 traffic is 16-byte vectorised (bf16x8 per
+// lane); pooling backward is a deterministic gather (no atomics).
+#include "mdtf_common.h"
+
+using namespace mdtf;
+
+namespace {
+
+constexpr int kT = 256;
+
+inline int grid_cap(long long work, int cap = 4096) {
+  long long b = ceil_div(work, kT);
+  return static_cast<int>(b < cap ? (b > 0 ? b : 1) : cap);
+}
+
+#define GRID_STRIDE(i, n) \
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (n); i += (long long)gridDim.x * blockDim.x)
+
+// ---------------------------------------------------------------- activations
+// act: 0 none, 1 relu, 2 gelu(tanh)
+__device__ __forceinline__ float act_f(float v, int act) {
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) {
+    float u = 0.7978845608f * (v + 0.044715f * v * v * v);
+    return 0.5f * v * (1.f + tanhf(u));
+  }
+  return v;
+}
+
+__device__ __forceinline__ float act_grad(float x, float y, int act) {
+  // x: pre-activation, y: post-activation
+  if (act == 1) return y > 0.f ? 1.f : 0.f;
+  if (act == 2) {
+    float x3 = x * x * x;
+    float u = 0.7978845608f * (x + 0.044715f * x3);
+    float t = tanhf(u);
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.7978845608f * (1.f + 3.f * 0.044715f * x * x);
+  }
+  return 1.f;
+}
+
+__global__ void bias_act_fwd(const bf16_t* __restrict__ x, const float* __restrict__ bias, bf16_t* __restrict__ y,
+                             bf16_t* __restrict__ pre, long long n8, int C, int act) {
+  GRID_STRIDE(i, n8) {
+    long long off = i * 8;
+    int c = static_cast<int>(off % C);
+    float v[8];
+    load_bf8(x + off, v);
+    if (bias) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += bias[c + k];
+    }
+    if (pre) store_bf8(pre + off, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = act_f(v[k], act);
+    store_bf8(y + off, v);
+  }
+}
+
+// dx = dy * act'(pre, y)
+__global__ void act_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ pre, const bf16_t* __restrict__ y,
+                        bf16_t* __restrict__ dx, long long n8, int act) {
+  GRID_STRIDE(i, n8) {
+    long long off = i * 8;
+    float g[8], p[8], o[8];
+    load_bf8(dy + off, g);
+    if (act == 1) {
+      load_bf8(y + off, o);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = o[k] > 0.f ? g[k] : 0.f;
+    } else if (act == 2) {
+      load_bf8(pre + off, p);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] *= act_grad(p[k], 0.f, 2);
+    }
+    store_bf8(dx + off, g);
+  }
+}
+
+// generic (any C, any length) scalar variants for shapes that are not bf16x8 friendly
+__global__ void bias_act_fwd_scalar(const bf16_t* __restrict__ x, const float* __restrict__ bias,
+                                    bf16_t* __restrict__ y, bf16_t* __restrict__ pre, long long n, int C, int act) {
+  GRID_STRIDE(i, n) {
+    float v = bf2f(x[i]);
+    if (bias) v += bias[i % C];
+    if (pre) pre[i] = f2bf(v);
+    y[i] = f2bf(act_f(v, act));
+  }
+}
+
+__global__ void act_bwd_scalar(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ pre,
+                               const bf16_t* __restrict__ y, bf16_t* __restrict__ dx, long long n, int act) {
+  GRID_STRIDE(i, n) {
+    float g = bf2f(dy[i]);
+    if (act == 1) g = bf2f(y[i]) > 0.f ? g : 0.f;
+    if (act == 2) g *= act_grad(bf2f(pre[i]), 0.f, 2);
+    dx[i] = f2bf(g);
+  }
+}
+
+__global__ void colsum_scalar(const bf16_t* __restrict__ x, long long M, int C, float* __restrict__ out) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (long long r = blockIdx.y; r < M; r += gridDim.y) s += bf2f(x[r * C + c]);
+  atomicAdd(out + c, s);
+}
+
+// column sums of a [M, C] bf16 matrix -> fp32 [C] (bias gradients). One block
+// per 8*64 channel slab x row split; partial results combined with atomics
+// (few, one per (block, channel)).
+__global__ void colsum_kernel(const bf16_t* __restrict__ x, long long M, int C, float* __restrict__ out) {
+  const int cv = C / 8;
+  const int lane = threadIdx.x % 64, grp = threadIdx.x / 64;  // 4 row groups
+  const int cvec = blockIdx.y * 64 + lane;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (cvec < cv) {
+    for (long long r = (long long)blockIdx.x * 4 + grp; r < M; r += (long long)gridDim.x * 4) {
+      float v[8];
+      load_bf8(x + r * C + cvec * 8, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += v[k];
+    }
+  }
+  __shared__ float L[4][64 * 8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) L[grp][lane * 8 + k] = s[k];
+  __syncthreads();
+  if (grp == 0 && cvec < cv) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float t = L[0][lane * 8 + k] + L[1][lane * 8 + k] + L[2][lane * 8 + k] + L[3][lane * 8 + k];
+      atomicAdd(out + cvec * 8 + k, t);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- pooling
+struct PoolGeo {
+  int N, H, W, C, OH, OW, KH, KW, SH, SW, PT, PL;
+};
+
+__global__ void maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ arg,
+                            PoolGeo g) {
+  const int cv = g.C / 8;
+  long long total = (long long)g.N * g.OH * g.OW * cv;
+  GRID_STRIDE(i, total) {
+    int c8 = static_cast<int>(i % cv);
+    long long p = i / cv;
+    int ow = static_cast<int>(p % g.OW);
+    p /= g.OW;
+    int oh = static_cast<int>(p % g.OH);
+    int n = static_cast<int>(p / g.OH);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      best[k] = -INFINITY;
+      bi[k] = 0;
+    }
+    for (int kh = 0; kh < g.KH; ++kh) {
+      int h = oh * g.SH - g.PT + kh;
+      if (h < 0 || h >= g.H) continue;
+      for (int kw = 0; kw < g.KW; ++kw) {
+        int w = ow * g.SW - g.PL + kw;
+        if (w < 0 || w >= g.W) continue;
+        float v[8];
+        load_bf8(x + (((long long)n * g.H + h) * g.W + w) * g.C + c8 * 8, v);
+        uint8_t idx = static_cast<uint8_t>(kh * g.KW + kw);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (v[k] > best[k]) {
+            best[k] = v[k];
+            bi[k] = idx;
+          }
+      }
+    }
+    long long o = (((long long)n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8;
+    store_bf8(y + o, best);
+    if (arg) {
+      uint2 packed;
+      packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+      packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+      *reinterpret_cast<uint2*>(arg + o) = packed;
+    }
+  }
+}
+
+// gather form: each input pixel collects dy from every window whose argmax it is
+__global__ void maxpool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
+                            PoolGeo g) {
+  const int cv = g.C / 8;
+  long long total = (long long)g.N * g.H * g.W * cv;
+  GRID_STRIDE(i, total) {
+    int c8 = static_cast<int>(i % cv);
+    long long p = i / cv;
+    int w = static_cast<int>(p % g.W);
+    p /= g.W;
+    int h = static_cast<int>(p % g.H);
+    int n = static_cast<int>(p / g.H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int oh0 = (h + g.PT - g.KH + 1 + g.SH - 1);
+    oh0 = oh0 < 0 ? 0 : oh0 / g.SH;
+    int oh1 = (h + g.PT) / g.SH;
+    int ow0 = (w + g.PL - g.KW + 1 + g.SW - 1);
+    ow0 = ow0 < 0 ? 0 : ow0 / g.SW;
+    int ow1 = (w + g.PL) / g.SW;
+    if (oh1 >= g.OH) oh1 = g.OH - 1;
+    if (ow1 >= g.OW) ow1 = g.OW - 1;
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      int kh = h - (oh * g.SH - g.PT);
+      if (kh < 0 || kh >= g.KH) continue;
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        int kw = w - (ow * g.SW - g.PL);
+        if (kw < 0 || kw >= g.KW) continue;
+        long long o = (((long long)n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8;
+        uint2 packed = *reinterpret_cast<const uint2*>(arg + o);
+        uint8_t id[8] = {(uint8_t)(packed.x), (uint8_t)(packed.x >> 8), (uint8_t)(packed.x >> 16),
+                         (uint8_t)(packed.x >> 24), (uint8_t)(packed.y), (uint8_t)(packed.y >> 8),
+                         (uint8_t)(packed.y >> 16), (uint8_t)(packed.y >> 24)};
+        float gv[8];
+        load_bf8(dy + o, gv);
+        uint8_t me = static_cast<uint8_t>(kh * g.KW + kw);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (id[k] == me) acc[k] += gv[k];
+      }
+    }
+    store_bf8(dx + (((long long)n * g.H + h) * g.W + w) * g.C + c8 * 8, acc);
+  }
+}
+
+__device__ __forceinline__ int win_count(const PoolGeo& g, int oh, int ow) {
+  int h0 = oh * g.SH - g.PT, w0 = ow * g.SW - g.PL;
+  int h1 = min(h0 + g.KH, g.H), w1 = min(w0 + g.KW, g.W);
+  h0 = max(h0, 0);
+  w0 = max(w0, 0);
+  return (h1 - h0) * (w1 - w0);
+}
+
+__global__ void avgpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, PoolGeo g) {
+  const int cv = g.C / 8;
+  long long total = (long long)g.N * g.OH * g.OW * cv;
+  GRID_STRIDE(i, total) {
+    int c8 = static_cast<int>(i % cv);
+    long long p = i / cv;
+    int ow = static_cast<int>(p % g.OW);
+    p /= g.OW;
+    int oh = static_cast<int>(p % g.OH);
+    int n = static_cast<int>(p / g.OH);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int kh = 0; kh < g.KH; ++kh) {
+      int h = oh * g.SH - g.PT + kh;
+      if (h < 0 || h >= g.H) continue;
+      for (int kw = 0; kw < g.KW; ++kw) {
+        int w = ow * g.SW - g.PL + kw;
+        if (w < 0 || w >= g.W) continue;
+        float v[8];
+        load_bf8(x + (((long long)n * g.H + h) * g.W + w) * g.C + c8 * 8, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += v[k];
+      }
+    }
+    float inv = 1.f / (float)win_count(g, oh, ow);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] *= inv;
+    store_bf8(y + (((long long)n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8, acc);
+  }
+}
+
+__global__ void avgpool_bwd(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, PoolGeo g) {
+  const int cv = g.C / 8;
+  long long total = (long long)g.N * g.H * g.W * cv;
+  GRID_STRIDE(i, total) {
+    int c8 = static_cast<int>(i % cv);
+    long long p = i / cv;
+    int w = static_cast<int>(p % g.W);
+    p /= g.W;
+    int h = static_cast<int>(p % g.H);
+    int n = static_cast<int>(p / g.H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int oh0 = h + g.PT - g.KH + 1;
+    oh0 = oh0 <= 0 ? 0 : (oh0 + g.SH - 1) / g.SH;
+    int oh1 = min((h + g.PT) / g.SH, g.OH - 1);
+    int ow0 = w + g.PL - g.KW + 1;
+    ow0 = ow0 <= 0 ? 0 : (ow0 + g.SW - 1) / g.SW;
+    int ow1 = min((w + g.PL) / g.SW, g.OW - 1);
+    for (int oh = oh0; oh <= oh1; ++oh)
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        float gv[8];
+        load_bf8(dy + (((long long)n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8, gv);
+        float inv = 1.f / (float)win_count(g, oh, ow);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += gv[k] * inv;
+      }
+    store_bf8(dx + (((long long)n * g.H + h) * g.W + w) * g.C + c8 * 8, acc);
+  }
+}
+
+// global average pool [N, HW, C] -> [N, C]; block = (n, 512-channel slab), 4 row groups
+__global__ void gap_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int HW, int C) {
+  const int n = blockIdx.x;
+  const int lane = threadIdx.x % 64, grp = threadIdx.x / 64;
+  const int cvec = blockIdx.y * 64 + lane;
+  const int cv = C / 8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (cvec < cv)
+    for (int r = grp; r < HW; r += 4) {
+      float v[8];
+      load_bf8(x + ((long long)n * HW + r) * C + cvec * 8, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += v[k];
+    }
+  __shared__ float L[4][64 * 8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) L[grp][lane * 8 + k] = s[k];
+  __syncthreads();
+  if (grp == 0 && cvec < cv) {
+    float o[8];
+    float inv = 1.f / (float)HW;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      o[k] = (L[0][lane * 8 + k] + L[1][lane * 8 + k] + L[2][lane * 8 + k] + L[3][lane * 8 + k]) * inv;
+    store_bf8(y + (long long)n * C + cvec * 8, o);
+  }
+}
+
+__global__ void gap_bwd(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int N, int HW, int C) {
+  const int cv = C / 8;
+  long long total = (long long)N * HW * cv;
+  float inv = 1.f / (float)HW;
+  GRID_STRIDE(i, total) {
+    int c8 = static_cast<int>(i % cv);
+    int n = static_cast<int>(i / ((long long)HW * cv));
+    float g[8];
+    load_bf8(dy + (long long)n * C + c8 * 8, g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] *= inv;
+    store_bf8(dx + i * 8, g);
+  }
+}
+
+// ---------------------------------------------------------------- softmax cross entropy
+// one wave per row; logits bf16 or fp32 (is_bf16); loss[n], lse[n] fp32
+template <typename T>
+__device__ __forceinline__ float ld(const T* p, long long i);
+template <>
+__device__ __forceinline__ float ld<bf16_t>(const bf16_t* p, long long i) {
+  return bf2f(p[i]);
+}
+template <>
+__device__ __forceinline__ float ld<float>(const float* p, long long i) {
+  return p[i];
+}
+
+template <typename T>
+__global__ void xent_fwd(const T* __restrict__ logits, const long long* __restrict__ labels, int N, int K,
+                         float* __restrict__ loss, float* __restrict__ lse) {
+  int row = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  int lane = threadIdx.x % 64;
+  if (row >= N) return;
+  const T* p = logits + (long long)row * K;
+  float m = -INFINITY;
+  for (int k = lane; k < K; k += 64) m = fmaxf(m, ld(p, k));
+  m = wave_max(m);
+  float s = 0.f;
+  for (int k = lane; k < K; k += 64) s += __expf(ld(p, k) - m);
+  s = wave_sum(s);
+  if (lane == 0) {
+    float l = m + __logf(s);
+    long long lab = labels[row];
+    float xl = (lab >= 0 && lab < K) ? ld(p, lab) : 0.f;
+    lse[row] = l;
+    loss[row] = l - xl;
+  }
+}
+
+template <typename T>
+__global__ void xent_bwd(const T* __restrict__ logits, const long long* __restrict__ labels,
+                         const float* __restrict__ lse, const float* __restrict__ dloss, T* __restrict__ dlogits,
+                         int N, int K) {
+  long long total = (long long)N * K;
+  GRID_STRIDE(i, total) {
+    int row = static_cast<int>(i / K);
+    int k = static_cast<int>(i % K);
+    float pr = __expf(ld(logits, i) - lse[row]);
+    float g = (pr - (labels[row] == k ? 1.f : 0.f)) * dloss[row];
+    if constexpr (sizeof(T) == 2)
+      dlogits[i] = f2bf(g);
+    else
+      dlogits[i] = g;
+  }
+}
+
+// ---------------------------------------------------------------- layout transform
+// [B, R, S] -> [B, S, R] (NCHW->NHWC: R=C, S=HW; NHWC->NCHW: R=HW, S=C)
+template <typename T>
+__global__ void transpose_kernel(const T* __restrict__ in, T* __restrict__ out, int R, int S) {
+  __shared__ T tile[64][65];
+  const int b = blockIdx.z;
+  const int r0 = blockIdx.y * 64, s0 = blockIdx.x * 64;
+  const T* src = in + (long long)b * R * S;
+  T* dst = out + (long long)b * R * S;
+  const int tx = threadIdx.x % 64, ty = threadIdx.x / 64;  // 64 x 4
+  for (int r = ty; r < 64; r += 4)
+    if (r0 + r < R && s0 + tx < S) tile[r][tx] = src[(long long)(r0 + r) * S + s0 + tx];
+  __syncthreads();
+  for (int s = ty; s < 64; s += 4)
+    if (s0 + s < S && r0 + tx < R) dst[(long long)(s0 + s) * R + r0 + tx] = tile[tx][s];
+}
+
+// ---------------------------------------------------------------- LRN (cross-channel)
+__global__ void lrn_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, float* __restrict__ dsave, long long P,
+                        int C, int r, float bias, float alpha, float beta) {
+  long long total = P * C;
+  GRID_STRIDE(i, total) {
+    int c = static_cast<int>(i % C);
+    long long base = i - c;
+    float s = 0.f;
+    for (int j = max(0, c - r); j <= min(C - 1, c + r); ++j) {
+      float v = bf2f(x[base + j]);
+      s += v * v;
+    }
+    float d = bias + alpha * s;
+    dsave[i] = d;
+    y[i] = f2bf(bf2f(x[i]) * __powf(d, -beta));
+  }
+}
+
+__global__ void lrn_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+                        const float* __restrict__ dsave, bf16_t* __restrict__ dx, long long P, int C, int r,
+                        float alpha, float beta) {
+  long long total = P * C;
+  GRID_STRIDE(i, total) {
+    int c = static_cast<int>(i % C);
+    long long base = i - c;
+    float xi = bf2f(x[i]);
+    float acc = bf2f(dy[i]) * __powf(dsave[i], -beta);
+    float t = 0.f;
+    for (int j = max(0, c - r); j <= min(C - 1, c + r); ++j)
+      t += bf2f(dy[base + j]) * bf2f(y[base + j]) / dsave[base + j];
+    acc -= 2.f * alpha * beta * xi * t;
+    dx[i] = f2bf(acc);
+  }
+}
+
+}  // namespace
+
+// ============================================================== exports
+MDTF_EXPORT int mdtf_bias_act_fwd(const void* x, const float* bias, void* y, void* pre, long long M, int C, int act,
+                                  hipStream_t st) {
+  if (C % 8) {
+    hipLaunchKernelGGL(bias_act_fwd_scalar, dim3(grid_cap(M * C)), dim3(kT), 0, st, (const bf16_t*)x, bias,
+                       (bf16_t*)y, (bf16_t*)pre, M * C, C, act);
+    MDTF_LAUNCH_CHECK();
+    return 0;
+  }
+  long long n8 = M * C / 8;
+  hipLaunchKernelGGL(bias_act_fwd, dim3(grid_cap(n8)), dim3(kT), 0, st, (const bf16_t*)x, bias, (bf16_t*)y,
+                     (bf16_t*)pre, n8, C, act);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_act_bwd(const void* dy, const void* pre, const void* y, void* dx, long long n, int act,
+                             hipStream_t st) {
+  if (n % 8) {
+    hipLaunchKernelGGL(act_bwd_scalar, dim3(grid_cap(n)), dim3(kT), 0, st, (const bf16_t*)dy, (const bf16_t*)pre,
+                       (const bf16_t*)y, (bf16_t*)dx, n, act);
+    MDTF_LAUNCH_CHECK();
+    return 0;
+  }
+  hipLaunchKernelGGL(act_bwd, dim3(grid_cap(n / 8)), dim3(kT), 0, st, (const bf16_t*)dy, (const bf16_t*)pre,
+                     (const bf16_t*)y, (bf16_t*)dx, n / 8, act);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// out must be zeroed by the caller
+MDTF_EXPORT int mdtf_colsum(const void* x, long long M, int C, float* out, hipStream_t st) {
+  if (C % 8) {
+    long long gy = M < 256 ? M : 256;
+    hipLaunchKernelGGL(colsum_scalar, dim3(ceil_div(C, kT), gy > 0 ? gy : 1), dim3(kT), 0, st, (const bf16_t*)x, M, C,
+                       out);
+    MDTF_LAUNCH_CHECK();
+    return 0;
+  }
+  int gy = static_cast<int>(ceil_div(C / 8, 64));
+  long long gx = ceil_div(M, 4 * 16);
+  if (gx > 512) gx = 512;
+  hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(kT), 0, st, (const bf16_t*)x, M, C, out);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_pool_fwd(int is_max, const void* x, void* y, void* argmax, int N, int H, int W, int C, int OH,
+                              int OW, int KH, int KW, int SH, int SW, int PT, int PL, hipStream_t st) {
+  if (C % 8 || KH * KW > 255) return MDTF_EINVAL;
+  PoolGeo g{N, H, W, C, OH, OW, KH, KW, SH, SW, PT, PL};
+  long long work = (long long)N * OH * OW * (C / 8);
+  if (is_max)
+    hipLaunchKernelGGL(maxpool_fwd, dim3(grid_cap(work)), dim3(kT), 0, st, (const bf16_t*)x, (bf16_t*)y,
+                       (uint8_t*)argmax, g);
+  else
+    hipLaunchKernelGGL(avgpool_fwd, dim3(grid_cap(work)), dim3(kT), 0, st, (const bf16_t*)x, (bf16_t*)y, g);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_pool_bwd(int is_max, const void* dy, const void* argmax, void* dx, int N, int H, int W, int C,
+                              int OH, int OW, int KH, int KW, int SH, int SW, int PT, int PL, hipStream_t st) {
+  if (C % 8) return MDTF_EINVAL;
+  PoolGeo g{N, H, W, C, OH, OW, KH, KW, SH, SW, PT, PL};
+  long long work = (long long)N * H * W * (C / 8);
+  if (is_max)
+    hipLaunchKernelGGL(maxpool_bwd, dim3(grid_cap(work)), dim3(kT), 0, st, (const bf16_t*)dy,
+                       (const uint8_t*)argmax, (bf16_t*)dx, g);
+  else
+    hipLaunchKernelGGL(avgpool_bwd, dim3(grid_cap(work)), dim3(kT), 0, st, (const bf16_t*)dy, (bf16_t*)dx, g);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st) {
+  if (C % 8) return MDTF_EINVAL;
+  hipLaunchKernelGGL(gap_fwd, dim3(N, ceil_div(C / 8, 64)), dim3(kT), 0, st, (const bf16_t*)x, (bf16_t*)y, HW, C);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st) {
+  if (C % 8) return MDTF_EINVAL;
+  hipLaunchKernelGGL(gap_bwd, dim3(grid_cap((long long)N * HW * C / 8)), dim3(kT), 0, st, (const bf16_t*)dy,
+                     (bf16_t*)dx, N, HW, C);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_xent_fwd(const void* logits, int is_bf16, const long long* labels, int N, int K, float* loss,
+                              float* lse, hipStream_t st) {
+  dim3 grid(ceil_div(N, 4));
+  if (is_bf16)
+    hipLaunchKernelGGL(xent_fwd<bf16_t>, grid, dim3(kT), 0, st, (const bf16_t*)logits, labels, N, K, loss, lse);
+  else
+    hipLaunchKernelGGL(xent_fwd<float>, grid, dim3(kT), 0, st, (const float*)logits, labels, N, K, loss, lse);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_xent_bwd(const void* logits, int is_bf16, const long long* labels, const float* lse,
+                              const float* dloss, void* dlogits, int N, int K, hipStream_t st) {
+  long long total = (long long)N * K;
+  if (is_bf16)
+    hipLaunchKernelGGL(xent_bwd<bf16_t>, dim3(grid_cap(total)), dim3(kT), 0, st, (const bf16_t*)logits, labels, lse,
+                       dloss, (bf16_t*)dlogits, N, K);
+  else
+    hipLaunchKernelGGL(xent_bwd<float>, dim3(grid_cap(total)), dim3(kT), 0, st, (const float*)logits, labels, lse,
+                       dloss, (float*)dlogits, N, K);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// elem_bytes: 2 (bf16/fp16) or 4 (fp32)
+MDTF_EXPORT int mdtf_transpose_brs(const void* in, void* out, int B, int R, int S, int elem_bytes, hipStream_t st) {
+  dim3 grid(ceil_div(S, 64), ceil_div(R, 64), B);
+  if (elem_bytes == 2)
+    hipLaunchKernelGGL(transpose_kernel<uint16_t>, grid, dim3(kT), 0, st, (const uint16_t*)in, (uint16_t*)out, R, S);
+  else if (elem_bytes == 4)
+    hipLaunchKernelGGL(transpose_kernel<uint32_t>, grid, dim3(kT), 0, st, (const uint32_t*)in, (uint32_t*)out, R, S);
+  else
+    return MDTF_EINVAL;
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_lrn_fwd(const void* x, void* y, float* dsave, long long P, int C, int r, float bias, float alpha,
+                             float beta, hipStream_t st) {
+  hipLaunchKernelGGL(lrn_fwd, dim3(grid_cap(P * C)), dim3(kT), 0, st, (const bf16_t*)x, (bf16_t*)y, dsave, P, C, r,
+                     bias, alpha, beta);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_lrn_bwd(const void* dy, const void* x, const void* y, const float* dsave, void* dx, long long P,
+                             int C, int r, float alpha, float beta, hipStream_t st) {
+  hipLaunchKernelGGL(lrn_bwd, dim3(grid_cap(P * C)), dim3(kT), 0, st, (const bf16_t*)dy, (const bf16_t*)x,
+                     (const bf16_t*)y, dsave, (bf16_t*)dx, P, C, r, alpha, beta);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,79 @@
+"""Fused BatchNorm(+residual)(+ReLU) autograd op on the HIP kernels of ``csrc/bn.hip``."""
+import torch
+
+from . import _native as N
+
+N.register("mdtf_bn_workspace_floats", [N.L, N.I], N.L)
+N.register("mdtf_bn_fwd_train", [N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P])
+N.register("mdtf_bn_fwd_eval", [N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.I, N.P, N.P])
+N.register("mdtf_bn_bwd", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P, N.P])
+
+
+def _check(x):
+    if x.dtype != torch.bfloat16:
+        raise TypeError("mdtf BN kernel expects bf16 NHWC activations, got %s" % x.dtype)
+    if x.shape[-1] % 8:
+        raise ValueError("mdtf BN kernel needs C % 8 == 0 (C=%d)" % x.shape[-1])
+
+
+def _f32(t):
+    return None if t is None else t.detach().float().contiguous()
+
+
+class _BNTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, mm, mv, decay, eps, relu):
+        x = x.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        y = torch.empty_like(x)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
+        g, b = _f32(gamma), _f32(beta)
+        res = residual.contiguous() if residual is not None else None
+        N.check(N.fn("mdtf_bn_fwd_train")(N.ptr(x), N.ptr(res), N.ptr(y), M, C, N.ptr(g), N.ptr(b), N.ptr(mm),
+                                          N.ptr(mv), float(decay), float(eps), int(relu), N.ptr(mean), N.ptr(invstd),
+                                          N.ptr(ws), N.stream_ptr()), "bn_fwd_train")
+        ctx.save_for_backward(x, y, g, mean, invstd)
+        ctx.has_res = residual is not None
+        ctx.relu = relu
+        ctx.gamma_dtype = gamma.dtype if gamma is not None else None
+        ctx.has_gamma = gamma is not None
+        ctx.has_beta = beta is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, g, mean, invstd = ctx.saved_tensors
+        dy = dy.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res else None
+        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+        dbeta = torch.empty_like(dgamma)
+        ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
+        N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(x), N.ptr(y), N.ptr(dx), N.ptr(dres), M, C, N.ptr(g),
+                                    N.ptr(mean), N.ptr(invstd), N.ptr(dgamma), N.ptr(dbeta), int(ctx.relu), N.ptr(ws),
+                                    N.stream_ptr()), "bn_bwd")
+        return (dx, dgamma if ctx.has_gamma else None, dbeta if ctx.has_beta else None, dres,
+                None, None, None, None, None)
+
+
+def batch_norm_nhwc(x, gamma, beta, moving_mean, moving_var, training, decay, epsilon, relu, residual):
+    _check(x)
+    if residual is not None and residual.dtype != x.dtype:
+        residual = residual.to(x.dtype)
+    if training:
+        return _BNTrain.apply(x, gamma, beta, residual, moving_mean, moving_var, decay, epsilon, bool(relu))
+    x = x.contiguous()
+    C = x.shape[-1]
+    M = x.numel() // C
+    y = torch.empty_like(x)
+    ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+    res = residual.contiguous() if residual is not None else None
+    N.check(N.fn("mdtf_bn_fwd_eval")(N.ptr(x), N.ptr(res), N.ptr(y), M, C, N.ptr(_f32(gamma)), N.ptr(_f32(beta)),
+                                     N.ptr(moving_mean), N.ptr(moving_var), float(epsilon), int(bool(relu)),
+                                     N.ptr(ws), N.stream_ptr()), "bn_fwd_eval")
+    return y

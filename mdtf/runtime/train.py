@@ -40,7 +40,12 @@ def configure_store_for(server):
     store = V.get_store()
     dev = server.device() if server is not None else torch.device("cpu")
     store.device = dev
-    store.compute_dtype = torch.bfloat16 if (FLAGS.use_fp16 and dev.type == "cuda") else None
+    # MI355X: bf16 compute on MFMA with fp32 master weights is the native mode on the GPU
+    # (the reference's --use_fp16 switch); CPU replicas compute in fp32 (or bf16 with --use_fp16).
+    if dev.type == "cuda":
+        store.compute_dtype = torch.bfloat16
+    else:
+        store.compute_dtype = torch.bfloat16 if FLAGS.use_fp16 else None
     return store
 
 

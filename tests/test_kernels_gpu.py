@@ -1,0 +1,225 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference (GPU only)."""
+import pytest
+import torch
+
+from mdtf.ops import _native
+from mdtf.ops import nn as ops
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def setup_module(module):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _native.lib()  # must load: no silent fallback
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _ref_bn(x, gamma, beta, res, relu, eps):
+    xf = x.float()
+    C = xf.shape[-1]
+    x2 = xf.reshape(-1, C)
+    mean = x2.mean(0)
+    var = x2.var(0, unbiased=False)
+    y = (x2 - mean) * torch.rsqrt(var + eps) * gamma + beta
+    y = y.reshape(xf.shape)
+    if res is not None:
+        y = y + res.float()
+    return torch.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("shape,relu,with_res", [((8, 14, 14, 64), True, False), ((4, 7, 7, 256), True, True),
+                                                  ((16, 3, 3, 2048), False, True), ((2, 28, 28, 128), False, False)])
+def test_batch_norm_fwd_bwd(shape, relu, with_res):
+    torch.manual_seed(0)
+    C = shape[-1]
+    x = (torch.randn(shape) * 2 + 0.5).to(DEV).bfloat16().requires_grad_(True)
+    res = torch.randn(shape).to(DEV).bfloat16().requires_grad_(True) if with_res else None
+    gamma = (torch.rand(C) + 0.5).to(DEV).requires_grad_(True)
+    beta = torch.randn(C).to(DEV).requires_grad_(True)
+    mm = torch.zeros(C, device=DEV)
+    mv = torch.ones(C, device=DEV)
+    y = ops.batch_norm(x, gamma, beta, mm, mv, True, 0.9, 1e-5, relu, res)
+    xr = x.detach().float().cpu().requires_grad_(True)
+    rr = res.detach().float().cpu().requires_grad_(True) if with_res else None
+    gr = gamma.detach().cpu().requires_grad_(True)
+    br = beta.detach().cpu().requires_grad_(True)
+    yr = _ref_bn(xr, gr, br, rr, relu, 1e-5)
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn(shape)
+    y.backward(dy.to(DEV).bfloat16())
+    yr.backward(dy.bfloat16().float())
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(gamma.grad, gr.grad) < 2e-2
+    assert _rel(beta.grad, br.grad) < 2e-2
+    if with_res:
+        assert _rel(res.grad, rr.grad) < 2e-2
+    m = xr.detach().reshape(-1, C).mean(0)
+    assert _rel(mm, 0.1 * m) < 1e-2
+    # eval path uses the moving statistics
+    ye = ops.batch_norm(x.detach(), gamma.detach(), beta.detach(), mm, mv, False, 0.9, 1e-5, relu, None)
+    xf = x.detach().float().cpu()
+    ref = (xf - mm.cpu()) * torch.rsqrt(mv.cpu() + 1e-5) * gamma.detach().cpu() + beta.detach().cpu()
+    assert _rel(ye, torch.relu(ref) if relu else ref) < 1e-2
+
+
+@pytest.mark.parametrize("is_max", [True, False])
+@pytest.mark.parametrize("k,s,pad", [(3, 2, "SAME"), (2, 2, "SAME"), (3, 1, "VALID")])
+def test_pool(is_max, k, s, pad):
+    torch.manual_seed(1)
+    x = torch.randn(4, 15, 15, 64)
+    xg = x.to(DEV).bfloat16().requires_grad_(True)
+    xc = x.bfloat16().float().requires_grad_(True)
+    f = ops.max_pool if is_max else ops.avg_pool
+    y = f(xg, k, s, pad)
+    yr = f(xc, k, s, pad)
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn(yr.shape)
+    y.backward(dy.to(DEV).bfloat16())
+    yr.backward(dy.bfloat16().float())
+    assert _rel(xg.grad, xc.grad) < 2e-2
+
+
+def test_global_avg_pool():
+    x = torch.randn(8, 7, 7, 512)
+    xg = x.to(DEV).bfloat16().requires_grad_(True)
+    xc = x.bfloat16().float().requires_grad_(True)
+    y = ops.global_avg_pool(xg)
+    yr = xc.mean(dim=(1, 2))
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn(8, 512)
+    y.backward(dy.to(DEV).bfloat16())
+    yr.backward(dy.bfloat16().float())
+    assert _rel(xg.grad, xc.grad) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_softmax_xent(dtype):
+    torch.manual_seed(2)
+    logits = torch.randn(37, 1000) * 3
+    labels = torch.randint(0, 1000, (37,))
+    lg = logits.to(DEV).to(dtype).requires_grad_(True)
+    lc = logits.to(dtype).float().requires_grad_(True)
+    l = ops.sparse_softmax_cross_entropy_with_logits(labels.to(DEV), lg)
+    lr = torch.nn.functional.cross_entropy(lc, labels, reduction="none")
+    assert _rel(l, lr) < 1e-3
+    l.mean().backward()
+    lr.mean().backward()
+    assert _rel(lg.grad, lc.grad) < 2e-2
+
+
+@pytest.mark.parametrize("act", ["relu", "gelu", None])
+@pytest.mark.parametrize("C", [64, 10])
+def test_bias_act(act, C):
+    x = torch.randn(33, C)
+    b = torch.randn(C)
+    xg = x.to(DEV).bfloat16().requires_grad_(True)
+    bg = b.to(DEV).requires_grad_(True)
+    y = ops.dense(xg, torch.eye(C, device=DEV), bg, act=act)
+    xc = x.bfloat16().float().requires_grad_(True)
+    bc = b.clone().requires_grad_(True)
+    yr = xc + bc
+    if act == "relu":
+        yr = torch.relu(yr)
+    elif act == "gelu":
+        yr = torch.nn.functional.gelu(yr, approximate="tanh")
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn(33, C)
+    y.backward(dy.to(DEV).bfloat16())
+    yr.backward(dy.bfloat16().float())
+    assert _rel(xg.grad, xc.grad) < 2e-2
+    assert _rel(bg.grad, bc.grad) < 2e-2
+
+
+def test_layout_transform():
+    from mdtf.ops import kernels
+    x = torch.randn(3, 17, 9, 11)
+    for dt in (torch.float32, torch.bfloat16):
+        xg = x.to(DEV).to(dt)
+        y = kernels.nchw_to_nhwc(xg)
+        assert torch.equal(y.cpu(), x.to(dt).permute(0, 2, 3, 1))
+        assert torch.equal(kernels.nhwc_to_nchw(y).cpu(), x.to(dt))
+
+
+def test_lrn():
+    x = torch.randn(2, 5, 5, 32)
+    xg = x.to(DEV).bfloat16().requires_grad_(True)
+    xc = x.bfloat16().float().requires_grad_(True)
+    y = ops.lrn(xg, 4, 1.0, 0.001 / 9, 0.75)
+    yr = ops.lrn(xc, 4, 1.0, 0.001 / 9, 0.75)
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn(x.shape)
+    y.backward(dy.to(DEV).bfloat16())
+    yr.backward(dy.bfloat16().float())
+    assert _rel(xg.grad, xc.grad) < 2e-2
+
+
+@pytest.mark.parametrize("kind", ["sgd", "momentum", "adam"])
+def test_fused_optimizers(kind):
+    from mdtf.ops import optim
+    torch.manual_seed(3)
+    n = 4096
+    w = torch.randn(n)
+    g = torch.randn(n)
+    s1 = torch.randn(n).abs()
+    s2 = torch.randn(n).abs()
+    wg, gg, s1g, s2g = w.to(DEV), g.to(DEV), s1.to(DEV), s2.to(DEV)
+    shadow = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    if kind == "sgd":
+        optim.sgd_(wg, gg, shadow, 0.1, 0.5, 1e-2)
+        optim.sgd_(w, g, None, 0.1, 0.5, 1e-2)
+    elif kind == "momentum":
+        optim.momentum_(wg, gg, s1g, shadow, 0.1, 0.9, 0.5, 1e-2, False)
+        optim.momentum_(w, g, s1, None, 0.1, 0.9, 0.5, 1e-2, False)
+    else:
+        optim.adam_(wg, gg, s1g, s2g, shadow, 1e-3, 0.9, 0.999, 1e-8, 3, 0.5, 1e-2, True)
+        optim.adam_(w, g, s1, s2, None, 1e-3, 0.9, 0.999, 1e-8, 3, 0.5, 1e-2, True)
+    assert _rel(wg, w) < 1e-6
+    assert _rel(shadow, w) < 1e-2
+
+
+def test_conv2d_matches_reference():
+    torch.manual_seed(4)
+    x = torch.randn(2, 9, 9, 16)
+    w = torch.randn(3, 3, 16, 32) * 0.1
+    for stride, pad in ((1, "SAME"), (2, (1, 1)), (2, "SAME"), (1, "VALID")):
+        y = ops.conv2d(x.to(DEV).bfloat16(), w.to(DEV).bfloat16(), stride, pad)
+        yr = ops.conv2d(x.bfloat16().float(), w.bfloat16().float(), stride, pad)
+        assert y.shape == yr.shape
+        assert _rel(y, yr) < 1e-2
+
+
+def test_resnet_train_step_gpu():
+    """A tiny ResNet step through the whole engine on the GPU kernels."""
+    import mdtf
+    from mdtf.data.loaders import SyntheticDataLoader
+    from mdtf.models import ResNet, SoftmaxCrossEntropyLoss
+    from mdtf.runtime import Net, Tower
+    from mdtf.train import variables as V
+    store = V.get_store()
+    store.device = torch.device(DEV)
+    store.compute_dtype = torch.bfloat16
+    loader = SyntheticDataLoader(shape=(64, 64, 3), num_classes=10, dtype=torch.bfloat16)
+    loader.batch_size = 8
+    raw, gt = loader.load_train_batch()
+    opt = mdtf.train.MomentumOptimizer(0.05, 0.9)
+    gs = mdtf.train.get_or_create_global_step()
+    tg = []
+    tower = Tower(Net(ResNet(50, num_classes=10)), "tower_0/", tg, raw, gt, SoftmaxCrossEntropyLoss(), opt,
+                  batch_size=8)
+    _, loss, _ = tower.process()
+    train_op = opt.apply_gradients(Tower.average_gradients(tg), global_step=gs)
+    sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
+    losses = []
+    for _ in range(8):
+        sess.run(train_op)
+        losses.append(float(sess.run(loss)))
+    assert all(l == l for l in losses)
+    assert losses[-1] < losses[0]
