@@ -119,18 +119,44 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
-__global__ void bn_finalize_fwd(const float* __restrict__ p0, const float* __restrict__ p1, int gx, long long M, int C,
-                                const float* __restrict__ gamma, const float* __restrict__ beta,
-                                float* __restrict__ mmean, float* __restrict__ mvar, float decay, float eps,
-                                float* __restrict__ mean_out, float* __restrict__ invstd_out,
-                                float* __restrict__ scale, float* __restrict__ shift) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int i = 0; i < gx; ++i) {
-    s += p0[(long long)i * C + c];
-    q += p1[(long long)i * C + c];
+// Sum the [gx][C] partials of 64 channels with a 64 x 16 thread block:
+// 16 row groups stream the partials in parallel (fp32), combined in fp64.
+constexpr int kFinCh = 64, kFinGroups = 16;
+
+__device__ __forceinline__ bool sum_partials(const float* __restrict__ p0, const float* __restrict__ p1, int gx, int C,
+                                             double& s, double& q) {
+  __shared__ double L0[kFinGroups][kFinCh], L1[kFinGroups][kFinCh];
+  const int lc = threadIdx.x % kFinCh, grp = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + lc;
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    for (int i = grp; i < gx; i += kFinGroups) {
+      a += p0[(long long)i * C + c];
+      b += p1[(long long)i * C + c];
+    }
   }
+  L0[grp][lc] = a;
+  L1[grp][lc] = b;
+  __syncthreads();
+  if (grp != 0 || c >= C) return false;
+  s = 0.0;
+  q = 0.0;
+#pragma unroll
+  for (int g = 0; g < kFinGroups; ++g) {
+    s += L0[g][lc];
+    q += L1[g][lc];
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(1024)
+    bn_finalize_fwd(const float* __restrict__ p0, const float* __restrict__ p1, int gx, long long M, int C,
+                    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ mmean,
+                    float* __restrict__ mvar, float decay, float eps, float* __restrict__ mean_out,
+                    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift) {
+  double s, q;
+  if (!sum_partials(p0, p1, gx, C, s, q)) return;
+  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
   double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
   if (var < 0) var = 0;
@@ -187,18 +213,14 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
-__global__ void bn_finalize_bwd(const float* __restrict__ p0, const float* __restrict__ p1, int gx, long long M, int C,
-                                const float* __restrict__ gamma, const float* __restrict__ mean,
-                                const float* __restrict__ invstd, float* __restrict__ dgamma,
-                                float* __restrict__ dbeta, float* __restrict__ k1, float* __restrict__ k2,
-                                float* __restrict__ k3) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double sdz = 0.0, sdzx = 0.0;
-  for (int i = 0; i < gx; ++i) {
-    sdz += p0[(long long)i * C + c];
-    sdzx += p1[(long long)i * C + c];
-  }
+__global__ void __launch_bounds__(1024)
+    bn_finalize_bwd(const float* __restrict__ p0, const float* __restrict__ p1, int gx, long long M, int C,
+                    const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
+                    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ k1,
+                    float* __restrict__ k2, float* __restrict__ k3) {
+  double sdz, sdzx;
+  if (!sum_partials(p0, p1, gx, C, sdz, sdzx)) return;
+  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
   float mu = mean[c], inv = invstd[c];
   float g = gamma ? gamma[c] : 1.f;
   float db = (float)sdz;
@@ -231,9 +253,15 @@ __global__ void __launch_bounds__(kThreads)
       for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
     }
     if (WRITE_DRES) store_bf8(dres + off, g);
+    float4 a0 = *reinterpret_cast<const float4*>(k1 + c), a1 = *reinterpret_cast<const float4*>(k1 + c + 4);
+    float4 b0 = *reinterpret_cast<const float4*>(k2 + c), b1 = *reinterpret_cast<const float4*>(k2 + c + 4);
+    float4 e0 = *reinterpret_cast<const float4*>(k3 + c), e1 = *reinterpret_cast<const float4*>(k3 + c + 4);
+    const float A[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float B[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    const float E[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
     float o[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = k1[c + k] * g[k] + k2[c + k] * xv[k] + k3[c + k];
+    for (int k = 0; k < 8; ++k) o[k] = A[k] * g[k] + B[k] * xv[k] + E[k];
     store_bf8(dx + off, o);
   }
 }
@@ -264,7 +292,7 @@ MDTF_EXPORT int mdtf_bn_fwd_train(const void* x, const void* res, void* y, long 
   size_t lds = 2 * sizeof(float) * g.rg * g.tpr * 8;
   hipLaunchKernelGGL((bn_reduce_kernel<false, false>), dim3(g.gx, g.gy), dim3(kThreads), lds, st,
                      (const bf16_t*)x, nullptr, nullptr, M, C, g.tpr, g.rg, p0, p1);
-  hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, 256)), dim3(256), 0, st, p0, p1, g.gx, M, C, gamma, beta,
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, p0, p1, g.gx, M, C, gamma, beta,
                      mmean, mvar, decay, eps, mean, invstd, scale, shift);
   long long n8 = M * C / 8;
   const bf16_t* r = (const bf16_t*)res;
@@ -329,7 +357,7 @@ MDTF_EXPORT int mdtf_bn_bwd(const void* dy, const void* x, const void* y, void* 
   else
     hipLaunchKernelGGL((bn_reduce_kernel<true, false>), dim3(g.gx, g.gy), dim3(kThreads), lds, st, (const bf16_t*)dy,
                        (const bf16_t*)x, nullptr, M, C, g.tpr, g.rg, p0, p1);
-  hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, 256)), dim3(256), 0, st, p0, p1, g.gx, M, C, gamma, mean,
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, p0, p1, g.gx, M, C, gamma, mean,
                      invstd, dgamma, dbeta, k1, k2, k3);
   long long n8 = M * C / 8;
   if (relu && dres)

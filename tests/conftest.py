@@ -18,8 +18,11 @@ def _fresh_graph():
     """Every test starts with an empty variable store / train-op registry."""
     from mdtf.train import variables as V
     from mdtf.train import step as S
+    from mdtf.cluster import server
     V.reset_default_graph()
     S.reset()
+    server._set_current(None)
     yield
     V.reset_default_graph()
     S.reset()
+    server._set_current(None)

@@ -1,0 +1,239 @@
+"""Variable store, step engine, sessions, hooks, optimizers (single process, CPU)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import mdtf
+from mdtf.data.loaders import SyntheticDataLoader
+from mdtf.layers import tools
+from mdtf.models import LeNet, SoftmaxCrossEntropyLoss
+from mdtf.runtime import Loss, Model, Net, Tower
+from mdtf.train import hooks as H
+from mdtf.train import step as S
+from mdtf.train import variables as V
+
+
+def test_variable_scopes_and_reuse():
+    with V.variable_scope("a"):
+        w = V.get_variable("w", [2, 3], initializer=V.constant_initializer(1.0))
+        with pytest.raises(ValueError):
+            V.get_variable("w", [2, 3])
+    with V.variable_scope("a", reuse=True):
+        w2 = V.get_variable("w", [2, 3])
+    assert torch.equal(w, w2)
+    with V.variable_scope("a", reuse=V.AUTO_REUSE):
+        V.get_variable("w", [2, 3])
+        V.get_variable("new", [1])
+    names = [v.name for v in V.global_variables()]
+    assert names == ["a/w", "a/new"]
+    with V.variable_scope("b", reuse=True):
+        with pytest.raises(ValueError):
+            V.get_variable("missing", [1])
+
+
+def test_collections_scoped():
+    with V.name_scope("tower_0"):
+        V.add_to_collection("losses", torch.tensor(1.0))
+    with V.name_scope("tower_1"):
+        V.add_to_collection("losses", torch.tensor(2.0))
+    assert len(V.get_collection("losses")) == 2
+    assert float(V.get_collection("losses", "tower_1")[0]) == 2.0
+
+
+def test_tools_variable_names():
+    x = torch.randn(2, 8, 8, 3)
+    with torch.no_grad():
+        y = tools.conv("conv1", x, 3, 4)
+        y = tools.conv_nonacti("conv2", y, 4, 4)
+        y = tools.pool("p", y)
+        y = tools.norm("n", y)
+        y = tools.FC_layer("fc", y, 5)
+        d = tools.deconv("dc", torch.randn(2, 4, 4, 6), 3, 6, output_shape=[2, 8, 8, 3], stride=[1, 2, 2, 1])
+    names = [v.name for v in V.global_variables()]
+    assert names == ["conv1/weights", "conv1/biases", "conv2/weights_nonacti", "conv2/biases_nonacti",
+                     "fc/weights", "fc/biases", "dc/weights"]
+    assert y.shape == (2, 5) and d.shape == (2, 8, 8, 3)
+    assert V.get_store().vars["fc/weights"].shape == (4 * 4 * 4, 5)
+
+
+def test_legacy_batch_norm_matches_reference():
+    x = torch.randn(4, 3, 3, 2)
+    y = tools.batch_norm(x, legacy=True)
+    m = x.mean(0)
+    v = x.var(0, unbiased=False)
+    assert torch.allclose(y, (x - m) / torch.sqrt(v + 1e-3), atol=1e-5)
+
+
+class _Linear(Model):
+    def inference(self, x):
+        w = V.get_variable("w", [4, 1], initializer=V.constant_initializer(0.0))
+        b = V.get_variable("b", [1], initializer=V.constant_initializer(0.0))
+        return x @ w + b
+
+
+class _MSE(Loss):
+    def loss(self, p, t):
+        return ((p - t) ** 2).mean()
+
+
+def _linear_problem(opt, steps=200, batch=32):
+    torch.manual_seed(0)
+    true_w = torch.tensor([[1.0], [-2.0], [0.5], [3.0]])
+    xs = torch.randn(batch, 4)
+    ys = xs @ true_w + 0.25
+    x_ph = mdtf.placeholder(torch.float32, [None, 4])
+    y_ph = mdtf.placeholder(torch.float32, [None, 1])
+    tg = []
+    gs = mdtf.train.get_or_create_global_step()
+    tower = Tower(Net(_Linear()), "tower_0/", tg, x_ph, y_ph, _MSE(), opt, batch_size=batch)
+    _, loss, _ = tower.process()
+    train_op = opt.apply_gradients(Tower.average_gradients(tg), global_step=gs)
+    with mdtf.train.MonitoredTrainingSession(hooks=[mdtf.train.StopAtStepHook(last_step=steps)],
+                                             log_step_count_steps=0) as sess:
+        while not sess.should_stop():
+            _, step, lv = sess.run([train_op, gs, loss], feed_dict={x_ph: xs, y_ph: ys})
+    return lv, step, V.get_store()
+
+
+@pytest.mark.parametrize("opt", [lambda: mdtf.train.GradientDescentOptimizer(0.1),
+                                 lambda: mdtf.train.MomentumOptimizer(0.05, 0.9),
+                                 lambda: mdtf.train.AdamOptimizer(0.05)])
+def test_optimizers_converge(opt):
+    lv, step, store = _linear_problem(opt())
+    assert step == 200
+    assert lv < 1e-3
+    assert abs(store.vars["w"].master[1, 0].item() + 2.0) < 0.05
+
+
+def test_session_fetch_structures_and_global_step():
+    lv, step, store = _linear_problem(mdtf.train.GradientDescentOptimizer(0.1), steps=5)
+    assert step == 5 and mdtf.train.get_global_step().value() == 5
+
+
+def test_forward_only_fetch_does_not_train():
+    x_ph = mdtf.placeholder(torch.float32, [None, 4])
+    y_ph = mdtf.placeholder(torch.float32, [None, 1])
+    opt = mdtf.train.GradientDescentOptimizer(0.1)
+    tg = []
+    tower = Tower(Net(_Linear()), "tower_0/", tg, x_ph, y_ph, _MSE(), opt, batch_size=4)
+    _, loss, logits = tower.process()
+    opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
+    sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
+    xs, ys = torch.ones(4, 4), torch.ones(4, 1)
+    out = sess.run({"loss": loss, "logits": logits}, feed_dict={x_ph: xs, y_ph: ys})
+    assert out["loss"] == pytest.approx(1.0) and out["logits"].shape == (4, 1)
+    assert mdtf.train.get_global_step().value() == 0
+    with pytest.raises(KeyError):
+        sess.run(loss)
+
+
+def test_step_counter_examples_hook_and_summaries(tmp_path):
+    loader = SyntheticDataLoader(shape=(28, 28, 1), num_classes=10)
+    loader.batch_size = 8
+    raw, gt = loader.load_train_batch()
+    opt = mdtf.train.AdamOptimizer(1e-3)
+    gs = mdtf.train.get_or_create_global_step()
+    tg = []
+    tower = Tower(Net(LeNet()), "tower_0/", tg, raw, gt, SoftmaxCrossEntropyLoss(), opt, batch_size=8)
+    _, loss, _ = tower.process()
+    train_op = opt.apply_gradients(Tower.average_gradients(tg), global_step=gs)
+    eps = H.ExamplesPerSecondHook(batch_size=8, every_n_steps=2)
+    nan = H.NanTensorHook(loss)
+    with mdtf.train.MonitoredTrainingSession(checkpoint_dir=str(tmp_path), hooks=[H.StopAtStepHook(num_steps=6), eps, nan],
+                                             save_summaries_steps=2, log_step_count_steps=2,
+                                             save_checkpoint_secs=None, save_checkpoint_steps=3) as sess:
+        while not sess.should_stop():
+            sess.run(train_op)
+    assert eps.average_examples_per_sec and eps.average_examples_per_sec > 0
+    from mdtf.utils import summary
+    import glob
+    ev = glob.glob(str(tmp_path / "events.out.tfevents.*"))
+    assert ev
+    tags = {t for _, t, _ in summary.read_events(ev[0])}
+    assert "total_loss" in tags
+    assert mdtf.train.latest_checkpoint(str(tmp_path)).endswith("model.ckpt-6")
+
+
+def test_checkpoint_restore_resumes(tmp_path):
+    def build():
+        V.reset_default_graph()
+        S.reset()
+        loader = SyntheticDataLoader(shape=(28, 28, 1), num_classes=10)
+        loader.batch_size = 4
+        raw, gt = loader.load_train_batch()
+        opt = mdtf.train.MomentumOptimizer(0.01, 0.9)
+        gs = mdtf.train.get_or_create_global_step()
+        tg = []
+        tower = Tower(Net(LeNet()), "tower_0/", tg, raw, gt, SoftmaxCrossEntropyLoss(), opt, batch_size=4)
+        _, loss, _ = tower.process()
+        return opt.apply_gradients(Tower.average_gradients(tg), global_step=gs), gs
+    train_op, gs = build()
+    with mdtf.train.MonitoredTrainingSession(checkpoint_dir=str(tmp_path), hooks=[H.StopAtStepHook(last_step=4)],
+                                             log_step_count_steps=0, save_checkpoint_secs=None,
+                                             save_checkpoint_steps=4) as sess:
+        while not sess.should_stop():
+            sess.run(train_op)
+    w_saved = V.get_store().vars["fc2/weights"].master.clone()
+    mom_saved = train_op.space.groups[0].state_buffer("full/momentum").clone()
+    train_op, gs = build()
+    assert not torch.equal(V.get_store().vars["fc2/weights"].master, w_saved)
+    with mdtf.train.MonitoredTrainingSession(checkpoint_dir=str(tmp_path), hooks=[H.StopAtStepHook(last_step=4)],
+                                             log_step_count_steps=0, save_checkpoint_secs=None) as sess:
+        assert sess.should_stop()          # already at last_step after restore
+    assert gs.value() == 4
+    assert torch.equal(V.get_store().vars["fc2/weights"].master, w_saved)
+    assert torch.equal(train_op.space.groups[0].state_buffer("full/momentum"), mom_saved)
+
+
+def test_weight_decay_collection_and_fused_decay_equivalent():
+    # l2 loss in the 'losses' collection == optimizer-fused decay (grad += wd * w)
+    torch.manual_seed(0)
+    x = torch.randn(8, 4)
+    y = torch.randn(8, 1)
+
+    def run(fused):
+        V.reset_default_graph()
+        S.reset()
+        x_ph, y_ph = mdtf.placeholder(torch.float32, [None, 4]), mdtf.placeholder(torch.float32, [None, 1])
+
+        class M(Model):
+            def inference(self, inp):
+                w = V.get_variable("w", [4, 1], initializer=V.constant_initializer(0.5))
+                if not fused:
+                    V.add_to_collection("losses", mdtf.nn.l2_loss(w) * 0.1)
+                return inp @ w
+        opt = mdtf.train.GradientDescentOptimizer(0.1, weight_decay=0.1 if fused else 0.0)
+        tg = []
+        t = Tower(Net(M()), "tower_0/", tg, x_ph, y_ph, _MSE(), opt, batch_size=8)
+        t.process()
+        op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
+        sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
+        for _ in range(3):
+            sess.run(op, feed_dict={x_ph: x, y_ph: y})
+        return V.get_store().vars["w"].master.clone()
+    assert torch.allclose(run(True), run(False), atol=1e-6)
+
+
+def test_learning_rate_json_and_schedules(tmp_path):
+    from mdtf.utils.learning_rate import LearningRate, piecewise_constant, warmup_linear_decay
+    p = str(tmp_path / "lr.json")
+    lr = LearningRate(0.1, p, decay_factor=0.5)
+    assert lr.learning_rate == 0.1
+    lr.update(0.05)
+    assert LearningRate(0.1, p).learning_rate == 0.05
+    assert lr.decay() == 0.025
+    f = piecewise_constant([10, 20], [1.0, 0.1, 0.01])
+    assert (f(0), f(15), f(25)) == (1.0, 0.1, 0.01)
+    g = warmup_linear_decay(1.0, 10, 110)
+    assert g(0) == pytest.approx(0.1) and g(60) == pytest.approx(0.5)
+
+
+def test_device_setter_round_robin():
+    from mdtf.train.device_setter import replica_device_setter
+    setter = replica_device_setter(cluster={"ps": ["a:1", "b:2"], "worker": ["c:3"]})
+    with V.device(setter):
+        for i in range(5):
+            V.get_variable("v%d" % i, [1])
+    assert [V.get_store().vars["v%d" % i].ps_task for i in range(5)] == [0, 1, 0, 1, 0]
