@@ -1,0 +1,148 @@
+#!/usr/bin/env python
+"""Per-shape conv backend/tile selection on the MI355X (writes mdtf/ops/conv_table.json).
+
+For every convolution of ResNet-v1.5 (depth/batch given) and each pass
+(fwd / dgrad / wgrad) this times MIOpen and the hand-written implicit-GEMM
+kernels at each tile configuration (CUDA events, median of ``--reps``
+launches after warmup, all variants interleaved in one process) and records
+the fastest.  A markdown summary with TFLOP/s per shape goes to ``--report``.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mdtf.ops import conv as C  # noqa: E402
+from mdtf.ops.padding import conv_geometry  # noqa: E402
+
+
+def resnet_convs(depth=50, batch=256, image=224, width=64):
+    from mdtf.models.resnet import DEPTHS
+    blocks = DEPTHS[depth]
+    out = []
+    h = image
+    out.append((batch, h, h, 3, 7, 7, width, 2, (3, 3, 3, 3)))
+    h = h // 2
+    h = (h + 1) // 2  # maxpool 3x3/2 SAME
+    cin = width
+    for s, n in enumerate(blocks):
+        f = width * 2 ** s
+        for u in range(n):
+            stride = 2 if (u == 0 and s > 0) else 1
+            if u == 0:
+                out.append((batch, h, h, cin, 1, 1, 4 * f, stride, (0, 0, 0, 0)))
+            out.append((batch, h, h, cin, 1, 1, f, 1, (0, 0, 0, 0)))
+            if stride == 1:
+                out.append((batch, h, h, f, 3, 3, f, 1, (1, 1, 1, 1)))
+            else:
+                out.append((batch, h, h, f, 3, 3, f, 2, (1, 1, 1, 1)))
+            h2 = (h + 2 - 3) // stride + 1
+            out.append((batch, h2, h2, f, 1, 1, 4 * f, 1, (0, 0, 0, 0)))
+            h = h2
+            cin = 4 * f
+    uniq = []
+    for c in out:
+        if c not in uniq:
+            uniq.append(c)
+    return uniq, out
+
+
+def timeit(fn, reps, warm=3):
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(reps):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return statistics.median(ts)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--depth", type=int, default=50)
+    p.add_argument("--batch", type=int, default=256)
+    p.add_argument("--reps", type=int, default=10)
+    p.add_argument("--out", default=C.TABLE_PATH)
+    p.add_argument("--report", default="gpurun_out/conv_autotune.md")
+    p.add_argument("--passes", default="fwd,dgrad,wgrad")
+    args = p.parse_args()
+    dev = torch.device("cuda")
+    shapes, all_convs = resnet_convs(args.depth, args.batch)
+    counts = {s: all_convs.count(s) for s in shapes}
+    table = {}
+    lines = ["| pass | shape (N,H,W,C,k,Co,s) | count | miopen ms | best mdtf ms (tile) | TF/s mdtf | choice |",
+             "|---|---|---|---|---|---|---|"]
+    tot = {"miopen": 0.0, "best": 0.0}
+    torch.manual_seed(0)
+    for (n, h, w, c, kh, kw, co, s, pads) in shapes:
+        x = torch.randn(n, h, w, c, device=dev).bfloat16()
+        wt = (torch.randn(kh, kw, c, co, device=dev) * 0.05).bfloat16()
+        oh, ow, pt, pb, pl, pr = conv_geometry(h, w, kh, kw, (s, s), (pads[0], pads[1], pads[2], pads[3]))
+        pads4 = (pt, pb, pl, pr)
+        dy = torch.randn(n, oh, ow, co, device=dev).bfloat16()
+        flops = 2.0 * n * oh * ow * co * kh * kw * c
+        native_ok = c % 8 == 0 and co % 8 == 0
+        for pass_ in args.passes.split(","):
+            key = C.shape_key(pass_, (n, h, w, c), (kh, kw, c, co), (s, s), pads4, (1, 1))
+            if pass_ == "fwd":
+                lib = lambda: C.miopen_fwd(x, wt, (s, s), pads4, (1, 1))  # noqa: E731
+                cands = [(bm, bn, 0) for bm, bn in ((128, 128), (128, 64), (64, 64), (256, 64))]
+                mk = lambda bm, bn, sp: (lambda: C.mdtf_fwd(x, wt, (oh, ow), (s, s), pads4, (1, 1), bm, bn))  # noqa
+            elif pass_ == "dgrad":
+                lib = lambda: C.miopen_bwd(x, wt, dy, (s, s), pads4, (1, 1), True, False)  # noqa: E731
+                cands = [(bm, bn, 0) for bm, bn in ((128, 128), (128, 64), (64, 64), (256, 64))]
+                mk = lambda bm, bn, sp: (lambda: C.mdtf_dgrad(dy, wt, x.shape, (s, s), pads4, (1, 1), bm, bn))  # noqa
+            else:
+                lib = lambda: C.miopen_bwd(x, wt, dy, (s, s), pads4, (1, 1), False, True)  # noqa: E731
+                cands = [(bm, bn, sp) for bm, bn in ((128, 128), (64, 64), (128, 64), (64, 128))
+                         for sp in (0, 256, 2048)]
+                mk = lambda bm, bn, sp: (lambda: C.mdtf_wgrad(x, dy, wt.shape, (s, s), pads4, (1, 1), bm, bn, sp))  # noqa
+            t_lib = timeit(lib, args.reps)
+            best = None
+            if native_ok:
+                for bm, bn, sp in cands:
+                    try:
+                        t = timeit(mk(bm, bn, sp), args.reps)
+                    except RuntimeError:
+                        continue
+                    if best is None or t < best[0]:
+                        best = (t, bm, bn, sp)
+            if best is not None and best[0] < t_lib:
+                table[key] = {"backend": "mdtf", "bm": best[1], "bn": best[2], "splits": best[3],
+                              "ms": round(best[0], 4), "miopen_ms": round(t_lib, 4)}
+                choice = "mdtf"
+            else:
+                table[key] = {"backend": "miopen", "ms": round(t_lib, 4),
+                              "mdtf_ms": round(best[0], 4) if best else None}
+                choice = "miopen"
+            k = counts[(n, h, w, c, kh, kw, co, s, pads)]
+            tot["miopen"] += k * t_lib
+            tot["best"] += k * min(t_lib, best[0] if best else 1e9)
+            lines.append("| %s | %d,%d,%d,%d,%dx%d,%d,s%d | %d | %.3f | %s | %s | %s |" % (
+                pass_, n, h, w, c, kh, kw, co, s, k, t_lib,
+                ("%.3f (%d,%d,%d)" % best) if best else "n/a",
+                ("%.0f" % (flops / best[0] / 1e9)) if best else "-", choice))
+            print(lines[-1], flush=True)
+    lines.append("")
+    lines.append("Total conv time per training step (sum over passes x occurrences): MIOpen %.2f ms, "
+                 "best-of %.2f ms" % (tot["miopen"], tot["best"]))
+    print(lines[-1])
+    with open(args.out, "w") as f:
+        json.dump(table, f, indent=1, sort_keys=True)
+    os.makedirs(os.path.dirname(args.report) or ".", exist_ok=True)
+    with open(args.report, "w") as f:
+        f.write("# Conv autotune (ResNet-%d, batch %d, bf16, MI355X)\n\n" % (args.depth, args.batch))
+        f.write("\n".join(lines) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,587 @@
+// Implicit-GEMM convolution on bf16 MFMA (gfx950), NHWC activations, HWIO filters.
+//
+// Replaces the cuDNN conv2d the reference reaches through tf.nn.conv2d
+// (distribute_tools.py:76,88,104,119) and its autodiff backward
+// (distribute_tower.py:27), SURVEY §2.5 K1/K4.  Three passes share one MFMA
+// core (v_mfma_f32_16x16x32_bf16, 4 waves per 256-thread block, register-staged
+// double-buffered LDS, one barrier per 32-deep K step):
+//
+//   fwd   : Y[m=(n,oh,ow)][co]   = Σ_{k=(kh,kw,ci)} X[n,ih,iw,ci] · W[k][co]
+//   dgrad : DX[m=(n,h,w)][ci]    = Σ_{k=(kh,kw,co)} DY[n,oh,ow,co] · W[kh][kw][ci][co]
+//           (oh = (h+ph-kh·dh)/sh, only where divisible — strided convs included)
+//   wgrad : DW[r=(kh,kw,ci)][co] = Σ_{m=(n,oh,ow)} X[n,ih,iw,ci] · DY[m][co]
+//           (split over the pixel dimension, fp32 atomics into DW)
+//
+// Operand staging: a tile whose reduction index is contiguous in memory
+// ("K-contiguous": the im2col gather of X/DY, and W^T for dgrad) is stored in
+// LDS as [rows][32 + 8 pad] and read with ds_read_b128; a tile whose reduction
+// index is the memory row ("N-contiguous": W for fwd, X and DY for wgrad) is
+// stored as [32][cols + 16 pad] and read transposed with two
+// ds_read_b64_tr_b16 per fragment (CDNA4 hardware transpose).  The pad makes
+// both reads conflict-free (row stride ≡ 8 dwords mod 64 for the transposed
+// reads; see frag_ncontig for the lane/row pairing).  Blocks are XCD-remapped
+// so the N-tiles of one M-tile share an L2.  Forward can emit per-channel
+// Σy / Σy² partials for the following BatchNorm (bn.hip consumes them).
+#include "mdtf_common.h"
+
+using namespace mdtf;
+
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+constexpr int BK = 32;
+constexpr int PADK = 8;    // K-contiguous rows: 32 + 8 elements = 80 B
+constexpr int PADN = 16;   // N-contiguous rows: cols + 16 elements
+constexpr int NT = 256;
+
+struct ConvArgs {
+  const bf16_t* src;   // gathered activation: X (fwd, wgrad) or DY (dgrad)
+  const bf16_t* wgt;   // W (fwd, dgrad)
+  const bf16_t* dy;    // DY (wgrad)
+  bf16_t* out;         // Y (fwd) / DX (dgrad)
+  float* dw;           // DW (wgrad, fp32, pre-zeroed)
+  float* stat_sum;     // fwd: per-channel partials [gridM][Cout] (optional)
+  float* stat_sq;
+  int N, H, W, Cin;    // X dims
+  int OH, OW, Cout;    // Y dims
+  int KH, KW, SH, SW, PH, PW, DH, DW;
+  long long M;         // GEMM rows
+  int Ncol;            // GEMM cols
+  int K;               // GEMM reduction length (fwd/dgrad)
+  int mtiles, ntiles;  // tile grid
+  int ksplit_steps;    // wgrad: K steps per split
+};
+
+__device__ __forceinline__ uint4 ld16(const bf16_t* p, bool ok) {
+  return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+}
+
+__device__ __forceinline__ void st16(bf16_t* lds, const uint4& v) { *reinterpret_cast<uint4*>(lds) = v; }
+
+// fragment of a K-contiguous LDS tile: lane l -> row (l&15), k = 8*(l>>4) .. +7
+__device__ __forceinline__ bf16x8_t frag_kcontig(const bf16_t* tile, int row0, int lane) {
+  const bf16_t* p = tile + (row0 + (lane & 15)) * (BK + PADK) + 8 * (lane >> 4);
+  uint4 v = *reinterpret_cast<const uint4*>(p);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// fragment of an N-contiguous LDS tile [BK][ld]: lane l -> col (l&15), k = 8*(l>>4) .. +7.
+// Two transposed reads; odd 16-lane groups fetch their upper k-half in the FIRST
+// instruction so each 32-lane half touches rows {0-3,12-15} then {4-7,8-11}
+// (conflict-free with row stride ≡ 8 dwords mod 64).
+__device__ __forceinline__ bf16x8_t frag_ncontig(const bf16_t* tile, int ld, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int odd = g & 1;
+  const int rfirst = 8 * g + (odd ? 4 : 0) + q;
+  const int rsecond = 8 * g + (odd ? 0 : 4) + q;
+  const bf16_t* a1 = tile + rfirst * ld + col0 + 4 * p;
+  const bf16_t* a2 = tile + rsecond * ld + col0 + 4 * p;
+  v4s r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a1);
+  v4s r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a2);
+  v4s lo = odd ? r2 : r1;
+  v4s hi = odd ? r1 : r2;
+  short8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, f);
+}
+
+__device__ __forceinline__ float4v mfma(const bf16x8_t& a, const bf16x8_t& b, const float4v& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// bijective XCD-aware remap of a 1-D block index (cdna_hip_programming.md §5 T1)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+// ============================================================================
+// forward / dgrad: rows = output pixels (K-contiguous gather), cols = channels
+// MODE 0 = fwd (B = W as N-contiguous [k][co]); MODE 1 = dgrad (B = W^T K-contiguous)
+// ============================================================================
+template <int BM, int BN, int MODE, bool STATS>
+__global__ void __launch_bounds__(NT) conv_fd_kernel(ConvArgs a) {
+  constexpr int WM = 2, WN = 2;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int A_CHUNKS = BM * BK / 8 / NT;                 // 16-B chunks per thread
+  constexpr int B_CHUNKS = BN * BK / 8 / NT;
+  constexpr int LDA = BK + PADK;
+  constexpr int LDB_N = BN + PADN;                           // fwd (N-contiguous)
+  constexpr int A_ELEMS = BM * LDA;
+  constexpr int B_ELEMS = MODE == 0 ? BK * LDB_N : BN * LDA;
+  static_assert(A_CHUNKS >= 1 && B_CHUNKS >= 1, "tile too small for 256 threads");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16_t* smem = reinterpret_cast<bf16_t*>(smem_raw);
+  bf16_t* As[2] = {smem, smem + A_ELEMS};
+  bf16_t* Bs[2] = {smem + 2 * A_ELEMS, smem + 2 * A_ELEMS + B_ELEMS};
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = tile / a.ntiles, nt = tile % a.ntiles;
+  const long long m0 = (long long)mt * BM;
+  const int n0 = nt * BN;
+
+  // ---- A (gather) per-thread setup: rows fixed across K, chunk column kc fixed
+  const int kc = tid & 3;
+  int a_n[A_CHUNKS], a_y[A_CHUNKS], a_x[A_CHUNKS];
+  bool a_ok[A_CHUNKS];
+  const int GH = MODE == 0 ? a.H : a.OH;          // gathered tensor (X or DY) dims
+  const int GW = MODE == 0 ? a.W : a.OW;
+  const int GC = MODE == 0 ? a.Cin : a.Cout;
+  const int RH = MODE == 0 ? a.OH : a.H;          // pixel grid of the GEMM rows
+  const int RW = MODE == 0 ? a.OW : a.W;
+#pragma unroll
+  for (int i = 0; i < A_CHUNKS; ++i) {
+    const int row = (tid >> 2) + i * (NT / 4);
+    const long long m = m0 + row;
+    a_ok[i] = m < a.M;
+    const long long mm = a_ok[i] ? m : 0;
+    const int ow = static_cast<int>(mm % RW);
+    const long long t = mm / RW;
+    const int oh = static_cast<int>(t % RH);
+    a_n[i] = static_cast<int>(t / RH);
+    if (MODE == 0) {
+      a_y[i] = oh * a.SH - a.PH;
+      a_x[i] = ow * a.SW - a.PW;
+    } else {
+      a_y[i] = oh + a.PH;   // dgrad: DY row = (h + ph - kh*dh) / sh where divisible
+      a_x[i] = ow + a.PW;
+    }
+  }
+  // incremental decomposition of this thread's k = kt*BK + kc*8 -> (kh, kw, c)
+  int g_c = kc * 8, g_kw = 0, g_kh = 0;
+  while (g_c >= GC) { g_c -= GC; if (++g_kw == a.KW) { g_kw = 0; ++g_kh; } }
+  // dgrad B: k = kt*BK + kcc*8 -> (tt = kh*KW+kw, co); kcc == kc for every chunk of this thread
+  int b_co = kc * 8, b_tt = 0;
+  if (MODE == 1) while (b_co >= a.Cout) { b_co -= a.Cout; ++b_tt; }
+
+  uint4 ra[A_CHUNKS], rb[B_CHUNKS];
+
+  // loads tile kt (called with kt = 0, 1, 2, ... in order) and advances the counters
+  auto load_tiles = [&](int kt) {
+    const bool kok = g_kh < a.KH;
+    const int c = g_c, kw = g_kw, kh = g_kh;
+#pragma unroll
+    for (int i = 0; i < A_CHUNKS; ++i) {
+      int iy, ix;
+      bool ok = kok && a_ok[i];
+      if (MODE == 0) {
+        iy = a_y[i] + kh * a.DH;
+        ix = a_x[i] + kw * a.DW;
+      } else {
+        const int ny = a_y[i] - kh * a.DH, nx = a_x[i] - kw * a.DW;
+        iy = ny / a.SH;
+        ix = nx / a.SW;
+        ok = ok && ny >= 0 && nx >= 0 && (ny - iy * a.SH) == 0 && (nx - ix * a.SW) == 0;
+      }
+      ok = ok && iy >= 0 && iy < GH && ix >= 0 && ix < GW;
+      const bf16_t* p = a.src + (((long long)a_n[i] * GH + (ok ? iy : 0)) * GW + (ok ? ix : 0)) * GC + c;
+      ra[i] = ld16(p, ok);
+    }
+    g_c += BK;
+    while (g_c >= GC) { g_c -= GC; if (++g_kw == a.KW) { g_kw = 0; ++g_kh; } }
+    if (MODE == 0) {
+      // W [K][Cout], tile rows = k, cols = n (N-contiguous)
+#pragma unroll
+      for (int i = 0; i < B_CHUNKS; ++i) {
+        const int cidx = tid + i * NT;
+        const int krow = cidx / (BN / 8), c8 = cidx % (BN / 8);
+        const int kg = kt * BK + krow, ng = n0 + c8 * 8;
+        const bool ok = kg < a.K && ng < a.Ncol;
+        rb[i] = ld16(a.wgt + (long long)(ok ? kg : 0) * a.Ncol + (ok ? ng : 0), ok);
+      }
+    } else {
+      // dgrad: B^T[n = ci][k = (kh,kw,co)] = W[kh][kw][ci][co]  (K-contiguous)
+      const bool bok = b_tt < a.KH * a.KW;
+#pragma unroll
+      for (int i = 0; i < B_CHUNKS; ++i) {
+        const int cidx = tid + i * NT;
+        const int ng = n0 + (cidx >> 2);
+        const bool ok = bok && ng < a.Ncol;
+        rb[i] = ld16(a.wgt + ((long long)(ok ? b_tt : 0) * a.Cin + (ok ? ng : 0)) * a.Cout + b_co, ok);
+      }
+      b_co += BK;
+      while (b_co >= a.Cout) { b_co -= a.Cout; ++b_tt; }
+    }
+  };
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_CHUNKS; ++i) {
+      const int row = (tid >> 2) + i * (NT / 4);
+      st16(As[buf] + row * LDA + kc * 8, ra[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < B_CHUNKS; ++i) {
+      const int cidx = tid + i * NT;
+      if (MODE == 0) {
+        const int krow = cidx / (BN / 8), c8 = cidx % (BN / 8);
+        st16(Bs[buf] + krow * LDB_N + c8 * 8, rb[i]);
+      } else {
+        const int nrow = cidx >> 2, kcc = cidx & 3;
+        st16(Bs[buf] + nrow * LDA + kcc * 8, rb[i]);
+      }
+    }
+  };
+
+  float4v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = (a.K + BK - 1) / BK;
+  load_tiles(0);
+  store_tiles(0);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < KT; ++kt) {
+    if (kt + 1 < KT) load_tiles(kt + 1);
+    bf16x8_t fa[TM], fb[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[i] = frag_kcontig(As[cur], wm * (TM * 16) + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (MODE == 0)
+        fb[j] = frag_ncontig(Bs[cur], LDB_N, wn * (TN * 16) + j * 16, lane);
+      else
+        fb[j] = frag_kcontig(Bs[cur], wn * (TN * 16) + j * 16, lane);
+    }
+    // D[n][m] = W^T · X^T  -> lane owns 4 consecutive channels of one pixel
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fb[j], fa[i], acc[i][j]);
+    if (kt + 1 < KT) store_tiles(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---- epilogue: bf16 stores (8 B per lane per tile) + optional BN statistics
+  const int g = lane >> 4, li = lane & 15;
+  float ssum[TN][4], ssq[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ssum[j][r] = ssq[j][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const long long m = m0 + wm * (TM * 16) + i * 16 + li;
+    const bool mok = m < a.M;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * (TN * 16) + j * 16 + 4 * g;
+      if (mok && n < a.Ncol) {
+        float4v v = acc[i][j];
+        uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(a.out + m * a.Ncol + n) = make_uint2(lo, hi);
+        if (STATS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            ssum[j][r] += v[r];
+            ssq[j][r] += v[r] * v[r];
+          }
+        }
+      }
+    }
+  }
+  if (STATS) {
+    // reduce over the 16 pixel lanes of each 16-lane group
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          ssum[j][r] += __shfl_xor(ssum[j][r], o, 64);
+          ssq[j][r] += __shfl_xor(ssq[j][r], o, 64);
+        }
+      }
+    __syncthreads();  // LDS tiles are free now
+    float* red = reinterpret_cast<float*>(smem_raw);   // [WM][BN] sums then [WM][BN] squares
+    if (li == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nl = wn * (TN * 16) + j * 16 + 4 * g + r;
+          red[wm * BN + nl] = ssum[j][r];
+          red[WM * BN + wm * BN + nl] = ssq[j][r];
+        }
+    }
+    __syncthreads();
+    for (int nl = tid; nl < BN; nl += NT) {
+      const int n = n0 + nl;
+      if (n < a.Ncol) {
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) {
+          s += red[w * BN + nl];
+          q += red[WM * BN + w * BN + nl];
+        }
+        a.stat_sum[(long long)mt * a.Ncol + n] = s;
+        a.stat_sq[(long long)mt * a.Ncol + n] = q;
+      }
+    }
+  }
+}
+
+// ============================================================================
+// wgrad: rows r = (kh,kw,ci), cols co, reduction over output pixels m (split-K)
+// A' = X gathered, staged [BK(m)][BM(r)] (r contiguous); B' = DY [BK(m)][BN(co)]
+// ============================================================================
+template <int BM, int BN>
+__global__ void __launch_bounds__(NT) conv_wgrad_kernel(ConvArgs a) {
+  constexpr int WM = 2, WN = 2;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int A_CHUNKS = BM * BK / 8 / NT;
+  constexpr int B_CHUNKS = BN * BK / 8 / NT;
+  constexpr int LDA = BM + PADN, LDB = BN + PADN;
+  constexpr int A_ELEMS = BK * LDA, B_ELEMS = BK * LDB;
+  static_assert(A_CHUNKS >= 1 && B_CHUNKS >= 1, "tile too small for 256 threads");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16_t* smem = reinterpret_cast<bf16_t*>(smem_raw);
+  bf16_t* As[2] = {smem, smem + A_ELEMS};
+  bf16_t* Bs[2] = {smem + 2 * A_ELEMS, smem + 2 * A_ELEMS + B_ELEMS};
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_mn = a.mtiles * a.ntiles;
+  const int tile = blockIdx.x % tiles_mn;
+  const int split = blockIdx.x / tiles_mn;
+  const int mt = tile / a.ntiles, nt = tile % a.ntiles;
+  const int r0 = mt * BM, n0 = nt * BN;
+  const int R = a.KH * a.KW * a.Cin;
+
+  // per-thread A columns (r) fixed: decompose once
+  int a_kh[A_CHUNKS], a_kw[A_CHUNKS], a_c[A_CHUNKS], a_mrow[A_CHUNKS], a_rc[A_CHUNKS];
+  bool a_rok[A_CHUNKS];
+#pragma unroll
+  for (int i = 0; i < A_CHUNKS; ++i) {
+    const int cidx = tid + i * NT;
+    a_mrow[i] = cidx / (BM / 8);
+    a_rc[i] = cidx % (BM / 8);
+    const int r = r0 + a_rc[i] * 8;
+    a_rok[i] = r < R;
+    const int rr = a_rok[i] ? r : 0;
+    a_c[i] = rr % a.Cin;
+    const int t = rr / a.Cin;
+    a_kw[i] = t % a.KW;
+    a_kh[i] = t / a.KW;
+  }
+  const long long Mpix = a.M;  // reduction length (pixels of DY)
+  const int KT_total = static_cast<int>((Mpix + BK - 1) / BK);
+  const int kt_begin = split * a.ksplit_steps;
+  const int kt_end = min(KT_total, kt_begin + a.ksplit_steps);
+  if (kt_begin >= kt_end) return;
+
+  // incremental pixel decomposition of m = kt*BK + mrow for each A chunk
+  int p_ow[A_CHUNKS], p_oh[A_CHUNKS], p_n[A_CHUNKS];
+#pragma unroll
+  for (int i = 0; i < A_CHUNKS; ++i) {
+    const long long m = (long long)kt_begin * BK + a_mrow[i];
+    p_ow[i] = static_cast<int>(m % a.OW);
+    const long long t = m / a.OW;
+    p_oh[i] = static_cast<int>(t % a.OH);
+    p_n[i] = static_cast<int>(t / a.OH);
+  }
+  uint4 ra[A_CHUNKS], rb[B_CHUNKS];
+  // loads tile kt (called in order kt_begin, kt_begin+1, ...) and advances the pixel counters
+  auto load_tiles = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < A_CHUNKS; ++i) {
+      const long long m = (long long)kt * BK + a_mrow[i];
+      const int iy = p_oh[i] * a.SH - a.PH + a_kh[i] * a.DH, ix = p_ow[i] * a.SW - a.PW + a_kw[i] * a.DW;
+      const bool ok = a_rok[i] && m < Mpix && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+      ra[i] = ld16(a.src + (((long long)p_n[i] * a.H + (ok ? iy : 0)) * a.W + (ok ? ix : 0)) * a.Cin + a_c[i], ok);
+      p_ow[i] += BK;
+      while (p_ow[i] >= a.OW) { p_ow[i] -= a.OW; if (++p_oh[i] == a.OH) { p_oh[i] = 0; ++p_n[i]; } }
+    }
+#pragma unroll
+    for (int i = 0; i < B_CHUNKS; ++i) {
+      const int cidx = tid + i * NT;
+      const int mrow = cidx / (BN / 8), c8 = cidx % (BN / 8);
+      const long long m = (long long)kt * BK + mrow;
+      const int n = n0 + c8 * 8;
+      const bool ok = m < Mpix && n < a.Cout;
+      rb[i] = ld16(a.dy + (ok ? m : 0) * a.Cout + (ok ? n : 0), ok);
+    }
+  };
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_CHUNKS; ++i) st16(As[buf] + a_mrow[i] * LDA + a_rc[i] * 8, ra[i]);
+#pragma unroll
+    for (int i = 0; i < B_CHUNKS; ++i) {
+      const int cidx = tid + i * NT;
+      st16(Bs[buf] + (cidx / (BN / 8)) * LDB + (cidx % (BN / 8)) * 8, rb[i]);
+    }
+  };
+
+  float4v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  load_tiles(kt_begin);
+  store_tiles(0);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    if (kt + 1 < kt_end) load_tiles(kt + 1);
+    bf16x8_t fa[TM], fb[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[i] = frag_ncontig(As[cur], LDA, wm * (TM * 16) + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[j] = frag_ncontig(Bs[cur], LDB, wn * (TN * 16) + j * 16, lane);
+    // D[r][co]: lane owns 4 consecutive r of one co -> row-contiguous atomics
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
+    if (kt + 1 < kt_end) store_tiles(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int co = n0 + wn * (TN * 16) + j * 16 + li;
+      if (co >= a.Cout) continue;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int r = r0 + wm * (TM * 16) + i * 16 + 4 * g + rr;
+        if (r < R) atomicAdd(a.dw + (long long)r * a.Cout + co, acc[i][j][rr]);
+      }
+    }
+}
+
+template <int BM, int BN, int MODE, bool STATS>
+size_t fd_lds() {
+  const size_t a = (size_t)BM * (BK + PADK);
+  const size_t b = MODE == 0 ? (size_t)BK * (BN + PADN) : (size_t)BN * (BK + PADK);
+  size_t bytes = 2 * (a + b) * sizeof(bf16_t);
+  const size_t red = 2 * 2 * BN * sizeof(float);
+  return bytes > red ? bytes : red;
+}
+
+template <int BM, int BN, int MODE, bool STATS>
+int launch_fd(ConvArgs& a, hipStream_t st) {
+  a.mtiles = static_cast<int>(ceil_div(a.M, BM));
+  a.ntiles = static_cast<int>(ceil_div(a.Ncol, BN));
+  const long long nblk = (long long)a.mtiles * a.ntiles;
+  if (nblk > 0x7fffffff) return MDTF_EUNSUPPORTED;
+  const size_t lds = fd_lds<BM, BN, MODE, STATS>();
+  hipLaunchKernelGGL((conv_fd_kernel<BM, BN, MODE, STATS>), dim3((unsigned)nblk), dim3(NT), lds, st, a);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+template <int MODE, bool STATS>
+int dispatch_fd(ConvArgs& a, int bm, int bn, hipStream_t st) {
+  if (bm == 128 && bn == 128) return launch_fd<128, 128, MODE, STATS>(a, st);
+  if (bm == 128 && bn == 64) return launch_fd<128, 64, MODE, STATS>(a, st);
+  if (bm == 64 && bn == 64) return launch_fd<64, 64, MODE, STATS>(a, st);
+  if (bm == 256 && bn == 64) return launch_fd<256, 64, MODE, STATS>(a, st);
+  return MDTF_EUNSUPPORTED;
+}
+
+template <int BM, int BN>
+int launch_wgrad(ConvArgs& a, int splits, hipStream_t st) {
+  const int R = a.KH * a.KW * a.Cin;
+  a.mtiles = static_cast<int>(ceil_div(R, BM));
+  a.ntiles = static_cast<int>(ceil_div(a.Cout, BN));
+  const int kt_total = static_cast<int>(ceil_div(a.M, BK));
+  if (splits < 1) {
+    const int tiles = a.mtiles * a.ntiles;
+    splits = (1024 + tiles - 1) / tiles;
+  }
+  if (splits > kt_total) splits = kt_total;
+  a.ksplit_steps = (kt_total + splits - 1) / splits;
+  splits = (kt_total + a.ksplit_steps - 1) / a.ksplit_steps;
+  const size_t lds = 2 * ((size_t)BK * (BM + PADN) + (size_t)BK * (BN + PADN)) * sizeof(bf16_t);
+  hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN>), dim3(a.mtiles * a.ntiles * splits), dim3(NT), lds, st, a);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+ConvArgs make_args(int N, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int SH, int SW, int PH,
+                   int PW, int DH, int DW) {
+  ConvArgs a{};
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.Cin = Cin;
+  a.OH = OH;
+  a.OW = OW;
+  a.Cout = Cout;
+  a.KH = KH;
+  a.KW = KW;
+  a.SH = SH;
+  a.SW = SW;
+  a.PH = PH;
+  a.PW = PW;
+  a.DH = DH;
+  a.DW = DW;
+  return a;
+}
+
+}  // namespace
+
+// Y = conv(X, W); optional per-M-tile BN partials (stat_sum/stat_sq [mtiles][Cout]).
+// Returns the number of M tiles through *mtiles_out (for the BN finalize).
+MDTF_EXPORT int mdtf_conv_fwd(const void* x, const void* w, void* y, float* stat_sum, float* stat_sq, int N, int H,
+                              int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int SH, int SW, int PH, int PW,
+                              int DH, int DW, int bm, int bn, int* mtiles_out, hipStream_t st) {
+  if (Cin % 8 || Cout % 8) return MDTF_EINVAL;
+  ConvArgs a = make_args(N, H, W, Cin, OH, OW, Cout, KH, KW, SH, SW, PH, PW, DH, DW);
+  a.src = (const bf16_t*)x;
+  a.wgt = (const bf16_t*)w;
+  a.out = (bf16_t*)y;
+  a.stat_sum = stat_sum;
+  a.stat_sq = stat_sq;
+  a.M = (long long)N * OH * OW;
+  a.Ncol = Cout;
+  a.K = KH * KW * Cin;
+  int rc = stat_sum ? dispatch_fd<0, true>(a, bm, bn, st) : dispatch_fd<0, false>(a, bm, bn, st);
+  if (mtiles_out) *mtiles_out = a.mtiles;
+  return rc;
+}
+
+// DX = dgrad(DY, W)   (DX [N,H,W,Cin], DY [N,OH,OW,Cout])
+MDTF_EXPORT int mdtf_conv_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int OH, int OW,
+                                int Cout, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW, int bm, int bn,
+                                hipStream_t st) {
+  if (Cin % 8 || Cout % 8) return MDTF_EINVAL;
+  ConvArgs a = make_args(N, H, W, Cin, OH, OW, Cout, KH, KW, SH, SW, PH, PW, DH, DW);
+  a.src = (const bf16_t*)dy;
+  a.wgt = (const bf16_t*)w;
+  a.out = (bf16_t*)dx;
+  a.M = (long long)N * H * W;
+  a.Ncol = Cin;
+  a.K = KH * KW * Cout;
+  return dispatch_fd<1, false>(a, bm, bn, st);
+}
+
+// DW (fp32, HWIO, must be zeroed) += wgrad(X, DY)
+MDTF_EXPORT int mdtf_conv_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int Cin, int OH, int OW,
+                                int Cout, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW, int bm, int bn,
+                                int splits, hipStream_t st) {
+  if (Cin % 8 || Cout % 8) return MDTF_EINVAL;
+  ConvArgs a = make_args(N, H, W, Cin, OH, OW, Cout, KH, KW, SH, SW, PH, PW, DH, DW);
+  a.src = (const bf16_t*)x;
+  a.dy = (const bf16_t*)dy;
+  a.dw = dw;
+  a.M = (long long)N * OH * OW;
+  a.Ncol = Cout;
+  if (bm == 128 && bn == 128) return launch_wgrad<128, 128>(a, splits, st);
+  if (bm == 64 && bn == 64) return launch_wgrad<64, 64>(a, splits, st);
+  if (bm == 128 && bn == 64) return launch_wgrad<128, 64>(a, splits, st);
+  if (bm == 64 && bn == 128) return launch_wgrad<64, 128>(a, splits, st);
+  return MDTF_EUNSUPPORTED;
+}

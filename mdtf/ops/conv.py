@@ -1,49 +1,262 @@
-"""Convolution dispatch for NHWC activations / HWIO filters on the GPU.
+"""Convolution on the GPU: hand-written implicit-GEMM MFMA kernels (``csrc/conv_igemm.hip``).
 
-Per-shape backend table (``CONV_BACKEND``): the hand-written implicit-GEMM
-MFMA kernels of ``csrc/conv_igemm.hip`` for the shapes where they beat the
-library; MIOpen (through ``torch.nn.functional.conv2d`` on channels-last
-views) otherwise.  The table is filled by ``mdtf/ops/autotune.py`` on the
-target GPU; until a shape is tuned, MIOpen is used.
+NHWC activations, HWIO filters (TF layouts, which are also the natural
+implicit-GEMM layouts: ``W[(kh,kw,ci)][co]`` is the row-major B matrix).
+Each pass (fwd / dgrad / wgrad) of each conv shape runs on the backend chosen
+by the per-shape table ``conv_table.json`` (written by
+``bench/conv_autotune.py`` on an MI355X: the hand-written kernel wherever it
+beats MIOpen, with its best tile); ``MDTF_CONV=mdtf|miopen`` forces one
+backend.  Shapes the HIP kernel cannot take (C % 8 != 0, e.g. a 3-channel
+stem) use MIOpen.
 """
+import json
+import os
+
 import torch
 import torch.nn.functional as F
 
 from . import _native as N
 
+N.register("mdtf_conv_fwd", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 17 + [N.P, N.P])
+N.register("mdtf_conv_dgrad", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
+N.register("mdtf_conv_wgrad", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 
-def _miopen_conv(x, w_hwio, stride, pads, dil):
+_HERE = os.path.dirname(os.path.abspath(__file__))
+TABLE_PATH = os.path.join(_HERE, "conv_table.json")
+_TABLE = None
+
+
+def table():
+    global _TABLE
+    if _TABLE is None:
+        _TABLE = {}
+        if os.path.exists(TABLE_PATH):
+            with open(TABLE_PATH) as f:
+                _TABLE = json.load(f)
+    return _TABLE
+
+
+def shape_key(pass_, x_shape, w_shape, stride, pads, dil):
+    n, h, w, c = x_shape
+    kh, kw, ci, co = w_shape
+    return "%s:%d,%d,%d,%d:%d,%d,%d:%d,%d:%d,%d,%d,%d:%d,%d" % (
+        pass_, n, h, w, c, kh, kw, co, stride[0], stride[1], pads[0], pads[1], pads[2], pads[3], dil[0], dil[1])
+
+
+def _default_tile(ncol):
+    return (128, 128) if ncol % 128 == 0 else (128, 64)
+
+
+def choose(pass_, x_shape, w_shape, stride, pads, dil):
+    """-> ('mdtf', bm, bn, splits) or ('miopen',)."""
+    n, h, w, c = x_shape
+    kh, kw, ci, co = w_shape
+    forced = os.environ.get("MDTF_CONV", "auto")
+    native_ok = c % 8 == 0 and co % 8 == 0
+    if not native_ok or forced == "miopen":
+        return ("miopen",)
+    ent = table().get(shape_key(pass_, x_shape, w_shape, stride, pads, dil))
+    if forced == "auto" and ent is not None:
+        if ent["backend"] == "miopen":
+            return ("miopen",)
+        return ("mdtf", ent["bm"], ent["bn"], ent.get("splits", 0))
+    if pass_ == "wgrad":
+        r = kh * kw * ci
+        return ("mdtf", 128 if r >= 128 else 64, 128 if co % 128 == 0 else 64, 0)
+    bm, bn = _default_tile(co if pass_ == "fwd" else ci)
+    return ("mdtf", bm, bn, 0)
+
+
+# ---------------------------------------------------------------------------
+# MIOpen (library) path through aten on channels-last views
+# ---------------------------------------------------------------------------
+def _nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+def _w_oihw(w):
+    return w.permute(3, 2, 0, 1).contiguous(memory_format=torch.channels_last)
+
+
+def _sym(pads):
     pt, pb, pl, pr = pads
-    xc = x.permute(0, 3, 1, 2)                                      # NCHW view, channels-last strides
-    if not (pt == pb and pl == pr):
+    return pt == pb and pl == pr
+
+
+def miopen_fwd(x, w, stride, pads, dil):
+    pt, pb, pl, pr = pads
+    xc = _nchw(x)
+    if not _sym(pads):
+        xc = F.pad(xc, (pl, pr, pt, pb))
+        pt = pl = 0
+    y = F.conv2d(xc, _w_oihw(w).to(x.dtype), None, stride, (pt, pl), dil)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+def miopen_bwd(x, w, dy, stride, pads, dil, need_dx, need_dw):
+    pt, pb, pl, pr = pads
+    xc = _nchw(x)
+    if not _sym(pads):
         xc = F.pad(xc, (pl, pr, pt, pb))
         ph, pw = 0, 0
     else:
         ph, pw = pt, pl
-    wt = w_hwio.permute(3, 2, 0, 1).contiguous(memory_format=torch.channels_last)
-    y = F.conv2d(xc, wt.to(x.dtype), None, stride, (ph, pw), dil)
-    return y.permute(0, 2, 3, 1)
+    wt = _w_oihw(w).to(x.dtype)
+    dyc = _nchw(dy)
+    dx_c, dw_c, _ = torch.ops.aten.convolution_backward(
+        dyc, xc, wt, None, list(stride), [ph, pw], list(dil), False, [0, 0], 1, [need_dx, need_dw, False])
+    dx = dw = None
+    if need_dx:
+        if not _sym(pads):
+            dx_c = dx_c[:, :, pt:pt + x.shape[1], pl:pl + x.shape[2]]
+        dx = dx_c.permute(0, 2, 3, 1).contiguous()
+    if need_dw:
+        dw = dw_c.permute(2, 3, 1, 0).contiguous()       # OIHW -> HWIO
+    return dx, dw
+
+
+# ---------------------------------------------------------------------------
+# hand-written kernels
+# ---------------------------------------------------------------------------
+def _geo(x, w, out_hw, stride, pads, dil):
+    n, h, wd, c = x.shape
+    kh, kw, ci, co = w.shape
+    return [n, h, wd, c, out_hw[0], out_hw[1], co, kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1]]
+
+
+def mdtf_fwd(x, w, out_hw, stride, pads, dil, bm, bn, stats=None):
+    n = x.shape[0]
+    co = w.shape[3]
+    y = torch.empty((n, out_hw[0], out_hw[1], co), dtype=x.dtype, device=x.device)
+    mt = N.I(0)
+    s_sum, s_sq = (stats if stats is not None else (None, None))
+    import ctypes
+    N.check(N.fn("mdtf_conv_fwd")(N.ptr(x), N.ptr(w), N.ptr(y), N.ptr(s_sum), N.ptr(s_sq),
+                                  *_geo(x, w, out_hw, stride, pads, dil), bm, bn, ctypes.byref(mt), N.stream_ptr()),
+            "conv_fwd")
+    return y
+
+
+def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn):
+    dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
+    n, h, wd, c = x_shape
+    kh, kw, ci, co = w.shape
+    N.check(N.fn("mdtf_conv_dgrad")(N.ptr(dy), N.ptr(w), N.ptr(dx), n, h, wd, c, dy.shape[1], dy.shape[2], co, kh,
+                                    kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1], bm, bn,
+                                    N.stream_ptr()), "conv_dgrad")
+    return dx
+
+
+def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits):
+    dw = torch.zeros(w_shape, dtype=torch.float32, device=x.device)
+    n, h, wd, c = x.shape
+    kh, kw, ci, co = w_shape
+    N.check(N.fn("mdtf_conv_wgrad")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co, kh,
+                                    kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1], bm, bn, int(splits),
+                                    N.stream_ptr()), "conv_wgrad")
+    return dw
+
+
+def _pads_ok(pads):
+    # the kernels take (top, left) padding; bottom/right are implied by the output size
+    return True
+
+
+class _Conv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pads, dil, out_hw):
+        x = x.contiguous()
+        w = w.contiguous()
+        ch = choose("fwd", x.shape, w.shape, stride, pads, dil)
+        if ch[0] == "mdtf":
+            y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2])
+        else:
+            y = miopen_fwd(x, w, stride, pads, dil)
+        ctx.save_for_backward(x, w)
+        ctx.args = (stride, pads, dil)
+        ctx.w_dtype = w.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pads, dil = ctx.args
+        dy = dy.contiguous()
+        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = None
+        cd = choose("dgrad", x.shape, w.shape, stride, pads, dil) if need_dx else None
+        cw = choose("wgrad", x.shape, w.shape, stride, pads, dil) if need_dw else None
+        lib_dx = need_dx and cd[0] == "miopen"
+        lib_dw = need_dw and cw[0] == "miopen"
+        if lib_dx or lib_dw:
+            ldx, ldw = miopen_bwd(x, w, dy, stride, pads, dil, lib_dx, lib_dw)
+            if lib_dx:
+                dx = ldx
+            if lib_dw:
+                dw = ldw
+        if need_dx and not lib_dx:
+            dx = mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2])
+        if need_dw and not lib_dw:
+            dw = mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3])
+        if dw is not None and dw.dtype != ctx.w_dtype:
+            dw = dw.to(ctx.w_dtype) if ctx.w_dtype != torch.bfloat16 else dw
+        return dx, dw, None, None, None, None
 
 
 def conv2d_nhwc(x, w, stride, pads, dil, bias=None, act=None):
-    y = _miopen_conv(x, w, stride, pads, dil)
-    if y.stride(-1) != 1:
-        y = y.contiguous()
+    if x.dtype != torch.bfloat16:
+        raise TypeError("mdtf conv kernels take bf16 activations, got %s" % x.dtype)
+    if w.dtype != x.dtype:
+        w = w.to(x.dtype)
+    n, h, wd, c = x.shape
+    kh, kw, _, co = w.shape
+    oh = (h + pads[0] + pads[1] - ((kh - 1) * dil[0] + 1)) // stride[0] + 1
+    ow = (wd + pads[2] + pads[3] - ((kw - 1) * dil[1] + 1)) // stride[1] + 1
+    y = _Conv.apply(x, w, tuple(stride), tuple(pads), tuple(dil), (oh, ow))
     if bias is not None or act is not None:
         from . import kernels
-        y = kernels.bias_act(y.contiguous(), bias, act)
+        y = kernels.bias_act(y, bias, act)
     return y
 
 
 def conv2d_dgrad_nhwc(x, w, out_shape, stride, pads):
-    """conv2d_transpose = data-gradient of conv2d (filter [kh, kw, cout, cin])."""
+    """conv2d_transpose == data-gradient of conv2d with filter [kh, kw, cout_op, cin_op]."""
     n, oh, ow, co = out_shape
-    kh, kw, _, ci = w.shape
-    pt, pb, pl, pr = pads
+    kh, kw, wco, wci = w.shape
+    wb = w.to(x.dtype).contiguous()
+    ch = choose("dgrad", (n, oh, ow, co), (kh, kw, co, wci), stride, pads, (1, 1))
+    if ch[0] == "mdtf":
+        return _ConvT.apply(x, wb, tuple(stride), tuple(pads), (n, oh, ow, co), ch[1], ch[2])
     xc = x.permute(0, 3, 1, 2)
-    wt = w.permute(3, 2, 0, 1).to(x.dtype)                           # [cin(x), cout, kh, kw]
+    wt = w.permute(3, 2, 0, 1).to(x.dtype)
     y = F.conv_transpose2d(xc, wt, None, stride, 0)
-    y = y[:, :, pt:pt + oh, pl:pl + ow]
+    y = y[:, :, pads[0]:pads[0] + oh, pads[2]:pads[2] + ow]
     if y.shape[2] < oh or y.shape[3] < ow:
         y = F.pad(y, (0, ow - y.shape[3], 0, oh - y.shape[2]))
     return y.permute(0, 2, 3, 1).contiguous()
+
+
+class _ConvT(torch.autograd.Function):
+    """Transposed conv as conv dgrad (fwd) with conv fwd / wgrad for its backward."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, pads, out_shape, bm, bn):
+        x = x.contiguous()
+        y = mdtf_dgrad(x, w, out_shape, stride, pads, (1, 1), bm, bn)
+        ctx.save_for_backward(x, w)
+        ctx.args = (stride, pads)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pads = ctx.args
+        dy = dy.contiguous()
+        oh, ow = x.shape[1], x.shape[2]
+        bm, bn = _default_tile(w.shape[3])
+        dx = mdtf_fwd(dy, w, (oh, ow), stride, pads, (1, 1), bm, bn) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = mdtf_wgrad(dy, x, w.shape, stride, pads, (1, 1), 128 if w.shape[0] * w.shape[1] * w.shape[2] >= 128
+                            else 64, 128 if w.shape[3] % 128 == 0 else 64, 0)
+        return dx, dw, None, None, None, None, None

@@ -223,3 +223,67 @@ def test_resnet_train_step_gpu():
         losses.append(float(sess.run(loss)))
     assert all(l == l for l in losses)
     assert losses[-1] < losses[0]
+
+
+CONV_CASES = [
+    # (N, H, W, C, KH, KW, CO, stride, padding)
+    (2, 9, 9, 16, 3, 3, 32, 1, "SAME"),
+    (3, 14, 14, 64, 1, 1, 256, 1, "VALID"),
+    (2, 15, 15, 32, 3, 3, 64, 2, (1, 1)),
+    (2, 16, 16, 64, 1, 1, 128, 2, "VALID"),
+    (1, 13, 11, 8, 3, 3, 72, 1, "SAME"),           # K=72 (not a multiple of 32), Cout=72
+    (2, 20, 20, 8, 7, 7, 64, 2, (3, 3)),           # stem-like 7x7/2 with 8 channels
+    (5, 7, 7, 128, 3, 3, 128, 1, "SAME"),          # M tail (245 rows)
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_hip_fwd_dgrad_wgrad(case, monkeypatch):
+    monkeypatch.setenv("MDTF_CONV", "mdtf")
+    n, h, w_, c, kh, kw, co, s, pad = case
+    torch.manual_seed(5)
+    x = torch.randn(n, h, w_, c)
+    w = torch.randn(kh, kw, c, co) * (1.0 / (kh * kw * c) ** 0.5)
+    xg = x.to(DEV).bfloat16().requires_grad_(True)
+    wg = w.to(DEV).bfloat16().requires_grad_(True)
+    y = ops.conv2d(xg, wg, s, pad)
+    xc = x.bfloat16().float().requires_grad_(True)
+    wc = w.bfloat16().float().requires_grad_(True)
+    yr = ops.conv2d(xc, wc, s, pad)
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn(yr.shape)
+    y.backward(dy.to(DEV).bfloat16())
+    yr.backward(dy.bfloat16().float())
+    assert _rel(xg.grad, xc.grad) < 2e-2
+    assert _rel(wg.grad, wc.grad) < 2e-2
+
+
+def test_conv_hip_exact_integers(monkeypatch):
+    """Small-integer data: bf16 products/sums are exact, so outputs must match bit for bit."""
+    monkeypatch.setenv("MDTF_CONV", "mdtf")
+    torch.manual_seed(6)
+    x = torch.randint(-3, 4, (2, 10, 10, 16)).float()
+    w = torch.randint(-2, 3, (3, 3, 16, 64)).float()
+    y = ops.conv2d(x.to(DEV).bfloat16(), w.to(DEV).bfloat16(), 1, "SAME")
+    yr = ops.conv2d(x, w, 1, "SAME")
+    assert torch.equal(y.float().cpu(), yr)
+
+
+def test_conv_transpose_hip(monkeypatch):
+    monkeypatch.setenv("MDTF_CONV", "mdtf")
+    torch.manual_seed(7)
+    x = torch.randn(2, 8, 8, 32)
+    w = torch.randn(3, 3, 16, 32) * 0.1                 # [kh, kw, cout, cin]
+    xg = x.to(DEV).bfloat16().requires_grad_(True)
+    wg = w.to(DEV).bfloat16().requires_grad_(True)
+    y = ops.conv2d_transpose(xg, wg, [2, 16, 16, 16], 2, "SAME")
+    xc = x.bfloat16().float().requires_grad_(True)
+    wc = w.bfloat16().float().requires_grad_(True)
+    yr = ops.conv2d_transpose(xc, wc, [2, 16, 16, 16], 2, "SAME")
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn(yr.shape)
+    y.backward(dy.to(DEV).bfloat16())
+    yr.backward(dy.bfloat16().float())
+    assert _rel(xg.grad, xc.grad) < 2e-2
+    assert _rel(wg.grad, wc.grad) < 2e-2
