@@ -150,6 +150,10 @@ DEFINE_string('learning_rate_json', 'YOUR LEARNING RATE SAVING PATH', "Path of t
 # framework extensions
 DEFINE_string('data_load_option', 'tfrecords', "DistributeExperiment input mode: tfrecords or placeholder.")
 DEFINE_string('ps_mode', 'sync', "Parameter-server mode: sync (RCCL reduce-scatter/all-gather) or async.")
+DEFINE_string('model_dir', '', "Override @model_dir (checkpoint directory).")
+DEFINE_string('data_dir', '', "Override @data_dir (input data).")
+DEFINE_string('mode', '', "Override @current_mode (Train / Eval).")
+DEFINE_integer('epochs', 0, "Override @epoch_num when > 0.")
 
 
 def apply_thread_flags():
