@@ -40,8 +40,8 @@ Geo make_geo(long long M, int C) {
   g.tpr = t;
   g.rg = kThreads / t;
   g.gy = static_cast<int>(ceil_div(cv, t));
-  long long gx = ceil_div(M, (long long)g.rg * 8);  // >= 8 rows per row-group
-  long long cap = 1024 / g.gy;
+  long long gx = ceil_div(M, (long long)g.rg * 16);  // >= 16 rows per row-group
+  long long cap = 256 / g.gy;
   if (cap < 1) cap = 1;
   if (gx > cap) gx = cap;
   if (gx < 1) gx = 1;
@@ -65,7 +65,30 @@ __global__ void __launch_bounds__(kThreads)
 #pragma unroll
   for (int i = 0; i < 8; ++i) s0[i] = s1[i] = 0.f;
   if (c0 < C) {
-    for (long long r = (long long)blockIdx.x * rg + rgi; r < M; r += (long long)gridDim.x * rg) {
+    const long long step = (long long)gridDim.x * rg;
+    long long r = (long long)blockIdx.x * rg + rgi;
+    // 4 rows per iteration: all loads issued before the first use (bytes in flight)
+    for (; r + 3 * step < M; r += 4 * step) {
+      float va[4][8], vb[4][8], vy[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long off = (r + u * step) * C + c0;
+        load_bf8(a + off, va[u]);
+        if (BWD) load_bf8(b + off, vb[u]);
+        if (BWD && RELU) load_bf8(y + off, vy[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float v = va[u][i];
+          if (BWD && RELU) v = vy[u][i] > 0.f ? v : 0.f;
+          s0[i] += v;
+          s1[i] += BWD ? v * vb[u][i] : v * v;
+        }
+      }
+    }
+    for (; r < M; r += step) {
       const long long off = r * C + c0;
       float va[8];
       load_bf8(a + off, va);
@@ -225,8 +248,8 @@ __global__ void __launch_bounds__(1024)
   float g = gamma ? gamma[c] : 1.f;
   float db = (float)sdz;
   float dg = (float)((sdzx - (double)mu * sdz) * inv);
-  if (dgamma) dgamma[c] = dg;
-  if (dbeta) dbeta[c] = db;
+  if (dgamma) dgamma[c] += dg;     // accumulate: zeroed buffer or the variable's fp32 grad slot
+  if (dbeta) dbeta[c] += db;
   float a = g * inv;
   float invM = 1.f / (float)M;
   // dx = a*(dz - db/M - xhat*dg/M), xhat = (x-mu)*inv
@@ -294,6 +317,35 @@ MDTF_EXPORT int mdtf_bn_fwd_train(const void* x, const void* res, void* y, long 
                      (const bf16_t*)x, nullptr, nullptr, M, C, g.tpr, g.rg, p0, p1);
   hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, p0, p1, g.gx, M, C, gamma, beta,
                      mmean, mvar, decay, eps, mean, invstd, scale, shift);
+  long long n8 = M * C / 8;
+  const bf16_t* r = (const bf16_t*)res;
+  if (r && relu)
+    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x, r,
+                       (bf16_t*)y, n8, C, scale, shift);
+  else if (r)
+    hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x, r,
+                       (bf16_t*)y, n8, C, scale, shift);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
+                       nullptr, (bf16_t*)y, n8, C, scale, shift);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
+                       nullptr, (bf16_t*)y, n8, C, scale, shift);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// Training forward when the producing conv already emitted Σx / Σx² partials
+// ([P][C] each, e.g. the conv epilogue's 64 atomic slots): finalize + apply only.
+MDTF_EXPORT int mdtf_bn_fwd_stats(const void* x, const void* res, void* y, long long M, int C, const float* gamma,
+                                  const float* beta, float* mmean, float* mvar, float decay, float eps, int relu,
+                                  float* mean, float* invstd, const float* psum, const float* psq, int P, float* ws,
+                                  hipStream_t st) {
+  if (C % 8) return MDTF_EINVAL;
+  float* scale = ws;
+  float* shift = ws + C;
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M,
+                     C, gamma, beta, mmean, mvar, decay, eps, mean, invstd, scale, shift);
   long long n8 = M * C / 8;
   const bf16_t* r = (const bf16_t*)res;
   if (r && relu)

@@ -36,6 +36,7 @@ constexpr int BK = 32;
 constexpr int PADK = 8;    // K-contiguous rows: 32 + 8 elements = 80 B
 constexpr int PADN = 16;   // N-contiguous rows: cols + 16 elements
 constexpr int NT = 256;
+constexpr int kStatSlots = 64;   // BN-statistics partial rows written by the fwd epilogue
 
 struct ConvArgs {
   const bf16_t* src;   // gathered activation: X (fwd, wgrad) or DY (dgrad)
@@ -322,8 +323,10 @@ __global__ void __launch_bounds__(NT) conv_fd_kernel(ConvArgs a) {
           s += red[w * BN + nl];
           q += red[WM * BN + w * BN + nl];
         }
-        a.stat_sum[(long long)mt * a.Ncol + n] = s;
-        a.stat_sq[(long long)mt * a.Ncol + n] = q;
+        // 64 atomic slots (zeroed by the caller) spread the M-tiles' partials
+        const long long slot = (long long)(mt & (kStatSlots - 1)) * a.Ncol + n;
+        atomicAdd(a.stat_sum + slot, s);
+        atomicAdd(a.stat_sq + slot, q);
       }
     }
   }

@@ -36,7 +36,10 @@ def _variable_with_weight_decay(name, shape, stddev, wd):
     """Truncated-normal variable; adds ``wd * l2_loss(var)`` to 'losses' (``:41-66``)."""
     var = _variable_on_cpu(name, shape, V.truncated_normal_initializer(stddev=stddev))
     if wd is not None and wd != 0.0:
-        V.add_to_collection("losses", ops.l2_loss(var) * wd)
+        store = V.get_store()
+        scope = V.get_variable_scope().name
+        full = "%s/%s" % (scope, name) if scope else name
+        V.add_to_collection("losses", ops.l2_loss(store.vars[full].read(store.compute_dtype)) * wd)
     return var
 
 
@@ -182,7 +185,6 @@ def conv_bn(layer_name, x, out_channels, kernel_size=3, stride=1, relu=True, res
         padding = "SAME" if stride == 1 else ((k - 1) // 2, (k - 1) // 2)
     with V.variable_scope(layer_name):
         w = V.get_variable('weights', [k, k, cin, out_channels], initializer=V.variance_scaling_initializer())
-        y = ops.conv2d(x, w, stride, padding)
         c = out_channels
         gamma = V.get_variable('BatchNorm/gamma', [c], initializer=V.constant_initializer(0.0 if zero_gamma else 1.0),
                                keep_fp32=True)
@@ -190,7 +192,7 @@ def conv_bn(layer_name, x, out_channels, kernel_size=3, stride=1, relu=True, res
         mm = V.get_variable('BatchNorm/moving_mean', [c], initializer=V.constant_initializer(0.0), trainable=False)
         mv = V.get_variable('BatchNorm/moving_variance', [c], initializer=V.constant_initializer(1.0),
                             trainable=False)
-        return ops.batch_norm(y, gamma, beta, mm, mv, training, bn_decay, bn_epsilon, relu, residual)
+        return ops.conv_bn(x, w, gamma, beta, mm, mv, stride, padding, training, bn_decay, bn_epsilon, relu, residual)
 
 
 def dense(layer_name, x, out_features, act=None, initializer=None):

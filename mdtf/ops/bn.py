@@ -2,11 +2,14 @@
 import torch
 
 from . import _native as N
+from ..train import variables as V
 
 N.register("mdtf_bn_workspace_floats", [N.L, N.I], N.L)
 N.register("mdtf_bn_fwd_train", [N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P])
 N.register("mdtf_bn_fwd_eval", [N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.I, N.P, N.P])
 N.register("mdtf_bn_bwd", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P, N.P])
+N.register("mdtf_bn_fwd_stats", [N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P,
+                                 N.I, N.P, N.P])
 
 
 def _check(x):
@@ -22,25 +25,36 @@ def _f32(t):
 
 class _BNTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, mm, mv, decay, eps, relu):
+    def forward(ctx, x, gamma, beta, residual, mm, mv, decay, eps, relu, stats):
         x = x.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
         y = torch.empty_like(x)
         mean = torch.empty(C, dtype=torch.float32, device=x.device)
         invstd = torch.empty_like(mean)
-        ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
         g, b = _f32(gamma), _f32(beta)
         res = residual.contiguous() if residual is not None else None
-        N.check(N.fn("mdtf_bn_fwd_train")(N.ptr(x), N.ptr(res), N.ptr(y), M, C, N.ptr(g), N.ptr(b), N.ptr(mm),
-                                          N.ptr(mv), float(decay), float(eps), int(relu), N.ptr(mean), N.ptr(invstd),
-                                          N.ptr(ws), N.stream_ptr()), "bn_fwd_train")
+        if stats is not None:
+            # Σx / Σx² already produced by the conv epilogue: finalize + apply only
+            psum, psq, P = stats
+            ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+            N.check(N.fn("mdtf_bn_fwd_stats")(N.ptr(x), N.ptr(res), N.ptr(y), M, C, N.ptr(g), N.ptr(b), N.ptr(mm),
+                                              N.ptr(mv), float(decay), float(eps), int(relu), N.ptr(mean),
+                                              N.ptr(invstd), N.ptr(psum), N.ptr(psq), int(P), N.ptr(ws),
+                                              N.stream_ptr()), "bn_fwd_stats")
+        else:
+            ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
+            N.check(N.fn("mdtf_bn_fwd_train")(N.ptr(x), N.ptr(res), N.ptr(y), M, C, N.ptr(g), N.ptr(b), N.ptr(mm),
+                                              N.ptr(mv), float(decay), float(eps), int(relu), N.ptr(mean),
+                                              N.ptr(invstd), N.ptr(ws), N.stream_ptr()), "bn_fwd_train")
         ctx.save_for_backward(x, y, g, mean, invstd)
         ctx.has_res = residual is not None
         ctx.relu = relu
-        ctx.gamma_dtype = gamma.dtype if gamma is not None else None
         ctx.has_gamma = gamma is not None
         ctx.has_beta = beta is not None
+        ctx.sinks = (V.grad_sink(gamma) if gamma is not None else None,
+                     V.grad_sink(beta) if beta is not None else None)
+        ctx.like = (gamma, beta)
         return y
 
     @staticmethod
@@ -51,22 +65,26 @@ class _BNTrain(torch.autograd.Function):
         M = x.numel() // C
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
-        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
-        dbeta = torch.empty_like(dgamma)
+        sg, sb = ctx.sinks
+        # dgamma/dbeta accumulate straight into the fp32 grad slots when available
+        dgamma = sg.grad if sg is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
+        dbeta = sb.grad if sb is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
         ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
         N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(x), N.ptr(y), N.ptr(dx), N.ptr(dres), M, C, N.ptr(g),
                                     N.ptr(mean), N.ptr(invstd), N.ptr(dgamma), N.ptr(dbeta), int(ctx.relu), N.ptr(ws),
                                     N.stream_ptr()), "bn_bwd")
-        return (dx, dgamma if ctx.has_gamma else None, dbeta if ctx.has_beta else None, dres,
-                None, None, None, None, None)
+        gamma, beta = ctx.like
+        rg = (V.grad_marker(gamma) if sg is not None else dgamma) if ctx.has_gamma else None
+        rb = (V.grad_marker(beta) if sb is not None else dbeta) if ctx.has_beta else None
+        return (dx, rg, rb, dres, None, None, None, None, None, None)
 
 
-def batch_norm_nhwc(x, gamma, beta, moving_mean, moving_var, training, decay, epsilon, relu, residual):
+def batch_norm_nhwc(x, gamma, beta, moving_mean, moving_var, training, decay, epsilon, relu, residual, stats=None):
     _check(x)
     if residual is not None and residual.dtype != x.dtype:
         residual = residual.to(x.dtype)
     if training:
-        return _BNTrain.apply(x, gamma, beta, residual, moving_mean, moving_var, decay, epsilon, bool(relu))
+        return _BNTrain.apply(x, gamma, beta, residual, moving_mean, moving_var, decay, epsilon, bool(relu), stats)
     x = x.contiguous()
     C = x.shape[-1]
     M = x.numel() // C

@@ -16,6 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
+from ..train import variables as V
 
 N.register("mdtf_conv_fwd", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 17 + [N.P, N.P])
 N.register("mdtf_conv_dgrad", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
@@ -147,8 +148,9 @@ def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn):
     return dx
 
 
-def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits):
-    dw = torch.zeros(w_shape, dtype=torch.float32, device=x.device)
+def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None):
+    """fp32 HWIO weight gradient; accumulates into ``out`` when given (must be zeroed or a grad slot)."""
+    dw = torch.zeros(w_shape, dtype=torch.float32, device=x.device) if out is None else out
     n, h, wd, c = x.shape
     kh, kw, ci, co = w_shape
     N.check(N.fn("mdtf_conv_wgrad")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co, kh,
@@ -162,23 +164,39 @@ def _pads_ok(pads):
     return True
 
 
+STAT_SLOTS = 64   # atomic partial rows of the fused BN statistics (csrc/conv_igemm.hip kStatSlots)
+
+
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pads, dil, out_hw):
+    def forward(ctx, x, w, stride, pads, dil, out_hw, want_stats):
         x = x.contiguous()
         w = w.contiguous()
         ch = choose("fwd", x.shape, w.shape, stride, pads, dil)
+        stats = None
         if ch[0] == "mdtf":
-            y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2])
+            if want_stats:
+                co = w.shape[3]
+                buf = torch.zeros((2, STAT_SLOTS, co), dtype=torch.float32, device=x.device)
+                stats = (buf[0], buf[1])
+            y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2], stats)
         else:
             y = miopen_fwd(x, w, stride, pads, dil)
         ctx.save_for_backward(x, w)
         ctx.args = (stride, pads, dil)
         ctx.w_dtype = w.dtype
+        ctx.sink = V.grad_sink(w)
+        if want_stats:
+            if stats is None:
+                empty = torch.empty(0, device=x.device)
+                ctx.mark_non_differentiable(empty, empty)
+                return y, empty, empty
+            ctx.mark_non_differentiable(stats[0], stats[1])
+            return y, stats[0], stats[1]
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, *unused):
         x, w = ctx.saved_tensors
         stride, pads, dil = ctx.args
         dy = dy.contiguous()
@@ -188,19 +206,37 @@ class _Conv(torch.autograd.Function):
         cw = choose("wgrad", x.shape, w.shape, stride, pads, dil) if need_dw else None
         lib_dx = need_dx and cd[0] == "miopen"
         lib_dw = need_dw and cw[0] == "miopen"
+        sink = ctx.sink
         if lib_dx or lib_dw:
             ldx, ldw = miopen_bwd(x, w, dy, stride, pads, dil, lib_dx, lib_dw)
             if lib_dx:
                 dx = ldx
             if lib_dw:
-                dw = ldw
+                if sink is not None:
+                    sink.grad.add_(ldw)            # straight into the fp32 grad slot
+                    dw = V.grad_marker(w)
+                else:
+                    dw = ldw
         if need_dx and not lib_dx:
             dx = mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2])
         if need_dw and not lib_dw:
-            dw = mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3])
-        if dw is not None and dw.dtype != ctx.w_dtype:
-            dw = dw.to(ctx.w_dtype) if ctx.w_dtype != torch.bfloat16 else dw
-        return dx, dw, None, None, None, None
+            if sink is not None:
+                # fp32 atomics of the wgrad kernel accumulate into the flat gradient buffer
+                mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], out=sink.grad)
+                dw = V.grad_marker(w)
+            else:
+                dw = mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3])
+                if dw.dtype != ctx.w_dtype:
+                    dw = dw.to(ctx.w_dtype)
+        return dx, dw, None, None, None, None, None
+
+
+def _out_hw(x, w, stride, pads, dil):
+    n, h, wd, c = x.shape
+    kh, kw, _, co = w.shape
+    oh = (h + pads[0] + pads[1] - ((kh - 1) * dil[0] + 1)) // stride[0] + 1
+    ow = (wd + pads[2] + pads[3] - ((kw - 1) * dil[1] + 1)) // stride[1] + 1
+    return oh, ow
 
 
 def conv2d_nhwc(x, w, stride, pads, dil, bias=None, act=None):
@@ -208,15 +244,23 @@ def conv2d_nhwc(x, w, stride, pads, dil, bias=None, act=None):
         raise TypeError("mdtf conv kernels take bf16 activations, got %s" % x.dtype)
     if w.dtype != x.dtype:
         w = w.to(x.dtype)
-    n, h, wd, c = x.shape
-    kh, kw, _, co = w.shape
-    oh = (h + pads[0] + pads[1] - ((kh - 1) * dil[0] + 1)) // stride[0] + 1
-    ow = (wd + pads[2] + pads[3] - ((kw - 1) * dil[1] + 1)) // stride[1] + 1
-    y = _Conv.apply(x, w, tuple(stride), tuple(pads), tuple(dil), (oh, ow))
+    y = _Conv.apply(x, w, tuple(stride), tuple(pads), tuple(dil), _out_hw(x, w, stride, pads, dil), False)
     if bias is not None or act is not None:
         from . import kernels
         y = kernels.bias_act(y, bias, act)
     return y
+
+
+def conv2d_stats_nhwc(x, w, stride, pads, dil):
+    """conv2d that also returns fused BN statistics partials ``(psum, psq, P)`` (or None)."""
+    if x.dtype != torch.bfloat16:
+        raise TypeError("mdtf conv kernels take bf16 activations, got %s" % x.dtype)
+    if w.dtype != x.dtype:
+        w = w.to(x.dtype)
+    y, psum, psq = _Conv.apply(x, w, tuple(stride), tuple(pads), tuple(dil), _out_hw(x, w, stride, pads, dil), True)
+    if psum.numel() == 0:
+        return y, None
+    return y, (psum, psq, STAT_SLOTS)
 
 
 def conv2d_dgrad_nhwc(x, w, out_shape, stride, pads):

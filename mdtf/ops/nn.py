@@ -231,6 +231,27 @@ def batch_norm(x, gamma, beta, moving_mean, moving_var, training=True, decay=0.9
     return y.to(x.dtype)
 
 
+def conv_bn(x, w, gamma, beta, moving_mean, moving_var, strides=1, padding="SAME", training=True, decay=0.9,
+            epsilon=1e-5, relu=True, residual=None):
+    """conv2d (no bias) -> batch_norm (+residual) (+ReLU).
+
+    On the GPU the conv epilogue emits the per-channel Σy/Σy² partials, so the
+    BN statistics pass over y disappears (BN runs finalize + apply only).
+    """
+    n, h, wd, c = x.shape
+    kh, kw, ci, co = w.shape
+    sh, sw = pair(strides)
+    oh, ow, pt, pb, pl, pr = conv_geometry(h, wd, kh, kw, (sh, sw), padding)
+    if _native.use_native(x) and training:
+        from . import conv as conv_mod
+        from . import bn
+        y, stats = conv_mod.conv2d_stats_nhwc(x, w, (sh, sw), (pt, pb, pl, pr), (1, 1))
+        return bn.batch_norm_nhwc(y, gamma, beta, moving_mean, moving_var, True, decay, epsilon, relu, residual,
+                                  stats=stats)
+    y = conv2d(x, w, strides, (pt, pb, pl, pr))
+    return batch_norm(y, gamma, beta, moving_mean, moving_var, training, decay, epsilon, relu, residual)
+
+
 def local_response_normalization(x, depth_radius=5, bias=1.0, alpha=1.0, beta=0.5, name=None):
     """``tf.nn.lrn`` over the channel (last) axis of an NHWC tensor."""
     if _native.use_native(x):

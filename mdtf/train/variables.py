@@ -178,7 +178,9 @@ class Variable(object):
             return self.master                      # moving statistics etc. are updated in place
         if torch.is_grad_enabled():
             self.uses += 1
-            return _VarRead.apply(_grad_token(), self, compute_dtype)
+            out = _VarRead.apply(_grad_token(), self, compute_dtype)
+            out._mdtf_var = self          # lets fused kernels accumulate straight into the grad slot
+            return out
         if self.shadow is not None:
             return self.shadow
         if compute_dtype is not None and not self.keep_fp32 and self.master.dtype != compute_dtype:
@@ -220,11 +222,53 @@ class _VarRead(torch.autograd.Function):
         var = ctx.var
         if var.grad is None:
             var.grad = torch.zeros_like(var.master)
-        var.grad.add_(g.to(var.grad.dtype) if g.dtype != var.grad.dtype else g)
-        var.uses -= 1
-        if var.uses <= 0 and var.on_grad_ready is not None:
-            var.on_grad_ready(var)
+        if not _is_marker(g):             # a sink-only gradient was already accumulated in place
+            var.grad.add_(g)              # one kernel, dtype promotion included
+        grad_done(var)
         return None, None, None
+
+
+_MARKERS = {}
+
+
+def grad_marker(t):
+    """Zero-cost stand-in gradient for ``t`` (an expanded 1-element zero tensor)."""
+    key = (t.dtype, t.device)
+    base = _MARKERS.get(key)
+    if base is None:
+        base = torch.zeros(1, dtype=t.dtype, device=t.device)
+        _MARKERS[key] = base
+    return base.expand(t.shape)
+
+
+def _is_marker(g):
+    base = _MARKERS.get((g.dtype, g.device))
+    return base is not None and g.data_ptr() == base.data_ptr() and all(st == 0 for st in g.stride())
+
+
+def grad_sink(t):
+    """The Variable whose fp32 grad slot a kernel may accumulate into directly.
+
+    Returns the Variable when ``t`` is the value a Variable handed to the model
+    (under grad mode) and its grad slot exists, else None.  A backward that
+    uses the sink *adds* its gradient into ``var.grad`` (zeroed at the start of
+    every step) and returns :func:`grad_marker` as the autograd gradient of
+    ``t``; ``_VarRead.backward`` then skips the add (or adds only the other
+    consumers' gradients) and fires the bucket hook as usual.  This removes the
+    zero/cast/add kernels between a weight-gradient kernel and the flat
+    gradient buffer that RCCL reduces.
+    """
+    var = getattr(t, "_mdtf_var", None)
+    if var is None or var.grad is None or var.grad.dtype != torch.float32 or not var.grad.is_contiguous():
+        return None
+    return var
+
+
+def grad_done(var):
+    """One use of ``var`` has contributed its gradient (fires the bucket hook)."""
+    var.uses -= 1
+    if var.uses <= 0 and var.on_grad_ready is not None:
+        var.on_grad_ready(var)
 
 
 # ---------------------------------------------------------------------------

@@ -287,3 +287,50 @@ def test_conv_transpose_hip(monkeypatch):
     yr.backward(dy.bfloat16().float())
     assert _rel(xg.grad, xc.grad) < 2e-2
     assert _rel(wg.grad, wc.grad) < 2e-2
+
+
+def _one_step(dev, dtype, x, y, depth=50):
+    import mdtf
+    from mdtf.models import ResNet, SoftmaxCrossEntropyLoss
+    from mdtf.runtime import Net, Tower
+    from mdtf.train import step as S
+    from mdtf.train import variables as V
+    V.reset_default_graph()
+    S.reset()
+    store = V.get_store()
+    store.device = torch.device(dev)
+    store.compute_dtype = dtype
+    store.generator.manual_seed(123)
+    xp = mdtf.placeholder(torch.float32, [None] + list(x.shape[1:]))
+    yp = mdtf.placeholder(torch.int64, [None])
+    opt = mdtf.train.GradientDescentOptimizer(0.1)
+    tg = []
+    tower = Tower(Net(ResNet(depth, num_classes=16, zero_init_residual=False)), "tower_0/", tg, xp, yp,
+                  SoftmaxCrossEntropyLoss(), opt, batch_size=x.shape[0])
+    _, loss, _ = tower.process()
+    op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
+    sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
+    before = {v.name: v.master.detach().float().cpu().clone() for v in store.trainable_variables()}
+    _, lv = sess.run([op, loss], feed_dict={xp: x, yp: y})
+    after = {v.name: v.master.detach().float().cpu().clone() for v in store.trainable_variables()}
+    return float(lv), before, after
+
+
+def test_resnet_step_matches_cpu_fp32_reference():
+    """One full training step (fused conv+BN kernels, sinks, fused SGD) vs the fp32 CPU engine."""
+    torch.manual_seed(9)
+    x = torch.randn(4, 32, 32, 3)
+    y = torch.randint(0, 16, (4,))
+    l_cpu, b_cpu, a_cpu = _one_step("cpu", None, x, y)
+    l_gpu, b_gpu, a_gpu = _one_step(DEV, torch.bfloat16, x, y)
+    assert abs(l_cpu - l_gpu) / abs(l_cpu) < 3e-2
+    checked = 0
+    for name in a_cpu:
+        assert torch.equal(b_cpu[name], b_gpu[name]), name          # identical init
+        d_cpu = a_cpu[name] - b_cpu[name]
+        d_gpu = a_gpu[name] - b_gpu[name]
+        if d_cpu.norm() < 1e-6:
+            continue
+        assert _rel(d_gpu, d_cpu) < 0.15, (name, _rel(d_gpu, d_cpu))
+        checked += 1
+    assert checked > 100
