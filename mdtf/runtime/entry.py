@@ -52,6 +52,8 @@ def run_from_annotations(main, module=None):
     """Build and run the operator described by ``main``'s annotations."""
     apply_thread_flags()
     ps_hosts = _flag_or(main, "ps_hosts") or ""
+    if str(ps_hosts).strip().lower() == "none":          # explicit "no parameter server" on the command line
+        ps_hosts = ""
     worker_hosts = _flag_or(main, "worker_hosts")
     job_name = _flag_or(main, "job_name")
     task_index = _flag_or(main, "task_index")

@@ -41,6 +41,7 @@ class Eval(object):
                       batch_size=self.batch_size)
         with S.training_mode(False):
             loss_h, logits_h = tower.tower_loss(post_process_fn, pre)
+        V.get_store().frozen = True           # variables exist now: later forwards reuse them
         V.get_or_create_global_step()
         ckpt = self._wait_for_checkpoint()
         if ckpt is not None:

@@ -1,0 +1,79 @@
+"""Worker bodies for the multi-process (gloo, CPU) tests; imported by spawned processes."""
+import json
+import os
+
+import torch
+
+
+def _linear_setup(rank, world, batch, seed=0):
+    import mdtf
+    from mdtf.runtime import Loss, Model, Net, Tower
+    from mdtf.train import variables as V
+
+    class Lin(Model):
+        def inference(self, x):
+            w = V.get_variable("dense/w", [8, 3], initializer=V.constant_initializer(0.1))
+            b = V.get_variable("dense/b", [3], initializer=V.constant_initializer(0.0))
+            h = V.get_variable("dense2/w", [3, 1], initializer=V.constant_initializer(0.2))
+            return torch.tanh(x @ w + b) @ h
+
+    class MSE(Loss):
+        def loss(self, p, t):
+            return ((p - t) ** 2).mean()
+
+    g = torch.Generator().manual_seed(seed)
+    xs = torch.randn(world * batch, 8, generator=g)
+    ys = torch.randn(world * batch, 1, generator=g)
+    x_ph = mdtf.placeholder(torch.float32, [None, 8])
+    y_ph = mdtf.placeholder(torch.float32, [None, 1])
+    return Lin, MSE, xs, ys, x_ph, y_ph, Tower, Net
+
+
+def sync_worker(rank, world, port, mode, steps, out_dir, replicas=None, batch=4):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    import mdtf
+    from mdtf.cluster import Server
+    from mdtf.train import variables as V
+    server = Server.from_env(backend="gloo")
+    Lin, MSE, xs, ys, x_ph, y_ph, Tower, Net = _linear_setup(rank, world, batch)
+    base = mdtf.train.MomentumOptimizer(0.1, 0.9)
+    tg = []
+    tower = Tower(Net(Lin()), "tower_0/", tg, x_ph, y_ph, MSE(), base, batch_size=batch)
+    _, loss, _ = tower.process()
+    opt = mdtf.train.SyncReplicasOptimizer(base, replicas_to_aggregate=replicas or world, total_num_replicas=world,
+                                           mode=mode, bucket_bytes=64)     # tiny buckets: several per group
+    gs = mdtf.train.get_or_create_global_step()
+    op = opt.apply_gradients(Tower.average_gradients(tg), global_step=gs)
+    hook = opt.make_session_run_hook(rank == 0)
+    sess = mdtf.train.MonitoredTrainingSession(is_chief=rank == 0, hooks=[hook], log_step_count_steps=0,
+                                               server=server)
+    lo, hi = rank * batch, (rank + 1) * batch
+    contributed = 0
+    for _ in range(steps):
+        sess.run(op, feed_dict={x_ph: xs[lo:hi], y_ph: ys[lo:hi]})
+        contributed += int(op.last_contributed)
+    sess.close()
+    op.reducer.gather_full_master()
+    w = {v.name: v.master.tolist() for v in V.get_store().trainable_variables()}
+    with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
+        json.dump({"weights": w, "contributed": contributed, "step": gs.value()}, f)
+    server.shutdown()
+
+
+def single_process_reference(world, steps, batch=4):
+    import mdtf
+    from mdtf.train import step as S
+    from mdtf.train import variables as V
+    V.reset_default_graph()
+    S.reset()
+    Lin, MSE, xs, ys, x_ph, y_ph, Tower, Net = _linear_setup(0, world, batch)
+    opt = mdtf.train.MomentumOptimizer(0.1, 0.9)
+    tg = []
+    tower = Tower(Net(Lin()), "tower_0/", tg, x_ph, y_ph, MSE(), opt, batch_size=world * batch)
+    tower.process()
+    op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
+    sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
+    for _ in range(steps):
+        sess.run(op, feed_dict={x_ph: xs, y_ph: ys})
+    return {v.name: v.master.tolist() for v in V.get_store().trainable_variables()}
