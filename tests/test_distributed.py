@@ -90,3 +90,20 @@ def test_eval_mode_restores_checkpoint(tmp_path):
                          stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert out.returncode == 0, out.stdout[-3000:]
     assert "Eval: {" in out.stdout and "model.ckpt-100" in out.stdout
+
+
+def test_async_ps_two_ps_two_workers(tmp_path):
+    """Async PS mode: variables sharded over 2 PS ranks, 2 workers push/pull independently."""
+    md = str(tmp_path / "async")
+    script = os.path.join(ROOT, "distribute.py")
+    codes = launch_local_cluster([script, "--model_dir=%s" % md, "--ps_mode=async"], num_ps=2, num_workers=2,
+                                 timeout_s=300)
+    assert codes == [0, 0, 0, 0]
+    from mdtf.ckpt.tensor_bundle import BundleReader
+    from mdtf.train.saver import latest_checkpoint
+    ck = latest_checkpoint(md)
+    r = BundleReader(ck)
+    assert r.num_shards == 2
+    shards = {r.entries[k].shard_id for k in r.keys()}
+    assert shards == {0, 1}                     # variables live on both PS tasks
+    assert int(r.get_tensor("global_step")) >= 100
