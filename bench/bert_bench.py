@@ -1,0 +1,168 @@
+#!/usr/bin/env python
+"""BERT pre-training throughput (sequences/sec, whole job) — BASELINE config 4.
+
+BERT-base (or --size large), sequence length 128, 20 masked predictions,
+synthetic token data, random-init weights, fused AdamWeightDecay; one process
+per GPU (torchrun) with bucketed RCCL gradient all-reduce.  ``--stock`` runs
+the comparator: a plain torch.nn BERT with scaled_dot_product_attention,
+autocast bf16, torch AdamW (fused=False/foreach) and DDP.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=64)
+    p.add_argument("--seq", type=int, default=128)
+    p.add_argument("--size", default="base")
+    p.add_argument("--stock", action="store_true")
+    return p.parse_args()
+
+
+class StockLayer(nn.Module):
+    def __init__(self, H, nh, I):
+        super().__init__()
+        self.nh = nh
+        self.qkv = nn.Linear(H, 3 * H)
+        self.o = nn.Linear(H, H)
+        self.ln1 = nn.LayerNorm(H, eps=1e-12)
+        self.i = nn.Linear(H, I)
+        self.out = nn.Linear(I, H)
+        self.ln2 = nn.LayerNorm(H, eps=1e-12)
+
+    def forward(self, x, mask):
+        B, S, H = x.shape
+        q, k, v = self.qkv(x).view(B, S, 3, self.nh, H // self.nh).permute(2, 0, 3, 1, 4)
+        a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=0.1)
+        a = a.transpose(1, 2).reshape(B, S, H)
+        x = self.ln1(x + F.dropout(self.o(a), 0.1))
+        return self.ln2(x + F.dropout(self.out(F.gelu(self.i(x), approximate="tanh")), 0.1))
+
+
+class StockBert(nn.Module):
+    def __init__(self, V=30522, H=768, L=12, nh=12, I=3072, S=512):
+        super().__init__()
+        self.word = nn.Embedding(V, H)
+        self.pos = nn.Embedding(S, H)
+        self.typ = nn.Embedding(2, H)
+        self.ln = nn.LayerNorm(H, eps=1e-12)
+        self.layers = nn.ModuleList([StockLayer(H, nh, I) for _ in range(L)])
+        self.pool = nn.Linear(H, H)
+        self.tr = nn.Linear(H, H)
+        self.tln = nn.LayerNorm(H, eps=1e-12)
+        self.obias = nn.Parameter(torch.zeros(V))
+        self.nsp = nn.Linear(H, 2)
+
+    def forward(self, ids, types, mask, positions):
+        B, S = ids.shape
+        x = self.word(ids) + self.pos(torch.arange(S, device=ids.device)) + self.typ(types)
+        x = F.dropout(self.ln(x), 0.1)
+        am = ((1.0 - mask.to(x.dtype)) * -10000.0)[:, None, None, :]
+        for l in self.layers:
+            x = l(x, am)
+        pooled = torch.tanh(self.pool(x[:, 0]))
+        idx = (positions + torch.arange(B, device=ids.device)[:, None] * S).reshape(-1)
+        h = self.tln(F.gelu(self.tr(x.reshape(B * S, -1).index_select(0, idx)), approximate="tanh"))
+        return h @ self.word.weight.t() + self.obias, self.nsp(pooled)
+
+
+def main():
+    args = parse()
+    distributed = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if distributed:
+        from mdtf.cluster import Server
+        server = Server.from_env()
+        rank, world = dist.get_rank(), dist.get_world_size()
+        pg = server.worker_group
+    else:
+        server, rank, world, pg = None, 0, 1, None
+    lr = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", lr)
+    torch.cuda.set_device(dev)
+    from mdtf.models import Bert, BertPretrainingLoss, SyntheticBertLoader
+    from mdtf.models.bert import CONFIGS
+    P = 20
+    if args.stock:
+        cfg = CONFIGS[args.size]
+        model = StockBert(H=cfg["hidden"], L=cfg["layers"], nh=cfg["heads"], I=cfg["intermediate"]).to(dev)
+        if distributed:
+            model = nn.parallel.DistributedDataParallel(model, device_ids=[lr], bucket_cap_mb=32)
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, foreach=True)
+        ld = SyntheticBertLoader(args.seq, P, seed=rank)
+        ld.batch_size = args.batch
+        from mdtf.train import variables as V
+        V.get_store().device = dev
+        raw, gt = ld._make()
+        S = args.seq
+        ids, types, mask, pos = raw[:, :S], raw[:, S:2 * S], raw[:, 2 * S:3 * S], raw[:, 3 * S:3 * S + P]
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                mlm, nsp = model(ids, types, mask, pos)
+                loss = F.cross_entropy(mlm.float(), gt[:, :P].reshape(-1)) + F.cross_entropy(nsp.float(), gt[:, P])
+            loss.backward()
+            opt.step()
+            return loss
+        run = step
+    else:
+        import mdtf
+        from mdtf.runtime import Net, Tower
+        from mdtf.train import variables as V
+        store = V.get_store()
+        store.device = dev
+        store.compute_dtype = torch.bfloat16
+        ld = SyntheticBertLoader(args.seq, P, seed=rank)
+        ld.batch_size = args.batch
+        raw, gt = ld.load_train_batch()
+        base = mdtf.train.AdamWeightDecayOptimizer(1e-4, weight_decay_rate=0.01)
+        tg = []
+        tower = Tower(Net(Bert(args.size, seq_len=args.seq, max_predictions=P)), "tower_0/", tg, raw, gt,
+                      BertPretrainingLoss(P), base, batch_size=args.batch)
+        _, loss_h, _ = tower.process()
+        opt = mdtf.train.SyncReplicasOptimizer(base, world, world)
+        op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
+        sess = mdtf.train.MonitoredTrainingSession(is_chief=rank == 0, log_step_count_steps=0, server=server)
+
+        def run():
+            sess.run(op)
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier(group=pg)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier(group=pg)
+    el = torch.tensor([time.perf_counter() - t0], device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX, group=pg)
+    el = float(el)
+    if rank == 0:
+        print(json.dumps({"metric": "sequences/sec BERT-%s pretraining seq%d" % (args.size, args.seq),
+                          "value": round(world * args.batch * args.steps / el, 2), "unit": "sequences/sec",
+                          "n_gpus": world, "ms_per_step": round(1000 * el / args.steps, 3),
+                          "per_gpu_batch": args.batch, "impl": "stock-pytorch" if args.stock else "mdtf",
+                          "dtype": "bf16", "data": "synthetic"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,343 @@
+// Transformer (BERT) kernels: fused residual+LayerNorm, masked scaled softmax,
+// embedding gather / scatter-add.  bf16 activations, fp32 statistics.
+//
+// BASELINE config "BERT-base data-parallel (MFMA bf16 GEMM + fused Adam)".  The
+// plain GEMMs go to hipBLASLt; everything between them runs here:
+//   * ln_fwd:  s = x (+ res);  y = (s - mean) * rstd * gamma + beta   (one wave per row,
+//              bf16x8 vectors, the row stays in registers: one read, two writes)
+//   * ln_bwd:  dx = rstd * (g·dy - mean(g·dy) - xhat·mean(g·dy·xhat)); per-block
+//              dgamma/dbeta partials accumulated in registers over many rows, then
+//              one fp32 atomic per column per block (low contention)
+//   * softmax: y = softmax(scale·x + mask[b, key]) over the key axis, one wave per row
+//   * embed:   out[t] = table[id[t]] gather; backward = fp32 atomic scatter-add
+#include "mdtf_common.h"
+
+using namespace mdtf;
+
+namespace {
+
+constexpr int kT = 256;
+constexpr int kMaxVec = 16;   // H <= 64 lanes * 8 * 16 = 8192
+
+template <int NV>
+__global__ void __launch_bounds__(kT) ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   bf16_t* __restrict__ y, bf16_t* __restrict__ s_out,
+                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                   long long rows, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nvec = H / 8;
+  float v[NV][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + i * 64);
+    if (c < nvec) {
+      load_bf8(x + row * H + c * 8, v[i]);
+      if (res) {
+        float r[8];
+        load_bf8(res + row * H + c * 8, r);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[i][k] += r[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sum += v[i][k];
+    }
+  }
+  const float mean = wave_sum(sum) / (float)H;
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + i * 64);
+    if (c < nvec) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = v[i][k] - mean;
+        sq += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(sq) / (float)H + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + i * 64);
+    if (c < nvec) {
+      if (s_out) store_bf8(s_out + row * H + c * 8, v[i]);
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = (v[i][k] - mean) * rstd * gamma[c * 8 + k] + beta[c * 8 + k];
+      store_bf8(y + row * H + c * 8, o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// each block (4 waves) walks rows_per_block rows; dgamma/dbeta partials live in registers
+template <int NV>
+__global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
+                                                   const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                   const float* __restrict__ rstd, bf16_t* __restrict__ dx,
+                                                   float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                   long long rows, int H, int rows_per_block) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nvec = H / 8;
+  float dg[NV][8], db[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dg[i][k] = db[i][k] = 0.f;
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+  for (long long row = r0 + wave; row < r1; row += kT / 64) {
+    const float mu = mean[row], rs = rstd[row];
+    float g[NV][8], xh[NV][8];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + i * 64;
+      if (c < nvec) {
+        float sv[8];
+        load_bf8(dy + row * H + c * 8, g[i]);
+        load_bf8(s + row * H + c * 8, sv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xh[i][k] = (sv[k] - mu) * rs;
+          dg[i][k] += g[i][k] * xh[i][k];
+          db[i][k] += g[i][k];
+          const float gg = g[i][k] * gamma[c * 8 + k];
+          a += gg;
+          b += gg * xh[i][k];
+        }
+      }
+    }
+    a = wave_sum(a) / (float)H;
+    b = wave_sum(b) / (float)H;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + i * 64;
+      if (c < nvec) {
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = rs * (g[i][k] * gamma[c * 8 + k] - a - xh[i][k] * b);
+        store_bf8(dx + row * H + c * 8, o);
+      }
+    }
+  }
+  // combine the 4 waves through LDS, then one atomic per column per block
+  __shared__ float L[2][kT / 64][64 * 8];   // one 512-column slab per pass over NV
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      L[0][wave][lane * 8 + k] = dg[i][k];
+      L[1][wave][lane * 8 + k] = db[i][k];
+    }
+    __syncthreads();
+    if (wave == 0 && c < nvec) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float tg = 0.f, tb = 0.f;
+#pragma unroll
+        for (int w = 0; w < kT / 64; ++w) {
+          tg += L[0][w][lane * 8 + k];
+          tb += L[1][w][lane * 8 + k];
+        }
+        atomicAdd(dgamma + c * 8 + k, tg);
+        atomicAdd(dbeta + c * 8 + k, tb);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// masked, scaled softmax over the last axis; rows = B*heads*Sq, cols = Sk
+// mask (optional): additive fp32 [B][Sk]; batch index of a row = row / rows_per_batch
+template <int NV>
+__global__ void __launch_bounds__(kT) softmax_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ mask,
+                                                        bf16_t* __restrict__ y, long long rows, int cols, float scale,
+                                                        long long rows_per_batch) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* mk = mask ? mask + (row / rows_per_batch) * cols : nullptr;
+  const int nvec = cols / 8;
+  float v[NV][8];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+      load_bf8(x + row * cols + c * 8, v[i]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[i][k] = v[i][k] * scale + (mk ? mk[c * 8 + k] : 0.f);
+        m = fmaxf(m, v[i][k]);
+      }
+    }
+  }
+  m = wave_max(m);
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[i][k] = __expf(v[i][k] - m);
+        sum += v[i][k];
+      }
+    }
+  }
+  const float inv = 1.f / wave_sum(sum);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[i][k] *= inv;
+      store_bf8(y + row * cols + c * 8, v[i]);
+    }
+  }
+}
+
+template <int NV>
+__global__ void __launch_bounds__(kT) softmax_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                        bf16_t* __restrict__ dx, long long rows, int cols, float scale) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nvec = cols / 8;
+  float g[NV][8], p[NV][8];
+  float dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+      load_bf8(dy + row * cols + c * 8, g[i]);
+      load_bf8(y + row * cols + c * 8, p[i]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dot += g[i][k] * p[i][k];
+    }
+  }
+  dot = wave_sum(dot);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = scale * p[i][k] * (g[i][k] - dot);
+      store_bf8(dx + row * cols + c * 8, o);
+    }
+  }
+}
+
+__global__ void embed_fwd_kernel(const bf16_t* __restrict__ table, const long long* __restrict__ ids,
+                                 bf16_t* __restrict__ out, long long n, int H, long long vocab) {
+  const int nvec = H / 8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n * nvec;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long t = i / nvec;
+    const int c = static_cast<int>(i % nvec);
+    long long id = ids[t];
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (id >= 0 && id < vocab) v = *reinterpret_cast<const uint4*>(table + id * H + c * 8);
+    *reinterpret_cast<uint4*>(out + t * H + c * 8) = v;
+  }
+}
+
+__global__ void embed_bwd_kernel(const bf16_t* __restrict__ dy, const long long* __restrict__ ids,
+                                 float* __restrict__ dtable, long long n, int H, long long vocab) {
+  const long long total = n * H;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long t = i / H;
+    const int c = static_cast<int>(i % H);
+    long long id = ids[t];
+    if (id >= 0 && id < vocab) atomicAdd(dtable + id * H + c, bf2f(dy[i]));
+  }
+}
+
+inline int gcap(long long work) {
+  long long b = ceil_div(work, kT);
+  return static_cast<int>(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+}  // namespace
+
+#define NV_DISPATCH(H, KERNEL, GRID, ...)                                                                  \
+  do {                                                                                                     \
+    const int nv_ = static_cast<int>(ceil_div((H) / 8, 64));                                               \
+    if (nv_ <= 1) hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(kT), 0, st, __VA_ARGS__);                       \
+    else if (nv_ <= 2) hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(kT), 0, st, __VA_ARGS__);                  \
+    else if (nv_ <= 4) hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(kT), 0, st, __VA_ARGS__);                  \
+    else if (nv_ <= 8) hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(kT), 0, st, __VA_ARGS__);                  \
+    else if (nv_ <= 16) hipLaunchKernelGGL(KERNEL<16>, GRID, dim3(kT), 0, st, __VA_ARGS__);                \
+    else return MDTF_EUNSUPPORTED;                                                                         \
+  } while (0)
+
+MDTF_EXPORT int mdtf_ln_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y, void* s,
+                            float* mean, float* rstd, long long rows, int H, float eps, hipStream_t st) {
+  if (H % 8) return MDTF_EINVAL;
+  NV_DISPATCH(H, ln_fwd_kernel, dim3(ceil_div(rows, kT / 64)), (const bf16_t*)x, (const bf16_t*)res, gamma, beta,
+              (bf16_t*)y, (bf16_t*)s, mean, rstd, rows, H, eps);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// dgamma/dbeta accumulate (zeroed buffers or fp32 grad slots)
+MDTF_EXPORT int mdtf_ln_bwd(const void* dy, const void* s, const float* gamma, const float* mean, const float* rstd,
+                            void* dx, float* dgamma, float* dbeta, long long rows, int H, hipStream_t st) {
+  if (H % 8) return MDTF_EINVAL;
+  int rpb = 64;
+  long long blocks = ceil_div(rows, rpb);
+  if (blocks > 2048) {
+    rpb = static_cast<int>(ceil_div(rows, 2048));
+    blocks = ceil_div(rows, rpb);
+  }
+  NV_DISPATCH(H, ln_bwd_kernel, dim3(blocks), (const bf16_t*)dy, (const bf16_t*)s, gamma, mean, rstd, (bf16_t*)dx,
+              dgamma, dbeta, rows, H, rpb);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_softmax_fwd(const void* x, const float* mask, void* y, long long rows, int cols, float scale,
+                                 long long rows_per_batch, hipStream_t st) {
+  if (cols % 8) return MDTF_EINVAL;
+  NV_DISPATCH(cols, softmax_fwd_kernel, dim3(ceil_div(rows, kT / 64)), (const bf16_t*)x, mask, (bf16_t*)y, rows,
+              cols, scale, rows_per_batch);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_softmax_bwd(const void* dy, const void* y, void* dx, long long rows, int cols, float scale,
+                                 hipStream_t st) {
+  if (cols % 8) return MDTF_EINVAL;
+  NV_DISPATCH(cols, softmax_bwd_kernel, dim3(ceil_div(rows, kT / 64)), (const bf16_t*)dy, (const bf16_t*)y,
+              (bf16_t*)dx, rows, cols, scale);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_embed_fwd(const void* table, const long long* ids, void* out, long long n, int H,
+                               long long vocab, hipStream_t st) {
+  if (H % 8) return MDTF_EINVAL;
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(gcap(n * H / 8)), dim3(kT), 0, st, (const bf16_t*)table, ids,
+                     (bf16_t*)out, n, H, vocab);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_embed_bwd(const void* dy, const long long* ids, float* dtable, long long n, int H,
+                               long long vocab, hipStream_t st) {
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(gcap(n * H)), dim3(kT), 0, st, (const bf16_t*)dy, ids, dtable, n, H,
+                     vocab);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,194 @@
+"""BERT (base / large) pre-training model on mdtf kernels.
+
+BASELINE config "BERT-base data-parallel 8×MI355X (MFMA bf16 GEMM + fused
+Adam)".  Variable names follow Google's TF BERT checkpoints
+(``bert/encoder/layer_0/attention/self/query/kernel`` ...), so checkpoints
+written by the tensor-bundle Saver line up with the TF layout.
+
+Compute: dense layers are bf16 GEMMs (hipBLASLt) with the fused bias(+GELU)
+epilogue kernel; Q/K/V projections run as ONE GEMM on the concatenated
+kernels; residual add + LayerNorm, the scaled masked softmax and the
+embedding gather/scatter-add are HIP kernels; the MLM decoder is tied to the
+word embeddings; the optimizer is the fused AdamWeightDecay kernel.
+
+Inputs (packed so the framework's (raw_data, ground_truth) tower API carries
+them): ``raw_data`` int64 ``[B, 3*S + P]`` = input_ids | token_type_ids |
+input_mask | masked_lm_positions; ``ground_truth`` int64 ``[B, P + 1]`` =
+masked_lm_ids | next_sentence_label.
+"""
+import math
+
+import torch
+
+from ..layers import tools
+from ..ops import nn as ops
+from ..ops import transformer as T
+from ..runtime.model import Loss, Model
+from ..train import step as S
+from ..train import variables as V
+
+CONFIGS = {
+    "base": dict(hidden=768, layers=12, heads=12, intermediate=3072),
+    "large": dict(hidden=1024, layers=24, heads=16, intermediate=4096),
+    "tiny": dict(hidden=128, layers=2, heads=2, intermediate=512),
+}
+
+
+def _init(std=0.02):
+    return V.truncated_normal_initializer(stddev=std)
+
+
+def _dense(name, x, out, act=None):
+    with V.variable_scope(name):
+        w = V.get_variable("kernel", [x.shape[-1], out], initializer=_init())
+        b = V.get_variable("bias", [out], initializer=V.constant_initializer(0.0))
+    shp = x.shape
+    y = ops.dense(x.reshape(-1, shp[-1]), w, b, act=act)
+    return y.reshape(*shp[:-1], out)
+
+
+def _ln(name, x, residual=None, eps=1e-12):
+    with V.variable_scope(name):
+        g = V.get_variable("gamma", [x.shape[-1]], initializer=V.constant_initializer(1.0), keep_fp32=True)
+        b = V.get_variable("beta", [x.shape[-1]], initializer=V.constant_initializer(0.0), keep_fp32=True)
+    return T.layer_norm(x, g, b, eps, residual=residual)
+
+
+def _dropout(x, rate):
+    if rate and S.is_training():
+        return torch.nn.functional.dropout(x, rate, True)
+    return x
+
+
+class Bert(Model):
+    def __init__(self, size="base", vocab_size=30522, max_position=512, type_vocab=2, max_predictions=20,
+                 seq_len=128, dropout=0.1):
+        cfg = CONFIGS[size]
+        self.H = cfg["hidden"]
+        self.L = cfg["layers"]
+        self.heads = cfg["heads"]
+        self.I = cfg["intermediate"]
+        self.vocab = vocab_size
+        self.max_position = max_position
+        self.type_vocab = type_vocab
+        self.P = max_predictions
+        self.S = seq_len
+        self.dropout = dropout
+
+    def unpack(self, raw):
+        S_, P = self.S, self.P
+        return raw[:, :S_], raw[:, S_:2 * S_], raw[:, 2 * S_:3 * S_], raw[:, 3 * S_:3 * S_ + P]
+
+    def inference(self, raw):
+        ids, types, mask, positions = self.unpack(raw)
+        B, S_ = ids.shape
+        store = V.get_store()
+        H, nh = self.H, self.heads
+        dh = H // nh
+        with V.variable_scope("bert"):
+            with V.variable_scope("embeddings"):
+                word = V.get_variable("word_embeddings", [self.vocab, H], initializer=_init())
+                pos = V.get_variable("position_embeddings", [self.max_position, H], initializer=_init())
+                typ = V.get_variable("token_type_embeddings", [self.type_vocab, H], initializer=_init())
+                pos_ids = torch.arange(S_, device=ids.device).unsqueeze(0).expand(B, S_)
+                e = T.embedding_lookup(word, ids)
+                e = e + T.embedding_lookup(pos, pos_ids) + T.embedding_lookup(typ, types)
+                x = _ln("LayerNorm", e)
+                x = _dropout(x, self.dropout)
+            # additive attention mask over keys: 0 keep, -10000 masked
+            amask = (1.0 - mask.float()) * -10000.0
+            with V.variable_scope("encoder"):
+                for l in range(self.L):
+                    with V.variable_scope("layer_%d" % l):
+                        x = self._layer(x, amask, B, S_, H, nh, dh)
+            with V.variable_scope("pooler"):
+                first = x[:, 0, :].contiguous()
+                pooled = torch.tanh(_dense("dense", first, H).float()).to(x.dtype)
+        # ---- pre-training heads
+        with V.variable_scope("cls"):
+            with V.variable_scope("predictions"):
+                flat = x.reshape(B * S_, H)
+                idx = (positions + torch.arange(B, device=ids.device).unsqueeze(1) * S_).reshape(-1)
+                h = flat.index_select(0, idx)
+                with V.variable_scope("transform"):
+                    h = _dense("dense", h, H, act="gelu")
+                    h = _ln("LayerNorm", h)
+                out_bias = V.get_variable("output_bias", [self.vocab], initializer=V.constant_initializer(0.0))
+                mlm = torch.matmul(h, word.t()) + out_bias.to(h.dtype)
+            with V.variable_scope("seq_relationship"):
+                w = V.get_variable("output_weights", [2, H], initializer=_init())
+                b = V.get_variable("output_bias", [2], initializer=V.constant_initializer(0.0))
+                nsp = torch.matmul(pooled, w.t()) + b.to(pooled.dtype)
+        return mlm, nsp
+
+    def _layer(self, x, amask, B, S_, H, nh, dh):
+        with V.variable_scope("attention"):
+            with V.variable_scope("self"):
+                ws, bs = [], []
+                for nm in ("query", "key", "value"):
+                    with V.variable_scope(nm):
+                        ws.append(V.get_variable("kernel", [H, H], initializer=_init()))
+                        bs.append(V.get_variable("bias", [H], initializer=V.constant_initializer(0.0)))
+                qkv = ops.dense(x.reshape(-1, H), torch.cat(ws, 1), torch.cat(bs, 0))      # one GEMM
+                qkv = qkv.view(B, S_, 3, nh, dh).permute(2, 0, 3, 1, 4)                     # [3, B, nh, S, dh]
+                ctx = T.attention(qkv[0], qkv[1], qkv[2], amask)
+                ctx = ctx.permute(0, 2, 1, 3).reshape(B, S_, H)
+            with V.variable_scope("output"):
+                a = _dense("dense", ctx, H)
+                a = _dropout(a, self.dropout)
+                x = _ln("LayerNorm", a, residual=x)
+        with V.variable_scope("intermediate"):
+            i = _dense("dense", x, self.I, act="gelu")
+        with V.variable_scope("output"):
+            o = _dense("dense", i, H)
+            o = _dropout(o, self.dropout)
+            x = _ln("LayerNorm", o, residual=x)
+        return x
+
+
+class BertPretrainingLoss(Loss):
+    """Masked-LM cross entropy + next-sentence cross entropy (fp32)."""
+
+    def __init__(self, max_predictions=20):
+        self.P = max_predictions
+
+    def loss(self, predict, ground_truth):
+        mlm, nsp = predict
+        lm_ids = ground_truth[:, :self.P].reshape(-1)
+        ns = ground_truth[:, self.P]
+        l1 = ops.sparse_softmax_cross_entropy_with_logits(lm_ids, mlm.reshape(-1, mlm.shape[-1])).mean()
+        l2 = ops.sparse_softmax_cross_entropy_with_logits(ns, nsp).mean()
+        return l1 + l2
+
+
+class SyntheticBertLoader(object):
+    """Synthetic pre-training batches of the packed BERT layout (device resident)."""
+    type = "SyntheticDataLoader"
+
+    def __init__(self, seq_len=128, max_predictions=20, vocab=30522, seed=0):
+        self.S, self.P, self.vocab, self.seed = seq_len, max_predictions, vocab, seed
+        self.batch_size = 32
+        self._batch = None
+
+    def _make(self):
+        g = torch.Generator().manual_seed(self.seed)
+        B, S_, P = self.batch_size, self.S, self.P
+        ids = torch.randint(0, self.vocab, (B, S_), generator=g)
+        types = (torch.arange(S_) >= S_ // 2).long().unsqueeze(0).expand(B, S_)
+        mask = torch.ones(B, S_, dtype=torch.long)
+        pos = torch.stack([torch.randperm(S_, generator=g)[:P].sort().values for _ in range(B)])
+        raw = torch.cat([ids, types, mask, pos], 1)
+        gt = torch.cat([torch.randint(0, self.vocab, (B, P), generator=g), torch.randint(0, 2, (B, 1), generator=g)], 1)
+        dev = V.get_store().device
+        return raw.to(dev), gt.to(dev)
+
+    def _next(self):
+        if self._batch is None:
+            self._batch = self._make()
+        return self._batch
+
+    def load_train_batch(self, name_queue=None, *args, **kwargs):
+        return S.BatchSource(self._next, name="synthetic-bert").outputs(2)
+
+    def load_eval_batch(self, *args, **kwargs):
+        return self.load_train_batch()

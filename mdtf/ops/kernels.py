@@ -2,6 +2,7 @@
 import torch
 
 from . import _native as N
+from ..train import variables as V
 
 N.register("mdtf_bias_act_fwd", [N.P, N.P, N.P, N.P, N.L, N.I, N.I, N.P])
 N.register("mdtf_act_bwd", [N.P, N.P, N.P, N.P, N.L, N.I, N.P])
@@ -47,6 +48,8 @@ class _BiasAct(torch.autograd.Function):
         ctx.act = act
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.sink = V.grad_sink(bias) if bias is not None else None
+        ctx.bias = bias
         ctx.save_for_backward(y if act == 1 else pre)
         return y
 
@@ -65,7 +68,12 @@ class _BiasAct(torch.autograd.Function):
         db = None
         if ctx.has_bias:
             C = dx.shape[-1]
-            db = colsum(dx.reshape(-1, C)).to(ctx.bias_dtype)
+            if ctx.sink is not None:       # column sums accumulate straight into the fp32 grad slot
+                N.check(N.fn("mdtf_colsum")(N.ptr(dx), dx.numel() // C, C, N.ptr(ctx.sink.grad), N.stream_ptr()),
+                        "colsum")
+                db = V.grad_marker(ctx.bias)
+            else:
+                db = colsum(dx.reshape(-1, C)).to(ctx.bias_dtype)
         return dx, db, None
 
 
@@ -231,7 +239,3 @@ class _LRN(torch.autograd.Function):
 def lrn(x, depth_radius, bias, alpha, beta):
     return _LRN.apply(x, int(depth_radius), float(bias), float(alpha), float(beta))
 
-
-def layer_norm(x, gamma, beta, eps):
-    from . import layernorm
-    return layernorm.layer_norm(x, gamma, beta, eps)

@@ -269,11 +269,10 @@ def local_response_normalization(x, depth_radius=5, bias=1.0, alpha=1.0, beta=0.
 lrn = local_response_normalization
 
 
-def layer_norm(x, gamma, beta, epsilon=1e-12):
-    if _native.use_native(x):
-        from . import kernels
-        return kernels.layer_norm(x, gamma, beta, epsilon)
-    return F.layer_norm(x.float(), (x.shape[-1],), gamma.float(), beta.float(), epsilon).to(x.dtype)
+def layer_norm(x, gamma, beta, epsilon=1e-12, residual=None):
+    """LayerNorm over the last axis (optionally of ``x + residual``, fused on the GPU)."""
+    from . import transformer
+    return transformer.layer_norm(x, gamma, beta, epsilon, residual)
 
 
 # ---------------------------------------------------------------------------

@@ -1,0 +1,165 @@
+"""Transformer ops (LayerNorm(+residual), masked softmax, embedding) on ``csrc/transformer.hip``.
+
+GPU path: the HIP kernels (bf16 activations, fp32 statistics; parameter
+gradients accumulate straight into the variables' fp32 grad slots when
+available).  CPU path: PyTorch reference implementations.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _native as N
+from ..train import variables as V
+
+N.register("mdtf_ln_fwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.F, N.P])
+N.register("mdtf_ln_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P])
+N.register("mdtf_softmax_fwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.L, N.P])
+N.register("mdtf_softmax_bwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.P])
+N.register("mdtf_embed_fwd", [N.P, N.P, N.P, N.L, N.I, N.L, N.P])
+N.register("mdtf_embed_bwd", [N.P, N.P, N.P, N.L, N.I, N.L, N.P])
+
+
+def _sink_or_zeros(t, n, device):
+    var = V.grad_sink(t) if t is not None else None
+    if var is not None:
+        return var, var.grad
+    return None, torch.zeros(n, dtype=torch.float32, device=device)
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, gamma, beta, eps):
+        x = x.contiguous()
+        H = x.shape[-1]
+        rows = x.numel() // H
+        y = torch.empty_like(x)
+        s = torch.empty_like(x)
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        g = gamma.detach().float().contiguous()
+        b = beta.detach().float().contiguous()
+        r = res.contiguous() if res is not None else None
+        N.check(N.fn("mdtf_ln_fwd")(N.ptr(x), N.ptr(r), N.ptr(g), N.ptr(b), N.ptr(y), N.ptr(s), N.ptr(mean),
+                                    N.ptr(rstd), rows, H, float(eps), N.stream_ptr()), "ln_fwd")
+        ctx.save_for_backward(s, g, mean, rstd)
+        ctx.has_res = res is not None
+        ctx.sinks = (V.grad_sink(gamma), V.grad_sink(beta))
+        ctx.like = (gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        s, g, mean, rstd = ctx.saved_tensors
+        dy = dy.contiguous()
+        H = s.shape[-1]
+        rows = s.numel() // H
+        dx = torch.empty_like(s)
+        sg, sb = ctx.sinks
+        dg = sg.grad if sg is not None else torch.zeros(H, dtype=torch.float32, device=s.device)
+        db = sb.grad if sb is not None else torch.zeros(H, dtype=torch.float32, device=s.device)
+        N.check(N.fn("mdtf_ln_bwd")(N.ptr(dy), N.ptr(s), N.ptr(g), N.ptr(mean), N.ptr(rstd), N.ptr(dx), N.ptr(dg),
+                                    N.ptr(db), rows, H, N.stream_ptr()), "ln_bwd")
+        gamma, beta = ctx.like
+        rg = V.grad_marker(gamma) if sg is not None else dg
+        rb = V.grad_marker(beta) if sb is not None else db
+        return dx, (dx if ctx.has_res else None), rg, rb, None
+
+
+def layer_norm(x, gamma, beta, eps=1e-12, residual=None):
+    """LayerNorm over the last axis of ``x (+ residual)``."""
+    if N.use_native(x):
+        if x.dtype != torch.bfloat16:
+            raise TypeError("mdtf LayerNorm kernel expects bf16, got %s" % x.dtype)
+        if residual is not None and residual.dtype != x.dtype:
+            residual = residual.to(x.dtype)
+        return _LayerNorm.apply(x, residual, gamma, beta, float(eps))
+    s = x if residual is None else x + residual
+    return F.layer_norm(s.float(), (s.shape[-1],), gamma.float(), beta.float(), eps).to(x.dtype)
+
+
+class _Softmax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mask, scale, rows_per_batch):
+        x = x.contiguous()
+        cols = x.shape[-1]
+        rows = x.numel() // cols
+        y = torch.empty_like(x)
+        m = mask.float().contiguous() if mask is not None else None
+        N.check(N.fn("mdtf_softmax_fwd")(N.ptr(x), N.ptr(m), N.ptr(y), rows, cols, float(scale), int(rows_per_batch),
+                                         N.stream_ptr()), "softmax_fwd")
+        ctx.save_for_backward(y)
+        ctx.scale = scale
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        cols = y.shape[-1]
+        dx = torch.empty_like(y)
+        N.check(N.fn("mdtf_softmax_bwd")(N.ptr(dy), N.ptr(y), N.ptr(dx), y.numel() // cols, cols, float(ctx.scale),
+                                         N.stream_ptr()), "softmax_bwd")
+        return dx, None, None, None
+
+
+def masked_softmax(scores, mask=None, scale=1.0):
+    """softmax(scale * scores + mask) over the last axis.
+
+    ``scores``: [B, heads, Sq, Sk]; ``mask``: additive [B, Sk] (0 / -10000) or None.
+    """
+    if N.use_native(scores):
+        b = scores.shape[0]
+        rows_per_batch = scores.numel() // scores.shape[-1] // b
+        return _Softmax.apply(scores, mask, float(scale), rows_per_batch)
+    s = scores.float() * scale
+    if mask is not None:
+        s = s + mask.float()[:, None, None, :]
+    return torch.softmax(s, -1).to(scores.dtype)
+
+
+class _Embed(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, table, ids):
+        ids = ids.to(torch.int64).contiguous()
+        vocab, H = table.shape
+        out = torch.empty(tuple(ids.shape) + (H,), dtype=table.dtype, device=table.device)
+        N.check(N.fn("mdtf_embed_fwd")(N.ptr(table), N.ptr(ids), N.ptr(out), ids.numel(), H, vocab, N.stream_ptr()),
+                "embed_fwd")
+        ctx.save_for_backward(ids)
+        ctx.shape = (vocab, H)
+        ctx.sink = V.grad_sink(table)
+        ctx.like = table
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        vocab, H = ctx.shape
+        dy = dy.contiguous()
+        sink = ctx.sink
+        dt = sink.grad if sink is not None else torch.zeros((vocab, H), dtype=torch.float32, device=dy.device)
+        N.check(N.fn("mdtf_embed_bwd")(N.ptr(dy), N.ptr(ids), N.ptr(dt), ids.numel(), H, vocab, N.stream_ptr()),
+                "embed_bwd")
+        if sink is not None:
+            return V.grad_marker(ctx.like), None
+        return dt.to(ctx.like.dtype), None
+
+
+def embedding_lookup(table, ids):
+    """``tf.nn.embedding_lookup``: rows of ``table`` [V, H] for integer ``ids``."""
+    if N.use_native(table):
+        return _Embed.apply(table, ids)
+    return F.embedding(ids.long(), table)
+
+
+def attention(q, k, v, mask=None):
+    """Multi-head attention core: q, k, v [B, heads, S, d] -> [B, heads, S, d].
+
+    The two batched GEMMs run on hipBLASLt; the scaled masked softmax (and its
+    backward) on the HIP kernel.
+    """
+    scale = 1.0 / math.sqrt(q.shape[-1])
+    scores = torch.matmul(q, k.transpose(-1, -2))
+    p = masked_softmax(scores, mask, scale)
+    return torch.matmul(p, v)

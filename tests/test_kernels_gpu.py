@@ -425,3 +425,82 @@ def test_conv_bn_fused_stats(shape, k, s, co, relu, res, monkeypatch):
         assert _rel(outs[DEV][key], outs["cpu"][key]) < 5e-2, key
     if res:
         assert _rel(outs[DEV]["dr"], outs["cpu"]["dr"]) < 5e-2
+
+
+@pytest.mark.parametrize("H,res", [(768, True), (1024, False), (64, True)])
+def test_layernorm_kernel(H, res):
+    from mdtf.ops import transformer as T
+    torch.manual_seed(11)
+    x = torch.randn(37, H) * 2 + 1
+    r = torch.randn(37, H) if res else None
+    g = torch.rand(H) + 0.5
+    b = torch.randn(H)
+    outs = {}
+    for dev, dt in ((DEV, torch.bfloat16), ("cpu", torch.float32)):
+        xx = x.to(dev).to(dt).requires_grad_(True)
+        rr = r.to(dev).to(dt).requires_grad_(True) if res else None
+        gg = g.to(dev).requires_grad_(True)
+        bb = b.to(dev).requires_grad_(True)
+        y = T.layer_norm(xx, gg, bb, 1e-12, residual=rr)
+        y.backward(torch.randn(37, H, generator=torch.Generator().manual_seed(2)).to(dev).to(dt))
+        outs[dev] = (y.detach(), xx.grad, gg.grad, bb.grad, rr.grad if res else None)
+    for i in range(4):
+        assert _rel(outs[DEV][i], outs["cpu"][i]) < 2e-2, i
+    if res:
+        assert _rel(outs[DEV][4], outs["cpu"][4]) < 2e-2
+
+
+@pytest.mark.parametrize("cols", [128, 512, 40])
+def test_masked_softmax_kernel(cols):
+    from mdtf.ops import transformer as T
+    torch.manual_seed(12)
+    x = torch.randn(2, 3, 5, cols) * 4
+    mask = (torch.rand(2, cols) < 0.2).float() * -10000.0
+    outs = {}
+    for dev, dt in ((DEV, torch.bfloat16), ("cpu", torch.float32)):
+        xx = x.to(dev).to(dt).requires_grad_(True)
+        y = T.masked_softmax(xx, mask.to(dev), 0.125)
+        y.backward(torch.randn(x.shape, generator=torch.Generator().manual_seed(3)).to(dev).to(dt))
+        outs[dev] = (y.detach(), xx.grad)
+    assert _rel(outs[DEV][0], outs["cpu"][0]) < 1e-2
+    assert _rel(outs[DEV][1], outs["cpu"][1]) < 2e-2
+
+
+def test_embedding_kernel():
+    from mdtf.ops import transformer as T
+    torch.manual_seed(13)
+    table = torch.randn(100, 64)
+    ids = torch.randint(0, 100, (7, 9))
+    outs = {}
+    for dev, dt in ((DEV, torch.bfloat16), ("cpu", torch.float32)):
+        tt = table.to(dev).to(dt).requires_grad_(True)
+        y = T.embedding_lookup(tt, ids.to(dev))
+        y.backward(torch.randn(7, 9, 64, generator=torch.Generator().manual_seed(4)).to(dev).to(dt))
+        outs[dev] = (y.detach(), tt.grad)
+    assert _rel(outs[DEV][0], outs["cpu"][0]) < 1e-2
+    assert _rel(outs[DEV][1], outs["cpu"][1]) < 2e-2
+
+
+def test_bert_tiny_train_step_gpu():
+    import mdtf
+    from mdtf.models import Bert, BertPretrainingLoss, SyntheticBertLoader
+    from mdtf.runtime import Net, Tower
+    from mdtf.train import variables as V
+    store = V.get_store()
+    store.device = torch.device(DEV)
+    store.compute_dtype = torch.bfloat16
+    ld = SyntheticBertLoader(seq_len=32, max_predictions=5, vocab=1000)
+    ld.batch_size = 8
+    raw, gt = ld.load_train_batch()
+    opt = mdtf.train.AdamWeightDecayOptimizer(1e-3)
+    tg = []
+    t = Tower(Net(Bert("tiny", vocab_size=1000, seq_len=32, max_predictions=5, dropout=0.0)), "tower_0/", tg, raw, gt,
+              BertPretrainingLoss(5), opt, batch_size=8)
+    _, loss, _ = t.process()
+    op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
+    sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
+    ls = []
+    for _ in range(20):
+        _, l = sess.run([op, loss])
+        ls.append(float(l))
+    assert ls[-1] < 0.5 * ls[0], ls
