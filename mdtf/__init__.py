@@ -20,3 +20,4 @@ from .train.variables import (get_variable, variable_scope, name_scope, get_vari
 from .train.step import placeholder  # noqa: F401
 from .cluster import ClusterSpec, Server  # noqa: F401
 from . import app  # noqa: F401
+from . import estimator  # noqa: F401

@@ -111,33 +111,82 @@ __global__ void colsum_scalar(const bf16_t* __restrict__ x, long long M, int C, 
   atomicAdd(out + c, s);
 }
 
-// column sums of a [M, C] bf16 matrix -> fp32 [C] (bias gradients). One block
-// per 8*64 channel slab x row split; partial results combined with atomics
-// (few, one per (block, channel)).
-__global__ void colsum_kernel(const bf16_t* __restrict__ x, long long M, int C, float* __restrict__ out) {
+// column sums of a [M, C] bf16 matrix -> fp32 [C] (bias gradients), two stages,
+// atomic-free in the hot part:
+//   colsum_partial: block (bx, by) sums rows [bx*rpb, (bx+1)*rpb) of a 512-column
+//     slab (64 lanes x bf16x8); each wave takes every 4th row with 4 independent
+//     loads in flight, the 4 waves combine through LDS, one coalesced fp32 row
+//     of partials per block goes to ws[bx][C];
+//   reduce_partials: out[c] += sum_b ws[b][c] (64 columns x 4 row groups per
+//     block, kSlices blocks per column slab, one atomic per column per slice).
+constexpr int kColsumWaves = 2048;   // target waves in flight for the partial pass
+constexpr int kSlices = 8;
+
+__global__ void __launch_bounds__(kT) colsum_partial(const bf16_t* __restrict__ x, long long M, int C, int rpb,
+                                                     float* __restrict__ ws) {
   const int cv = C / 8;
-  const int lane = threadIdx.x % 64, grp = threadIdx.x / 64;  // 4 row groups
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int cvec = blockIdx.y * 64 + lane;
+  const long long r0 = (long long)blockIdx.x * rpb;
+  const long long r1 = r0 + rpb < M ? r0 + rpb : M;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (cvec < cv) {
-    for (long long r = (long long)blockIdx.x * 4 + grp; r < M; r += (long long)gridDim.x * 4) {
-      float v[8];
-      load_bf8(x + r * C + cvec * 8, v);
+    long long r = r0 + wave;
+    for (; r + 12 < r1; r += 16) {
+      float a[4][8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s[k] += v[k];
+      for (int u = 0; u < 4; ++u) load_bf8(x + (r + 4 * u) * C + cvec * 8, a[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] += a[u][k];
+    }
+    for (; r < r1; r += 4) {
+      float a[8];
+      load_bf8(x + r * C + cvec * 8, a);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += a[k];
     }
   }
   __shared__ float L[4][64 * 8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) L[grp][lane * 8 + k] = s[k];
+  for (int k = 0; k < 8; ++k) L[wave][lane * 8 + k] = s[k];
   __syncthreads();
-  if (grp == 0 && cvec < cv) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float t = L[0][lane * 8 + k] + L[1][lane * 8 + k] + L[2][lane * 8 + k] + L[3][lane * 8 + k];
-      atomicAdd(out + cvec * 8 + k, t);
-    }
+  // 256 threads write the slab's 512 partial columns, two each, coalesced
+  for (int j = threadIdx.x; j < 512; j += kT) {
+    const int col = blockIdx.y * 512 + j;
+    if (col < C) ws[(long long)blockIdx.x * C + col] = L[0][j] + L[1][j] + L[2][j] + L[3][j];
   }
+}
+
+__global__ void __launch_bounds__(kT) reduce_partials(const float* __restrict__ ws, int B, int C, long long ld,
+                                                      float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float t = 0.f;
+  if (c < C) {
+    int b = blockIdx.y * 4 + grp;
+    const int step = gridDim.y * 4;
+    for (; b + 3 * step < B; b += 4 * step)
+      t += ws[(long long)b * ld + c] + ws[(long long)(b + step) * ld + c] + ws[(long long)(b + 2 * step) * ld + c] +
+           ws[(long long)(b + 3 * step) * ld + c];
+    for (; b < B; b += step) t += ws[(long long)b * ld + c];
+  }
+  __shared__ float L[4][64];
+  L[grp][lane] = t;
+  __syncthreads();
+  if (grp == 0 && c < C) atomicAdd(out + c, L[0][lane] + L[1][lane] + L[2][lane] + L[3][lane]);
+}
+
+void colsum_geometry(long long M, int C, int* gx, int* rpb) {
+  const int gy = static_cast<int>(ceil_div(C / 8, 64));
+  long long want = kColsumWaves / 4 / gy;
+  if (want < 1) want = 1;
+  long long g = ceil_div(M, 16);
+  if (g > want) g = want;
+  if (g < 1) g = 1;
+  *rpb = static_cast<int>(ceil_div(M, g));
+  *gx = static_cast<int>(ceil_div(M, *rpb));
 }
 
 // ---------------------------------------------------------------- pooling
@@ -482,7 +531,31 @@ MDTF_EXPORT int mdtf_act_bwd(const void* dy, const void* pre, const void* y, voi
 }
 
 // out must be zeroed by the caller
-MDTF_EXPORT int mdtf_colsum(const void* x, long long M, int C, float* out, hipStream_t st) {
+// out[c] += sum_b ws[b][c]   (shared by every two-stage column reduction)
+// (row stride ld >= C)
+MDTF_EXPORT int mdtf_reduce_partials_strided(const float* ws, int B, int C, long long ld, float* out, hipStream_t st) {
+  int slices = B < kSlices * 4 ? static_cast<int>(ceil_div(B, 4)) : kSlices;
+  if (slices < 1) slices = 1;
+  hipLaunchKernelGGL(reduce_partials, dim3(ceil_div(C, 64), slices), dim3(kT), 0, st, ws, B, C, ld, out);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_reduce_partials(const float* ws, int B, int C, float* out, hipStream_t st) {
+  return mdtf_reduce_partials_strided(ws, B, C, C, out, st);
+}
+
+// fp32 workspace (elements) mdtf_colsum needs for an [M, C] input
+MDTF_EXPORT long long mdtf_colsum_ws(long long M, int C) {
+  if (C % 8) return 0;
+  int gx, rpb;
+  colsum_geometry(M, C, &gx, &rpb);
+  return (long long)gx * C;
+}
+
+// out[c] += sum_r x[r][c]; ws: mdtf_colsum_ws(M, C) floats (unused when C % 8)
+MDTF_EXPORT int mdtf_colsum(const void* x, long long M, int C, float* out, float* ws, hipStream_t st) {
+  if (M <= 0) return 0;
   if (C % 8) {
     long long gy = M < 256 ? M : 256;
     hipLaunchKernelGGL(colsum_scalar, dim3(ceil_div(C, kT), gy > 0 ? gy : 1), dim3(kT), 0, st, (const bf16_t*)x, M, C,
@@ -490,12 +563,12 @@ MDTF_EXPORT int mdtf_colsum(const void* x, long long M, int C, float* out, hipSt
     MDTF_LAUNCH_CHECK();
     return 0;
   }
-  int gy = static_cast<int>(ceil_div(C / 8, 64));
-  long long gx = ceil_div(M, 4 * 16);
-  if (gx > 512) gx = 512;
-  hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(kT), 0, st, (const bf16_t*)x, M, C, out);
+  int gx, rpb;
+  colsum_geometry(M, C, &gx, &rpb);
+  const int gy = static_cast<int>(ceil_div(C / 8, 64));
+  hipLaunchKernelGGL(colsum_partial, dim3(gx, gy), dim3(kT), 0, st, (const bf16_t*)x, M, C, rpb, ws);
   MDTF_LAUNCH_CHECK();
-  return 0;
+  return mdtf_reduce_partials(ws, gx, C, out, st);
 }
 
 MDTF_EXPORT int mdtf_pool_fwd(int is_max, const void* x, void* y, void* argmax, int N, int H, int W, int C, int OH,

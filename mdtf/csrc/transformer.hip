@@ -6,8 +6,9 @@
 //   * ln_fwd:  s = x (+ res);  y = (s - mean) * rstd * gamma + beta   (one wave per row,
 //              bf16x8 vectors, the row stays in registers: one read, two writes)
 //   * ln_bwd:  dx = rstd * (g·dy - mean(g·dy) - xhat·mean(g·dy·xhat)); per-block
-//              dgamma/dbeta partials accumulated in registers over many rows, then
-//              one fp32 atomic per column per block (low contention)
+//              dgamma/dbeta partials accumulated in registers over the block's rows,
+//              stored to a workspace, then summed by the shared partial-reduction
+//              kernel (no hot atomics; ~1024 blocks keep every CU busy)
 //   * softmax: y = softmax(scale·x + mask[b, key]) over the key axis, one wave per row
 //   * embed:   out[t] = table[id[t]] gather; backward = fp32 atomic scatter-add
 #include "mdtf_common.h"
@@ -82,8 +83,8 @@ template <int NV>
 __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
                                                    const float* __restrict__ gamma, const float* __restrict__ mean,
                                                    const float* __restrict__ rstd, bf16_t* __restrict__ dx,
-                                                   float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                   long long rows, int H, int rows_per_block) {
+                                                   float* __restrict__ ws, long long rows, int H,
+                                                   int rows_per_block) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nvec = H / 8;
   float dg[NV][8], db[NV][8];
@@ -128,28 +129,25 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
       }
     }
   }
-  // combine the 4 waves through LDS, then one atomic per column per block
+  // combine the 4 waves through LDS; block partials -> ws[block][2][H] (plain stores)
   __shared__ float L[2][kT / 64][64 * 8];   // one 512-column slab per pass over NV
+  float* wg = ws + (long long)blockIdx.x * 2 * H;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int c = lane + i * 64;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       L[0][wave][lane * 8 + k] = dg[i][k];
       L[1][wave][lane * 8 + k] = db[i][k];
     }
     __syncthreads();
-    if (wave == 0 && c < nvec) {
+    for (int j = threadIdx.x; j < 2 * 512; j += kT) {
+      const int which = j >> 9, cc = j & 511;
+      const int col = i * 512 + cc;
+      if (col < H) {
+        float t = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float tg = 0.f, tb = 0.f;
-#pragma unroll
-        for (int w = 0; w < kT / 64; ++w) {
-          tg += L[0][w][lane * 8 + k];
-          tb += L[1][w][lane * 8 + k];
-        }
-        atomicAdd(dgamma + c * 8 + k, tg);
-        atomicAdd(dbeta + c * 8 + k, tb);
+        for (int w = 0; w < kT / 64; ++w) t += L[which][w][cc];
+        wg[which * H + col] = t;
       }
     }
     __syncthreads();
@@ -291,20 +289,42 @@ MDTF_EXPORT int mdtf_ln_fwd(const void* x, const void* res, const float* gamma, 
   return 0;
 }
 
-// dgamma/dbeta accumulate (zeroed buffers or fp32 grad slots)
+extern "C" int mdtf_reduce_partials(const float* ws, int B, int C, float* out, hipStream_t st);
+extern "C" int mdtf_reduce_partials_strided(const float* ws, int B, int C, long long ld, float* out, hipStream_t st);
+
+static void ln_bwd_geometry(long long rows, int* blocks, int* rpb) {
+  long long b = ceil_div(rows, 8);          // >= 2 rows per wave
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  *rpb = static_cast<int>(ceil_div(rows, b));
+  *blocks = static_cast<int>(ceil_div(rows, *rpb));
+}
+
+// fp32 workspace elements mdtf_ln_bwd needs
+MDTF_EXPORT long long mdtf_ln_bwd_ws(long long rows, int H) {
+  int blocks, rpb;
+  ln_bwd_geometry(rows, &blocks, &rpb);
+  return (long long)blocks * 2 * H;
+}
+
+// dgamma/dbeta accumulate (+=) into zeroed buffers or fp32 grad slots;
+// dgamma and dbeta must be ONE buffer pair [dgamma | dbeta] when contiguous is
+// not guaranteed -> reduced separately.
 MDTF_EXPORT int mdtf_ln_bwd(const void* dy, const void* s, const float* gamma, const float* mean, const float* rstd,
-                            void* dx, float* dgamma, float* dbeta, long long rows, int H, hipStream_t st) {
+                            void* dx, float* dgamma, float* dbeta, float* ws, long long rows, int H, hipStream_t st) {
   if (H % 8) return MDTF_EINVAL;
-  int rpb = 64;
-  long long blocks = ceil_div(rows, rpb);
-  if (blocks > 2048) {
-    rpb = static_cast<int>(ceil_div(rows, 2048));
-    blocks = ceil_div(rows, rpb);
-  }
-  NV_DISPATCH(H, ln_bwd_kernel, dim3(blocks), (const bf16_t*)dy, (const bf16_t*)s, gamma, mean, rstd, (bf16_t*)dx,
-              dgamma, dbeta, rows, H, rpb);
+  if (rows <= 0) return 0;
+  int blocks, rpb;
+  ln_bwd_geometry(rows, &blocks, &rpb);
+  NV_DISPATCH(H, ln_bwd_kernel, dim3(blocks), (const bf16_t*)dy, (const bf16_t*)s, gamma, mean, rstd, (bf16_t*)dx, ws,
+              rows, H, rpb);
   MDTF_LAUNCH_CHECK();
-  return 0;
+  // ws rows are [dgamma(H) | dbeta(H)]: reduce as a [blocks, 2H] matrix when the
+  // two outputs are adjacent, else as two strided passes
+  if (dbeta == dgamma + H) return mdtf_reduce_partials(ws, blocks, 2 * H, dgamma, st);
+  int rc = mdtf_reduce_partials_strided(ws, blocks, H, 2 * H, dgamma, st);
+  if (rc) return rc;
+  return mdtf_reduce_partials_strided(ws + H, blocks, H, 2 * H, dbeta, st);
 }
 
 MDTF_EXPORT int mdtf_softmax_fwd(const void* x, const float* mask, void* y, long long rows, int cols, float scale,

@@ -114,11 +114,11 @@ class Bert(Model):
                     h = _dense("dense", h, H, act="gelu")
                     h = _ln("LayerNorm", h)
                 out_bias = V.get_variable("output_bias", [self.vocab], initializer=V.constant_initializer(0.0))
-                mlm = torch.matmul(h, word.t()) + out_bias.to(h.dtype)
+                mlm = ops.dense_transposed(h, word, out_bias)                # tied decoder
             with V.variable_scope("seq_relationship"):
                 w = V.get_variable("output_weights", [2, H], initializer=_init())
                 b = V.get_variable("output_bias", [2], initializer=V.constant_initializer(0.0))
-                nsp = torch.matmul(pooled, w.t()) + b.to(pooled.dtype)
+                nsp = ops.dense_transposed(pooled, w, b)
         return mlm, nsp
 
     def _layer(self, x, amask, B, S_, H, nh, dh):
@@ -129,7 +129,7 @@ class Bert(Model):
                     with V.variable_scope(nm):
                         ws.append(V.get_variable("kernel", [H, H], initializer=_init()))
                         bs.append(V.get_variable("bias", [H], initializer=V.constant_initializer(0.0)))
-                qkv = ops.dense(x.reshape(-1, H), torch.cat(ws, 1), torch.cat(bs, 0))      # one GEMM
+                qkv = ops.dense_multi(x.reshape(-1, H), ws, bs)                               # one GEMM
                 qkv = qkv.view(B, S_, 3, nh, dh).permute(2, 0, 3, 1, 4)                     # [3, B, nh, S, dh]
                 ctx = T.attention(qkv[0], qkv[1], qkv[2], amask)
                 ctx = ctx.permute(0, 2, 1, 3).reshape(B, S_, H)

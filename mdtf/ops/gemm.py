@@ -1,29 +1,156 @@
-"""Dense / matmul on the GPU: GEMM + fused bias/activation epilogue kernel.
+"""Dense / matmul on the GPU: hipBLASLt GEMMs with fp32 weight-gradient sinks.
 
-The plain GEMM goes to hipBLASLt (``torch.matmul``) — the library path the
-design allows for plain GEMMs — and bias + activation (+ their gradients, the
-bias column sums) run on the mdtf kernels.  The hand-written MFMA GEMM of
-``csrc/gemm.hip`` takes over per shape once it wins (see ``ops/autotune.py``).
+Forward: ``y = act(x @ W + b)`` — the GEMM and the bias run as ONE hipBLASLt
+call (``addmm``'s bias epilogue); GELU/ReLU (which must keep the
+pre-activation for backward) is the mdtf activation kernel.  Several weight
+matrices that share an input (BERT's query/key/value) run as one GEMM on the
+column-concatenated weights.
+
+Backward: ``dx = dpre @ W^T`` (bf16), and the weight gradient is computed by
+hipBLASLt *directly into the variable's fp32 gradient slot* with
+``C += A^T B`` (bf16 inputs, fp32 accumulate/output), so no bf16 weight
+gradient is materialised and no separate cast/accumulate kernel runs; the
+bias gradient is the two-stage column-sum kernel, also accumulating into the
+fp32 slot.  (The library GEMM is used for these plain GEMMs; everything
+between them is mdtf kernels.)
 """
 import torch
 
+from . import _native as N
 from . import kernels
+from ..train import variables as V
+
+_ACT = {None: 0, "relu": 1, "gelu": 2}
+_fp32_out_ok = None      # does this torch build accept addmm(out_dtype=float32, out=...)?
+
+
+def _accum_mm(out, a, b):
+    """``out += a @ b`` with bf16 a/b and fp32 out."""
+    global _fp32_out_ok
+    if _fp32_out_ok is None or _fp32_out_ok:
+        try:
+            torch.addmm(out, a, b, out_dtype=torch.float32, out=out)
+            _fp32_out_ok = True
+            return
+        except (RuntimeError, TypeError):
+            _fp32_out_ok = False
+    out.add_(torch.mm(a, b))
+
+
+def _act_fwd(pre, act):
+    y = torch.empty_like(pre)
+    C = pre.shape[-1]
+    N.check(N.fn("mdtf_bias_act_fwd")(N.ptr(pre), None, N.ptr(y), None, pre.numel() // C, C, act, N.stream_ptr()),
+            "act_fwd")
+    return y
+
+
+def _act_bwd(dy, saved, act):
+    dx = torch.empty_like(dy)
+    pre = saved if act == 2 else None
+    y = saved if act == 1 else None
+    N.check(N.fn("mdtf_act_bwd")(N.ptr(dy), N.ptr(pre), N.ptr(y), N.ptr(dx), dy.numel(), act, N.stream_ptr()),
+            "act_bwd")
+    return dx
+
+
+class _Dense(torch.autograd.Function):
+    """y = act(x @ [W_1 | ... | W_n] + [b_1 | ... | b_n]); ``trans``: W given as [N, K]."""
+
+    @staticmethod
+    def forward(ctx, x, act, trans, nw, *wb):
+        ws, bs = wb[:nw], wb[nw:]
+        w = ws[0] if nw == 1 else torch.cat(ws, 1)
+        if trans:
+            w = w.t()
+        has_b = bs[0] is not None
+        b = (bs[0] if nw == 1 else torch.cat(bs, 0)).to(x.dtype) if has_b else None
+        pre = torch.addmm(b, x, w) if has_b else torch.mm(x, w)
+        if act == 0:
+            y, saved = pre, None
+        else:
+            y = _act_fwd(pre, act)
+            saved = pre if act == 2 else y
+        ctx.act, ctx.trans, ctx.nw, ctx.has_b = act, trans, nw, has_b
+        ctx.widths = [t.shape[0] if trans else t.shape[1] for t in ws]
+        ctx.wsinks = [V.grad_sink(t) for t in ws]
+        ctx.bsinks = [V.grad_sink(t) if t is not None else None for t in bs]
+        ctx.like = wb
+        ctx.save_for_backward(x, w, saved)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, saved = ctx.saved_tensors
+        dy = dy.contiguous()
+        dpre = dy if ctx.act == 0 else _act_bwd(dy, saved, ctx.act)
+        dx = torch.mm(dpre, w.t()) if ctx.needs_input_grad[0] else None
+        ws, bs = ctx.like[:ctx.nw], ctx.like[ctx.nw:]
+        gws, gbs = [], []
+        col = 0
+        for j, n in enumerate(ctx.widths):
+            d = dpre[:, col:col + n] if ctx.nw > 1 else dpre
+            col += n
+            sink = ctx.wsinks[j]
+            if sink is not None:
+                if ctx.trans:
+                    _accum_mm(sink.grad, d.t(), x)
+                else:
+                    _accum_mm(sink.grad, x.t(), d)
+                gws.append(V.grad_marker(ws[j]))
+            elif ctx.needs_input_grad[4 + j]:
+                g = torch.mm(d.t(), x) if ctx.trans else torch.mm(x.t(), d)
+                gws.append(g.to(ws[j].dtype))
+            else:
+                gws.append(None)
+        if ctx.has_b:
+            if ctx.nw == 1 and ctx.bsinks[0] is not None:
+                kernels.colsum_into(dpre, ctx.bsinks[0].grad)
+                gbs.append(V.grad_marker(bs[0]))
+            else:
+                tot = kernels.colsum(dpre)
+                col = 0
+                for j, n in enumerate(ctx.widths):
+                    part = tot[col:col + n]
+                    col += n
+                    if ctx.bsinks[j] is not None:
+                        ctx.bsinks[j].grad.add_(part)
+                        gbs.append(V.grad_marker(bs[j]))
+                    else:
+                        gbs.append(part.to(bs[j].dtype))
+        else:
+            gbs = [None] * ctx.nw
+        return (dx, None, None, None) + tuple(gws) + tuple(gbs)
 
 
 def matmul(a, b):
     return torch.matmul(a, b)
 
 
-def dense(x, w, b=None, act=None):
-    y = torch.matmul(x, w.to(x.dtype))
+def _check(x, what):
     if x.dtype != torch.bfloat16:
-        if b is not None:
-            y = y + b.to(y.dtype)
-        if act == "relu":
-            y = torch.relu(y)
-        elif act == "gelu":
-            y = torch.nn.functional.gelu(y, approximate="tanh")
-        return y
-    if b is None and act is None:
-        return y
-    return kernels.bias_act(y, b, act)
+        raise TypeError("mdtf %s expects bf16 activations on the GPU, got %s" % (what, x.dtype))
+
+
+def dense(x, w, b=None, act=None):
+    """``act(x @ w + b)`` for x [..., K], w [K, N]."""
+    return dense_multi(x, [w], [b], act)
+
+
+def dense_multi(x, ws, bs, act=None):
+    """One GEMM for several weight matrices sharing input ``x`` (outputs concatenated)."""
+    _check(x, "dense")
+    shp = x.shape
+    x2 = x.reshape(-1, shp[-1])
+    ws = [w.to(x.dtype) if w.dtype != x.dtype else w for w in ws]
+    y = _Dense.apply(x2, _ACT[act], False, len(ws), *ws, *bs)
+    return y.reshape(*shp[:-1], y.shape[-1])
+
+
+def dense_transposed(x, w, b=None):
+    """``x @ w^T + b`` with w [N, K] (tied embedding decoders)."""
+    _check(x, "dense")
+    shp = x.shape
+    w = w.to(x.dtype) if w.dtype != x.dtype else w
+    y = _Dense.apply(x.reshape(-1, shp[-1]), 0, True, 1, w, b)
+    return y.reshape(*shp[:-1], y.shape[-1])

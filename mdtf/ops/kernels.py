@@ -6,7 +6,8 @@ from ..train import variables as V
 
 N.register("mdtf_bias_act_fwd", [N.P, N.P, N.P, N.P, N.L, N.I, N.I, N.P])
 N.register("mdtf_act_bwd", [N.P, N.P, N.P, N.P, N.L, N.I, N.P])
-N.register("mdtf_colsum", [N.P, N.L, N.I, N.P, N.P])
+N.register("mdtf_colsum", [N.P, N.L, N.I, N.P, N.P, N.P])
+N.register("mdtf_colsum_ws", [N.L, N.I], restype=N.L)
 N.register("mdtf_pool_fwd", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.P])
 N.register("mdtf_pool_bwd", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.P])
 N.register("mdtf_gap_fwd", [N.P, N.P, N.I, N.I, N.I, N.P])
@@ -26,12 +27,17 @@ def _bf16(x, what):
     return x.contiguous()
 
 
+def colsum_into(x2d, out):
+    """``out += x2d.sum(0)`` for a bf16 [M, C] matrix and an fp32 [C] ``out``."""
+    M, C = x2d.shape
+    ws = torch.empty(max(N.fn("mdtf_colsum_ws")(M, C), 1), dtype=torch.float32, device=x2d.device)
+    N.check(N.fn("mdtf_colsum")(N.ptr(x2d), M, C, N.ptr(out), N.ptr(ws), N.stream_ptr()), "colsum")
+    return out
+
+
 def colsum(x2d):
     """Column sums of a bf16 [M, C] matrix -> fp32 [C]."""
-    M, C = x2d.shape
-    out = torch.zeros(C, dtype=torch.float32, device=x2d.device)
-    N.check(N.fn("mdtf_colsum")(N.ptr(x2d), M, C, N.ptr(out), N.stream_ptr()), "colsum")
-    return out
+    return colsum_into(x2d, torch.zeros(x2d.shape[1], dtype=torch.float32, device=x2d.device))
 
 
 class _BiasAct(torch.autograd.Function):
@@ -69,8 +75,7 @@ class _BiasAct(torch.autograd.Function):
         if ctx.has_bias:
             C = dx.shape[-1]
             if ctx.sink is not None:       # column sums accumulate straight into the fp32 grad slot
-                N.check(N.fn("mdtf_colsum")(N.ptr(dx), dx.numel() // C, C, N.ptr(ctx.sink.grad), N.stream_ptr()),
-                        "colsum")
+                colsum_into(dx.view(-1, C), ctx.sink.grad)
                 db = V.grad_marker(ctx.bias)
             else:
                 db = colsum(dx.reshape(-1, C)).to(ctx.bias_dtype)

@@ -306,6 +306,25 @@ def dense(x, w, b=None, act=None):
     return y
 
 
+def dense_multi(x, ws, bs, act=None):
+    """One GEMM for several ``[K, N_i]`` weights sharing input ``x``; outputs concatenated on the last axis."""
+    if _native.use_native(x):
+        from . import gemm
+        return gemm.dense_multi(x, ws, bs, act)
+    w = torch.cat([t.to(x.dtype) for t in ws], 1)
+    b = torch.cat(list(bs), 0) if bs[0] is not None else None
+    return dense(x, w, b, act)
+
+
+def dense_transposed(x, w, b=None):
+    """``x @ w^T + b`` for w [N, K] (tied embedding decoders)."""
+    if _native.use_native(x):
+        from . import gemm
+        return gemm.dense_transposed(x, w, b)
+    y = torch.matmul(x, w.to(x.dtype).t())
+    return y + b.to(y.dtype) if b is not None else y
+
+
 def gelu(x):
     return F.gelu(x.float(), approximate="tanh").to(x.dtype)
 

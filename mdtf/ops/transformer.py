@@ -13,7 +13,8 @@ from . import _native as N
 from ..train import variables as V
 
 N.register("mdtf_ln_fwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.F, N.P])
-N.register("mdtf_ln_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P])
+N.register("mdtf_ln_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P])
+N.register("mdtf_ln_bwd_ws", [N.L, N.I], restype=N.L)
 N.register("mdtf_softmax_fwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.L, N.P])
 N.register("mdtf_softmax_bwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.P])
 N.register("mdtf_embed_fwd", [N.P, N.P, N.P, N.L, N.I, N.L, N.P])
@@ -58,8 +59,9 @@ class _LayerNorm(torch.autograd.Function):
         sg, sb = ctx.sinks
         dg = sg.grad if sg is not None else torch.zeros(H, dtype=torch.float32, device=s.device)
         db = sb.grad if sb is not None else torch.zeros(H, dtype=torch.float32, device=s.device)
+        ws = torch.empty(N.fn("mdtf_ln_bwd_ws")(rows, H), dtype=torch.float32, device=s.device)
         N.check(N.fn("mdtf_ln_bwd")(N.ptr(dy), N.ptr(s), N.ptr(g), N.ptr(mean), N.ptr(rstd), N.ptr(dx), N.ptr(dg),
-                                    N.ptr(db), rows, H, N.stream_ptr()), "ln_bwd")
+                                    N.ptr(db), N.ptr(ws), rows, H, N.stream_ptr()), "ln_bwd")
         gamma, beta = ctx.like
         rg = V.grad_marker(gamma) if sg is not None else dg
         rb = V.grad_marker(beta) if sb is not None else db

@@ -11,6 +11,7 @@ train op.  Updates are applied by one fused HIP launch per parameter group
 (``<var>/Momentum``, ``<var>/Adam``, ``<var>/Adam_1``, ``beta1_power``,
 ``beta2_power``).
 """
+import torch
 from ..ops import optim as K
 from . import step as step_mod
 
@@ -46,6 +47,15 @@ class Optimizer(object):
         return step_mod.TrainOp(self, grads_and_vars, global_step)
 
     def minimize(self, loss, global_step=None, var_list=None, name=None):
+        if isinstance(loss, torch.Tensor):
+            # inside an Estimator model_fn (re-run eagerly every step): the estimator
+            # turns this request into ONE TrainOp over the recorded program's loss
+            from ..estimator.estimator import current_capture
+            cap = current_capture()
+            if cap is None:
+                raise TypeError("minimize() of a concrete tensor is only valid inside an Estimator model_fn; "
+                                "use the loss handle returned by Tower.process()")
+            return cap.record(self, global_step, var_list)
         return self.apply_gradients(self.compute_gradients(loss, var_list), global_step, name)
 
     # -- fused update over one UpdateTarget ------------------------------

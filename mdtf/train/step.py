@@ -140,7 +140,7 @@ def resolve(x, ctx):
     if isinstance(x, Fetchable):
         return x.evaluate(ctx)
     if isinstance(x, (list, tuple)):
-        return type(x)(resolve(i, ctx) for i in x)
+        return type(x)([resolve(i, ctx) for i in x])
     if isinstance(x, dict):
         return {k: resolve(v, ctx) for k, v in x.items()}
     return x
