@@ -51,6 +51,11 @@ def resnet_convs(depth=50, batch=256, image=224, width=64):
     return uniq, out
 
 
+# (bm, bn, stages): LDS = stages * (bm + bn) * 128 B <= 160 KiB
+V2_TILES = ((128, 128, 2), (128, 128, 3), (128, 128, 4), (128, 64, 3), (128, 64, 4), (256, 128, 2), (256, 128, 3),
+            (256, 64, 3), (64, 128, 2), (64, 128, 3), (64, 128, 4), (64, 64, 4))
+
+
 def timeit(fn, reps, warm=3):
     for _ in range(warm):
         fn()
@@ -95,30 +100,40 @@ def main():
             key = C.shape_key(pass_, (n, h, w, c), (kh, kw, c, co), (s, s), pads4, (1, 1))
             if pass_ == "fwd":
                 lib = lambda: C.miopen_fwd(x, wt, (s, s), pads4, (1, 1))  # noqa: E731
-                cands = [(bm, bn, 0) for bm, bn in ((128, 128), (128, 64), (64, 64), (256, 64))]
-                mk = lambda bm, bn, sp: (lambda: C.mdtf_fwd(x, wt, (oh, ow), (s, s), pads4, (1, 1), bm, bn))  # noqa
+                cands = [(bm, bn, 0, 1) for bm, bn in ((128, 128), (128, 64), (64, 64), (256, 64))]
+                if C.v2_ok("fwd", c, co, (s, s), kh * kw):
+                    cands += [(bm, bn, st, 2) for bm, bn, st in V2_TILES]
+                mk = lambda bm, bn, sp, v: (lambda: C.mdtf_fwd(x, wt, (oh, ow), (s, s), pads4, (1, 1), bm, bn,  # noqa
+                                                             None, v, sp))
             elif pass_ == "dgrad":
                 lib = lambda: C.miopen_bwd(x, wt, dy, (s, s), pads4, (1, 1), True, False)  # noqa: E731
-                cands = [(bm, bn, 0) for bm, bn in ((128, 128), (128, 64), (64, 64), (256, 64))]
-                mk = lambda bm, bn, sp: (lambda: C.mdtf_dgrad(dy, wt, x.shape, (s, s), pads4, (1, 1), bm, bn))  # noqa
+                cands = [(bm, bn, 0, 1) for bm, bn in ((128, 128), (128, 64), (64, 64), (256, 64))]
+                if C.v2_ok("dgrad", c, co, (s, s), kh * kw):
+                    cands += [(bm, bn, st, 2) for bm, bn, st in V2_TILES]
+                mk = lambda bm, bn, sp, v: (lambda: C.mdtf_dgrad(dy, wt, x.shape, (s, s), pads4, (1, 1), bm, bn,  # noqa
+                                                               v, sp))
             else:
                 lib = lambda: C.miopen_bwd(x, wt, dy, (s, s), pads4, (1, 1), False, True)  # noqa: E731
-                cands = [(bm, bn, sp) for bm, bn in ((128, 128), (64, 64), (128, 64), (64, 128))
+                cands = [(bm, bn, sp, 1) for bm, bn in ((128, 128), (64, 64), (128, 64), (64, 128))
                          for sp in (0, 256, 2048)]
-                mk = lambda bm, bn, sp: (lambda: C.mdtf_wgrad(x, dy, wt.shape, (s, s), pads4, (1, 1), bm, bn, sp))  # noqa
+                mk = lambda bm, bn, sp, v: (lambda: C.mdtf_wgrad(x, dy, wt.shape, (s, s), pads4, (1, 1), bm, bn,  # noqa
+                                                               sp))
             t_lib = timeit(lib, args.reps)
             best = None
             if native_ok:
-                for bm, bn, sp in cands:
+                for bm, bn, sp, v in cands:
                     try:
-                        t = timeit(mk(bm, bn, sp), args.reps)
+                        t = timeit(mk(bm, bn, sp, v), args.reps)
                     except RuntimeError:
                         continue
                     if best is None or t < best[0]:
-                        best = (t, bm, bn, sp)
+                        best = (t, bm, bn, sp, v)
             if best is not None and best[0] < t_lib:
-                table[key] = {"backend": "mdtf", "bm": best[1], "bn": best[2], "splits": best[3],
-                              "ms": round(best[0], 4), "miopen_ms": round(t_lib, 4)}
+                ent = {"backend": "mdtf", "bm": best[1], "bn": best[2], "splits": best[3], "ver": best[4],
+                       "ms": round(best[0], 4), "miopen_ms": round(t_lib, 4)}
+                if best[4] == 2:                      # v2: the third field is the pipeline depth
+                    ent["stages"], ent["splits"] = best[3], 0
+                table[key] = ent
                 choice = "mdtf"
             else:
                 table[key] = {"backend": "miopen", "ms": round(t_lib, 4),
@@ -129,7 +144,7 @@ def main():
             tot["best"] += k * min(t_lib, best[0] if best else 1e9)
             lines.append("| %s | %d,%d,%d,%d,%dx%d,%d,s%d | %d | %.3f | %s | %s | %s |" % (
                 pass_, n, h, w, c, kh, kw, co, s, k, t_lib,
-                ("%.3f (%d,%d,%d)" % best) if best else "n/a",
+                ("%.3f (%d,%d,%d,v%d)" % best) if best else "n/a",
                 ("%.0f" % (flops / best[0] / 1e9)) if best else "-", choice))
             print(lines[-1], flush=True)
     lines.append("")

@@ -464,6 +464,286 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(ConvArgs a) {
     }
 }
 
+// ============================================================================
+// v2 forward / dgrad for C % 64 == 0: BK = 64, both operands K-contiguous in
+// LDS (fwd takes the filter pre-transposed to Wt[co][(kh,kw,ci)]), staged by
+// LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB = 8 rows x 128 B per wave
+// instruction, no VGPR round trip) into a STAGES-deep ring with counted
+// vmcnt waits and one raw barrier per K step.  Address generation is nearly
+// free: per A row a 32-bit base offset and a bitmask of the taps that stay
+// inside the image are computed once; each K step adds a wave-uniform tap
+// offset and tests one bit; padding taps and rows past M/N get an offset
+// beyond the buffer's num_records, which the hardware returns as zeros.
+// LDS rows are 128 B; 16-B chunk c of row r lives at chunk c ^ ((r >> 1) & 7)
+// (the swizzle is applied to the per-lane SOURCE address, the LDS image
+// stays lane-linear), which makes the ds_read_b128 fragment reads of 16 rows
+// conflict-free.  dgrad v2 covers stride 1 (strided dgrad: v1 / MIOpen).
+// ============================================================================
+// 16 B per lane global -> LDS (buffer_load_dwordx4 ... lds): LDS destination = wave-uniform
+// `lds` + 16 * lane; offsets at or past `nbytes` read zeros
+__device__ __forceinline__ void dma16(const void* base, int nbytes, char* lds, unsigned voff, int soff) {
+  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nbytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
+// s_waitcnt vmcnt(N) leaving lgkm/exp counters alone (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int BM, int BN, int MODE, bool STATS, int STAGES>
+__global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
+  constexpr int WM = 2, WN = 2;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int RA = BM / 32, RB = BN / 32;       // DMA instructions per wave per K step
+  constexpr int ROWB = 128;                       // bytes per LDS row (64 bf16)
+  constexpr int STAGE = (BM + BN) * ROWB;
+  constexpr int PER_STAGE = RA + RB;               // LDS-DMA wave-instructions per stage
+  constexpr unsigned OOB = 0x80000000u;            // buffer offset past num_records -> zero fill
+  static_assert(RA >= 1 && RB >= 1, "tile too small");
+  static_assert(STAGES >= 2 && (STAGES - 2) * PER_STAGE < 64, "pipeline depth");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = tile / a.ntiles, nt = tile % a.ntiles;
+  const long long m0 = (long long)mt * BM;
+  const int n0 = nt * BN;
+
+  const int GH = MODE == 0 ? a.H : a.OH;
+  const int GW = MODE == 0 ? a.W : a.OW;
+  const int GC = MODE == 0 ? a.Cin : a.Cout;
+  const int RH = MODE == 0 ? a.OH : a.H;
+  const int RW = MODE == 0 ? a.OW : a.W;
+  const int lrow = lane >> 3;
+  const int ntaps = a.KH * a.KW;                   // <= 32 (host-checked)
+
+  // buffer ranges: bounds-checked loads, out-of-range offsets read as zero (host checks < 2 GiB)
+  const int bytes_a = (int)((long long)a.N * GH * GW * GC * 2);
+  const int bytes_b = (int)((long long)a.K * a.Ncol * 2);
+
+  // per A row: element offset of tap (0,0) (may be "negative", wraps) + valid-tap bitmask
+  unsigned a_off[RA], a_mask[RA];
+#pragma unroll
+  for (int i = 0; i < RA; ++i) {
+    const int row = 8 * (wave + 4 * i) + lrow;
+    const long long m = m0 + row;
+    const bool ok = m < a.M;
+    const long long mm = ok ? m : 0;
+    const int ow = static_cast<int>(mm % RW);
+    const long long t = mm / RW;
+    const int oh = static_cast<int>(t % RH);
+    const int n = static_cast<int>(t / RH);
+    const int y0 = MODE == 0 ? oh * a.SH - a.PH : oh + a.PH;
+    const int x0 = MODE == 0 ? ow * a.SW - a.PW : ow + a.PW;
+    const int ch = 8 * ((lane & 7) ^ ((row >> 1) & 7));
+    a_off[i] = (unsigned)((((long long)n * GH + y0) * GW + x0) * GC + ch);
+    unsigned mask = 0;
+    if (ok) {
+      for (int tt = 0; tt < ntaps; ++tt) {
+        const int kh = tt / a.KW, kw = tt - kh * a.KW;
+        const int iy = MODE == 0 ? y0 + kh * a.DH : y0 - kh * a.DH;
+        const int ix = MODE == 0 ? x0 + kw * a.DW : x0 - kw * a.DW;
+        if (iy >= 0 && iy < GH && ix >= 0 && ix < GW) mask |= 1u << tt;
+      }
+    }
+    a_mask[i] = mask;
+  }
+  // per B row: byte offset of k = 0 (OOB for rows past Ncol)
+  unsigned b_off[RB];
+#pragma unroll
+  for (int i = 0; i < RB; ++i) {
+    const int row = 8 * (wave + 4 * i) + lrow;
+    const int n = n0 + row;
+    const int ch = 8 * ((lane & 7) ^ ((row >> 1) & 7));
+    const long long e = MODE == 0 ? (long long)n * a.K + ch : (long long)n * a.Cout + ch;
+    b_off[i] = n < a.Ncol ? (unsigned)(e * 2) : OOB;
+  }
+
+  // scalar K-walk state: tap index, (kh, kw), channel offset c0 within the tap
+  int s_t = 0, s_kh = 0, s_kw = 0, s_c0 = 0, s_k0 = 0;
+  auto stage = [&](int buf) {
+    const int tap_e = (MODE == 0 ? (s_kh * a.DH * GW + s_kw * a.DW) : -(s_kh * a.DH * GW + s_kw * a.DW)) * GC + s_c0;
+    char* lds = smem_raw + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      const bool ok = (a_mask[i] >> s_t) & 1u;
+      const unsigned voff = ok ? (a_off[i] + (unsigned)tap_e) * 2u : OOB;
+      dma16(a.src, bytes_a, lds + (wave + 4 * i) * 1024, voff, 0);
+    }
+    char* ldsb = lds + BM * ROWB;
+    const int sb = MODE == 0 ? s_k0 * 2 : (s_t * a.Cin * a.Cout + s_c0) * 2;
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+      dma16(a.wgt, bytes_b, ldsb + (wave + 4 * i) * 1024, b_off[i], sb);
+    // advance the K walk by 64
+    s_k0 += 64;
+    s_c0 += 64;
+    if (s_c0 == GC) {
+      s_c0 = 0;
+      ++s_t;
+      if (++s_kw == a.KW) {
+        s_kw = 0;
+        ++s_kh;
+      }
+    }
+  };
+
+  float4v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = a.K / 64;
+  // prologue: stages 0 .. STAGES-2 in flight
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < KT) stage(s);
+  const int fr = lane & 15, fq = lane >> 4;
+  int cur = 0;
+  for (int kt = 0; kt < KT; ++kt) {
+    // stage kt must have landed: leave the (STAGES-2) younger stages in flight
+    if (kt + STAGES - 2 < KT)
+      wait_vmcnt<(STAGES - 2) * PER_STAGE>();
+    else
+      wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();          // every wave's DMA for stage kt is in; buffer (kt-1) is free
+    {
+      const int nk = kt + STAGES - 1;
+      if (nk < KT) stage(nk % STAGES);
+    }
+    const char* As = smem_raw + cur * STAGE;
+    cur = cur + 1 == STAGES ? 0 : cur + 1;
+    const char* Bs = As + BM * ROWB;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8_t fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * (TM * 16) + i * 16 + fr;
+        const int pc = (h * 4 + fq) ^ ((row >> 1) & 7);
+        fa[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(As + row * ROWB + pc * 16));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * (TN * 16) + j * 16 + fr;
+        const int pc = (h * 4 + fq) ^ ((row >> 1) & 7);
+        fb[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(Bs + row * ROWB + pc * 16));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fb[j], fa[i], acc[i][j]);
+    }
+  }
+
+  // ---- epilogue (same as v1): bf16 stores + optional BN statistics
+  const int g = lane >> 4, li = lane & 15;
+  float ssum[TN][4], ssq[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ssum[j][r] = ssq[j][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const long long m = m0 + wm * (TM * 16) + i * 16 + li;
+    const bool mok = m < a.M;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * (TN * 16) + j * 16 + 4 * g;
+      if (mok && n < a.Ncol) {
+        float4v v = acc[i][j];
+        uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(a.out + m * a.Ncol + n) = make_uint2(lo, hi);
+        if (STATS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            ssum[j][r] += v[r];
+            ssq[j][r] += v[r] * v[r];
+          }
+        }
+      }
+    }
+  }
+  if (STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          ssum[j][r] += __shfl_xor(ssum[j][r], o, 64);
+          ssq[j][r] += __shfl_xor(ssq[j][r], o, 64);
+        }
+      }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem_raw);
+    if (li == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nl = wn * (TN * 16) + j * 16 + 4 * g + r;
+          red[wm * BN + nl] = ssum[j][r];
+          red[WM * BN + wm * BN + nl] = ssq[j][r];
+        }
+    }
+    __syncthreads();
+    for (int nl = tid; nl < BN; nl += NT) {
+      const int n = n0 + nl;
+      if (n < a.Ncol) {
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) {
+          s += red[w * BN + nl];
+          q += red[WM * BN + w * BN + nl];
+        }
+        const long long slot = (long long)(mt & (kStatSlots - 1)) * a.Ncol + n;
+        atomicAdd(a.stat_sum + slot, s);
+        atomicAdd(a.stat_sq + slot, q);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int MODE, bool STATS, int STAGES>
+int launch_fd_v2(ConvArgs& a, hipStream_t st) {
+  a.mtiles = static_cast<int>(ceil_div(a.M, BM));
+  a.ntiles = static_cast<int>(ceil_div(a.Ncol, BN));
+  const long long nblk = (long long)a.mtiles * a.ntiles;
+  if (nblk > 0x7fffffff) return MDTF_EUNSUPPORTED;
+  const size_t lds = STAGES * (size_t)(BM + BN) * 128;
+  hipLaunchKernelGGL((conv_fd_v2<BM, BN, MODE, STATS, STAGES>), dim3((unsigned)nblk), dim3(NT), lds, st, a);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// tile code: bm, bn and the pipeline depth (stages 2..4)
+template <int MODE, bool STATS, int STAGES>
+int dispatch_fd_v2s(ConvArgs& a, int bm, int bn, hipStream_t st) {
+  if (bm == 128 && bn == 128) return launch_fd_v2<128, 128, MODE, STATS, STAGES>(a, st);
+  if (bm == 128 && bn == 64) return launch_fd_v2<128, 64, MODE, STATS, STAGES>(a, st);
+  if (bm == 256 && bn == 128) return launch_fd_v2<256, 128, MODE, STATS, STAGES>(a, st);
+  if (bm == 256 && bn == 64) return launch_fd_v2<256, 64, MODE, STATS, STAGES>(a, st);
+  if (bm == 64 && bn == 128) return launch_fd_v2<64, 128, MODE, STATS, STAGES>(a, st);
+  if (bm == 64 && bn == 64) return launch_fd_v2<64, 64, MODE, STATS, STAGES>(a, st);
+  return MDTF_EUNSUPPORTED;
+}
+
+template <int MODE, bool STATS>
+int dispatch_fd_v2(ConvArgs& a, int bm, int bn, int stages, hipStream_t st) {
+  if (stages == 2) return dispatch_fd_v2s<MODE, STATS, 2>(a, bm, bn, st);
+  if (stages == 3) return dispatch_fd_v2s<MODE, STATS, 3>(a, bm, bn, st);
+  if (stages == 4) return dispatch_fd_v2s<MODE, STATS, 4>(a, bm, bn, st);
+  return MDTF_EUNSUPPORTED;
+}
+
 template <int BM, int BN, int MODE, bool STATS>
 size_t fd_lds() {
   const size_t a = (size_t)BM * (BK + PADK);
@@ -587,4 +867,45 @@ MDTF_EXPORT int mdtf_conv_wgrad(const void* x, const void* dy, float* dw, int N,
   if (bm == 128 && bn == 64) return launch_wgrad<128, 64>(a, splits, st);
   if (bm == 64 && bn == 128) return launch_wgrad<64, 128>(a, splits, st);
   return MDTF_EUNSUPPORTED;
+}
+
+// v2 (C % 64 == 0): Y = conv(X, W) with the filter given transposed, Wt[co][(kh,kw,ci)]
+MDTF_EXPORT int mdtf_conv_fwd_v2(const void* x, const void* wt, void* y, float* stat_sum, float* stat_sq, int N,
+                                 int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int SH, int SW,
+                                 int PH, int PW, int DH, int DW, int bm, int bn, int* mtiles_out, hipStream_t st) {
+  if (Cin % 64 || Cout % 8) return MDTF_EINVAL;
+  if (KH * KW > 32 || (long long)N * H * W * Cin * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
+  ConvArgs a = make_args(N, H, W, Cin, OH, OW, Cout, KH, KW, SH, SW, PH, PW, DH, DW);
+  a.src = (const bf16_t*)x;
+  a.wgt = (const bf16_t*)wt;
+  a.out = (bf16_t*)y;
+  a.stat_sum = stat_sum;
+  a.stat_sq = stat_sq;
+  a.M = (long long)N * OH * OW;
+  a.Ncol = Cout;
+  a.K = KH * KW * Cin;
+  const int stages = bm / 1000 ? bm / 1000 : 2;   // bm = stages * 1000 + tile rows
+  bm %= 1000;
+  int rc = stat_sum ? dispatch_fd_v2<0, true>(a, bm, bn, stages, st) : dispatch_fd_v2<0, false>(a, bm, bn, stages, st);
+  if (mtiles_out) *mtiles_out = a.mtiles;
+  return rc;
+}
+
+// v2 (Cout % 64 == 0): DX = dgrad(DY, W), W in HWIO
+MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int OH,
+                                   int OW, int Cout, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW,
+                                   int bm, int bn, hipStream_t st) {
+  if (Cout % 64 || Cin % 8) return MDTF_EINVAL;
+  if (SH != 1 || SW != 1 || KH * KW > 32 || (long long)N * OH * OW * Cout * 2 > 0x7fffffffLL)
+    return MDTF_EUNSUPPORTED;
+  ConvArgs a = make_args(N, H, W, Cin, OH, OW, Cout, KH, KW, SH, SW, PH, PW, DH, DW);
+  a.src = (const bf16_t*)dy;
+  a.wgt = (const bf16_t*)w;
+  a.out = (bf16_t*)dx;
+  a.M = (long long)N * H * W;
+  a.Ncol = Cin;
+  a.K = KH * KW * Cout;
+  const int stages = bm / 1000 ? bm / 1000 : 2;
+  bm %= 1000;
+  return dispatch_fd_v2<1, false>(a, bm, bn, stages, st);
 }

@@ -21,6 +21,8 @@ from ..train import variables as V
 N.register("mdtf_conv_fwd", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 17 + [N.P, N.P])
 N.register("mdtf_conv_dgrad", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
 N.register("mdtf_conv_wgrad", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
+N.register("mdtf_conv_fwd_v2", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 17 + [N.P, N.P])
+N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 TABLE_PATH = os.path.join(_HERE, "conv_table.json")
@@ -48,8 +50,23 @@ def _default_tile(ncol):
     return (128, 128) if ncol % 128 == 0 else (128, 64)
 
 
+def v2_ok(pass_, c, co, stride=(1, 1), taps=1):
+    """The BK=64 LDS-DMA kernels: gathered channels % 64 == 0, <= 32 filter taps; dgrad stride 1."""
+    if taps > 32:
+        return False
+    if pass_ == "fwd":
+        return c % 64 == 0 and co % 8 == 0
+    if pass_ == "dgrad":
+        return co % 64 == 0 and c % 8 == 0 and tuple(stride) == (1, 1)
+    return False
+
+
 def choose(pass_, x_shape, w_shape, stride, pads, dil):
-    """-> ('mdtf', bm, bn, splits) or ('miopen',)."""
+    """-> ('mdtf', bm, bn, splits, version, stages) or ('miopen',).
+
+    ``MDTF_CONV``: ``auto`` (table, else defaults), ``mdtf`` (v1 kernels),
+    ``mdtf2`` (v2 kernels where the channels allow, else v1), ``miopen``.
+    """
     n, h, w, c = x_shape
     kh, kw, ci, co = w_shape
     forced = os.environ.get("MDTF_CONV", "auto")
@@ -60,12 +77,14 @@ def choose(pass_, x_shape, w_shape, stride, pads, dil):
     if forced == "auto" and ent is not None:
         if ent["backend"] == "miopen":
             return ("miopen",)
-        return ("mdtf", ent["bm"], ent["bn"], ent.get("splits", 0))
+        return ("mdtf", ent["bm"], ent["bn"], ent.get("splits", 0), ent.get("ver", 1), ent.get("stages", 2))
     if pass_ == "wgrad":
         r = kh * kw * ci
-        return ("mdtf", 128 if r >= 128 else 64, 128 if co % 128 == 0 else 64, 0)
-    bm, bn = _default_tile(co if pass_ == "fwd" else ci)
-    return ("mdtf", bm, bn, 0)
+        return ("mdtf", 128 if r >= 128 else 64, 128 if co % 128 == 0 else 64, 0, 1, 2)
+    ncol = co if pass_ == "fwd" else ci
+    bm, bn = _default_tile(ncol)
+    ver = 2 if (forced in ("auto", "mdtf2") and v2_ok(pass_, c, co, stride, kh * kw)) else 1
+    return ("mdtf", bm, bn, 0, ver, 3 if ver == 2 else 2)
 
 
 # ---------------------------------------------------------------------------
@@ -125,26 +144,40 @@ def _geo(x, w, out_hw, stride, pads, dil):
     return [n, h, wd, c, out_hw[0], out_hw[1], co, kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1]]
 
 
-def mdtf_fwd(x, w, out_hw, stride, pads, dil, bm, bn, stats=None):
+def transpose_filter(w):
+    """HWIO [kh,kw,ci,co] -> Wt [co][(kh,kw,ci)] (the v2 forward kernel's K-contiguous B operand)."""
+    from . import kernels
+    kh, kw, ci, co = w.shape
+    return kernels.transpose_brs(w.reshape(1, kh * kw * ci, co), 1, kh * kw * ci, co).view(co, kh * kw * ci)
+
+
+def mdtf_fwd(x, w, out_hw, stride, pads, dil, bm, bn, stats=None, ver=1, stages=2):
     n = x.shape[0]
     co = w.shape[3]
     y = torch.empty((n, out_hw[0], out_hw[1], co), dtype=x.dtype, device=x.device)
     mt = N.I(0)
     s_sum, s_sq = (stats if stats is not None else (None, None))
     import ctypes
+    if ver == 2:
+        wt = transpose_filter(w)
+        N.check(N.fn("mdtf_conv_fwd_v2")(N.ptr(x), N.ptr(wt), N.ptr(y), N.ptr(s_sum), N.ptr(s_sq),
+                                         *_geo(x, w, out_hw, stride, pads, dil), bm + 1000 * stages, bn,
+                                         ctypes.byref(mt),
+                                         N.stream_ptr()), "conv_fwd_v2")
+        return y
     N.check(N.fn("mdtf_conv_fwd")(N.ptr(x), N.ptr(w), N.ptr(y), N.ptr(s_sum), N.ptr(s_sq),
                                   *_geo(x, w, out_hw, stride, pads, dil), bm, bn, ctypes.byref(mt), N.stream_ptr()),
             "conv_fwd")
     return y
 
 
-def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn):
+def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn, ver=1, stages=2):
     dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
     n, h, wd, c = x_shape
     kh, kw, ci, co = w.shape
-    N.check(N.fn("mdtf_conv_dgrad")(N.ptr(dy), N.ptr(w), N.ptr(dx), n, h, wd, c, dy.shape[1], dy.shape[2], co, kh,
-                                    kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1], bm, bn,
-                                    N.stream_ptr()), "conv_dgrad")
+    N.check(N.fn("mdtf_conv_dgrad_v2" if ver == 2 else "mdtf_conv_dgrad")(N.ptr(dy), N.ptr(w), N.ptr(dx), n, h, wd, c, dy.shape[1], dy.shape[2], co, kh,
+                                    kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
+                                    bm + 1000 * stages if ver == 2 else bm, bn, N.stream_ptr()), "conv_dgrad")
     return dx
 
 
@@ -179,7 +212,7 @@ class _Conv(torch.autograd.Function):
                 co = w.shape[3]
                 buf = torch.zeros((2, STAT_SLOTS, co), dtype=torch.float32, device=x.device)
                 stats = (buf[0], buf[1])
-            y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2], stats)
+            y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2], stats, ch[4], ch[5])
         else:
             y = miopen_fwd(x, w, stride, pads, dil)
         ctx.save_for_backward(x, w)
@@ -218,7 +251,7 @@ class _Conv(torch.autograd.Function):
                 else:
                     dw = ldw
         if need_dx and not lib_dx:
-            dx = mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2])
+            dx = mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5])
         if need_dw and not lib_dw:
             if sink is not None:
                 # fp32 atomics of the wgrad kernel accumulate into the flat gradient buffer
@@ -270,7 +303,7 @@ def conv2d_dgrad_nhwc(x, w, out_shape, stride, pads):
     wb = w.to(x.dtype).contiguous()
     ch = choose("dgrad", (n, oh, ow, co), (kh, kw, co, wci), stride, pads, (1, 1))
     if ch[0] == "mdtf":
-        return _ConvT.apply(x, wb, tuple(stride), tuple(pads), (n, oh, ow, co), ch[1], ch[2])
+        return _ConvT.apply(x, wb, tuple(stride), tuple(pads), (n, oh, ow, co), ch[1], ch[2], ch[4], ch[5])
     xc = x.permute(0, 3, 1, 2)
     wt = w.permute(3, 2, 0, 1).to(x.dtype)
     y = F.conv_transpose2d(xc, wt, None, stride, 0)
@@ -284,9 +317,9 @@ class _ConvT(torch.autograd.Function):
     """Transposed conv as conv dgrad (fwd) with conv fwd / wgrad for its backward."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, pads, out_shape, bm, bn):
+    def forward(ctx, x, w, stride, pads, out_shape, bm, bn, ver, stages):
         x = x.contiguous()
-        y = mdtf_dgrad(x, w, out_shape, stride, pads, (1, 1), bm, bn)
+        y = mdtf_dgrad(x, w, out_shape, stride, pads, (1, 1), bm, bn, ver, stages)
         ctx.save_for_backward(x, w)
         ctx.args = (stride, pads)
         return y
@@ -303,4 +336,4 @@ class _ConvT(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = mdtf_wgrad(dy, x, w.shape, stride, pads, (1, 1), 128 if w.shape[0] * w.shape[1] * w.shape[2] >= 128
                             else 64, 128 if w.shape[3] % 128 == 0 else 64, 0)
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None

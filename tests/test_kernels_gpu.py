@@ -235,12 +235,16 @@ CONV_CASES = [
     (1, 13, 11, 8, 3, 3, 72, 1, "SAME"),           # K=72 (not a multiple of 32), Cout=72
     (2, 20, 20, 8, 7, 7, 64, 2, (3, 3)),           # stem-like 7x7/2 with 8 channels
     (5, 7, 7, 128, 3, 3, 128, 1, "SAME"),          # M tail (245 rows)
+    (2, 14, 14, 64, 3, 3, 128, 2, (1, 1)),         # v2: strided 3x3 (dgrad divisibility path)
+    (3, 9, 9, 128, 3, 3, 64, 1, "SAME"),           # v2: BN=64 tiles, dgrad Ncol=128
+    (2, 8, 8, 192, 1, 1, 320, 1, "VALID"),         # v2: N tail (320 = 2.5 x 128)
 ]
 
 
+@pytest.mark.parametrize("backend", ["mdtf", "mdtf2"])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_hip_fwd_dgrad_wgrad(case, monkeypatch):
-    monkeypatch.setenv("MDTF_CONV", "mdtf")
+def test_conv_hip_fwd_dgrad_wgrad(case, backend, monkeypatch):
+    monkeypatch.setenv("MDTF_CONV", backend)
     n, h, w_, c, kh, kw, co, s, pad = case
     torch.manual_seed(5)
     x = torch.randn(n, h, w_, c)
