@@ -51,6 +51,7 @@ def resnet_convs(depth=50, batch=256, image=224, width=64):
     return uniq, out
 
 
+WG2_TILES = ((128, 128, 2), (128, 128, 3), (128, 64, 2), (64, 128, 2), (64, 64, 3))
 # (bm, bn, stages): LDS = stages * (bm + bn) * 128 B <= 160 KiB
 V2_TILES = ((128, 128, 2), (128, 128, 3), (128, 128, 4), (128, 64, 3), (128, 64, 4), (256, 128, 2), (256, 128, 3),
             (256, 64, 3), (64, 128, 2), (64, 128, 3), (64, 128, 4), (64, 64, 4))
@@ -116,8 +117,11 @@ def main():
                 lib = lambda: C.miopen_bwd(x, wt, dy, (s, s), pads4, (1, 1), False, True)  # noqa: E731
                 cands = [(bm, bn, sp, 1) for bm, bn in ((128, 128), (64, 64), (128, 64), (64, 128))
                          for sp in (0, 256, 2048)]
-                mk = lambda bm, bn, sp, v: (lambda: C.mdtf_wgrad(x, dy, wt.shape, (s, s), pads4, (1, 1), bm, bn,  # noqa
-                                                               sp))
+                if C.v2_ok("wgrad", c, co, (s, s), kh * kw):
+                    cands += [((bm, st), bn, sp, 2) for bm, bn, st in WG2_TILES for sp in (0, 256, 2048)]
+                mk = lambda bm, bn, sp, v: (lambda: C.mdtf_wgrad(  # noqa
+                    x, dy, wt.shape, (s, s), pads4, (1, 1), bm[0] if v == 2 else bm, bn, sp, None, v,
+                    bm[1] if v == 2 else 2))
             t_lib = timeit(lib, args.reps)
             best = None
             if native_ok:
@@ -131,7 +135,9 @@ def main():
             if best is not None and best[0] < t_lib:
                 ent = {"backend": "mdtf", "bm": best[1], "bn": best[2], "splits": best[3], "ver": best[4],
                        "ms": round(best[0], 4), "miopen_ms": round(t_lib, 4)}
-                if best[4] == 2:                      # v2: the third field is the pipeline depth
+                if best[4] == 2 and pass_ == "wgrad":     # v2 wgrad: bm field carries (rows, stages)
+                    ent["bm"], ent["stages"] = best[1]
+                elif best[4] == 2:                        # v2 fwd/dgrad: the third field is the pipeline depth
                     ent["stages"], ent["splits"] = best[3], 0
                 table[key] = ent
                 choice = "mdtf"
@@ -144,7 +150,7 @@ def main():
             tot["best"] += k * min(t_lib, best[0] if best else 1e9)
             lines.append("| %s | %d,%d,%d,%d,%dx%d,%d,s%d | %d | %.3f | %s | %s | %s |" % (
                 pass_, n, h, w, c, kh, kw, co, s, k, t_lib,
-                ("%.3f (%d,%d,%d,v%d)" % best) if best else "n/a",
+                ("%.3f (%s,%d,%d,v%d)" % best) if best else "n/a",
                 ("%.0f" % (flops / best[0] / 1e9)) if best else "-", choice))
             print(lines[-1], flush=True)
     lines.append("")

@@ -146,8 +146,9 @@ __global__ void __launch_bounds__(kThreads)
 // 16 row groups stream the partials in parallel (fp32), combined in fp64.
 constexpr int kFinCh = 64, kFinGroups = 16;
 
+// Σ over gx partial rows; zero_after: reset the rows read (persistent, reusable stats buffers)
 __device__ __forceinline__ bool sum_partials(const float* __restrict__ p0, const float* __restrict__ p1, int gx, int C,
-                                             double& s, double& q) {
+                                             double& s, double& q, bool zero_after = false) {
   __shared__ double L0[kFinGroups][kFinCh], L1[kFinGroups][kFinCh];
   const int lc = threadIdx.x % kFinCh, grp = threadIdx.x / kFinCh;
   const int c = blockIdx.x * kFinCh + lc;
@@ -156,6 +157,12 @@ __device__ __forceinline__ bool sum_partials(const float* __restrict__ p0, const
     for (int i = grp; i < gx; i += kFinGroups) {
       a += p0[(long long)i * C + c];
       b += p1[(long long)i * C + c];
+    }
+    if (zero_after) {
+      for (int i = grp; i < gx; i += kFinGroups) {
+        const_cast<float*>(p0)[(long long)i * C + c] = 0.f;
+        const_cast<float*>(p1)[(long long)i * C + c] = 0.f;
+      }
     }
   }
   L0[grp][lc] = a;
@@ -176,9 +183,10 @@ __global__ void __launch_bounds__(1024)
     bn_finalize_fwd(const float* __restrict__ p0, const float* __restrict__ p1, int gx, long long M, int C,
                     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ mmean,
                     float* __restrict__ mvar, float decay, float eps, float* __restrict__ mean_out,
-                    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift) {
+                    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift,
+                    int zero_after) {
   double s, q;
-  if (!sum_partials(p0, p1, gx, C, s, q)) return;
+  if (!sum_partials(p0, p1, gx, C, s, q, zero_after != 0)) return;
   const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
   double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
@@ -316,7 +324,7 @@ MDTF_EXPORT int mdtf_bn_fwd_train(const void* x, const void* res, void* y, long 
   hipLaunchKernelGGL((bn_reduce_kernel<false, false>), dim3(g.gx, g.gy), dim3(kThreads), lds, st,
                      (const bf16_t*)x, nullptr, nullptr, M, C, g.tpr, g.rg, p0, p1);
   hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, p0, p1, g.gx, M, C, gamma, beta,
-                     mmean, mvar, decay, eps, mean, invstd, scale, shift);
+                     mmean, mvar, decay, eps, mean, invstd, scale, shift, 0);
   long long n8 = M * C / 8;
   const bf16_t* r = (const bf16_t*)res;
   if (r && relu)
@@ -344,8 +352,9 @@ MDTF_EXPORT int mdtf_bn_fwd_stats(const void* x, const void* res, void* y, long 
   if (C % 8) return MDTF_EINVAL;
   float* scale = ws;
   float* shift = ws + C;
+  // the conv-epilogue partials live in a persistent buffer: re-zero it for the next conv
   hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M,
-                     C, gamma, beta, mmean, mvar, decay, eps, mean, invstd, scale, shift);
+                     C, gamma, beta, mmean, mvar, decay, eps, mean, invstd, scale, shift, 1);
   long long n8 = M * C / 8;
   const bf16_t* r = (const bf16_t*)res;
   if (r && relu)

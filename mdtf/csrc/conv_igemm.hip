@@ -642,36 +642,52 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
     }
   }
 
-  // ---- epilogue (same as v1): bf16 stores + optional BN statistics
+  // ---- epilogue: the C tile goes through LDS ([px][ch], rows padded by 16 B) so the
+  // global stores are 16 B per lane along full output rows; BN statistics from the
+  // fp32 accumulators (16-lane shuffles, then one atomic per channel per block)
+  constexpr int LDC = BN * 2 + 16;
+  static_assert(BM * LDC <= STAGES * STAGE, "C tile must fit the stage buffers");
   const int g = lane >> 4, li = lane & 15;
-  float ssum[TN][4], ssq[TN][4];
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) ssum[j][r] = ssq[j][r] = 0.f;
+  __syncthreads();                           // every wave is done reading the stage buffers
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const long long m = m0 + wm * (TM * 16) + i * 16 + li;
-    const bool mok = m < a.M;
+    const int pl = wm * (TM * 16) + i * 16 + li;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * (TN * 16) + j * 16 + 4 * g;
-      if (mok && n < a.Ncol) {
-        float4v v = acc[i][j];
-        uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>(a.out + m * a.Ncol + n) = make_uint2(lo, hi);
-        if (STATS) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            ssum[j][r] += v[r];
-            ssq[j][r] += v[r] * v[r];
-          }
-        }
-      }
+      const int cl = wn * (TN * 16) + j * 16 + 4 * g;
+      float4v v = acc[i][j];
+      uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(smem_raw + pl * LDC + cl * 2) = make_uint2(lo, hi);
     }
   }
+  __syncthreads();
+  for (int idx = tid; idx < BM * (BN / 8); idx += NT) {
+    const int row = idx / (BN / 8), c8 = idx - row * (BN / 8);
+    const long long m = m0 + row;
+    const int n = n0 + c8 * 8;
+    if (m < a.M && n < a.Ncol)
+      *reinterpret_cast<uint4*>(a.out + m * a.Ncol + n) = *reinterpret_cast<const uint4*>(smem_raw + row * LDC + c8 * 16);
+  }
   if (STATS) {
+    float ssum[TN][4], ssq[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ssum[j][r] = ssq[j][r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const bool mok = m0 + wm * (TM * 16) + i * 16 + li < a.M;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        if (mok) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            ssum[j][r] += acc[i][j][r];
+            ssq[j][r] += acc[i][j][r] * acc[i][j][r];
+          }
+        }
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -682,7 +698,7 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
           ssq[j][r] += __shfl_xor(ssq[j][r], o, 64);
         }
       }
-    __syncthreads();
+    __syncthreads();                         // the C tile copy-out is done with the LDS
     float* red = reinterpret_cast<float*>(smem_raw);
     if (li == 0) {
 #pragma unroll
@@ -698,14 +714,14 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
     for (int nl = tid; nl < BN; nl += NT) {
       const int n = n0 + nl;
       if (n < a.Ncol) {
-        float s = 0.f, q = 0.f;
+        float sv = 0.f, q = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) {
-          s += red[w * BN + nl];
+          sv += red[w * BN + nl];
           q += red[WM * BN + w * BN + nl];
         }
         const long long slot = (long long)(mt & (kStatSlots - 1)) * a.Ncol + n;
-        atomicAdd(a.stat_sum + slot, s);
+        atomicAdd(a.stat_sum + slot, sv);
         atomicAdd(a.stat_sq + slot, q);
       }
     }
@@ -742,6 +758,207 @@ int dispatch_fd_v2(ConvArgs& a, int bm, int bn, int stages, hipStream_t st) {
   if (stages == 3) return dispatch_fd_v2s<MODE, STATS, 3>(a, bm, bn, st);
   if (stages == 4) return dispatch_fd_v2s<MODE, STATS, 4>(a, bm, bn, st);
   return MDTF_EUNSUPPORTED;
+}
+
+// ============================================================================
+// v2 wgrad (Cin % 64 == 0, Cout % 64 == 0): DW[r=(kh,kw,ci)][co] += sum_m X[m; r] DY[m][co]
+// K = output pixels in steps of 64.  Both operands are k-strided (row = pixel),
+// so the LDS images are [64 pixel rows][64 channels] half-tiles filled by
+// LDS-DMA, and fragments are read with ds_read_b64_tr_b16 (CDNA4 transposed
+// read, 4 pixels x 16 channels per 16-lane group).  Chunk swizzle for the tr
+// reads: 16-B chunk c of row k lives at c ^ 2 f(k), f(k) = ((k>>1)&1) | ((k>>3)&1)<<1,
+// which puts the 8 rows a 32-lane half reads at 8 distinct 32-B bank slots.
+// Each lane walks two pixel rows (k and k + 32 of every step) incrementally; the
+// split-K partial tiles accumulate into DW with fp32 atomics (16 consecutive
+// co per 16-lane group).
+// ============================================================================
+__device__ __forceinline__ int trswz(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
+
+// fragment (16 cols x 32 k) of a [64 k][64 col] half-image: lane l -> col (l&15), k = 8*(l>>4) .. +7
+__device__ __forceinline__ bf16x8_t frag_tr(const char* img, int col0, int kbase, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int c = col0 + 4 * p;                       // first of this lane's 4 columns
+  const int k1 = kbase + 8 * g + q, k2 = k1 + 4;
+  const char* a1 = img + k1 * 128 + (((c >> 3) ^ trswz(k1)) << 4) + (c & 7) * 2;
+  const char* a2 = img + k2 * 128 + (((c >> 3) ^ trswz(k2)) << 4) + (c & 7) * 2;
+  v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a1);
+  v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a2);
+  short8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, f);
+}
+
+template <int BM, int BN, int STAGES>
+__global__ void __launch_bounds__(NT) conv_wgrad_v2(ConvArgs a) {
+  constexpr int WM = 2, WN = 2;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int HA = BM / 64, HB = BN / 64;       // 64-column half-images per operand
+  constexpr int IA = HA * 2, IB = HB * 2;         // DMA instructions per wave per stage
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int PER_STAGE = IA + IB;
+  constexpr unsigned OOB = 0x80000000u;
+  static_assert(HA >= 1 && HB >= 1, "tile too small");
+  static_assert(STAGES >= 2 && (STAGES - 2) * PER_STAGE < 64, "pipeline depth");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_mn = a.mtiles * a.ntiles;
+  const int tile = blockIdx.x % tiles_mn;
+  const int split = blockIdx.x / tiles_mn;
+  const int mt = tile / a.ntiles, nt = tile % a.ntiles;
+  const int r0 = mt * BM, n0 = nt * BN;
+  const int R = a.KH * a.KW * a.Cin;
+  const long long Mpix = a.M;
+  const int KT_total = static_cast<int>((Mpix + 63) / 64);
+  const int kt_begin = split * a.ksplit_steps;
+  const int kt_end = min(KT_total, kt_begin + a.ksplit_steps);
+  if (kt_begin >= kt_end) return;
+
+  const int bytes_x = (int)((long long)a.N * a.H * a.W * a.Cin * 2);
+  const int bytes_dy = (int)(Mpix * a.Cout * 2);
+
+  // A half h: rows r0 + 64h .. +63 lie in one tap (Cin % 64 == 0)
+  int h_dy[HA], h_dx[HA], h_c[HA];
+  bool h_ok[HA];
+#pragma unroll
+  for (int h = 0; h < HA; ++h) {
+    const int r = r0 + 64 * h;
+    h_ok[h] = r < R;
+    const int rr = h_ok[h] ? r : 0;
+    const int t = rr / a.Cin;
+    h_c[h] = rr - t * a.Cin;
+    const int kh = t / a.KW, kw = t - kh * a.KW;
+    h_dy[h] = kh * a.DH - a.PH;
+    h_dx[h] = kw * a.DW - a.PW;
+  }
+  // this lane's two pixel rows per step: k = 8*wave + (lane>>3) and k + 32
+  const int krow0 = 8 * wave + (lane >> 3);
+  const int gch[2] = {((lane & 7) ^ trswz(krow0)) * 8, ((lane & 7) ^ trswz(krow0 + 32)) * 8};
+  int p_ow[2], p_oh[2], p_n[2];
+  long long p_m[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const long long m = (long long)kt_begin * 64 + krow0 + 32 * u;
+    p_m[u] = m;
+    p_ow[u] = static_cast<int>(m % a.OW);
+    const long long t = m / a.OW;
+    p_oh[u] = static_cast<int>(t % a.OH);
+    p_n[u] = static_cast<int>(t / a.OH);
+  }
+  const int d_ow = 64 % a.OW, d_oh = (64 / a.OW) % a.OH, d_n = 64 / (a.OW * a.OH);
+
+  auto stage = [&](int buf) {
+    char* lds = smem_raw + buf * STAGE;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool mok = p_m[u] < Mpix;
+      const int iy0 = p_oh[u] * a.SH, ix0 = p_ow[u] * a.SW;
+      // A halves: X[n, iy, ix, c + chunk]
+#pragma unroll
+      for (int h = 0; h < HA; ++h) {
+        const int iy = iy0 + h_dy[h], ix = ix0 + h_dx[h];
+        const bool ok = mok && h_ok[h] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+        const unsigned voff =
+            ok ? (unsigned)((((p_n[u] * a.H + iy) * a.W + ix) * a.Cin + h_c[h] + gch[u]) * 2) : OOB;
+        // instruction slot: half h, row block (wave + 4u) -> LDS rows 8*(wave+4u) ..
+        dma16(a.src, bytes_x, lds + h * 8192 + (wave + 4 * u) * 1024, voff, 0);
+      }
+      // B halves: DY[m, n0 + 64h + chunk]
+      char* ldsb = lds + BM * 128;
+#pragma unroll
+      for (int h = 0; h < HB; ++h) {
+        const int co = n0 + 64 * h;
+        const unsigned voff = (mok && co < a.Cout) ? (unsigned)((p_m[u] * a.Cout + co + gch[u]) * 2) : OOB;
+        dma16(a.dy, bytes_dy, ldsb + h * 8192 + (wave + 4 * u) * 1024, voff, 0);
+      }
+      // advance this row by 64 pixels
+      p_m[u] += 64;
+      p_ow[u] += d_ow;
+      int c1 = p_ow[u] >= a.OW;
+      p_ow[u] -= c1 ? a.OW : 0;
+      p_oh[u] += d_oh + c1;
+      int c2 = p_oh[u] >= a.OH;
+      p_oh[u] -= c2 ? a.OH : 0;
+      p_n[u] += d_n + c2;
+    }
+  };
+
+  float4v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = kt_end - kt_begin;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < KT) stage(s);
+  int cur = 0;
+  for (int kt = 0; kt < KT; ++kt) {
+    if (kt + STAGES - 2 < KT)
+      wait_vmcnt<(STAGES - 2) * PER_STAGE>();
+    else
+      wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    {
+      const int nk = kt + STAGES - 1;
+      if (nk < KT) stage(nk % STAGES);
+    }
+    const char* As = smem_raw + cur * STAGE;
+    const char* Bs = As + BM * 128;
+    cur = cur + 1 == STAGES ? 0 : cur + 1;
+#pragma unroll
+    for (int kh2 = 0; kh2 < 2; ++kh2) {
+      bf16x8_t fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wm * (TM * 16) + i * 16;           // column within the BM tile
+        fa[i] = frag_tr(As + (col >> 6) * 8192, col & 63, 32 * kh2, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * (TN * 16) + j * 16;
+        fb[j] = frag_tr(Bs + (col >> 6) * 8192, col & 63, 32 * kh2, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
+    }
+  }
+  const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int co = n0 + wn * (TN * 16) + j * 16 + li;
+      if (co >= a.Cout) continue;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int r = r0 + wm * (TM * 16) + i * 16 + 4 * g + rr;
+        if (r < R) atomicAdd(a.dw + (long long)r * a.Cout + co, acc[i][j][rr]);
+      }
+    }
+}
+
+template <int BM, int BN, int STAGES>
+int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
+  const int R = a.KH * a.KW * a.Cin;
+  a.mtiles = static_cast<int>(ceil_div(R, BM));
+  a.ntiles = static_cast<int>(ceil_div(a.Cout, BN));
+  const int kt_total = static_cast<int>(ceil_div(a.M, 64));
+  if (splits < 1) {
+    const int tiles = a.mtiles * a.ntiles;
+    splits = (1024 + tiles - 1) / tiles;
+  }
+  if (splits > kt_total) splits = kt_total;
+  a.ksplit_steps = (kt_total + splits - 1) / splits;
+  splits = (kt_total + a.ksplit_steps - 1) / a.ksplit_steps;
+  const size_t lds = STAGES * (size_t)(BM + BN) * 128;
+  hipLaunchKernelGGL((conv_wgrad_v2<BM, BN, STAGES>), dim3(a.mtiles * a.ntiles * splits), dim3(NT), lds, st, a);
+  MDTF_LAUNCH_CHECK();
+  return 0;
 }
 
 template <int BM, int BN, int MODE, bool STATS>
@@ -908,4 +1125,28 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
   const int stages = bm / 1000 ? bm / 1000 : 2;
   bm %= 1000;
   return dispatch_fd_v2<1, false>(a, bm, bn, stages, st);
+}
+
+// v2 wgrad (Cin % 64 == 0, Cout % 64 == 0): DW (fp32, HWIO, zeroed or a grad slot) += wgrad(X, DY)
+// bm encodes stages * 1000 + tile rows
+MDTF_EXPORT int mdtf_conv_wgrad_v2(const void* x, const void* dy, float* dw, int N, int H, int W, int Cin, int OH,
+                                   int OW, int Cout, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW,
+                                   int bm, int bn, int splits, hipStream_t st) {
+  if (Cin % 64 || Cout % 64) return MDTF_EINVAL;
+  if ((long long)N * H * W * Cin * 2 > 0x7fffffffLL || (long long)N * OH * OW * Cout * 2 > 0x7fffffffLL)
+    return MDTF_EUNSUPPORTED;
+  ConvArgs a = make_args(N, H, W, Cin, OH, OW, Cout, KH, KW, SH, SW, PH, PW, DH, DW);
+  a.src = (const bf16_t*)x;
+  a.dy = (const bf16_t*)dy;
+  a.dw = dw;
+  a.M = (long long)N * OH * OW;
+  a.Ncol = Cout;
+  const int stages = bm / 1000 ? bm / 1000 : 2;
+  bm %= 1000;
+#define WG2(BM_, BN_, S_) \
+  if (bm == BM_ && bn == BN_ && stages == S_) return launch_wgrad_v2<BM_, BN_, S_>(a, splits, st);
+  WG2(128, 128, 2) WG2(128, 128, 3) WG2(128, 64, 2) WG2(128, 64, 3) WG2(64, 128, 2) WG2(64, 128, 3)
+  WG2(64, 64, 2) WG2(64, 64, 3) WG2(64, 64, 4)
+#undef WG2
+  return MDTF_EUNSUPPORTED;
 }

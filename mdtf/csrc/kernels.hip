@@ -463,6 +463,44 @@ __global__ void transpose_kernel(const T* __restrict__ in, T* __restrict__ out, 
     if (s0 + s < S && r0 + tx < R) dst[(long long)(s0 + s) * R + r0 + tx] = tile[tx][s];
 }
 
+// bf16 [B, R, S] -> [B, S, R] in 64x64 tiles, 16-B global accesses on both sides:
+// each thread loads 2 x 8 consecutive s of one r row, the tile is stored
+// transposed in LDS (pad 1 column per 64: conflict-light scalar writes), then
+// each thread emits 2 x 8 consecutive r of one s row.  Requires R % 8 == S % 8 == 0.
+__global__ void __launch_bounds__(256) transpose16_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                          int R, int S) {
+  __shared__ uint16_t tile[64][66];   // [s][r]
+  const int b = blockIdx.z;
+  const int r0 = blockIdx.y * 64, s0 = blockIdx.x * 64;
+  const uint16_t* src = in + (long long)b * R * S;
+  uint16_t* dst = out + (long long)b * R * S;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = t + h * 256;           // 512 chunks: 64 rows x 8 chunks
+    const int rr = idx >> 3, sc = (idx & 7) * 8;
+    if (r0 + rr < R && s0 + sc < S) {
+      uint4 v = *reinterpret_cast<const uint4*>(src + (long long)(r0 + rr) * S + s0 + sc);
+      const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) tile[sc + k][rr] = e[k];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = t + h * 256;
+    const int ss = idx >> 3, rc = (idx & 7) * 8;
+    if (s0 + ss < S && r0 + rc < R) {
+      uint4 v;
+      uint16_t* e = reinterpret_cast<uint16_t*>(&v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e[k] = tile[ss][rc + k];
+      *reinterpret_cast<uint4*>(dst + (long long)(s0 + ss) * R + r0 + rc) = v;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- LRN (cross-channel)
 __global__ void lrn_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, float* __restrict__ dsave, long long P,
                         int C, int r, float bias, float alpha, float beta) {
@@ -641,7 +679,9 @@ MDTF_EXPORT int mdtf_xent_bwd(const void* logits, int is_bf16, const long long* 
 // elem_bytes: 2 (bf16/fp16) or 4 (fp32)
 MDTF_EXPORT int mdtf_transpose_brs(const void* in, void* out, int B, int R, int S, int elem_bytes, hipStream_t st) {
   dim3 grid(ceil_div(S, 64), ceil_div(R, 64), B);
-  if (elem_bytes == 2)
+  if (elem_bytes == 2 && R % 8 == 0 && S % 8 == 0)
+    hipLaunchKernelGGL(transpose16_kernel, grid, dim3(256), 0, st, (const uint16_t*)in, (uint16_t*)out, R, S);
+  else if (elem_bytes == 2)
     hipLaunchKernelGGL(transpose_kernel<uint16_t>, grid, dim3(kT), 0, st, (const uint16_t*)in, (uint16_t*)out, R, S);
   else if (elem_bytes == 4)
     hipLaunchKernelGGL(transpose_kernel<uint32_t>, grid, dim3(kT), 0, st, (const uint32_t*)in, (uint32_t*)out, R, S);

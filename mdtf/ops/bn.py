@@ -42,6 +42,8 @@ class _BNTrain(torch.autograd.Function):
                                               N.ptr(mv), float(decay), float(eps), int(relu), N.ptr(mean),
                                               N.ptr(invstd), N.ptr(psum), N.ptr(psq), int(P), N.ptr(ws),
                                               N.stream_ptr()), "bn_fwd_stats")
+            from . import conv as _conv
+            _conv.stats_consumed(x.device)           # the finalize kernel re-zeroed the partials
         else:
             ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
             N.check(N.fn("mdtf_bn_fwd_train")(N.ptr(x), N.ptr(res), N.ptr(y), M, C, N.ptr(g), N.ptr(b), N.ptr(mm),

@@ -23,6 +23,7 @@ N.register("mdtf_conv_dgrad", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
 N.register("mdtf_conv_wgrad", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 N.register("mdtf_conv_fwd_v2", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 17 + [N.P, N.P])
 N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
+N.register("mdtf_conv_wgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 TABLE_PATH = os.path.join(_HERE, "conv_table.json")
@@ -58,6 +59,8 @@ def v2_ok(pass_, c, co, stride=(1, 1), taps=1):
         return c % 64 == 0 and co % 8 == 0
     if pass_ == "dgrad":
         return co % 64 == 0 and c % 8 == 0 and tuple(stride) == (1, 1)
+    if pass_ == "wgrad":
+        return c % 64 == 0 and co % 64 == 0
     return False
 
 
@@ -80,7 +83,8 @@ def choose(pass_, x_shape, w_shape, stride, pads, dil):
         return ("mdtf", ent["bm"], ent["bn"], ent.get("splits", 0), ent.get("ver", 1), ent.get("stages", 2))
     if pass_ == "wgrad":
         r = kh * kw * ci
-        return ("mdtf", 128 if r >= 128 else 64, 128 if co % 128 == 0 else 64, 0, 1, 2)
+        ver = 2 if (forced in ("auto", "mdtf2") and v2_ok(pass_, c, co, stride, kh * kw)) else 1
+        return ("mdtf", 128 if r >= 128 else 64, 128 if co % 128 == 0 else 64, 0, ver, 2)
     ncol = co if pass_ == "fwd" else ci
     bm, bn = _default_tile(ncol)
     ver = 2 if (forced in ("auto", "mdtf2") and v2_ok(pass_, c, co, stride, kh * kw)) else 1
@@ -181,11 +185,16 @@ def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn, ver=1, stages=2):
     return dx
 
 
-def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None):
+def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=1, stages=2):
     """fp32 HWIO weight gradient; accumulates into ``out`` when given (must be zeroed or a grad slot)."""
     dw = torch.zeros(w_shape, dtype=torch.float32, device=x.device) if out is None else out
     n, h, wd, c = x.shape
     kh, kw, ci, co = w_shape
+    if ver == 2:
+        N.check(N.fn("mdtf_conv_wgrad_v2")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co,
+                                           kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
+                                           bm + 1000 * stages, bn, int(splits), N.stream_ptr()), "conv_wgrad_v2")
+        return dw
     N.check(N.fn("mdtf_conv_wgrad")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co, kh,
                                     kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1], bm, bn, int(splits),
                                     N.stream_ptr()), "conv_wgrad")
@@ -198,11 +207,37 @@ def _pads_ok(pads):
 
 
 STAT_SLOTS = 64   # atomic partial rows of the fused BN statistics (csrc/conv_igemm.hip kStatSlots)
+_STATS = {}       # device -> [flat fp32 buffer, dirty]: persistent, re-zeroed by the BN finalize kernel
+
+
+def _stats_buffer(co, device):
+    """Zeroed [2, STAT_SLOTS, co] partial-sum buffer for a conv epilogue.
+
+    One persistent buffer per device: the following BatchNorm's finalize
+    kernel reads and re-zeroes it (``bn_fwd_stats``), so no fill kernel runs per
+    conv.  If a previous conv's statistics were never consumed, zero it here.
+    """
+    ent = _STATS.get(device)
+    need = 2 * STAT_SLOTS * co
+    if ent is None or ent[0].numel() < need:
+        ent = [torch.zeros(max(need, 2 * STAT_SLOTS * 2048), dtype=torch.float32, device=device), False]
+        _STATS[device] = ent
+    if ent[1]:
+        ent[0].zero_()
+    ent[1] = True
+    return ent[0][:need].view(2, STAT_SLOTS, co)
+
+
+def stats_consumed(device):
+    ent = _STATS.get(device)
+    if ent is not None:
+        ent[1] = False
 
 
 class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, pads, dil, out_hw, want_stats):
+        ctx.set_materialize_grads(False)      # no zero-filled grads for the (non-differentiable) stats outputs
         x = x.contiguous()
         w = w.contiguous()
         ch = choose("fwd", x.shape, w.shape, stride, pads, dil)
@@ -210,7 +245,7 @@ class _Conv(torch.autograd.Function):
         if ch[0] == "mdtf":
             if want_stats:
                 co = w.shape[3]
-                buf = torch.zeros((2, STAT_SLOTS, co), dtype=torch.float32, device=x.device)
+                buf = _stats_buffer(co, x.device)
                 stats = (buf[0], buf[1])
             y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2], stats, ch[4], ch[5])
         else:
@@ -231,6 +266,8 @@ class _Conv(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, *unused):
         x, w = ctx.saved_tensors
+        if dy is None:
+            return None, None, None, None, None, None, None
         stride, pads, dil = ctx.args
         dy = dy.contiguous()
         need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
@@ -255,10 +292,11 @@ class _Conv(torch.autograd.Function):
         if need_dw and not lib_dw:
             if sink is not None:
                 # fp32 atomics of the wgrad kernel accumulate into the flat gradient buffer
-                mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], out=sink.grad)
+                mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], out=sink.grad, ver=cw[4],
+                           stages=cw[5])
                 dw = V.grad_marker(w)
             else:
-                dw = mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3])
+                dw = mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], ver=cw[4], stages=cw[5])
                 if dw.dtype != ctx.w_dtype:
                     dw = dw.to(ctx.w_dtype)
         return dx, dw, None, None, None, None, None

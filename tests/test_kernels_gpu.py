@@ -565,3 +565,29 @@ def test_colsum_kernel(M, C):
     K.colsum_into(x.to(DEV).bfloat16(), out)
     ref = x.bfloat16().float().sum(0) + 1
     assert _rel(out.cpu(), ref) < 1e-4
+
+
+@pytest.mark.parametrize("B,R,S", [(2, 72, 200), (1, 4608, 512), (3, 8, 64)])
+def test_transpose16(B, R, S):
+    from mdtf.ops import kernels
+    x = torch.randn(B, R, S).bfloat16()
+    y = kernels.transpose_brs(x.to(DEV), B, R, S)
+    assert torch.equal(y.cpu(), x.transpose(1, 2))
+
+
+def test_conv_stats_buffer_reuse(monkeypatch):
+    """Back-to-back fused conv->BN layers share the persistent, kernel-re-zeroed statistics buffer."""
+    monkeypatch.setenv("MDTF_CONV", "mdtf2")
+    torch.manual_seed(9)
+    x = torch.randn(4, 8, 8, 64)
+    ws = [torch.randn(3, 3, 64, 64) * 0.05 for _ in range(3)]
+    outs = {}
+    for dev, dt in ((DEV, torch.bfloat16), ("cpu", torch.float32)):
+        h = x.to(dev).to(dt)
+        for w in ws:
+            g = torch.ones(64, device=dev)
+            b = torch.zeros(64, device=dev)
+            h = ops.conv_bn(h, w.to(dev).to(dt), g, b, torch.zeros(64, device=dev), torch.ones(64, device=dev),
+                            strides=1, padding="SAME", relu=True)
+        outs[dev] = h.float().cpu()
+    assert _rel(outs[DEV], outs["cpu"]) < 3e-2
