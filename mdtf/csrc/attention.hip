@@ -1,0 +1,483 @@
+// Fused multi-head attention for BERT-style encoders on bf16 MFMA (gfx950).
+//
+// BASELINE config "BERT-base data-parallel (MFMA bf16 GEMM + fused Adam)": the
+// attention core softmax(Q K^T * scale + mask) V of every (batch, head) runs as
+// ONE workgroup that reads Q/K/V straight out of the fused QKV projection
+// output [B*S, 3H] and writes the context straight into [B*S, H] (the layout
+// the output projection consumes) -- no permute copies, no [B, heads, S, S]
+// score tensor in HBM.  Sequence length 128, head dim 64 (BERT-base/large).
+//
+// Forward (per workgroup = (b, h), 4 waves, wave w owns queries 32w..32w+31):
+//   * K and V head slices ([128][64] bf16) -> LDS by LDS-DMA (buffer_load ... lds);
+//     Q fragments straight to registers;
+//   * S^T = K Q^T on v_mfma_f32_16x16x32_bf16 (lane owns one query column);
+//   * scale + additive key mask, softmax over keys (in-lane over 32 values, then
+//     2 cross-lane shuffles), attention dropout (counter-hash RNG, regenerated
+//     identically in backward), logsumexp saved per query;
+//   * O^T = V^T P^T with P^T fed from registers (bf16) as the B operand and V^T
+//     read with ds_read_b64_tr_b16 (hardware transpose) -- the key order of the two
+//     operands is permuted identically, which the k-reduction does not see.
+// Backward (one workgroup per (b, h), 144 KiB LDS):
+//   phase 1 (wave = 32 queries): recompute P from the saved logsumexp,
+//     dP = dO V^T, D = rowsum(dO * O), dS = P (dP - D); P_drop and dS go to LDS
+//     as [q][k] images;
+//   phase 2 (wave = 32 keys for dK/dV, 32 queries for dQ):
+//     dV = P_drop^T dO, dK = scale dS^T Q, dQ = scale dS K, all operands from LDS
+//     (row reads or transposed reads), written into dQKV [B*S, 3H] directly.
+// LDS images use XOR chunk swizzles chosen per access pattern so the 16-row
+// ds_read_b128 and the 8-row transposed reads are (near) conflict-free.
+#include "mdtf_common.h"
+
+using namespace mdtf;
+
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+constexpr int S = 128;   // sequence length (keys = queries)
+constexpr int D = 64;    // head dim
+constexpr int NT = 256;
+
+// 16-B chunk swizzles (involutions): logical chunk c of row r sits at physical chunk swz(r, c)
+struct SwzA {    // 128-B rows read 16 rows at a time with ds_read_b128
+  __device__ static int f(int r, int c) { return c ^ ((r >> 1) & 7); }
+};
+struct SwzT {    // 128-B rows read transposed, rows {8g+q} / {8g+4+q}
+  __device__ static int f(int r, int c) { return c ^ ((((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1); }
+};
+struct SwzV {    // 128-B rows read transposed, rows {4g+q} / {16+4g+q}
+  __device__ static int f(int r, int c) { return c ^ (((r >> 1) & 3) << 1); }
+};
+struct Swz256 {  // 256-B rows ([q][k] images): transposed reads rows {8g+q}/{8g+4+q}, and row reads
+  __device__ static int f(int r, int c) { return c ^ (((r & 3) | (((r >> 3) & 1) << 2)) << 1); }
+};
+
+__device__ __forceinline__ float4v mfma(const bf16x8_t& a, const bf16x8_t& b, const float4v& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+// keep bit of attention-dropout element (bh, q, k)
+__device__ __forceinline__ bool keep_elem(uint32_t seed, int bh, int q, int k, uint32_t thr) {
+  const uint32_t idx = ((uint32_t)bh * S + (uint32_t)q) * S + (uint32_t)k;
+  return hash_u32(idx * 0x9E3779B1u ^ seed) >= thr;
+}
+
+// DMA a [128 rows][64 cols] bf16 slice (row r at elements row0 + r * ld) into a 16 KiB image
+template <class SW>
+__device__ __forceinline__ void load_head(const bf16_t* t, int tbytes, long long row0, int ld, char* img, int wave,
+                                          int lane) {
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const int j = wave + 4 * jj;                  // 8-row block
+    const int r = 8 * j + (lane >> 3);
+    const int c = SW::f(r, lane & 7);             // logical chunk this lane's LDS slot holds
+    const unsigned voff = (unsigned)((row0 + (long long)r * ld + c * 8) * 2);
+    dma16(t, tbytes, img + j * 1024, voff, 0);
+  }
+}
+
+// row-read fragment (16 rows x 32 k) of a 128-B-row image: lane -> row r0 + (l & 15), k chunk c0 + (l >> 4)
+template <class SW>
+__device__ __forceinline__ bf16x8_t row_frag(const char* img, int r0, int c0, int lane) {
+  const int r = r0 + (lane & 15);
+  const int c = c0 + (lane >> 4);
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(img + r * 128 + (SW::f(r, c) << 4)));
+}
+
+// same for a 256-B-row image
+template <class SW>
+__device__ __forceinline__ bf16x8_t row_frag256(const char* img, int r0, int c0, int lane) {
+  const int r = r0 + (lane & 15);
+  const int c = c0 + (lane >> 4);
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(img + r * 256 + (SW::f(r, c) << 4)));
+}
+
+// one ds_read_b64_tr_b16: rows r..r+3 of the lane's 16-lane group block, columns col0 + 4p
+template <class SW, int ROWB>
+__device__ __forceinline__ v4s tr4(const char* img, int r, int col) {
+  const char* p = img + r * ROWB + (SW::f(r, col >> 3) << 4) + (col & 7) * 2;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p);
+}
+
+// transposed fragment: lane -> column col0 + (l & 15), k rows kb + 8g + (0..3) and kb + 8g + 4 + (0..3)
+template <class SW, int ROWB>
+__device__ __forceinline__ bf16x8_t tr_frag(const char* img, int kb, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  v4s lo = tr4<SW, ROWB>(img, kb + 8 * g + q, col0 + 4 * p);
+  v4s hi = tr4<SW, ROWB>(img, kb + 8 * g + 4 + q, col0 + 4 * p);
+  short8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, f);
+}
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ bf16x8_t load_frag_global(const bf16_t* p) {
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p));
+}
+
+// ============================================================================ forward
+__global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+                                                      bf16_t* __restrict__ out, float* __restrict__ lse_out, int B,
+                                                      int nh, float scale, float p_drop, uint32_t seed) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * S * D * 2];
+  char* Kimg = smem;
+  char* Vimg = smem + S * D * 2;
+  const int bh = blockIdx.x, b = bh / nh, h = bh - b * nh;
+  const int H = nh * D, ld = 3 * H;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const long long row0 = (long long)b * S * ld;
+  const int tbytes = (int)((long long)B * S * ld * 2);
+
+  load_head<SwzA>(qkv, tbytes, row0 + H + h * D, ld, Kimg, wave, lane);
+  load_head<SwzV>(qkv, tbytes, row0 + 2 * H + h * D, ld, Vimg, wave, lane);
+  bf16x8_t qf[2][2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) {
+      const int q = 32 * wave + 16 * qt + li;
+      qf[qt][ds] = load_frag_global(qkv + row0 + (long long)q * ld + h * D + 32 * ds + 8 * g);
+    }
+  float mk[8][4];
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+    if (mask) {
+      const float4 m4 = *reinterpret_cast<const float4*>(mask + (long long)b * S + kt * 16 + 4 * g);
+      mk[kt][0] = m4.x;
+      mk[kt][1] = m4.y;
+      mk[kt][2] = m4.z;
+      mk[kt][3] = m4.w;
+    } else {
+      mk[kt][0] = mk[kt][1] = mk[kt][2] = mk[kt][3] = 0.f;
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  // S^T[k][q] = K Q^T
+  float4v sacc[8][2];
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) sacc[kt][qt] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ds = 0; ds < 2; ++ds)
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      const bf16x8_t kf = row_frag<SwzA>(Kimg, kt * 16, 4 * ds, lane);
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) sacc[kt][qt] = mfma(kf, qf[qt][ds], sacc[kt][qt]);
+    }
+
+  // softmax over keys for each query column (scale, mask), dropout, logsumexp
+  const uint32_t thr = p_drop > 0.f ? (uint32_t)fminf(p_drop * 4294967296.f, 4294967295.f) : 0u;
+  const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    float m = -3.0e38f;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float s = sacc[kt][qt][i] * scale + mk[kt][i];
+        sacc[kt][qt][i] = s;
+        m = fmaxf(m, s);
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = __expf(sacc[kt][qt][i] - m);
+        sacc[kt][qt][i] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.f / sum;
+    const int q = 32 * wave + 16 * qt + li;
+    if (g == 0) lse_out[(long long)bh * S + q] = m + __logf(sum);
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float p = sacc[kt][qt][i] * inv;
+        if (thr) p = keep_elem(seed, bh, q, kt * 16 + 4 * g + i, thr) ? p * inv_keep : 0.f;
+        sacc[kt][qt][i] = p;
+      }
+  }
+
+  // O^T[d][q] = V^T P^T ; key order inside each 32-key step: {4g..4g+3, 16+4g..16+4g+3}
+  float4v oacc[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) oacc[dt][qt] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    bf16x8_t pf[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float4v a0 = sacc[2 * ks][qt], a1 = sacc[2 * ks + 1][qt];
+      uint4 w = make_uint4(pack2(a0[0], a0[1]), pack2(a0[2], a0[3]), pack2(a1[0], a1[1]), pack2(a1[2], a1[3]));
+      pf[qt] = __builtin_bit_cast(bf16x8_t, w);
+    }
+    const int q4 = li >> 2, p4 = li & 3;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      v4s lo = tr4<SwzV, 128>(Vimg, 32 * ks + 4 * g + q4, dt * 16 + 4 * p4);
+      v4s hi = tr4<SwzV, 128>(Vimg, 32 * ks + 16 + 4 * g + q4, dt * 16 + 4 * p4);
+      short8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const bf16x8_t vf = __builtin_bit_cast(bf16x8_t, f);
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) oacc[dt][qt] = mfma(vf, pf[qt], oacc[dt][qt]);
+    }
+  }
+  // context rows [b*S + q][h*D + d]: lane holds 4 consecutive d of one query
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = 32 * wave + 16 * qt + li;
+    bf16_t* o = out + ((long long)b * S + q) * H + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const float4v v = oacc[dt][qt];
+      *reinterpret_cast<uint2*>(o + dt * 16 + 4 * g) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
+  }
+}
+
+// ============================================================================ backward
+constexpr int kBwdLds = 5 * S * D * 2 + 2 * S * S * 2;   // K_A V_A K_T Q_T dO_T | P dS  = 144 KiB
+
+__global__ void __launch_bounds__(NT) attn_bwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+                                                      const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
+                                                      const float* __restrict__ lse, bf16_t* __restrict__ dqkv, int B,
+                                                      int nh, float scale, float p_drop, uint32_t seed) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* KA = smem;
+  char* VA = KA + S * D * 2;
+  char* KT = VA + S * D * 2;
+  char* QT = KT + S * D * 2;
+  char* OT = QT + S * D * 2;
+  char* PI = OT + S * D * 2;        // P_drop [q][k]
+  char* SI = PI + S * S * 2;        // dS     [q][k]
+  const int bh = blockIdx.x, b = bh / nh, h = bh - b * nh;
+  const int H = nh * D, ld = 3 * H;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const long long row0 = (long long)b * S * ld;
+  const long long orow0 = (long long)b * S * H;
+  const int tbytes = (int)((long long)B * S * ld * 2);
+  const int obytes = (int)((long long)B * S * H * 2);
+
+  load_head<SwzA>(qkv, tbytes, row0 + H + h * D, ld, KA, wave, lane);
+  load_head<SwzA>(qkv, tbytes, row0 + 2 * H + h * D, ld, VA, wave, lane);
+  load_head<SwzT>(qkv, tbytes, row0 + H + h * D, ld, KT, wave, lane);
+  load_head<SwzT>(qkv, tbytes, row0 + h * D, ld, QT, wave, lane);
+  load_head<SwzT>(dout, obytes, orow0 + h * D, H, OT, wave, lane);
+
+  // phase-1 register operands: Q and dO fragments (B operands), D = rowsum(dO * O), lse, mask
+  bf16x8_t qf[2][2], of[2][2];
+  float Dq[2], lq[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = 32 * wave + 16 * qt + li;
+    float part = 0.f;
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) {
+      const int d = 32 * ds + 8 * g;
+      qf[qt][ds] = load_frag_global(qkv + row0 + (long long)q * ld + h * D + d);
+      of[qt][ds] = load_frag_global(dout + orow0 + (long long)q * H + h * D + d);
+      float o8[8], do8[8];
+      load_bf8(out + orow0 + (long long)q * H + h * D + d, o8);
+      load_bf8(dout + orow0 + (long long)q * H + h * D + d, do8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part += o8[e] * do8[e];
+    }
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    Dq[qt] = part;
+    lq[qt] = lse[(long long)bh * S + q];
+  }
+  float mk[8][4];
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+    if (mask) {
+      const float4 m4 = *reinterpret_cast<const float4*>(mask + (long long)b * S + kt * 16 + 4 * g);
+      mk[kt][0] = m4.x;
+      mk[kt][1] = m4.y;
+      mk[kt][2] = m4.z;
+      mk[kt][3] = m4.w;
+    } else {
+      mk[kt][0] = mk[kt][1] = mk[kt][2] = mk[kt][3] = 0.f;
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  // ---- phase 1: S^T and dP'^T = V dO^T for this wave's 32 queries
+  const uint32_t thr = p_drop > 0.f ? (uint32_t)fminf(p_drop * 4294967296.f, 4294967295.f) : 0u;
+  const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  {
+    float4v sacc[8][2], pacc[8][2];
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) sacc[kt][qt] = pacc[kt][qt] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds)
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt) {
+        const bf16x8_t kf = row_frag<SwzA>(KA, kt * 16, 4 * ds, lane);
+        const bf16x8_t vf = row_frag<SwzA>(VA, kt * 16, 4 * ds, lane);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          sacc[kt][qt] = mfma(kf, qf[qt][ds], sacc[kt][qt]);
+          pacc[kt][qt] = mfma(vf, of[qt][ds], pacc[kt][qt]);
+        }
+      }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int q = 32 * wave + 16 * qt + li;
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt) {
+        float pd[4], dsv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = kt * 16 + 4 * g + i;
+          const float p = __expf(sacc[kt][qt][i] * scale + mk[kt][i] - lq[qt]);
+          float dp = pacc[kt][qt][i];
+          float pk = p;
+          if (thr) {
+            const bool keep = keep_elem(seed, bh, q, k, thr);
+            pk = keep ? p * inv_keep : 0.f;
+            dp = keep ? dp * inv_keep : 0.f;
+          }
+          pd[i] = pk;
+          dsv[i] = p * (dp - Dq[qt]);
+        }
+        const int k0 = kt * 16 + 4 * g;
+        const int off = q * 256 + (Swz256::f(q, k0 >> 3) << 4) + (k0 & 7) * 2;
+        *reinterpret_cast<uint2*>(PI + off) = make_uint2(pack2(pd[0], pd[1]), pack2(pd[2], pd[3]));
+        *reinterpret_cast<uint2*>(SI + off) = make_uint2(pack2(dsv[0], dsv[1]), pack2(dsv[2], dsv[3]));
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2a: dV^T[d][k] = dO^T P_drop, dK^T[d][k] = scale Q^T dS for keys 32w .. 32w+31
+  {
+    float4v vacc[4][2], kacc[4][2];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) vacc[dt][kt] = kacc[dt][kt] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {          // 32 queries per step
+      bf16x8_t pf[2], sf[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        pf[kt] = tr_frag<Swz256, 256>(PI, 32 * ks, 32 * wave + 16 * kt, lane);
+        sf[kt] = tr_frag<Swz256, 256>(SI, 32 * ks, 32 * wave + 16 * kt, lane);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8_t df = tr_frag<SwzT, 128>(OT, 32 * ks, dt * 16, lane);
+        const bf16x8_t qq = tr_frag<SwzT, 128>(QT, 32 * ks, dt * 16, lane);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          vacc[dt][kt] = mfma(df, pf[kt], vacc[dt][kt]);
+          kacc[dt][kt] = mfma(qq, sf[kt], kacc[dt][kt]);
+        }
+      }
+    }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int k = 32 * wave + 16 * kt + li;
+      bf16_t* rowp = dqkv + row0 + (long long)k * ld + h * D;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const float4v kv = kacc[dt][kt], vv = vacc[dt][kt];
+        *reinterpret_cast<uint2*>(rowp + H + dt * 16 + 4 * g) =
+            make_uint2(pack2(kv[0] * scale, kv[1] * scale), pack2(kv[2] * scale, kv[3] * scale));
+        *reinterpret_cast<uint2*>(rowp + 2 * H + dt * 16 + 4 * g) =
+            make_uint2(pack2(vv[0], vv[1]), pack2(vv[2], vv[3]));
+      }
+    }
+  }
+  // ---- phase 2b: dQ^T[d][q] = scale K^T dS^T for this wave's queries
+  {
+    float4v qacc[4][2];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) qacc[dt][qt] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {          // 32 keys per step
+      bf16x8_t sf[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) sf[qt] = row_frag256<Swz256>(SI, 32 * wave + 16 * qt, 4 * ks, lane);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8_t kf = tr_frag<SwzT, 128>(KT, 32 * ks, dt * 16, lane);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) qacc[dt][qt] = mfma(kf, sf[qt], qacc[dt][qt]);
+      }
+    }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int q = 32 * wave + 16 * qt + li;
+      bf16_t* rowp = dqkv + row0 + (long long)q * ld + h * D;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const float4v v = qacc[dt][qt];
+        *reinterpret_cast<uint2*>(rowp + dt * 16 + 4 * g) =
+            make_uint2(pack2(v[0] * scale, v[1] * scale), pack2(v[2] * scale, v[3] * scale));
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// ctx[B*S, H] = attention(qkv[B*S, 3H]); lse [B*nh, S] (fp32) saved for backward
+MDTF_EXPORT int mdtf_attn_fwd(const void* qkv, const float* mask, void* out, float* lse, int B, int seq, int nh,
+                              int dh, float scale, float p_drop, unsigned seed, hipStream_t st) {
+  if (seq != S || dh != D) return MDTF_EUNSUPPORTED;
+  if ((long long)B * S * 3 * nh * D * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * nh), dim3(NT), 0, st, (const bf16_t*)qkv, mask, (bf16_t*)out, lse, B,
+                     nh, scale, p_drop, (uint32_t)seed);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// dqkv[B*S, 3H] (every element written) from dout[B*S, H]
+MDTF_EXPORT int mdtf_attn_bwd(const void* qkv, const float* mask, const void* out, const void* dout, const float* lse,
+                              void* dqkv, int B, int seq, int nh, int dh, float scale, float p_drop, unsigned seed,
+                              hipStream_t st) {
+  if (seq != S || dh != D) return MDTF_EUNSUPPORTED;
+  if ((long long)B * S * 3 * nh * D * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(B * nh), dim3(NT), kBwdLds, st, (const bf16_t*)qkv, mask,
+                     (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv, B, nh, scale, p_drop,
+                     (uint32_t)seed);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}

@@ -479,20 +479,6 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(ConvArgs a) {
 // stays lane-linear), which makes the ds_read_b128 fragment reads of 16 rows
 // conflict-free.  dgrad v2 covers stride 1 (strided dgrad: v1 / MIOpen).
 // ============================================================================
-// 16 B per lane global -> LDS (buffer_load_dwordx4 ... lds): LDS destination = wave-uniform
-// `lds` + 16 * lane; offsets at or past `nbytes` read zeros
-__device__ __forceinline__ void dma16(const void* base, int nbytes, char* lds, unsigned voff, int soff) {
-  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nbytes, 0x00020000);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
-}
-
-// s_waitcnt vmcnt(N) leaving lgkm/exp counters alone (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14)
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-
 template <int BM, int BN, int MODE, bool STATS, int STAGES>
 __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
   constexpr int WM = 2, WN = 2;

@@ -71,4 +71,18 @@ __device__ __forceinline__ void store_bf8(bf16_t* p, const float (&f)[8]) {
 
 __host__ __device__ __forceinline__ int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// 16 B per lane global -> LDS (buffer_load_dwordx4 ... lds): LDS destination = wave-uniform
+// `lds` + 16 * lane; offsets at or past `nbytes` read zeros
+__device__ __forceinline__ void dma16(const void* base, int nbytes, char* lds, unsigned voff, int soff) {
+  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nbytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
+// s_waitcnt vmcnt(N) leaving lgkm/exp counters alone (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
 }  // namespace mdtf

@@ -130,9 +130,8 @@ class Bert(Model):
                         ws.append(V.get_variable("kernel", [H, H], initializer=_init()))
                         bs.append(V.get_variable("bias", [H], initializer=V.constant_initializer(0.0)))
                 qkv = ops.dense_multi(x.reshape(-1, H), ws, bs)                               # one GEMM
-                qkv = qkv.view(B, S_, 3, nh, dh).permute(2, 0, 3, 1, 4)                     # [3, B, nh, S, dh]
-                ctx = T.attention(qkv[0], qkv[1], qkv[2], amask)
-                ctx = ctx.permute(0, 2, 1, 3).reshape(B, S_, H)
+                drop = self.dropout if S.is_training() else 0.0
+                ctx = T.fused_attention(qkv, B, S_, nh, amask, drop).reshape(B, S_, H)
             with V.variable_scope("output"):
                 a = _dense("dense", ctx, H)
                 a = _dropout(a, self.dropout)

@@ -129,3 +129,4 @@ def fn(name):
 
 
 P, I, L, F = _P, _I, _L, _F
+U = ctypes.c_uint

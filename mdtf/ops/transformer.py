@@ -19,6 +19,8 @@ N.register("mdtf_softmax_fwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.L, N.P])
 N.register("mdtf_softmax_bwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.P])
 N.register("mdtf_embed_fwd", [N.P, N.P, N.P, N.L, N.I, N.L, N.P])
 N.register("mdtf_embed_bwd", [N.P, N.P, N.P, N.L, N.I, N.L, N.P])
+N.register("mdtf_attn_fwd", [N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P])
+N.register("mdtf_attn_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P])
 
 
 def _sink_or_zeros(t, n, device):
@@ -155,13 +157,66 @@ def embedding_lookup(table, ids):
     return F.embedding(ids.long(), table)
 
 
-def attention(q, k, v, mask=None):
+def attention(q, k, v, mask=None, dropout=0.0):
     """Multi-head attention core: q, k, v [B, heads, S, d] -> [B, heads, S, d].
 
-    The two batched GEMMs run on hipBLASLt; the scaled masked softmax (and its
-    backward) on the HIP kernel.
+    Unfused path: two batched GEMMs (hipBLASLt on the GPU) around the scaled
+    masked softmax kernel; attention-probability dropout as in TF BERT.
     """
     scale = 1.0 / math.sqrt(q.shape[-1])
     scores = torch.matmul(q, k.transpose(-1, -2))
     p = masked_softmax(scores, mask, scale)
+    if dropout:
+        p = F.dropout(p, dropout, True)
     return torch.matmul(p, v)
+
+
+FUSED_SEQ, FUSED_DIM = 128, 64      # shapes csrc/attention.hip is built for
+
+
+class _FusedAttention(torch.autograd.Function):
+    """softmax(Q K^T / sqrt(d) + mask) V for all heads, straight from/to the fused QKV layout."""
+
+    @staticmethod
+    def forward(ctx, qkv, mask, B, S_, nh, p_drop, seed):
+        qkv = qkv.contiguous()
+        H = nh * FUSED_DIM
+        out = torch.empty((B * S_, H), dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty((B * nh, S_), dtype=torch.float32, device=qkv.device)
+        m = mask.float().contiguous() if mask is not None else None
+        scale = 1.0 / math.sqrt(FUSED_DIM)
+        N.check(N.fn("mdtf_attn_fwd")(N.ptr(qkv), N.ptr(m), N.ptr(out), N.ptr(lse), B, S_, nh, FUSED_DIM, scale,
+                                      float(p_drop), seed, N.stream_ptr()), "attn_fwd")
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.mask = m
+        ctx.args = (B, S_, nh, float(p_drop), seed, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        B, S_, nh, p_drop, seed, scale = ctx.args
+        dout = dout.contiguous()
+        dqkv = torch.empty_like(qkv)
+        N.check(N.fn("mdtf_attn_bwd")(N.ptr(qkv), N.ptr(ctx.mask), N.ptr(out), N.ptr(dout), N.ptr(lse), N.ptr(dqkv),
+                                      B, S_, nh, FUSED_DIM, scale, p_drop, seed, N.stream_ptr()), "attn_bwd")
+        return dqkv, None, None, None, None, None, None
+
+
+def fused_attention(qkv, batch, seq, heads, mask=None, dropout=0.0):
+    """Self-attention from the fused projection ``qkv`` [B*S, 3H] (q | k | v, heads
+    contiguous inside each) to the context [B*S, H].
+
+    GPU, S = 128, head dim 64: one fused HIP kernel per direction
+    (``csrc/attention.hip``); otherwise the unfused matmul/softmax path.
+    ``mask``: additive [B, S] key mask (0 keep, -10000 drop) or None.
+    """
+    H3 = qkv.shape[-1]
+    H = H3 // 3
+    dh = H // heads
+    if N.use_native(qkv) and seq == FUSED_SEQ and dh == FUSED_DIM and qkv.dtype == torch.bfloat16:
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if dropout else 0
+        return _FusedAttention.apply(qkv.reshape(batch * seq, H3), mask, batch, seq, heads, float(dropout), seed)
+    q, k, v = qkv.reshape(batch, seq, 3, heads, dh).unbind(2)
+    ctx = attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), mask, dropout)
+    return ctx.transpose(1, 2).reshape(batch * seq, H)

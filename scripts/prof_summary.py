@@ -5,9 +5,10 @@ import re
 import sys
 
 
-CATS = [("conv(mdtf)", r"conv_fd|conv_wgrad"), ("conv(MIOpen)", r"^(naive_conv|igemm|Cijk|MIOpen|miopen|ck_|gridwise|sp3A|kernel_batched)"),
-        ("batchnorm", r"bn_|batchnorm"), ("gemm(hipBLASLt)", r"Cijk"), ("optimizer", r"adam_kernel|sgd|momentum"),
-        ("transformer", r"ln_|softmax|embed|attn"), ("elementwise(torch)", r"at::native"),
+CATS = [("conv(mdtf)", r"conv_fd|conv_wgrad"), ("gemm(hipBLASLt)", r"Cijk"),
+        ("conv(MIOpen)", r"^(naive_conv|igemm|MIOpen|miopen|ck::|gridwise|sp3A|kernel_batched|SubTensor)"),
+        ("batchnorm", r"bn_|batchnorm"), ("optimizer", r"adam_kernel|sgd|momentum"),
+        ("attention(mdtf)", r"attn_"), ("transformer", r"ln_|softmax|embed"), ("elementwise(torch)", r"at::native"),
         ("mdtf misc", r"bias_act|act_bwd|colsum|reduce_partials|pool|gap_|xent|transpose|lrn")]
 
 

@@ -511,7 +511,7 @@ def test_bert_tiny_train_step_gpu():
     assert ls[-1] < 0.5 * ls[0], ls
 
 
-def _bert_step(dev, dt, raw, gt):
+def _bert_step(dev, dt, raw, gt, seq=32, heads_dim=None):
     import mdtf
     from mdtf.models import Bert, BertPretrainingLoss
     from mdtf.runtime import Net, Tower
@@ -527,8 +527,10 @@ def _bert_step(dev, dt, raw, gt):
     gp = mdtf.placeholder(torch.int64, [None, gt.shape[1]])
     opt = mdtf.train.GradientDescentOptimizer(0.1)
     tg = []
-    t = Tower(Net(Bert("tiny", vocab_size=512, seq_len=32, max_predictions=5, dropout=0.0)), "tower_0/", tg, rp, gp,
-              BertPretrainingLoss(5), opt, batch_size=raw.shape[0])
+    model = Bert("tiny", vocab_size=512, seq_len=seq, max_predictions=5, dropout=0.0)
+    if heads_dim:                      # tiny width, but head dim 64 (2 heads) so the fused kernel applies
+        model.heads = model.H // heads_dim
+    t = Tower(Net(model), "tower_0/", tg, rp, gp, BertPretrainingLoss(5), opt, batch_size=raw.shape[0])
     _, loss, _ = t.process()
     op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
     sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
@@ -591,3 +593,71 @@ def test_conv_stats_buffer_reuse(monkeypatch):
                             strides=1, padding="SAME", relu=True)
         outs[dev] = h.float().cpu()
     assert _rel(outs[DEV], outs["cpu"]) < 3e-2
+
+
+def _attn_keep_mask(seed, B, nh, S, p):
+    """Reproduce csrc/attention.hip's dropout keep bits (hash of (bh, q, k) and the seed)."""
+    import numpy as np
+    idx = np.arange(B * nh * S * S, dtype=np.uint64).astype(np.uint32)
+    x = (idx * np.uint32(0x9E3779B1)) ^ np.uint32(seed)
+    x ^= x >> np.uint32(16)
+    x = x * np.uint32(0x7feb352d)
+    x ^= x >> np.uint32(15)
+    x = x * np.uint32(0x846ca68b)
+    x ^= x >> np.uint32(16)
+    thr = np.uint32(min(int(p * 4294967296.0), 4294967295))
+    return torch.from_numpy((x >= thr).reshape(B, nh, S, S))
+
+
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+def test_fused_attention_fwd_bwd(p_drop):
+    from mdtf.ops import transformer as T
+    torch.manual_seed(21)
+    B, S, nh, dh = 3, 128, 4, 64
+    H = nh * dh
+    qkv = torch.randn(B * S, 3 * H) * 0.5
+    mask = (torch.rand(B, S) < 0.15).float() * -10000.0
+    seed = 1234567
+    dout = torch.randn(B * S, H)
+    # kernel
+    xg = qkv.to(DEV).bfloat16().requires_grad_(True)
+    out = T._FusedAttention.apply(xg, mask.to(DEV), B, S, nh, p_drop, seed)
+    out.backward(dout.to(DEV).bfloat16())
+    # fp32 reference with the same dropout bits
+    xr = qkv.bfloat16().float().requires_grad_(True)
+    q, k, v = xr.reshape(B, S, 3, nh, dh).unbind(2)
+    q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+    s = q @ k.transpose(-1, -2) / dh ** 0.5 + mask[:, None, None, :]
+    pr = torch.softmax(s, -1)
+    if p_drop:
+        keep = _attn_keep_mask(seed, B, nh, S, p_drop)
+        pr = pr * keep / (1 - p_drop)
+    ref = (pr @ v).transpose(1, 2).reshape(B * S, H)
+    ref.backward(dout.bfloat16().float())
+    assert _rel(out, ref) < 1.5e-2
+    g, gr = xg.grad.float().cpu(), xr.grad
+    for part in range(3):      # dq, dk, dv
+        sl = slice(part * H, (part + 1) * H)
+        assert _rel(g[:, sl], gr[:, sl]) < 3e-2, part
+
+
+def test_bert_fused_vs_unfused_attention_path(monkeypatch):
+    """BERT step: fused-attention kernel path == unfused matmul/softmax path (same weights, no dropout)."""
+    from mdtf.models import SyntheticBertLoader
+    from mdtf.ops import transformer as T
+    from mdtf.train import variables as V
+    V.get_store().device = torch.device("cpu")
+    ld = SyntheticBertLoader(seq_len=128, max_predictions=5, vocab=512, seed=4)
+    ld.batch_size = 4
+    raw, gt = ld._make()
+
+    def run(fused):
+        monkeypatch.setattr(T, "FUSED_SEQ", 128 if fused else -1)
+        return _bert_step(DEV, torch.bfloat16, raw, gt, seq=128, heads_dim=64)
+    lf, gf = run(True)
+    lu, gu = run(False)
+    assert abs(lf - lu) / lu < 1e-2
+    for k in gf:
+        if k.endswith("key/bias"):
+            continue
+        assert _rel(gf[k], gu[k]) < 0.1, (k, _rel(gf[k], gu[k]))
