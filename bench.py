@@ -22,9 +22,12 @@ import os
 import sys
 import time
 
-# Comparator (stock PyTorch-ROCm: MIOpen conv/BN, torch DDP, torch SGD) images/sec measured on
-# MI355X with bench/stock_pytorch.py at the same config; None until measured (vs_baseline null).
-BASELINE_IMAGES_PER_SEC_PER_GPU = None
+# The reference publishes no numbers; its comparator is stock PyTorch-ROCm on the
+# same MI355X (MIOpen conv/BN, torch DDP over RCCL, torch SGD, channels-last autocast bf16),
+# measured with bench/stock_pytorch.py at this config on 1 GPU: 5966.38 images/sec
+# (profiles/rocprof_resnet50_stock_torch_ops_r1.md).  vs_baseline divides by that rate x N
+# (ideal linear scaling of the comparator, i.e. a conservative ratio for N > 1).
+BASELINE_IMAGES_PER_SEC_PER_GPU = 5966.38
 
 
 def parse():
@@ -128,6 +131,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(ips / (base_ips * world), 4) if base_ips else None,
+            "baseline": "stock PyTorch-ROCm comparator, %.2f img/s/GPU x %d" % (base_ips, world) if base_ips else None,
             "dtype": "bf16", "data": "synthetic (random 224x224x3 NHWC images, random labels; random-init weights)",
             "config": {"model": "resnet%d_v1.5" % args.depth, "global_batch": args.batch * world, "seq_len": None,
                        "per_gpu_batch": args.batch, "image_size": 224, "parallelism": "dp%d" % world,

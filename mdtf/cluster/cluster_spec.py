@@ -140,6 +140,17 @@ class RankLayout(object):
     def worker_ranks(self):
         return list(range(self.worker_offset, self.worker_offset + self.num_worker_ranks))
 
+    @property
+    def num_processes(self):
+        """Every process of the job: one per PS task plus one per worker tower."""
+        return self.num_ps + self.num_worker_ranks
+
+    def process_index(self, job_name, task_index, tower=0):
+        """Dense id over ALL processes (PS tasks first) -- heartbeat ids, independent of the ps mode."""
+        if job_name == "ps":
+            return task_index
+        return self.num_ps + task_index * self.towers_per_worker + tower
+
     def ps_ranks(self):
         return list(range(self.ps_offset, self.ps_offset + self.num_ps)) if self.async_ps else []
 

@@ -84,25 +84,41 @@ def free_port(host="127.0.0.1"):
     return port
 
 
+def cluster_commands(script_argv, num_ps, num_workers, host="127.0.0.1"):
+    """argv lists of every ps/worker task of a localhost ClusterSpec (fresh ports)."""
+    ports = [free_port(host) for _ in range(num_ps + num_workers)]
+    ps_hosts = ",".join("%s:%d" % (host, p) for p in ports[:num_ps]) or "none"
+    worker_hosts = ",".join("%s:%d" % (host, p) for p in ports[num_ps:])
+    cmds = []
+    for job, n in (("ps", num_ps), ("worker", num_workers)):
+        for i in range(n):
+            cmds.append([sys.executable] + list(script_argv) + [
+                "--job_name=%s" % job, "--task_index=%d" % i,
+                "--ps_hosts=%s" % ps_hosts, "--worker_hosts=%s" % worker_hosts])
+    return cmds
+
+
 def launch_local_cluster(script_argv, num_ps, num_workers, extra_env=None, host="127.0.0.1",
-                         timeout_s=600, cwd=None):
+                         timeout_s=600, cwd=None, max_restarts=0, log_dir=None):
     """Start ``num_ps`` ps + ``num_workers`` worker tasks of ``script_argv`` locally.
 
     Every task receives ``--job_name/--task_index/--ps_hosts/--worker_hosts``.
-    Returns the list of exit codes (ps tasks first).
+    Returns the list of exit codes (ps tasks first).  With ``max_restarts > 0``
+    the job runs under :func:`mdtf.cluster.health.supervise`: a failed task
+    stops the job and the whole job is restarted (resuming from its latest
+    checkpoint), and the codes are those of the last attempt.
     """
-    ports = [free_port(host) for _ in range(num_ps + num_workers)]
-    ps_hosts = ",".join("%s:%d" % (host, p) for p in ports[:num_ps])
-    worker_hosts = ",".join("%s:%d" % (host, p) for p in ports[num_ps:])
-    procs = []
+    if max_restarts:
+        from . import health
+        codes, attempts = health.supervise(cluster_commands(script_argv, num_ps, num_workers, host),
+                                           env=extra_env, max_restarts=max_restarts, timeout_s=timeout_s, cwd=cwd,
+                                           log_dir=log_dir)
+        launch_local_cluster.last_attempts = attempts
+        return codes
     env = dict(os.environ)
     env.update(extra_env or {})
-    for job, n in (("ps", num_ps), ("worker", num_workers)):
-        for i in range(n):
-            cmd = [sys.executable] + list(script_argv) + [
-                "--job_name=%s" % job, "--task_index=%d" % i,
-                "--ps_hosts=%s" % ps_hosts, "--worker_hosts=%s" % worker_hosts]
-            procs.append(subprocess.Popen(cmd, env=env, cwd=cwd))
+    procs = [subprocess.Popen(cmd, env=env, cwd=cwd)
+             for cmd in cluster_commands(script_argv, num_ps, num_workers, host)]
     deadline = time.time() + timeout_s
     codes = []
     for p in procs:
@@ -115,3 +131,26 @@ def launch_local_cluster(script_argv, num_ps, num_workers, extra_env=None, host=
                     q.kill()
             raise
     return codes
+
+
+def main(argv=None):
+    """``python -m mdtf.cluster.launcher --num_ps 1 --num_workers 2 [--max_restarts N] script.py [args]``:
+    run a whole ps+worker job on this host, optionally supervised (restart on failure)."""
+    import argparse
+    p = argparse.ArgumentParser(description=main.__doc__)
+    p.add_argument("--num_ps", type=int, default=1)
+    p.add_argument("--num_workers", type=int, default=1)
+    p.add_argument("--max_restarts", type=int, default=0)
+    p.add_argument("--timeout_s", type=float, default=None)
+    p.add_argument("script", nargs=argparse.REMAINDER)
+    a = p.parse_args(argv)
+    if not a.script:
+        p.error("missing script")
+    codes = launch_local_cluster(a.script, a.num_ps, a.num_workers, timeout_s=a.timeout_s or 10 ** 9,
+                                 max_restarts=a.max_restarts)
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -65,6 +65,7 @@ class Server(object):
         self.rank = self.layout.rank_of(job_name, self.task_index, local_rank if job_name == "worker" else 0)
         self.world_size = self.layout.world_size
         self.worker_group = None
+        self.heartbeat = None
         self._torchrun = False
         self._started = False
         _set_current(self)
@@ -131,6 +132,8 @@ class Server(object):
         import torch.distributed as dist
         os.environ.setdefault("MDTF_RANK_TAG", "[%s:%d%s]" % (
             self.job_name, self.task_index, "/%d" % self.local_rank if self.layout.gpu_num > 1 else ""))
+        # surface RCCL errors / dead peers as exceptions instead of silent hangs
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         timeout = datetime.timedelta(seconds=self.store_timeout_s)
         if self._torchrun:
             backend = self.backend or ("nccl" if torch.cuda.is_available() else "gloo")
@@ -141,6 +144,7 @@ class Server(object):
             self.store = dist.distributed_c10d._get_default_store()
             self.worker_group = dist.group.WORLD
             self._started = True
+            self._start_heartbeat(dist.get_rank(), dist.get_world_size())
             return
         host, port = split_address(self.cluster.coordinator_address())
         self.store = dist.TCPStore(host, port, is_master=self.is_coordinator, timeout=timeout,
@@ -159,12 +163,24 @@ class Server(object):
             else:
                 self.worker_group = dist.group.WORLD
         self._started = True
+        self._start_heartbeat(self.layout.process_index(self.job_name, self.task_index,
+                                                        self.local_rank if self.job_name == "worker" else 0),
+                              self.layout.num_processes)
         logger.info("Server started: %s task %d (rank %s of %d) target %s" % (
             self.job_name, self.task_index, self.rank, self.world_size, self.target))
+
+    def _start_heartbeat(self, hb_id, hb_world):
+        from . import health
+        enabled, interval, timeout = health.heartbeat_settings()
+        if enabled and hb_world > 1 and self.store is not None:
+            self.heartbeat = health.Heartbeat(self.store, hb_id, hb_world, interval=interval, timeout=timeout)
+            self.heartbeat.start()
 
     # -- done-queue barrier (distribute_train.py:43-46, 86-90, 202-205) ---
     def signal_done(self):
         """A worker tower reports completion (the reference's done-queue enqueue)."""
+        if self.heartbeat is not None:
+            self.heartbeat.stop(done=True)      # finished, not failed
         n = self.store.add("mdtf/done_queue0", 1)
         logger.info("done token enqueued (%d received)" % n)
         return n
@@ -193,6 +209,8 @@ class Server(object):
 
     def shutdown(self):
         import torch.distributed as dist
+        if self.heartbeat is not None:
+            self.heartbeat.stop(done=True)
         if dist.is_initialized() and not self._torchrun:
             dist.destroy_process_group()
         _set_current(None)

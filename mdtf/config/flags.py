@@ -154,6 +154,8 @@ DEFINE_string('model_dir', '', "Override @model_dir (checkpoint directory).")
 DEFINE_string('data_dir', '', "Override @data_dir (input data).")
 DEFINE_string('mode', '', "Override @current_mode (Train / Eval).")
 DEFINE_integer('epochs', 0, "Override @epoch_num when > 0.")
+DEFINE_integer('save_checkpoint_steps', 0, "Checkpoint every N global steps (0: every save_checkpoint_secs).")
+DEFINE_integer('save_checkpoint_secs', 600, "Checkpoint period in seconds (chief), as MonitoredTrainingSession.")
 
 
 def apply_thread_flags():

@@ -114,9 +114,13 @@ class Train(object):
             logger.info("Worker %d: Initializing session..." % self.task_index)
         else:
             logger.info("Worker %d: Waiting for session to be initialized..." % self.task_index)
-        save_secs = getattr(self, "save_checkpoint_secs", 600)
-        save_steps = getattr(self, "save_checkpoint_steps", None)
+        save_secs = getattr(self, "save_checkpoint_secs", None) or FLAGS.save_checkpoint_secs
+        save_steps = getattr(self, "save_checkpoint_steps", None) or FLAGS.save_checkpoint_steps or None
         hooks = [H.StopAtStepHook(last_step=total_step), sync_replicas_hook]
+        from ..cluster.health import FaultInjectionHook
+        fault = FaultInjectionHook.from_env(self.job_name, self.task_index)
+        if fault is not None:
+            hooks.append(fault)
         ckpt_kwargs = {}
         if ps_mode == "sharded" and num_replicas > 1 and self.model_dir:
             # collective save: every replica runs the checkpoint hook on the same steps

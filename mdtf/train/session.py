@@ -166,24 +166,35 @@ class MonitoredSession(Session):
         if V.get_global_step() is None:
             V.get_or_create_global_step()
         from .saver import Saver, latest_checkpoint
-        restored = False
-        if self.is_chief:
-            ckpt = latest_checkpoint(self.checkpoint_dir) if self.checkpoint_dir else None
-            if ckpt:
-                saver = self.scaffold.saver or Saver()
-                saver.restore(self, ckpt)
-                self.restored_from = ckpt
-                restored = True
-                logger.info("Restored from checkpoint %s (global_step %d)" % (ckpt, V.get_global_step().value()))
         distributed = dist.is_available() and dist.is_initialized() and pg is not None
-        if distributed and dist.get_world_size(pg) > 1:
+        multi = distributed and dist.get_world_size(pg) > 1
+        # the chief picks the checkpoint; EVERY replica restores it (each takes its own
+        # optimizer-state shard in sharded mode), so no restored state is broadcast
+        ckpt = None
+        if self.is_chief and self.checkpoint_dir:
+            ckpt = latest_checkpoint(self.checkpoint_dir)
+        if multi:
+            box = [ckpt]
+            src = dist.get_global_rank(pg, 0) if pg is not dist.group.WORLD else 0
+            dist.broadcast_object_list(box, src=src, group=pg)
+            ckpt = box[0]
+        restored = False
+        if ckpt:
+            saver = self.scaffold.saver or Saver()
+            saver.restore(self, ckpt)
+            self.restored_from = ckpt
+            restored = True
+            logger.info("Restored from checkpoint %s (global_step %d)" % (ckpt, V.get_global_step().value()))
+            for op in ops:
+                op.step_count = V.get_global_step().value()
+        elif multi:
             self._broadcast_state(pg)
         else:
             for op in ops:
                 op.reducer.load_shards_from_master()
         if self.is_chief and not restored and self.scaffold.init_fn is not None:
             self.scaffold.init_fn(self.scaffold, self)
-            if distributed and dist.get_world_size(pg) > 1:
+            if multi:
                 self._broadcast_state(pg)
         for op in ops:
             op.space.refresh_shadows()
@@ -197,8 +208,8 @@ class MonitoredSession(Session):
         for op in S.train_ops():
             for g in op.space.groups:
                 dist.broadcast(g.master, src=src, group=pg)
-                for buf in g.state.values():
-                    dist.broadcast(buf, src=src, group=pg)
+                for key in sorted(g.state):     # same order on every rank
+                    dist.broadcast(g.state[key], src=src, group=pg)
         for v in store.global_variables():
             if not v.trainable:
                 dist.broadcast(v.master, src=src, group=pg)

@@ -107,3 +107,56 @@ def test_async_ps_two_ps_two_workers(tmp_path):
     shards = {r.entries[k].shard_id for k in r.keys()}
     assert shards == {0, 1}                     # variables live on both PS tasks
     assert int(r.get_tensor("global_step")) >= 100
+
+
+@pytest.mark.slow
+def test_fault_injection_restart_resumes_from_checkpoint(tmp_path):
+    """Kill worker 1 at global step 37; the heartbeat watchdog stops the surviving tasks, the supervisor
+    restarts the job, the chief resumes from the last checkpoint (step 30) and training completes."""
+    md = str(tmp_path / "ft")
+    script = os.path.join(ROOT, "distribute.py")
+    env = {"MDTF_FAULT_STEP": "37", "MDTF_FAULT_TASK": "worker:1", "MDTF_HEARTBEAT_INTERVAL": "0.5",
+           "MDTF_HEARTBEAT_TIMEOUT": "5"}
+    codes = launch_local_cluster([script, "--model_dir=%s" % md, "--epochs=1", "--save_checkpoint_steps=10"],
+                                 num_ps=1, num_workers=2, extra_env=env, timeout_s=600, max_restarts=2,
+                                 log_dir=str(tmp_path / "logs"))
+    assert codes == [0, 0, 0]
+    assert launch_local_cluster.last_attempts == 1
+    from mdtf.train.saver import latest_checkpoint
+    from mdtf.ckpt.tensor_bundle import BundleReader
+    ck = latest_checkpoint(md)
+    assert ck.endswith("model.ckpt-100")
+    assert int(BundleReader(ck).get_tensor("global_step")) == 100
+    logs = tmp_path / "logs"
+    assert "injected fault at global step 37" in (logs / "task2.attempt0.log").read_text()
+    resumed = (logs / "task1.attempt1.log").read_text()
+    assert "Restored from checkpoint" in resumed and "model.ckpt-30 (global_step 30)" in resumed
+
+
+def test_heartbeat_detects_silent_peer():
+    """Two heartbeats on one TCPStore: when one stops beating (without 'done'), the other reports it."""
+    import torch.distributed as dist
+    from mdtf.cluster.health import Heartbeat
+    port = free_port()
+    store = dist.TCPStore("127.0.0.1", port, is_master=True, wait_for_workers=False)
+    failed = []
+    a = Heartbeat(store, 0, 2, interval=0.1, timeout=0.6, on_failure=failed.append).start()
+    b = Heartbeat(store, 1, 2, interval=0.1, timeout=0.6, on_failure=failed.append).start()
+    import time
+    time.sleep(0.5)
+    assert failed == []
+    b.stop(done=False)            # rank 1 goes silent
+    t0 = time.time()
+    while not failed and time.time() - t0 < 5:
+        time.sleep(0.05)
+    a.stop()
+    assert failed == [1]
+    # a peer that finishes cleanly is never reported
+    failed.clear()
+    c = Heartbeat(store, 0, 2, interval=0.1, timeout=0.4, prefix="mdtf/hb2", on_failure=failed.append).start()
+    d = Heartbeat(store, 1, 2, interval=0.1, timeout=0.4, prefix="mdtf/hb2", on_failure=failed.append).start()
+    time.sleep(0.3)
+    d.stop(done=True)
+    time.sleep(1.0)
+    c.stop()
+    assert failed == []
