@@ -54,6 +54,8 @@ struct ConvArgs {
   int K;               // GEMM reduction length (fwd/dgrad)
   int mtiles, ntiles;  // tile grid
   int ksplit_steps;    // wgrad: K steps per split
+  int stat_slots;      // fwd: BN-statistics partial rows (power of two: atomics spread; = mtiles: deterministic)
+  int ld_dy, ld_dw;    // wgrad v2: row strides of DY and DW in elements (Cout for convolutions)
 };
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p, bool ok) {
@@ -324,7 +326,7 @@ __global__ void __launch_bounds__(NT) conv_fd_kernel(ConvArgs a) {
           q += red[WM * BN + w * BN + nl];
         }
         // 64 atomic slots (zeroed by the caller) spread the M-tiles' partials
-        const long long slot = (long long)(mt & (kStatSlots - 1)) * a.Ncol + n;
+        const long long slot = (long long)(mt % a.stat_slots) * a.Ncol + n;
         atomicAdd(a.stat_sum + slot, s);
         atomicAdd(a.stat_sq + slot, q);
       }
@@ -706,7 +708,7 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
           sv += red[w * BN + nl];
           q += red[WM * BN + w * BN + nl];
         }
-        const long long slot = (long long)(mt & (kStatSlots - 1)) * a.Ncol + n;
+        const long long slot = (long long)(mt % a.stat_slots) * a.Ncol + n;
         atomicAdd(a.stat_sum + slot, sv);
         atomicAdd(a.stat_sq + slot, q);
       }
@@ -802,7 +804,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_v2(ConvArgs a) {
   if (kt_begin >= kt_end) return;
 
   const int bytes_x = (int)((long long)a.N * a.H * a.W * a.Cin * 2);
-  const int bytes_dy = (int)(Mpix * a.Cout * 2);
+  const int bytes_dy = (int)((Mpix - 1) * a.ld_dy * 2 + a.Cout * 2);
 
   // A half h: rows r0 + 64h .. +63 lie in one tap (Cin % 64 == 0)
   int h_dy[HA], h_dx[HA], h_c[HA];
@@ -855,7 +857,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_v2(ConvArgs a) {
 #pragma unroll
       for (int h = 0; h < HB; ++h) {
         const int co = n0 + 64 * h;
-        const unsigned voff = (mok && co < a.Cout) ? (unsigned)((p_m[u] * a.Cout + co + gch[u]) * 2) : OOB;
+        const unsigned voff = (mok && co < a.Cout) ? (unsigned)((p_m[u] * a.ld_dy + co + gch[u]) * 2) : OOB;
         dma16(a.dy, bytes_dy, ldsb + h * 8192 + (wave + 4 * u) * 1024, voff, 0);
       }
       // advance this row by 64 pixels
@@ -923,7 +925,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_v2(ConvArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int r = r0 + wm * (TM * 16) + i * 16 + 4 * g + rr;
-        if (r < R) atomicAdd(a.dw + (long long)r * a.Cout + co, acc[i][j][rr]);
+        if (r < R) atomicAdd(a.dw + (long long)r * a.ld_dw + co, acc[i][j][rr]);
       }
     }
 }
@@ -1021,9 +1023,9 @@ ConvArgs make_args(int N, int H, int W, int Cin, int OH, int OW, int Cout, int K
 
 // Y = conv(X, W); optional per-M-tile BN partials (stat_sum/stat_sq [mtiles][Cout]).
 // Returns the number of M tiles through *mtiles_out (for the BN finalize).
-MDTF_EXPORT int mdtf_conv_fwd(const void* x, const void* w, void* y, float* stat_sum, float* stat_sq, int N, int H,
-                              int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int SH, int SW, int PH, int PW,
-                              int DH, int DW, int bm, int bn, int* mtiles_out, hipStream_t st) {
+MDTF_EXPORT int mdtf_conv_fwd(const void* x, const void* w, void* y, float* stat_sum, float* stat_sq, int stat_slots,
+                              int N, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int SH, int SW,
+                              int PH, int PW, int DH, int DW, int bm, int bn, int* mtiles_out, hipStream_t st) {
   if (Cin % 8 || Cout % 8) return MDTF_EINVAL;
   ConvArgs a = make_args(N, H, W, Cin, OH, OW, Cout, KH, KW, SH, SW, PH, PW, DH, DW);
   a.src = (const bf16_t*)x;
@@ -1031,6 +1033,7 @@ MDTF_EXPORT int mdtf_conv_fwd(const void* x, const void* w, void* y, float* stat
   a.out = (bf16_t*)y;
   a.stat_sum = stat_sum;
   a.stat_sq = stat_sq;
+  a.stat_slots = stat_slots > 0 ? stat_slots : kStatSlots;
   a.M = (long long)N * OH * OW;
   a.Ncol = Cout;
   a.K = KH * KW * Cin;
@@ -1073,9 +1076,10 @@ MDTF_EXPORT int mdtf_conv_wgrad(const void* x, const void* dy, float* dw, int N,
 }
 
 // v2 (C % 64 == 0): Y = conv(X, W) with the filter given transposed, Wt[co][(kh,kw,ci)]
-MDTF_EXPORT int mdtf_conv_fwd_v2(const void* x, const void* wt, void* y, float* stat_sum, float* stat_sq, int N,
-                                 int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int SH, int SW,
-                                 int PH, int PW, int DH, int DW, int bm, int bn, int* mtiles_out, hipStream_t st) {
+MDTF_EXPORT int mdtf_conv_fwd_v2(const void* x, const void* wt, void* y, float* stat_sum, float* stat_sq,
+                                 int stat_slots, int N, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
+                                 int SH, int SW, int PH, int PW, int DH, int DW, int bm, int bn, int* mtiles_out,
+                                 hipStream_t st) {
   if (Cin % 64 || Cout % 8) return MDTF_EINVAL;
   if (KH * KW > 32 || (long long)N * H * W * Cin * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
   ConvArgs a = make_args(N, H, W, Cin, OH, OW, Cout, KH, KW, SH, SW, PH, PW, DH, DW);
@@ -1084,6 +1088,7 @@ MDTF_EXPORT int mdtf_conv_fwd_v2(const void* x, const void* wt, void* y, float* 
   a.out = (bf16_t*)y;
   a.stat_sum = stat_sum;
   a.stat_sq = stat_sq;
+  a.stat_slots = stat_slots > 0 ? stat_slots : kStatSlots;
   a.M = (long long)N * OH * OW;
   a.Ncol = Cout;
   a.K = KH * KW * Cin;
@@ -1125,10 +1130,33 @@ MDTF_EXPORT int mdtf_conv_wgrad_v2(const void* x, const void* dy, float* dw, int
   a.src = (const bf16_t*)x;
   a.dy = (const bf16_t*)dy;
   a.dw = dw;
+  a.ld_dy = a.ld_dw = Cout;
   a.M = (long long)N * OH * OW;
   a.Ncol = Cout;
   const int stages = bm / 1000 ? bm / 1000 : 2;
   bm %= 1000;
+#define WG2(BM_, BN_, S_) \
+  if (bm == BM_ && bn == BN_ && stages == S_) return launch_wgrad_v2<BM_, BN_, S_>(a, splits, st);
+  WG2(128, 128, 2) WG2(128, 128, 3) WG2(128, 64, 2) WG2(128, 64, 3) WG2(64, 128, 2) WG2(64, 128, 3)
+  WG2(64, 64, 2) WG2(64, 64, 3) WG2(64, 64, 4)
+#undef WG2
+  return MDTF_EUNSUPPORTED;
+}
+
+// dW[K][N] (fp32, row stride ld_dw) += X[M][K]^T DY[M][N] (DY row stride ld_dy): the dense-layer
+// weight gradient on the v2 wgrad kernel (a 1x1 convolution over M "pixels").  K % 64 == 0, N % 64 == 0.
+MDTF_EXPORT int mdtf_gemm_wgrad(const void* x, const void* dy, float* dw, long long M, int K, int N, int ld_dy,
+                                int ld_dw, int bm, int bn, int stages, int splits, hipStream_t st) {
+  if (K % 64 || N % 64 || ld_dy % 8 || M > 0x7fffffff) return MDTF_EINVAL;
+  if (M * K * 2 > 0x7fffffffLL || M * (long long)ld_dy * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
+  ConvArgs a = make_args((int)M, 1, 1, K, 1, 1, N, 1, 1, 1, 1, 0, 0, 1, 1);
+  a.src = (const bf16_t*)x;
+  a.dy = (const bf16_t*)dy;
+  a.dw = dw;
+  a.ld_dy = ld_dy;
+  a.ld_dw = ld_dw;
+  a.M = M;
+  a.Ncol = N;
 #define WG2(BM_, BN_, S_) \
   if (bm == BM_ && bn == BN_ && stages == S_) return launch_wgrad_v2<BM_, BN_, S_>(a, splits, st);
   WG2(128, 128, 2) WG2(128, 128, 3) WG2(128, 64, 2) WG2(128, 64, 3) WG2(64, 128, 2) WG2(64, 128, 3)

@@ -570,14 +570,19 @@ MDTF_EXPORT int mdtf_act_bwd(const void* dy, const void* pre, const void* y, voi
 
 // out must be zeroed by the caller
 // out[c] += sum_b ws[b][c]   (shared by every two-stage column reduction)
+int g_deterministic = 0;   // 1: fixed-order reductions (no cross-block float atomics)
+
 // (row stride ld >= C)
 MDTF_EXPORT int mdtf_reduce_partials_strided(const float* ws, int B, int C, long long ld, float* out, hipStream_t st) {
   int slices = B < kSlices * 4 ? static_cast<int>(ceil_div(B, 4)) : kSlices;
-  if (slices < 1) slices = 1;
+  if (slices < 1 || g_deterministic) slices = 1;
   hipLaunchKernelGGL(reduce_partials, dim3(ceil_div(C, 64), slices), dim3(kT), 0, st, ws, B, C, ld, out);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
+
+MDTF_EXPORT void mdtf_set_deterministic(int on) { g_deterministic = on ? 1 : 0; }
+MDTF_EXPORT int mdtf_get_deterministic() { return g_deterministic; }
 
 MDTF_EXPORT int mdtf_reduce_partials(const float* ws, int B, int C, float* out, hipStream_t st) {
   return mdtf_reduce_partials_strided(ws, B, C, C, out, st);

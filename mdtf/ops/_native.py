@@ -50,6 +50,8 @@ def lib():
         _load_error = RuntimeError("failed to load %s: %s" % (LIB_PATH, e))
         raise _load_error
     _declare(_lib)
+    if _DETERMINISTIC:
+        _lib.mdtf_set_deterministic(ctypes.c_int(1))
     return _lib
 
 
@@ -80,9 +82,41 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+_SYNC_CHECK = os.environ.get("MDTF_SYNC_CHECK", "0") not in ("0", "", "false")
+_DETERMINISTIC = os.environ.get("MDTF_DETERMINISTIC", "0") not in ("0", "", "false")
+
+
 def check(rc, what):
     if rc != 0:
         raise RuntimeError("mdtf kernel %s failed: %s (code %d)" % (what, _error_string(rc), rc))
+    if _SYNC_CHECK:
+        # debug mode (MDTF_SYNC_CHECK=1): serialize after every native launch so a faulting
+        # kernel is named here instead of surfacing at some later synchronization
+        import torch
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:
+            raise RuntimeError("mdtf kernel %s faulted: %s" % (what, e))
+
+
+def set_deterministic(flag=True):
+    """Fixed-order reductions everywhere the native kernels would use cross-block float
+    atomics (BN statistics rows, split-K weight gradients, column-sum / LayerNorm
+    partial reductions, embedding scatter-add).  Slower; for debugging and
+    bitwise-reproducible runs.  Also settable with ``MDTF_DETERMINISTIC=1``."""
+    global _DETERMINISTIC
+    _DETERMINISTIC = bool(flag)
+    if _lib is not None:
+        _lib.mdtf_set_deterministic(ctypes.c_int(int(_DETERMINISTIC)))
+
+
+def deterministic():
+    return _DETERMINISTIC
+
+
+def set_sync_check(flag=True):
+    global _SYNC_CHECK
+    _SYNC_CHECK = bool(flag)
 
 
 def _error_string(rc):

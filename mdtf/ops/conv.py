@@ -18,10 +18,10 @@ import torch.nn.functional as F
 from . import _native as N
 from ..train import variables as V
 
-N.register("mdtf_conv_fwd", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 17 + [N.P, N.P])
+N.register("mdtf_conv_fwd", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P])
 N.register("mdtf_conv_dgrad", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
 N.register("mdtf_conv_wgrad", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
-N.register("mdtf_conv_fwd_v2", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 17 + [N.P, N.P])
+N.register("mdtf_conv_fwd_v2", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P])
 N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
 N.register("mdtf_conv_wgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 
@@ -77,6 +77,10 @@ def choose(pass_, x_shape, w_shape, stride, pads, dil):
     if not native_ok or forced == "miopen":
         return ("miopen",)
     ent = table().get(shape_key(pass_, x_shape, w_shape, stride, pads, dil))
+    if N.deterministic() and pass_ == "wgrad":
+        # no split-K atomics, no library algorithm choice: one block per DW tile
+        ver = 2 if v2_ok(pass_, c, co, stride, kh * kw) else 1
+        return ("mdtf", 128 if kh * kw * ci >= 128 else 64, 128 if co % 128 == 0 else 64, 1, ver, 2)
     if forced == "auto" and ent is not None:
         if ent["backend"] == "miopen":
             return ("miopen",)
@@ -161,15 +165,16 @@ def mdtf_fwd(x, w, out_hw, stride, pads, dil, bm, bn, stats=None, ver=1, stages=
     y = torch.empty((n, out_hw[0], out_hw[1], co), dtype=x.dtype, device=x.device)
     mt = N.I(0)
     s_sum, s_sq = (stats if stats is not None else (None, None))
+    slots = s_sum.shape[0] if s_sum is not None else 0
     import ctypes
     if ver == 2:
         wt = transpose_filter(w)
-        N.check(N.fn("mdtf_conv_fwd_v2")(N.ptr(x), N.ptr(wt), N.ptr(y), N.ptr(s_sum), N.ptr(s_sq),
+        N.check(N.fn("mdtf_conv_fwd_v2")(N.ptr(x), N.ptr(wt), N.ptr(y), N.ptr(s_sum), N.ptr(s_sq), slots,
                                          *_geo(x, w, out_hw, stride, pads, dil), bm + 1000 * stages, bn,
                                          ctypes.byref(mt),
                                          N.stream_ptr()), "conv_fwd_v2")
         return y
-    N.check(N.fn("mdtf_conv_fwd")(N.ptr(x), N.ptr(w), N.ptr(y), N.ptr(s_sum), N.ptr(s_sq),
+    N.check(N.fn("mdtf_conv_fwd")(N.ptr(x), N.ptr(w), N.ptr(y), N.ptr(s_sum), N.ptr(s_sq), slots,
                                   *_geo(x, w, out_hw, stride, pads, dil), bm, bn, ctypes.byref(mt), N.stream_ptr()),
             "conv_fwd")
     return y
@@ -210,7 +215,7 @@ STAT_SLOTS = 64   # atomic partial rows of the fused BN statistics (csrc/conv_ig
 _STATS = {}       # device -> [flat fp32 buffer, dirty]: persistent, re-zeroed by the BN finalize kernel
 
 
-def _stats_buffer(co, device):
+def _stats_buffer(co, device, slots=STAT_SLOTS):
     """Zeroed [2, STAT_SLOTS, co] partial-sum buffer for a conv epilogue.
 
     One persistent buffer per device: the following BatchNorm's finalize
@@ -218,14 +223,14 @@ def _stats_buffer(co, device):
     conv.  If a previous conv's statistics were never consumed, zero it here.
     """
     ent = _STATS.get(device)
-    need = 2 * STAT_SLOTS * co
+    need = 2 * slots * co
     if ent is None or ent[0].numel() < need:
         ent = [torch.zeros(max(need, 2 * STAT_SLOTS * 2048), dtype=torch.float32, device=device), False]
         _STATS[device] = ent
     if ent[1]:
         ent[0].zero_()
     ent[1] = True
-    return ent[0][:need].view(2, STAT_SLOTS, co)
+    return ent[0][:need].view(2, slots, co)
 
 
 def stats_consumed(device):
@@ -245,7 +250,10 @@ class _Conv(torch.autograd.Function):
         if ch[0] == "mdtf":
             if want_stats:
                 co = w.shape[3]
-                buf = _stats_buffer(co, x.device)
+                slots = STAT_SLOTS
+                if N.deterministic():       # one partial row per M tile: no atomic reordering
+                    slots = -(-x.shape[0] * out_hw[0] * out_hw[1] // ch[1])
+                buf = _stats_buffer(co, x.device, slots)
                 stats = (buf[0], buf[1])
             y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2], stats, ch[4], ch[5])
         else:
@@ -331,7 +339,7 @@ def conv2d_stats_nhwc(x, w, stride, pads, dil):
     y, psum, psq = _Conv.apply(x, w, tuple(stride), tuple(pads), tuple(dil), _out_hw(x, w, stride, pads, dil), True)
     if psum.numel() == 0:
         return y, None
-    return y, (psum, psq, STAT_SLOTS)
+    return y, (psum, psq, psum.shape[0])
 
 
 def conv2d_dgrad_nhwc(x, w, out_shape, stride, pads):

@@ -23,6 +23,28 @@ from ..train import variables as V
 _ACT = {None: 0, "relu": 1, "gelu": 2}
 _fp32_out_ok = None      # does this torch build accept addmm(out_dtype=float32, out=...)?
 
+N.register("mdtf_gemm_wgrad", [N.P, N.P, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.P])
+
+
+def wgrad_into(out, x, d):
+    """``out[K][N] += x[M][K]^T d[M][N]`` in fp32 (``d`` may be a column slice).
+
+    The mdtf weight-gradient kernel where it applies (K, N multiples of 64 -- it beats
+    the library's fp32-output GEMM on the BERT shapes, bench/gemm_micro.py), else
+    hipBLASLt.  Deterministic mode uses the unsplit kernel.
+    """
+    M, K = x.shape
+    Nn = d.shape[1]
+    if (K % 64 == 0 and Nn % 64 == 0 and x.is_contiguous() and d.stride(1) == 1 and out.is_contiguous()
+            and x.dtype == torch.bfloat16 and d.dtype == torch.bfloat16 and out.dtype == torch.float32):
+        splits = 1 if N.deterministic() else (8 if K * Nn <= 768 * 768 else 0)
+        bm, bn = (128, 128) if M < 4096 else (64, 128)
+        rc = N.fn("mdtf_gemm_wgrad")(N.ptr(x), N.ptr(d), N.ptr(out), M, K, Nn, d.stride(0), out.stride(0), bm, bn, 2,
+                                     splits, N.stream_ptr())
+        if rc == 0:
+            return
+    _accum_mm(out, x.t(), d)
+
 
 def _accum_mm(out, a, b):
     """``out += a @ b`` with bf16 a/b and fp32 out."""
@@ -96,7 +118,7 @@ class _Dense(torch.autograd.Function):
                 if ctx.trans:
                     _accum_mm(sink.grad, d.t(), x)
                 else:
-                    _accum_mm(sink.grad, x.t(), d)
+                    wgrad_into(sink.grad, x, d)
                 gws.append(V.grad_marker(ws[j]))
             elif ctx.needs_input_grad[4 + j]:
                 g = torch.mm(d.t(), x) if ctx.trans else torch.mm(x.t(), d)

@@ -143,8 +143,17 @@ class _Embed(torch.autograd.Function):
         dy = dy.contiguous()
         sink = ctx.sink
         dt = sink.grad if sink is not None else torch.zeros((vocab, H), dtype=torch.float32, device=dy.device)
-        N.check(N.fn("mdtf_embed_bwd")(N.ptr(dy), N.ptr(ids), N.ptr(dt), ids.numel(), H, vocab, N.stream_ptr()),
-                "embed_bwd")
+        if N.deterministic():
+            # sorted (deterministic) scatter-add instead of the atomic kernel
+            prev = torch.are_deterministic_algorithms_enabled()
+            torch.use_deterministic_algorithms(True)
+            try:
+                dt.index_add_(0, ids.reshape(-1), dy.reshape(-1, H).float())
+            finally:
+                torch.use_deterministic_algorithms(prev)
+        else:
+            N.check(N.fn("mdtf_embed_bwd")(N.ptr(dy), N.ptr(ids), N.ptr(dt), ids.numel(), H, vocab,
+                                           N.stream_ptr()), "embed_bwd")
         if sink is not None:
             return V.grad_marker(ctx.like), None
         return dt.to(ctx.like.dtype), None

@@ -661,3 +661,49 @@ def test_bert_fused_vs_unfused_attention_path(monkeypatch):
         if k.endswith("key/bias"):
             continue
         assert _rel(gf[k], gu[k]) < 0.1, (k, _rel(gf[k], gu[k]))
+
+
+def test_deterministic_mode_bitwise_repeatable():
+    """MDTF deterministic mode: two identical engine steps give bit-identical gradients
+    (BN statistics rows per M tile, unsplit weight-gradient GEMMs, fixed-order reductions)."""
+    from mdtf.ops import _native
+    torch.manual_seed(0)
+    x = torch.randn(32, 16, 16, 64)
+    y = torch.randint(0, 16, (32,))
+    _native.set_deterministic(True)
+    try:
+        l1, g1 = _tiny_step(DEV, torch.bfloat16, x, y)
+        l2, g2 = _tiny_step(DEV, torch.bfloat16, x, y)
+    finally:
+        _native.set_deterministic(False)
+    assert l1 == l2
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
+    from mdtf.models import SyntheticBertLoader
+    from mdtf.train import variables as V
+    V.get_store().device = torch.device("cpu")
+    ld = SyntheticBertLoader(seq_len=32, max_predictions=5, vocab=512, seed=3)
+    ld.batch_size = 8
+    raw, gt = ld._make()
+    _native.set_deterministic(True)
+    try:
+        b1 = _bert_step(DEV, torch.bfloat16, raw, gt)
+        b2 = _bert_step(DEV, torch.bfloat16, raw, gt)
+    finally:
+        _native.set_deterministic(False)
+    assert b1[0] == b2[0]
+    for k in b1[1]:
+        assert torch.equal(b1[1][k], b2[1][k]), k
+
+
+@pytest.mark.parametrize("M,K,N,col0,ld", [(8192, 768, 768, 768, 2304), (1000, 128, 192, 0, 192), (64, 64, 64, 64, 256)])
+def test_gemm_wgrad_into_strided(M, K, N, col0, ld):
+    from mdtf.ops import gemm
+    torch.manual_seed(31)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    dfull = torch.randn(M, ld, device=DEV).bfloat16()
+    d = dfull[:, col0:col0 + N]
+    out = torch.full((K, N), 0.5, device=DEV)
+    gemm.wgrad_into(out, x, d)
+    ref = x.float().t() @ d.float() + 0.5
+    assert _rel(out, ref) < 1e-4
