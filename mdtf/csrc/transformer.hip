@@ -20,12 +20,24 @@ namespace {
 constexpr int kT = 256;
 constexpr int kMaxVec = 16;   // H <= 64 lanes * 8 * 16 = 8192
 
+// dropout keep bit of element idx (same counter-hash as csrc/attention.hip)
+__device__ __forceinline__ bool drop_keep(uint32_t idx, uint32_t seed, uint32_t thr) {
+  uint32_t x = idx * 0x9E3779B1u ^ seed;
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x >= thr;
+}
+
 template <int NV>
 __global__ void __launch_bounds__(kT) ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                                    bf16_t* __restrict__ y, bf16_t* __restrict__ s_out,
                                                    float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                   long long rows, int H, float eps) {
+                                                   long long rows, int H, float eps, uint32_t thr, float inv_keep,
+                                                   uint32_t seed) {
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -37,6 +49,11 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const bf16_t* __restrict__ x
     const int c = (lane + i * 64);
     if (c < nvec) {
       load_bf8(x + row * H + c * 8, v[i]);
+      if (thr) {      // fused dropout on the branch input (before the residual add)
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          v[i][k] = drop_keep((uint32_t)(row * H + c * 8 + k), seed, thr) ? v[i][k] * inv_keep : 0.f;
+      }
       if (res) {
         float r[8];
         load_bf8(res + row * H + c * 8, r);
@@ -83,8 +100,9 @@ template <int NV>
 __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
                                                    const float* __restrict__ gamma, const float* __restrict__ mean,
                                                    const float* __restrict__ rstd, bf16_t* __restrict__ dx,
-                                                   float* __restrict__ ws, long long rows, int H,
-                                                   int rows_per_block) {
+                                                   bf16_t* __restrict__ dx_branch, float* __restrict__ ws,
+                                                   long long rows, int H, int rows_per_block, int beta_first,
+                                                   uint32_t thr, float inv_keep, uint32_t seed) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nvec = H / 8;
   float dg[NV][8], db[NV][8];
@@ -126,6 +144,12 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = rs * (g[i][k] * gamma[c * 8 + k] - a - xh[i][k] * b);
         store_bf8(dx + row * H + c * 8, o);
+        if (dx_branch) {     // gradient of the dropped-out branch input
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            o[k] = (!thr || drop_keep((uint32_t)(row * H + c * 8 + k), seed, thr)) ? o[k] * inv_keep : 0.f;
+          store_bf8(dx_branch + row * H + c * 8, o);
+        }
       }
     }
   }
@@ -141,13 +165,13 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
     }
     __syncthreads();
     for (int j = threadIdx.x; j < 2 * 512; j += kT) {
-      const int which = j >> 9, cc = j & 511;
+      const int which = j >> 9, cc = j & 511;       // 0: dgamma, 1: dbeta
       const int col = i * 512 + cc;
       if (col < H) {
         float t = 0.f;
 #pragma unroll
         for (int w = 0; w < kT / 64; ++w) t += L[which][w][cc];
-        wg[which * H + col] = t;
+        wg[(which ^ beta_first) * H + col] = t;      // partial rows follow the grad slots' order
       }
     }
     __syncthreads();
@@ -280,11 +304,22 @@ inline int gcap(long long work) {
     else return MDTF_EUNSUPPORTED;                                                                         \
   } while (0)
 
+static uint32_t drop_thr(float p) {
+  if (p <= 0.f) return 0u;
+  double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
+}
+
+// y = LN(dropout_p(x) + res); s = dropout_p(x) + res saved for backward (p = 0: no dropout)
 MDTF_EXPORT int mdtf_ln_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y, void* s,
-                            float* mean, float* rstd, long long rows, int H, float eps, hipStream_t st) {
+                            float* mean, float* rstd, long long rows, int H, float eps, float p_drop, unsigned seed,
+                            hipStream_t st) {
   if (H % 8) return MDTF_EINVAL;
+  if (rows * H > 0xffffffffLL && p_drop > 0.f) return MDTF_EUNSUPPORTED;
+  const uint32_t thr = drop_thr(p_drop);
+  const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   NV_DISPATCH(H, ln_fwd_kernel, dim3(ceil_div(rows, kT / 64)), (const bf16_t*)x, (const bf16_t*)res, gamma, beta,
-              (bf16_t*)y, (bf16_t*)s, mean, rstd, rows, H, eps);
+              (bf16_t*)y, (bf16_t*)s, mean, rstd, rows, H, eps, thr, inv_keep, (uint32_t)seed);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
@@ -310,15 +345,22 @@ MDTF_EXPORT long long mdtf_ln_bwd_ws(long long rows, int H) {
 // dgamma/dbeta accumulate (+=) into zeroed buffers or fp32 grad slots;
 // dgamma and dbeta must be ONE buffer pair [dgamma | dbeta] when contiguous is
 // not guaranteed -> reduced separately.
+// dx = d(loss)/d(s); dx_branch (optional) = d(loss)/d(x) through the fused dropout
 MDTF_EXPORT int mdtf_ln_bwd(const void* dy, const void* s, const float* gamma, const float* mean, const float* rstd,
-                            void* dx, float* dgamma, float* dbeta, float* ws, long long rows, int H, hipStream_t st) {
+                            void* dx, void* dx_branch, float* dgamma, float* dbeta, float* ws, long long rows, int H,
+                            float p_drop, unsigned seed, hipStream_t st) {
   if (H % 8) return MDTF_EINVAL;
   if (rows <= 0) return 0;
   int blocks, rpb;
   ln_bwd_geometry(rows, &blocks, &rpb);
-  NV_DISPATCH(H, ln_bwd_kernel, dim3(blocks), (const bf16_t*)dy, (const bf16_t*)s, gamma, mean, rstd, (bf16_t*)dx, ws,
-              rows, H, rpb);
+  // gamma/beta grad slots adjacent in either order -> one [blocks, 2H] reduction into the pair
+  const int beta_first = (dgamma == dbeta + H) ? 1 : 0;
+  const uint32_t thr = drop_thr(p_drop);
+  const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  NV_DISPATCH(H, ln_bwd_kernel, dim3(blocks), (const bf16_t*)dy, (const bf16_t*)s, gamma, mean, rstd, (bf16_t*)dx,
+              (bf16_t*)dx_branch, ws, rows, H, rpb, beta_first, thr, inv_keep, (uint32_t)seed);
   MDTF_LAUNCH_CHECK();
+  if (beta_first) return mdtf_reduce_partials(ws, blocks, 2 * H, dbeta, st);
   // ws rows are [dgamma(H) | dbeta(H)]: reduce as a [blocks, 2H] matrix when the
   // two outputs are adjacent, else as two strided passes
   if (dbeta == dgamma + H) return mdtf_reduce_partials(ws, blocks, 2 * H, dgamma, st);

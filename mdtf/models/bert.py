@@ -47,11 +47,12 @@ def _dense(name, x, out, act=None):
     return y.reshape(*shp[:-1], out)
 
 
-def _ln(name, x, residual=None, eps=1e-12):
+def _ln(name, x, residual=None, eps=1e-12, dropout=0.0):
+    """LayerNorm(dropout(x) + residual): the dropout of TF BERT's dense outputs is fused into the LN kernel."""
     with V.variable_scope(name):
         g = V.get_variable("gamma", [x.shape[-1]], initializer=V.constant_initializer(1.0), keep_fp32=True)
         b = V.get_variable("beta", [x.shape[-1]], initializer=V.constant_initializer(0.0), keep_fp32=True)
-    return T.layer_norm(x, g, b, eps, residual=residual)
+    return T.layer_norm(x, g, b, eps, residual=residual, dropout=dropout if S.is_training() else 0.0)
 
 
 def _dropout(x, rate):
@@ -134,14 +135,12 @@ class Bert(Model):
                 ctx = T.fused_attention(qkv, B, S_, nh, amask, drop).reshape(B, S_, H)
             with V.variable_scope("output"):
                 a = _dense("dense", ctx, H)
-                a = _dropout(a, self.dropout)
-                x = _ln("LayerNorm", a, residual=x)
+                x = _ln("LayerNorm", a, residual=x, dropout=self.dropout)
         with V.variable_scope("intermediate"):
             i = _dense("dense", x, self.I, act="gelu")
         with V.variable_scope("output"):
             o = _dense("dense", i, H)
-            o = _dropout(o, self.dropout)
-            x = _ln("LayerNorm", o, residual=x)
+            x = _ln("LayerNorm", o, residual=x, dropout=self.dropout)
         return x
 
 

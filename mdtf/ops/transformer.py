@@ -12,8 +12,8 @@ import torch.nn.functional as F
 from . import _native as N
 from ..train import variables as V
 
-N.register("mdtf_ln_fwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.F, N.P])
-N.register("mdtf_ln_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P])
+N.register("mdtf_ln_fwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.F, N.F, N.U, N.P])
+N.register("mdtf_ln_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.F, N.U, N.P])
 N.register("mdtf_ln_bwd_ws", [N.L, N.I], restype=N.L)
 N.register("mdtf_softmax_fwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.L, N.P])
 N.register("mdtf_softmax_bwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.P])
@@ -31,8 +31,10 @@ def _sink_or_zeros(t, n, device):
 
 
 class _LayerNorm(torch.autograd.Function):
+    """y = LN(dropout_p(x) + residual) with the dropout mask regenerated from a counter hash."""
+
     @staticmethod
-    def forward(ctx, x, res, gamma, beta, eps):
+    def forward(ctx, x, res, gamma, beta, eps, p_drop, seed):
         x = x.contiguous()
         H = x.shape[-1]
         rows = x.numel() // H
@@ -44,9 +46,10 @@ class _LayerNorm(torch.autograd.Function):
         b = beta.detach().float().contiguous()
         r = res.contiguous() if res is not None else None
         N.check(N.fn("mdtf_ln_fwd")(N.ptr(x), N.ptr(r), N.ptr(g), N.ptr(b), N.ptr(y), N.ptr(s), N.ptr(mean),
-                                    N.ptr(rstd), rows, H, float(eps), N.stream_ptr()), "ln_fwd")
+                                    N.ptr(rstd), rows, H, float(eps), float(p_drop), seed, N.stream_ptr()), "ln_fwd")
         ctx.save_for_backward(s, g, mean, rstd)
         ctx.has_res = res is not None
+        ctx.drop = (float(p_drop), seed)
         ctx.sinks = (V.grad_sink(gamma), V.grad_sink(beta))
         ctx.like = (gamma, beta)
         return y
@@ -57,27 +60,34 @@ class _LayerNorm(torch.autograd.Function):
         dy = dy.contiguous()
         H = s.shape[-1]
         rows = s.numel() // H
-        dx = torch.empty_like(s)
+        p_drop, seed = ctx.drop
+        ds = torch.empty_like(s)
+        dxb = torch.empty_like(s) if p_drop > 0 else None     # gradient of the dropped-out branch input
         sg, sb = ctx.sinks
         dg = sg.grad if sg is not None else torch.zeros(H, dtype=torch.float32, device=s.device)
         db = sb.grad if sb is not None else torch.zeros(H, dtype=torch.float32, device=s.device)
         ws = torch.empty(N.fn("mdtf_ln_bwd_ws")(rows, H), dtype=torch.float32, device=s.device)
-        N.check(N.fn("mdtf_ln_bwd")(N.ptr(dy), N.ptr(s), N.ptr(g), N.ptr(mean), N.ptr(rstd), N.ptr(dx), N.ptr(dg),
-                                    N.ptr(db), N.ptr(ws), rows, H, N.stream_ptr()), "ln_bwd")
+        N.check(N.fn("mdtf_ln_bwd")(N.ptr(dy), N.ptr(s), N.ptr(g), N.ptr(mean), N.ptr(rstd), N.ptr(ds), N.ptr(dxb),
+                                    N.ptr(dg), N.ptr(db), N.ptr(ws), rows, H, p_drop, seed, N.stream_ptr()),
+                "ln_bwd")
         gamma, beta = ctx.like
         rg = V.grad_marker(gamma) if sg is not None else dg
         rb = V.grad_marker(beta) if sb is not None else db
-        return dx, (dx if ctx.has_res else None), rg, rb, None
+        dx = dxb if dxb is not None else ds
+        return dx, (ds if ctx.has_res else None), rg, rb, None, None, None
 
 
-def layer_norm(x, gamma, beta, eps=1e-12, residual=None):
-    """LayerNorm over the last axis of ``x (+ residual)``."""
+def layer_norm(x, gamma, beta, eps=1e-12, residual=None, dropout=0.0):
+    """LayerNorm over the last axis of ``dropout(x) (+ residual)`` (dropout fused on the GPU)."""
     if N.use_native(x):
         if x.dtype != torch.bfloat16:
             raise TypeError("mdtf LayerNorm kernel expects bf16, got %s" % x.dtype)
         if residual is not None and residual.dtype != x.dtype:
             residual = residual.to(x.dtype)
-        return _LayerNorm.apply(x, residual, gamma, beta, float(eps))
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if dropout else 0
+        return _LayerNorm.apply(x, residual, gamma, beta, float(eps), float(dropout), seed)
+    if dropout:
+        x = F.dropout(x, dropout, True)
     s = x if residual is None else x + residual
     return F.layer_norm(s.float(), (s.shape[-1],), gamma.float(), beta.float(), eps).to(x.dtype)
 

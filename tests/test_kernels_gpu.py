@@ -707,3 +707,39 @@ def test_gemm_wgrad_into_strided(M, K, N, col0, ld):
     gemm.wgrad_into(out, x, d)
     ref = x.float().t() @ d.float() + 0.5
     assert _rel(out, ref) < 1e-4
+
+
+def _hash_keep(seed, n, p):
+    import numpy as np
+    idx = np.arange(n, dtype=np.uint64).astype(np.uint32)
+    x = (idx * np.uint32(0x9E3779B1)) ^ np.uint32(seed)
+    x ^= x >> np.uint32(16)
+    x = x * np.uint32(0x7feb352d)
+    x ^= x >> np.uint32(15)
+    x = x * np.uint32(0x846ca68b)
+    x ^= x >> np.uint32(16)
+    return torch.from_numpy(x >= np.uint32(min(int(p * 4294967296.0), 4294967295)))
+
+
+def test_layernorm_fused_dropout():
+    from mdtf.ops import transformer as T
+    torch.manual_seed(41)
+    rows, H, p, seed = 300, 768, 0.1, 987654
+    x = torch.randn(rows, H)
+    r = torch.randn(rows, H)
+    g = torch.rand(H) + 0.5
+    b = torch.randn(H)
+    dy = torch.randn(rows, H)
+    xg = x.to(DEV).bfloat16().requires_grad_(True)
+    rg = r.to(DEV).bfloat16().requires_grad_(True)
+    y = T._LayerNorm.apply(xg, rg, g.to(DEV), b.to(DEV), 1e-12, p, seed)
+    y.backward(dy.to(DEV).bfloat16())
+    keep = _hash_keep(seed, rows * H, p).view(rows, H).float()
+    xc = x.bfloat16().float().requires_grad_(True)
+    rc = r.bfloat16().float().requires_grad_(True)
+    s = xc * keep / (1 - p) + rc
+    yr = torch.nn.functional.layer_norm(s, (H,), g, b, 1e-12)
+    yr.backward(dy.bfloat16().float())
+    assert _rel(y, yr) < 2e-2
+    assert _rel(xg.grad, xc.grad) < 2e-2
+    assert _rel(rg.grad, rc.grad) < 2e-2
