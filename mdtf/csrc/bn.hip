@@ -13,7 +13,8 @@
 //      shift=β-mean·scale, moving-average update (unbiased variance).
 //   3. bn_apply_kernel: y = x·scale + shift (+ res) (ReLU), bf16x8 vectors.
 // Backward:
-//   1. bn_reduce_kernel<BWD>: Σdz, Σdz·x with dz = dy·[y>0] (ReLU mask from y).
+//   1. bn_reduce_kernel<BWD>: Σdz, Σdz·x with dz = dy·[y>0] (ReLU mask: the 1-bit-per-element
+//      mask the forward apply wrote, 1/16 of the bytes of re-reading y).
 //   2. bn_finalize_bwd: dβ, dγ and dx = k1·dz + k2·x + k3 coefficients.
 //   3. bn_dx_kernel: dx (and d(residual) = dz) in one pass.
 // All passes are HBM-bound; workspaces are caller-allocated (graph-capture safe).
@@ -53,7 +54,7 @@ template <bool BWD, bool RELU>
 __global__ void __launch_bounds__(kThreads)
     bn_reduce_kernel(const bf16_t* __restrict__ a,   // FWD: x      BWD: dy
                      const bf16_t* __restrict__ b,   // FWD: unused BWD: x
-                     const bf16_t* __restrict__ y,   // BWD+RELU: output (mask)
+                     const uint8_t* __restrict__ mk, // BWD+RELU: forward ReLU bitmask (1 bit / element)
                      long long M, int C, int tpr, int rg, float* __restrict__ p0, float* __restrict__ p1) {
   extern __shared__ float smem[];  // [2][rg][tpr*8]
   const int t = threadIdx.x;
@@ -69,22 +70,32 @@ __global__ void __launch_bounds__(kThreads)
     long long r = (long long)blockIdx.x * rg + rgi;
     // 4 rows per iteration: all loads issued before the first use (bytes in flight)
     for (; r + 3 * step < M; r += 4 * step) {
-      float va[4][8], vb[4][8], vy[4][8];
+      // raw 16-B vectors (4 VGPRs each) so every load is in flight before the first use
+      uint4 ra[4], rb[4];
+      uint32_t vm[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const long long off = (r + u * step) * C + c0;
-        load_bf8(a + off, va[u]);
-        if (BWD) load_bf8(b + off, vb[u]);
-        if (BWD && RELU) load_bf8(y + off, vy[u]);
+        ra[u] = *reinterpret_cast<const uint4*>(a + off);
+        if (BWD) rb[u] = *reinterpret_cast<const uint4*>(b + off);
+        if (BWD && RELU) vm[u] = mk[off >> 3];
       }
+      __builtin_amdgcn_sched_barrier(0);     // keep all 12 loads ahead of the first use
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
+        const uint32_t wa[4] = {ra[u].x, ra[u].y, ra[u].z, ra[u].w};
+        const uint32_t wb[4] = {BWD ? rb[u].x : 0u, BWD ? rb[u].y : 0u, BWD ? rb[u].z : 0u, BWD ? rb[u].w : 0u};
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          float v = va[u][i];
-          if (BWD && RELU) v = vy[u][i] > 0.f ? v : 0.f;
+          float v = (i & 1) ? __uint_as_float(wa[i >> 1] & 0xffff0000u) : __uint_as_float(wa[i >> 1] << 16);
+          if (BWD && RELU) v = ((vm[u] >> i) & 1u) ? v : 0.f;
           s0[i] += v;
-          s1[i] += BWD ? v * vb[u][i] : v * v;
+          if (BWD) {
+            const float xb = (i & 1) ? __uint_as_float(wb[i >> 1] & 0xffff0000u) : __uint_as_float(wb[i >> 1] << 16);
+            s1[i] += v * xb;
+          } else {
+            s1[i] += v * v;
+          }
         }
       }
     }
@@ -102,10 +113,9 @@ __global__ void __launch_bounds__(kThreads)
         float vb[8];
         load_bf8(b + off, vb);
         if (RELU) {
-          float vy[8];
-          load_bf8(y + off, vy);
+          const uint32_t m8 = mk[off >> 3];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) va[i] = vy[i] > 0.f ? va[i] : 0.f;
+          for (int i = 0; i < 8; ++i) va[i] = ((m8 >> i) & 1u) ? va[i] : 0.f;
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -219,7 +229,8 @@ __global__ void bn_eval_coeffs(int C, const float* __restrict__ gamma, const flo
 template <bool HAS_RES, bool RELU>
 __global__ void __launch_bounds__(kThreads)
     bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
-                    long long n8, int C, const float* __restrict__ scale, const float* __restrict__ shift) {
+                    uint8_t* __restrict__ mask, long long n8, int C, const float* __restrict__ scale,
+                    const float* __restrict__ shift) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
     long long off = i * 8;
     int c = static_cast<int>(off % C);
@@ -233,14 +244,19 @@ __global__ void __launch_bounds__(kThreads)
     const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
     float r[8];
     if (HAS_RES) load_bf8(res + off, r);
+    uint32_t bits = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float o = v[k] * sc[k] + sh[k];
       if (HAS_RES) o += r[k];
-      if (RELU) o = fmaxf(o, 0.f);
+      if (RELU) {
+        o = fmaxf(o, 0.f);
+        bits |= (o > 0.f ? 1u : 0u) << k;
+      }
       v[k] = o;
     }
     store_bf8(y + off, v);
+    if (RELU && mask) mask[i] = static_cast<uint8_t>(bits);   // 1 bit per element: the backward's ReLU mask
   }
 }
 
@@ -268,7 +284,7 @@ __global__ void __launch_bounds__(1024)
 
 template <bool RELU, bool WRITE_DRES>
 __global__ void __launch_bounds__(kThreads)
-    bn_dx_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+    bn_dx_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const uint8_t* __restrict__ mk,
                  bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long n8, int C, const float* __restrict__ k1,
                  const float* __restrict__ k2, const float* __restrict__ k3) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
@@ -278,10 +294,9 @@ __global__ void __launch_bounds__(kThreads)
     load_bf8(dy + off, g);
     load_bf8(x + off, xv);
     if (RELU) {
-      float yv[8];
-      load_bf8(y + off, yv);
+      const uint32_t m8 = mk[i];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+      for (int k = 0; k < 8; ++k) g[k] = ((m8 >> k) & 1u) ? g[k] : 0.f;
     }
     if (WRITE_DRES) store_bf8(dres + off, g);
     float4 a0 = *reinterpret_cast<const float4*>(k1 + c), a1 = *reinterpret_cast<const float4*>(k1 + c + 4);
@@ -295,6 +310,27 @@ __global__ void __launch_bounds__(kThreads)
     for (int k = 0; k < 8; ++k) o[k] = A[k] * g[k] + B[k] * xv[k] + E[k];
     store_bf8(dx + off, o);
   }
+}
+
+inline int ew_grid(long long n8);
+
+void launch_apply(const void* x, const void* res, void* y, uint8_t* mask, long long n8, int C, const float* scale,
+                  const float* shift, int relu, hipStream_t st) {
+  const bf16_t* r = (const bf16_t*)res;
+  const bf16_t* xx = (const bf16_t*)x;
+  bf16_t* yy = (bf16_t*)y;
+  if (r && relu)
+    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, xx, r, yy, mask, n8, C,
+                       scale, shift);
+  else if (r)
+    hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, xx, r, yy, nullptr,
+                       n8, C, scale, shift);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, xx, nullptr, yy, mask,
+                       n8, C, scale, shift);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, xx, nullptr, yy,
+                       nullptr, n8, C, scale, shift);
 }
 
 inline int ew_grid(long long n8) {
@@ -311,9 +347,9 @@ MDTF_EXPORT long long mdtf_bn_workspace_floats(long long M, int C) {
 }
 
 // Training forward. mean/invstd (fp32 [C]) are saved for backward.
-MDTF_EXPORT int mdtf_bn_fwd_train(const void* x, const void* res, void* y, long long M, int C, const float* gamma,
-                                  const float* beta, float* mmean, float* mvar, float decay, float eps, int relu,
-                                  float* mean, float* invstd, float* ws, hipStream_t st) {
+MDTF_EXPORT int mdtf_bn_fwd_train(const void* x, const void* res, void* y, uint8_t* mask, long long M, int C,
+                                  const float* gamma, const float* beta, float* mmean, float* mvar, float decay,
+                                  float eps, int relu, float* mean, float* invstd, float* ws, hipStream_t st) {
   if (C % 8) return MDTF_EINVAL;
   Geo g = make_geo(M, C);
   float* p0 = ws;
@@ -326,29 +362,17 @@ MDTF_EXPORT int mdtf_bn_fwd_train(const void* x, const void* res, void* y, long 
   hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, p0, p1, g.gx, M, C, gamma, beta,
                      mmean, mvar, decay, eps, mean, invstd, scale, shift, 0);
   long long n8 = M * C / 8;
-  const bf16_t* r = (const bf16_t*)res;
-  if (r && relu)
-    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x, r,
-                       (bf16_t*)y, n8, C, scale, shift);
-  else if (r)
-    hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x, r,
-                       (bf16_t*)y, n8, C, scale, shift);
-  else if (relu)
-    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
-                       nullptr, (bf16_t*)y, n8, C, scale, shift);
-  else
-    hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
-                       nullptr, (bf16_t*)y, n8, C, scale, shift);
+  launch_apply(x, res, y, mask, n8, C, scale, shift, relu, st);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
 
 // Training forward when the producing conv already emitted Σx / Σx² partials
 // ([P][C] each, e.g. the conv epilogue's 64 atomic slots): finalize + apply only.
-MDTF_EXPORT int mdtf_bn_fwd_stats(const void* x, const void* res, void* y, long long M, int C, const float* gamma,
-                                  const float* beta, float* mmean, float* mvar, float decay, float eps, int relu,
-                                  float* mean, float* invstd, const float* psum, const float* psq, int P, float* ws,
-                                  hipStream_t st) {
+MDTF_EXPORT int mdtf_bn_fwd_stats(const void* x, const void* res, void* y, uint8_t* mask, long long M, int C,
+                                  const float* gamma, const float* beta, float* mmean, float* mvar, float decay,
+                                  float eps, int relu, float* mean, float* invstd, const float* psum, const float* psq,
+                                  int P, float* ws, hipStream_t st) {
   if (C % 8) return MDTF_EINVAL;
   float* scale = ws;
   float* shift = ws + C;
@@ -356,19 +380,7 @@ MDTF_EXPORT int mdtf_bn_fwd_stats(const void* x, const void* res, void* y, long 
   hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M,
                      C, gamma, beta, mmean, mvar, decay, eps, mean, invstd, scale, shift, 1);
   long long n8 = M * C / 8;
-  const bf16_t* r = (const bf16_t*)res;
-  if (r && relu)
-    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x, r,
-                       (bf16_t*)y, n8, C, scale, shift);
-  else if (r)
-    hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x, r,
-                       (bf16_t*)y, n8, C, scale, shift);
-  else if (relu)
-    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
-                       nullptr, (bf16_t*)y, n8, C, scale, shift);
-  else
-    hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
-                       nullptr, (bf16_t*)y, n8, C, scale, shift);
+  launch_apply(x, res, y, mask, n8, C, scale, shift, relu, st);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
@@ -377,31 +389,20 @@ MDTF_EXPORT int mdtf_bn_fwd_stats(const void* x, const void* res, void* y, long 
 MDTF_EXPORT int mdtf_bn_fwd_eval(const void* x, const void* res, void* y, long long M, int C, const float* gamma,
                                  const float* beta, const float* mmean, const float* mvar, float eps, int relu,
                                  float* ws, hipStream_t st) {
+  uint8_t* mask = nullptr;
   if (C % 8) return MDTF_EINVAL;
   float* scale = ws;
   float* shift = ws + C;
   hipLaunchKernelGGL(bn_eval_coeffs, dim3(ceil_div(C, 256)), dim3(256), 0, st, C, gamma, beta, mmean, mvar, eps,
                      scale, shift);
   long long n8 = M * C / 8;
-  const bf16_t* r = (const bf16_t*)res;
-  if (r && relu)
-    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x, r,
-                       (bf16_t*)y, n8, C, scale, shift);
-  else if (r)
-    hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x, r,
-                       (bf16_t*)y, n8, C, scale, shift);
-  else if (relu)
-    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
-                       nullptr, (bf16_t*)y, n8, C, scale, shift);
-  else
-    hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
-                       nullptr, (bf16_t*)y, n8, C, scale, shift);
+  launch_apply(x, res, y, mask, n8, C, scale, shift, relu, st);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
 
-// Backward. y is the forward output (ReLU mask); dres may be null.
-MDTF_EXPORT int mdtf_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* dres, long long M, int C,
+// Backward. mask: the forward's ReLU bitmask (relu only); dres may be null.
+MDTF_EXPORT int mdtf_bn_bwd(const void* dy, const void* x, const void* mask, void* dx, void* dres, long long M, int C,
                             const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
                             int relu, float* ws, hipStream_t st) {
   if (C % 8) return MDTF_EINVAL;
@@ -414,7 +415,7 @@ MDTF_EXPORT int mdtf_bn_bwd(const void* dy, const void* x, const void* y, void* 
   size_t lds = 2 * sizeof(float) * g.rg * g.tpr * 8;
   if (relu)
     hipLaunchKernelGGL((bn_reduce_kernel<true, true>), dim3(g.gx, g.gy), dim3(kThreads), lds, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, (const bf16_t*)y, M, C, g.tpr, g.rg, p0, p1);
+                       (const bf16_t*)x, (const uint8_t*)mask, M, C, g.tpr, g.rg, p0, p1);
   else
     hipLaunchKernelGGL((bn_reduce_kernel<true, false>), dim3(g.gx, g.gy), dim3(kThreads), lds, st, (const bf16_t*)dy,
                        (const bf16_t*)x, nullptr, M, C, g.tpr, g.rg, p0, p1);
@@ -423,10 +424,10 @@ MDTF_EXPORT int mdtf_bn_bwd(const void* dy, const void* x, const void* y, void* 
   long long n8 = M * C / 8;
   if (relu && dres)
     hipLaunchKernelGGL((bn_dx_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, (const bf16_t*)y, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3);
+                       (const bf16_t*)x, (const uint8_t*)mask, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3);
   else if (relu)
     hipLaunchKernelGGL((bn_dx_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, (const bf16_t*)y, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3);
+                       (const bf16_t*)x, (const uint8_t*)mask, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3);
   else if (dres)
     hipLaunchKernelGGL((bn_dx_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
                        (const bf16_t*)x, nullptr, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3);

@@ -5,10 +5,10 @@ from . import _native as N
 from ..train import variables as V
 
 N.register("mdtf_bn_workspace_floats", [N.L, N.I], N.L)
-N.register("mdtf_bn_fwd_train", [N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P])
+N.register("mdtf_bn_fwd_train", [N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P])
 N.register("mdtf_bn_fwd_eval", [N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.I, N.P, N.P])
 N.register("mdtf_bn_bwd", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P, N.P])
-N.register("mdtf_bn_fwd_stats", [N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P,
+N.register("mdtf_bn_fwd_stats", [N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P,
                                  N.I, N.P, N.P])
 
 
@@ -32,24 +32,26 @@ class _BNTrain(torch.autograd.Function):
         y = torch.empty_like(x)
         mean = torch.empty(C, dtype=torch.float32, device=x.device)
         invstd = torch.empty_like(mean)
+        # ReLU: 1-bit-per-element mask for the backward (instead of keeping / re-reading y)
+        mask = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device) if relu else None
         g, b = _f32(gamma), _f32(beta)
         res = residual.contiguous() if residual is not None else None
         if stats is not None:
             # Σx / Σx² already produced by the conv epilogue: finalize + apply only
             psum, psq, P = stats
             ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
-            N.check(N.fn("mdtf_bn_fwd_stats")(N.ptr(x), N.ptr(res), N.ptr(y), M, C, N.ptr(g), N.ptr(b), N.ptr(mm),
-                                              N.ptr(mv), float(decay), float(eps), int(relu), N.ptr(mean),
+            N.check(N.fn("mdtf_bn_fwd_stats")(N.ptr(x), N.ptr(res), N.ptr(y), N.ptr(mask), M, C, N.ptr(g), N.ptr(b),
+                                              N.ptr(mm), N.ptr(mv), float(decay), float(eps), int(relu), N.ptr(mean),
                                               N.ptr(invstd), N.ptr(psum), N.ptr(psq), int(P), N.ptr(ws),
                                               N.stream_ptr()), "bn_fwd_stats")
             from . import conv as _conv
             _conv.stats_consumed(x.device)           # the finalize kernel re-zeroed the partials
         else:
             ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
-            N.check(N.fn("mdtf_bn_fwd_train")(N.ptr(x), N.ptr(res), N.ptr(y), M, C, N.ptr(g), N.ptr(b), N.ptr(mm),
-                                              N.ptr(mv), float(decay), float(eps), int(relu), N.ptr(mean),
+            N.check(N.fn("mdtf_bn_fwd_train")(N.ptr(x), N.ptr(res), N.ptr(y), N.ptr(mask), M, C, N.ptr(g), N.ptr(b),
+                                              N.ptr(mm), N.ptr(mv), float(decay), float(eps), int(relu), N.ptr(mean),
                                               N.ptr(invstd), N.ptr(ws), N.stream_ptr()), "bn_fwd_train")
-        ctx.save_for_backward(x, y, g, mean, invstd)
+        ctx.save_for_backward(x, mask if mask is not None else y.new_empty(0), g, mean, invstd)
         ctx.has_res = residual is not None
         ctx.relu = relu
         ctx.has_gamma = gamma is not None
@@ -61,7 +63,7 @@ class _BNTrain(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, g, mean, invstd = ctx.saved_tensors
+        x, mask, g, mean, invstd = ctx.saved_tensors
         dy = dy.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
@@ -72,7 +74,8 @@ class _BNTrain(torch.autograd.Function):
         dgamma = sg.grad if sg is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
         dbeta = sb.grad if sb is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
         ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
-        N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(x), N.ptr(y), N.ptr(dx), N.ptr(dres), M, C, N.ptr(g),
+        N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(x), N.ptr(mask if ctx.relu else None), N.ptr(dx), N.ptr(dres), M,
+                                    C, N.ptr(g),
                                     N.ptr(mean), N.ptr(invstd), N.ptr(dgamma), N.ptr(dbeta), int(ctx.relu), N.ptr(ws),
                                     N.stream_ptr()), "bn_bwd")
         gamma, beta = ctx.like
