@@ -224,7 +224,14 @@ class AsyncWorker(object):
         t0 = time.time()
         window = t0
         last = None
+        import os
+        bench_warmup = int(os.environ.get("MDTF_BENCH_WARMUP", "0"))
+        t_bench = None
         while True:
+            if self.steps_done == bench_warmup and t_bench is None:
+                if V.get_store().device.type == "cuda":
+                    torch.cuda.synchronize()
+                t_bench = time.time()
             ctx = S.RunContext({})
             for v in self.vars:
                 v.uses = 0
@@ -243,6 +250,14 @@ class AsyncWorker(object):
                 window = now
             if step >= self.total_step:
                 break
+        if V.get_store().device.type == "cuda":
+            torch.cuda.synchronize()
+        out_dir = os.environ.get("MDTF_BENCH_OUT")
+        if out_dir and t_bench is not None:
+            timed = self.steps_done - bench_warmup
+            with open(os.path.join(out_dir, "worker%d.json" % self.op.task_index), "w") as f:
+                json.dump({"steps": timed, "seconds": time.time() - t_bench, "batch": self.op.batch_size,
+                           "staleness": getattr(self, "staleness", None)}, f)
         if is_chief and self.op.model_dir:
             self.pull_masters()
             V.get_or_create_global_step().assign(self.store.add(gs_key, 0))
