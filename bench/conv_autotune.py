@@ -54,7 +54,8 @@ def resnet_convs(depth=50, batch=256, image=224, width=64):
 WG2_TILES = ((128, 128, 2), (128, 128, 3), (128, 64, 2), (64, 128, 2), (64, 64, 3))
 # (bm, bn, stages): LDS = stages * (bm + bn) * 128 B <= 160 KiB
 V2_TILES = ((128, 128, 2), (128, 128, 3), (128, 128, 4), (128, 64, 3), (128, 64, 4), (256, 128, 2), (256, 128, 3),
-            (256, 64, 3), (64, 128, 2), (64, 128, 3), (64, 128, 4), (64, 64, 4))
+            (256, 64, 3), (64, 128, 2), (64, 128, 3), (64, 128, 4), (64, 64, 4),
+            (128, 128, 1), (128, 64, 1), (256, 128, 1), (64, 128, 1), (256, 64, 1))   # stages 1: K == 64 only
 
 
 def timeit(fn, reps, warm=3):

@@ -129,7 +129,7 @@ def heartbeat_settings():
     """(enabled, interval, timeout) from MDTF_HEARTBEAT / _INTERVAL / _TIMEOUT."""
     enabled = os.environ.get("MDTF_HEARTBEAT", "1") not in ("0", "false", "off")
     return (enabled, float(os.environ.get("MDTF_HEARTBEAT_INTERVAL", "1.0")),
-            float(os.environ.get("MDTF_HEARTBEAT_TIMEOUT", "60.0")))
+            float(os.environ.get("MDTF_HEARTBEAT_TIMEOUT", "300.0")))
 
 
 class FaultInjectionHook(H.SessionRunHook):

@@ -144,7 +144,10 @@ class Server(object):
             self.store = dist.distributed_c10d._get_default_store()
             self.worker_group = dist.group.WORLD
             self._started = True
-            self._start_heartbeat(dist.get_rank(), dist.get_world_size())
+            # torchrun's elastic agent already tears the job down when a rank dies;
+            # the heartbeat watchdog is opt-in there (MDTF_HEARTBEAT=1)
+            if os.environ.get("MDTF_HEARTBEAT") == "1":
+                self._start_heartbeat(dist.get_rank(), dist.get_world_size())
             return
         host, port = split_address(self.cluster.coordinator_address())
         self.store = dist.TCPStore(host, port, is_master=self.is_coordinator, timeout=timeout,

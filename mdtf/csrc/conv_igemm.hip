@@ -491,7 +491,7 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
   constexpr int PER_STAGE = RA + RB;               // LDS-DMA wave-instructions per stage
   constexpr unsigned OOB = 0x80000000u;            // buffer offset past num_records -> zero fill
   static_assert(RA >= 1 && RB >= 1, "tile too small");
-  static_assert(STAGES >= 2 && (STAGES - 2) * PER_STAGE < 64, "pipeline depth");
+  static_assert(STAGES >= 1 && (STAGES < 2 || (STAGES - 2) * PER_STAGE < 64), "pipeline depth");  // 1: K == 64 only
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -590,18 +590,18 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
   const int KT = a.K / 64;
   // prologue: stages 0 .. STAGES-2 in flight
 #pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
+  for (int s = 0; s < (STAGES > 1 ? STAGES - 1 : 1); ++s)
     if (s < KT) stage(s);
   const int fr = lane & 15, fq = lane >> 4;
   int cur = 0;
   for (int kt = 0; kt < KT; ++kt) {
     // stage kt must have landed: leave the (STAGES-2) younger stages in flight
-    if (kt + STAGES - 2 < KT)
-      wait_vmcnt<(STAGES - 2) * PER_STAGE>();
+    if (STAGES >= 2 && kt + STAGES - 2 < KT)
+      wait_vmcnt<(STAGES >= 2 ? (STAGES - 2) * PER_STAGE : 0)>();
     else
       wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();          // every wave's DMA for stage kt is in; buffer (kt-1) is free
-    {
+    if (STAGES >= 2) {
       const int nk = kt + STAGES - 1;
       if (nk < KT) stage(nk % STAGES);
     }
@@ -634,7 +634,7 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
   // global stores are 16 B per lane along full output rows; BN statistics from the
   // fp32 accumulators (16-lane shuffles, then one atomic per channel per block)
   constexpr int LDC = BN * 2 + 16;
-  static_assert(BM * LDC <= STAGES * STAGE, "C tile must fit the stage buffers");
+  // (the launcher sizes the LDS as max(stages, C tile))
   const int g = lane >> 4, li = lane & 15;
   __syncthreads();                           // every wave is done reading the stage buffers
 #pragma unroll
@@ -722,7 +722,9 @@ int launch_fd_v2(ConvArgs& a, hipStream_t st) {
   a.ntiles = static_cast<int>(ceil_div(a.Ncol, BN));
   const long long nblk = (long long)a.mtiles * a.ntiles;
   if (nblk > 0x7fffffff) return MDTF_EUNSUPPORTED;
-  const size_t lds = STAGES * (size_t)(BM + BN) * 128;
+  const size_t stage_bytes = STAGES * (size_t)(BM + BN) * 128, ctile = (size_t)BM * (BN * 2 + 16);
+  const size_t lds = stage_bytes > ctile ? stage_bytes : ctile;
+  if (STAGES == 1 && a.K != 64) return MDTF_EINVAL;     // single buffer: one K step only
   hipLaunchKernelGGL((conv_fd_v2<BM, BN, MODE, STATS, STAGES>), dim3((unsigned)nblk), dim3(NT), lds, st, a);
   MDTF_LAUNCH_CHECK();
   return 0;
@@ -742,6 +744,7 @@ int dispatch_fd_v2s(ConvArgs& a, int bm, int bn, hipStream_t st) {
 
 template <int MODE, bool STATS>
 int dispatch_fd_v2(ConvArgs& a, int bm, int bn, int stages, hipStream_t st) {
+  if (stages == 1) return dispatch_fd_v2s<MODE, STATS, 1>(a, bm, bn, st);
   if (stages == 2) return dispatch_fd_v2s<MODE, STATS, 2>(a, bm, bn, st);
   if (stages == 3) return dispatch_fd_v2s<MODE, STATS, 3>(a, bm, bn, st);
   if (stages == 4) return dispatch_fd_v2s<MODE, STATS, 4>(a, bm, bn, st);

@@ -743,3 +743,20 @@ def test_layernorm_fused_dropout():
     assert _rel(y, yr) < 2e-2
     assert _rel(xg.grad, xc.grad) < 2e-2
     assert _rel(rg.grad, rc.grad) < 2e-2
+
+
+@pytest.mark.parametrize("stages", [1, 2, 3])
+def test_conv_v2_stages_k64(stages):
+    """v2 forward/dgrad with a single K step (1x1 conv, 64 channels) at every pipeline depth."""
+    from mdtf.ops import conv as C
+    torch.manual_seed(17)
+    x = torch.randn(4, 10, 10, 64, device=DEV).bfloat16()
+    w = (torch.randn(1, 1, 64, 192, device=DEV) * 0.1).bfloat16()
+    y = C.mdtf_fwd(x, w, (10, 10), (1, 1), (0, 0, 0, 0), (1, 1), 128, 64, None, 2, stages)
+    ref = (x.float().reshape(-1, 64) @ w.float().reshape(64, 192)).reshape(4, 10, 10, 192)
+    assert _rel(y, ref) < 1e-2
+    dy = torch.randn(4, 10, 10, 64, device=DEV).bfloat16()
+    w2 = (torch.randn(1, 1, 192, 64, device=DEV) * 0.1).bfloat16()
+    dx = C.mdtf_dgrad(dy, w2, (4, 10, 10, 192), (1, 1), (0, 0, 0, 0), (1, 1), 128, 64, 2, stages)
+    ref = (dy.float().reshape(-1, 64) @ w2.float().reshape(192, 64).t()).reshape(4, 10, 10, 192)
+    assert _rel(dx, ref) < 1e-2
