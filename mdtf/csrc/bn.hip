@@ -286,7 +286,7 @@ template <bool RELU, bool WRITE_DRES>
 __global__ void __launch_bounds__(kThreads)
     bn_dx_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const uint8_t* __restrict__ mk,
                  bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long n8, int C, const float* __restrict__ k1,
-                 const float* __restrict__ k2, const float* __restrict__ k3) {
+                 const float* __restrict__ k2, const float* __restrict__ k3, int accum_dres) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
     long long off = i * 8;
     int c = static_cast<int>(off % C);
@@ -298,7 +298,17 @@ __global__ void __launch_bounds__(kThreads)
 #pragma unroll
       for (int k = 0; k < 8; ++k) g[k] = ((m8 >> k) & 1u) ? g[k] : 0.f;
     }
-    if (WRITE_DRES) store_bf8(dres + off, g);
+    if (WRITE_DRES) {
+      if (accum_dres) {          // fan-out: add to the other consumer's gradient already there
+        float o[8];
+        load_bf8(dres + off, o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] += g[k];
+        store_bf8(dres + off, o);
+      } else {
+        store_bf8(dres + off, g);
+      }
+    }
     float4 a0 = *reinterpret_cast<const float4*>(k1 + c), a1 = *reinterpret_cast<const float4*>(k1 + c + 4);
     float4 b0 = *reinterpret_cast<const float4*>(k2 + c), b1 = *reinterpret_cast<const float4*>(k2 + c + 4);
     float4 e0 = *reinterpret_cast<const float4*>(k3 + c), e1 = *reinterpret_cast<const float4*>(k3 + c + 4);
@@ -404,7 +414,7 @@ MDTF_EXPORT int mdtf_bn_fwd_eval(const void* x, const void* res, void* y, long l
 // Backward. mask: the forward's ReLU bitmask (relu only); dres may be null.
 MDTF_EXPORT int mdtf_bn_bwd(const void* dy, const void* x, const void* mask, void* dx, void* dres, long long M, int C,
                             const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
-                            int relu, float* ws, hipStream_t st) {
+                            int relu, float* ws, int accum_dres, hipStream_t st) {
   if (C % 8) return MDTF_EINVAL;
   Geo g = make_geo(M, C);
   float* p0 = ws;
@@ -424,16 +434,16 @@ MDTF_EXPORT int mdtf_bn_bwd(const void* dy, const void* x, const void* mask, voi
   long long n8 = M * C / 8;
   if (relu && dres)
     hipLaunchKernelGGL((bn_dx_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, (const uint8_t*)mask, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3);
+                       (const bf16_t*)x, (const uint8_t*)mask, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3, accum_dres);
   else if (relu)
     hipLaunchKernelGGL((bn_dx_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, (const uint8_t*)mask, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3);
+                       (const bf16_t*)x, (const uint8_t*)mask, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3, 0);
   else if (dres)
     hipLaunchKernelGGL((bn_dx_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, nullptr, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3);
+                       (const bf16_t*)x, nullptr, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3, accum_dres);
   else
     hipLaunchKernelGGL((bn_dx_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, nullptr, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3);
+                       (const bf16_t*)x, nullptr, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3, 0);
   MDTF_LAUNCH_CHECK();
   return 0;
 }

@@ -56,6 +56,7 @@ struct ConvArgs {
   int ksplit_steps;    // wgrad: K steps per split
   int stat_slots;      // fwd: BN-statistics partial rows (power of two: atomics spread; = mtiles: deterministic)
   int ld_dy, ld_dw;    // wgrad v2: row strides of DY and DW in elements (Cout for convolutions)
+  int accumulate;      // fwd/dgrad v2: out += result (fan-out gradient accumulation) instead of out = result
 };
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p, bool ok) {
@@ -654,8 +655,25 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
     const int row = idx / (BN / 8), c8 = idx - row * (BN / 8);
     const long long m = m0 + row;
     const int n = n0 + c8 * 8;
-    if (m < a.M && n < a.Ncol)
-      *reinterpret_cast<uint4*>(a.out + m * a.Ncol + n) = *reinterpret_cast<const uint4*>(smem_raw + row * LDC + c8 * 16);
+    if (m < a.M && n < a.Ncol) {
+      uint4 v = *reinterpret_cast<const uint4*>(smem_raw + row * LDC + c8 * 16);
+      bf16_t* dst = a.out + m * a.Ncol + n;
+      if (a.accumulate) {        // second contribution to a fanned-out activation gradient
+        float o[8], c[8];
+        load_bf8(dst, o);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          c[2 * k] = __uint_as_float(w4[k] << 16);
+          c[2 * k + 1] = __uint_as_float(w4[k] & 0xffff0000u);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] += c[k];
+        store_bf8(dst, o);
+      } else {
+        *reinterpret_cast<uint4*>(dst) = v;
+      }
+    }
   }
   if (STATS) {
     float ssum[TN][4], ssq[TN][4];
@@ -1105,7 +1123,7 @@ MDTF_EXPORT int mdtf_conv_fwd_v2(const void* x, const void* wt, void* y, float* 
 // v2 (Cout % 64 == 0): DX = dgrad(DY, W), W in HWIO
 MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int OH,
                                    int OW, int Cout, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW,
-                                   int bm, int bn, hipStream_t st) {
+                                   int bm, int bn, int accumulate, hipStream_t st) {
   if (Cout % 64 || Cin % 8) return MDTF_EINVAL;
   if (SH != 1 || SW != 1 || KH * KW > 32 || (long long)N * OH * OW * Cout * 2 > 0x7fffffffLL)
     return MDTF_EUNSUPPORTED;
@@ -1113,6 +1131,7 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
   a.src = (const bf16_t*)dy;
   a.wgt = (const bf16_t*)w;
   a.out = (bf16_t*)dx;
+  a.accumulate = accumulate;
   a.M = (long long)N * H * W;
   a.Ncol = Cin;
   a.K = KH * KW * Cout;

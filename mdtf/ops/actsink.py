@@ -1,0 +1,69 @@
+"""Fan-out activation gradients accumulated in place (no autograd add kernel).
+
+A ResNet block input feeds two consumers: the first conv of the block and
+the residual branch (the identity into the last BatchNorm, or the projection
+conv).  In stock autograd each consumer returns its own full-size gradient and
+the engine adds them (a read-read-write bf16 pass per block).  Here the
+producing BatchNorm attaches an :class:`ActGradSink` to its output.  A
+sink-aware consumer writes its gradient straight into the sink buffer:
+- the first contributor's tensor is adopted as the buffer;
+- a later contributor accumulates into it (the v2 conv dgrad epilogue and the
+  BN backward's residual-gradient store both have an accumulate mode);
+- the contributor then returns ``None`` to autograd.
+The producer's backward (called with ``None`` once all consumers are done)
+takes the summed gradient from the sink. It also adds whatever ordinary autograd
+gradient arrived, so consumers that are not sink-aware stay correct.
+"""
+
+
+class ActGradSink(object):
+    __slots__ = ("buf", "count")
+
+    def __init__(self):
+        self.buf = None
+        self.count = 0
+
+    def adopt_or_add(self, g):
+        """Contribute a materialised gradient tensor."""
+        if self.buf is None:
+            self.buf = g
+        else:
+            self.buf.add_(g)
+        self.count += 1
+
+    def target(self):
+        """(buffer, accumulate) for a kernel that writes its contribution in place; call
+        :meth:`written` after launching it.  ``None`` buffer: allocate and write (accumulate False)."""
+        return self.buf, self.buf is not None
+
+    def written(self, buf):
+        self.buf = buf
+        self.count += 1
+
+    def take(self, dy):
+        """Producer side: the total gradient (autograd's ``dy`` may be None)."""
+        if self.count == 0:
+            return dy
+        total = self.buf
+        if dy is not None:
+            total = total.add_(dy)
+        self.buf, self.count = None, 0
+        return total
+
+
+ENABLED = True      # switch for A/B tests (tests/test_kernels_gpu.py)
+
+
+def attach(t):
+    if not ENABLED:
+        return None
+    s = ActGradSink()
+    try:
+        t._mdtf_act_sink = s
+    except AttributeError:          # pragma: no cover
+        return None
+    return s
+
+
+def sink_of(t):
+    return getattr(t, "_mdtf_act_sink", None) if t is not None else None

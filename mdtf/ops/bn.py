@@ -7,7 +7,7 @@ from ..train import variables as V
 N.register("mdtf_bn_workspace_floats", [N.L, N.I], N.L)
 N.register("mdtf_bn_fwd_train", [N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P])
 N.register("mdtf_bn_fwd_eval", [N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.I, N.P, N.P])
-N.register("mdtf_bn_bwd", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P, N.P])
+N.register("mdtf_bn_bwd", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P, N.I, N.P])
 N.register("mdtf_bn_fwd_stats", [N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P,
                                  N.I, N.P, N.P])
 
@@ -26,6 +26,9 @@ def _f32(t):
 class _BNTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, mm, mv, decay, eps, relu, stats):
+        from . import actsink
+        ctx.set_materialize_grads(False)
+        ctx.res_sink = actsink.sink_of(residual)       # residual fan-out: write dres into the producer's sink
         x = x.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
@@ -59,16 +62,28 @@ class _BNTrain(torch.autograd.Function):
         ctx.sinks = (V.grad_sink(gamma) if gamma is not None else None,
                      V.grad_sink(beta) if beta is not None else None)
         ctx.like = (gamma, beta)
+        ctx.out_sink = actsink.attach(y)             # this output's consumers may accumulate here
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mask, g, mean, invstd = ctx.saved_tensors
+        if ctx.out_sink is not None:
+            dy = ctx.out_sink.take(dy)
+        if dy is None:
+            return (None,) * 10
         dy = dy.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
         dx = torch.empty_like(x)
-        dres = torch.empty_like(x) if ctx.has_res else None
+        dres, accum = None, 0
+        rs = ctx.res_sink if ctx.needs_input_grad[3] else None
+        if ctx.has_res:
+            if rs is not None:
+                dres, acc = rs.target()
+                accum = int(acc)
+            if dres is None:
+                dres = torch.empty_like(x)
         sg, sb = ctx.sinks
         # dgamma/dbeta accumulate straight into the fp32 grad slots when available
         dgamma = sg.grad if sg is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
@@ -77,7 +92,10 @@ class _BNTrain(torch.autograd.Function):
         N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(x), N.ptr(mask if ctx.relu else None), N.ptr(dx), N.ptr(dres), M,
                                     C, N.ptr(g),
                                     N.ptr(mean), N.ptr(invstd), N.ptr(dgamma), N.ptr(dbeta), int(ctx.relu), N.ptr(ws),
-                                    N.stream_ptr()), "bn_bwd")
+                                    accum, N.stream_ptr()), "bn_bwd")
+        if rs is not None and dres is not None:
+            rs.written(dres)
+            dres = None                                  # delivered through the sink
         gamma, beta = ctx.like
         rg = (V.grad_marker(gamma) if sg is not None else dgamma) if ctx.has_gamma else None
         rb = (V.grad_marker(beta) if sb is not None else dbeta) if ctx.has_beta else None

@@ -22,7 +22,7 @@ N.register("mdtf_conv_fwd", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P])
 N.register("mdtf_conv_dgrad", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
 N.register("mdtf_conv_wgrad", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 N.register("mdtf_conv_fwd_v2", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P])
-N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
+N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 N.register("mdtf_conv_wgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -180,13 +180,19 @@ def mdtf_fwd(x, w, out_hw, stride, pads, dil, bm, bn, stats=None, ver=1, stages=
     return y
 
 
-def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn, ver=1, stages=2):
-    dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
+def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn, ver=1, stages=2, out=None, accumulate=False):
+    """DX of a conv; v2 can write into ``out`` and accumulate (out += dgrad) in its epilogue."""
+    dx = out if out is not None else torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
     n, h, wd, c = x_shape
     kh, kw, ci, co = w.shape
-    N.check(N.fn("mdtf_conv_dgrad_v2" if ver == 2 else "mdtf_conv_dgrad")(N.ptr(dy), N.ptr(w), N.ptr(dx), n, h, wd, c, dy.shape[1], dy.shape[2], co, kh,
-                                    kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
-                                    bm + 1000 * stages if ver == 2 else bm, bn, N.stream_ptr()), "conv_dgrad")
+    geo = [n, h, wd, c, dy.shape[1], dy.shape[2], co, kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1]]
+    if ver == 2:
+        N.check(N.fn("mdtf_conv_dgrad_v2")(N.ptr(dy), N.ptr(w), N.ptr(dx), *geo, bm + 1000 * stages, bn,
+                                           int(bool(accumulate)), N.stream_ptr()), "conv_dgrad_v2")
+        return dx
+    if accumulate:
+        raise ValueError("accumulating dgrad needs the v2 kernel")
+    N.check(N.fn("mdtf_conv_dgrad")(N.ptr(dy), N.ptr(w), N.ptr(dx), *geo, bm, bn, N.stream_ptr()), "conv_dgrad")
     return dx
 
 
@@ -242,7 +248,9 @@ def stats_consumed(device):
 class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, pads, dil, out_hw, want_stats):
+        from . import actsink
         ctx.set_materialize_grads(False)      # no zero-filled grads for the (non-differentiable) stats outputs
+        ctx.x_sink = actsink.sink_of(x)       # fanned-out input: dgrad accumulates into the producer's sink
         x = x.contiguous()
         w = w.contiguous()
         ch = choose("fwd", x.shape, w.shape, stride, pads, dil)
@@ -295,8 +303,18 @@ class _Conv(torch.autograd.Function):
                     dw = V.grad_marker(w)
                 else:
                     dw = ldw
+        xs = ctx.x_sink if need_dx else None
         if need_dx and not lib_dx:
-            dx = mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5])
+            if xs is not None and cd[4] == 2:
+                buf, acc = xs.target()
+                xs.written(mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5], out=buf,
+                                      accumulate=acc))
+                dx = None
+            else:
+                dx = mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5])
+        if xs is not None and dx is not None:
+            xs.adopt_or_add(dx)                    # library / v1 dgrad: contribute the tensor
+            dx = None
         if need_dw and not lib_dw:
             if sink is not None:
                 # fp32 atomics of the wgrad kernel accumulate into the flat gradient buffer

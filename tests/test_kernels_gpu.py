@@ -760,3 +760,50 @@ def test_conv_v2_stages_k64(stages):
     dx = C.mdtf_dgrad(dy, w2, (4, 10, 10, 192), (1, 1), (0, 0, 0, 0), (1, 1), 128, 64, 2, stages)
     ref = (dy.float().reshape(-1, 64) @ w2.float().reshape(192, 64).t()).reshape(4, 10, 10, 192)
     assert _rel(dx, ref) < 1e-2
+
+
+class _TinyRes(object):
+    """Fan-out activations as in ResNet: a BN output feeding a conv AND a residual (identity block),
+    then a block input feeding two convs (projection shortcut) -- exercises the activation-gradient sinks."""
+
+    def inference(self, x):
+        from mdtf.layers import tools
+        from mdtf.train import variables as V
+        store = V.get_store()
+        if store.compute_dtype is not None:
+            x = x.to(store.compute_dtype)
+        s = tools.conv_bn("c1", x, 64, 3, 1, relu=True)
+        y = tools.conv_bn("c2", s, 64, 1, 1, relu=True)
+        x = tools.conv_bn("c3", y, 64, 3, 1, relu=True, residual=s)          # s: conv + identity residual
+        sc = tools.conv_bn("sc", x, 128, 1, 1, relu=False)                   # x: projection conv + main conv
+        z = tools.conv_bn("c4", x, 64, 1, 1, relu=True)
+        x = tools.conv_bn("c5", z, 128, 3, 1, relu=True, residual=sc)
+        x = ops.global_avg_pool(x)
+        return tools.dense("logits", x, 16)
+
+
+@pytest.mark.parametrize("conv_backend", ["mdtf2", "miopen"])
+def test_fanout_gradient_sinks(conv_backend, monkeypatch):
+    """In-place fan-out gradient accumulation == autograd's add (same kernels otherwise), and both ~ fp32 CPU."""
+    from mdtf.ops import actsink
+    monkeypatch.setenv("MDTF_CONV", conv_backend)
+    global _Tiny
+    saved = _Tiny
+    _Tiny = _TinyRes
+    try:
+        torch.manual_seed(3)
+        x = torch.randn(16, 12, 12, 64)
+        y = torch.randint(0, 16, (16,))
+        lc, gc = _tiny_step("cpu", None, x, y)
+        lg, gg = _tiny_step(DEV, torch.bfloat16, x, y)
+        actsink.ENABLED = False
+        try:
+            lo, go = _tiny_step(DEV, torch.bfloat16, x, y)
+        finally:
+            actsink.ENABLED = True
+    finally:
+        _Tiny = saved
+    assert abs(lc - lg) / lc < 5e-3 and lo == lg
+    for k in gc:
+        assert _rel(gg[k], go[k]) < 2e-2, (k, _rel(gg[k], go[k]))        # sinks vs autograd adds
+        assert _rel(gg[k], gc[k]) < 0.25, (k, _rel(gg[k], gc[k]))        # bf16 path vs fp32 (deep-layer noise)
