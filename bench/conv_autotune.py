@@ -58,6 +58,17 @@ V2_TILES = ((128, 128, 2), (128, 128, 3), (128, 128, 4), (128, 64, 3), (128, 64,
             (128, 128, 1), (128, 64, 1), (256, 128, 1), (64, 128, 1), (256, 64, 1))   # stages 1: K == 64 only
 
 
+def _stats(co, bm, M):
+    """Statistics buffer as conv_bn uses it (slot count as in ops/conv.py)."""
+    import torch
+    mtiles = -(-M // bm)
+    slots = C.STAT_SLOTS
+    while slots < 1024 and slots * 8 < mtiles:
+        slots *= 2
+    buf = torch.zeros((2, slots, co), dtype=torch.float32, device="cuda")
+    return (buf[0], buf[1])
+
+
 def timeit(fn, reps, warm=3):
     for _ in range(warm):
         fn()
@@ -105,8 +116,9 @@ def main():
                 cands = [(bm, bn, 0, 1) for bm, bn in ((128, 128), (128, 64), (64, 64), (256, 64))]
                 if C.v2_ok("fwd", c, co, (s, s), kh * kw):
                     cands += [(bm, bn, st, 2) for bm, bn, st in V2_TILES]
-                mk = lambda bm, bn, sp, v: (lambda: C.mdtf_fwd(x, wt, (oh, ow), (s, s), pads4, (1, 1), bm, bn,  # noqa
-                                                             None, v, sp))
+                # training always runs conv -> BN: time the forward with its fused statistics epilogue
+                mk = lambda bm, bn, sp, v: (lambda st=_stats(co, bm, n * oh * ow): C.mdtf_fwd(  # noqa
+                    x, wt, (oh, ow), (s, s), pads4, (1, 1), bm, bn, st, v, sp))
             elif pass_ == "dgrad":
                 lib = lambda: C.miopen_bwd(x, wt, dy, (s, s), pads4, (1, 1), True, False)  # noqa: E731
                 cands = [(bm, bn, 0, 1) for bm, bn in ((128, 128), (128, 64), (64, 64), (256, 64))]

@@ -258,9 +258,13 @@ class _Conv(torch.autograd.Function):
         if ch[0] == "mdtf":
             if want_stats:
                 co = w.shape[3]
-                slots = STAT_SLOTS
+                mtiles = -(-x.shape[0] * out_hw[0] * out_hw[1] // ch[1])
                 if N.deterministic():       # one partial row per M tile: no atomic reordering
-                    slots = -(-x.shape[0] * out_hw[0] * out_hw[1] // ch[1])
+                    slots = mtiles
+                else:                       # ~8 M tiles per atomic row: low contention, small finalize
+                    slots = STAT_SLOTS
+                    while slots < 1024 and slots * 8 < mtiles:
+                        slots *= 2
                 buf = _stats_buffer(co, x.device, slots)
                 stats = (buf[0], buf[1])
             y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2], stats, ch[4], ch[5])
