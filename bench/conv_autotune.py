@@ -92,6 +92,8 @@ def main():
     p.add_argument("--out", default=C.TABLE_PATH)
     p.add_argument("--report", default="gpurun_out/conv_autotune.md")
     p.add_argument("--passes", default="fwd,dgrad,wgrad")
+    p.add_argument("--strides", default="", help="only shapes with these strides (e.g. 2)")
+    p.add_argument("--merge", action="store_true", help="update the existing table at --out instead of replacing it")
     args = p.parse_args()
     dev = torch.device("cuda")
     shapes, all_convs = resnet_convs(args.depth, args.batch)
@@ -101,6 +103,9 @@ def main():
              "|---|---|---|---|---|---|---|"]
     tot = {"miopen": 0.0, "best": 0.0}
     torch.manual_seed(0)
+    if args.strides:
+        keep = {int(v) for v in args.strides.split(",")}
+        shapes = [sh for sh in shapes if sh[7] in keep]
     for (n, h, w, c, kh, kw, co, s, pads) in shapes:
         x = torch.randn(n, h, w, c, device=dev).bfloat16()
         wt = (torch.randn(kh, kw, c, co, device=dev) * 0.05).bfloat16()
@@ -170,6 +175,11 @@ def main():
     lines.append("Total conv time per training step (sum over passes x occurrences): MIOpen %.2f ms, "
                  "best-of %.2f ms" % (tot["miopen"], tot["best"]))
     print(lines[-1])
+    if args.merge and os.path.exists(args.out):
+        with open(args.out) as f:
+            merged = json.load(f)
+        merged.update(table)
+        table = merged
     with open(args.out, "w") as f:
         json.dump(table, f, indent=1, sort_keys=True)
     os.makedirs(os.path.dirname(args.report) or ".", exist_ok=True)

@@ -42,7 +42,7 @@ Geo make_geo(long long M, int C) {
   g.rg = kThreads / t;
   g.gy = static_cast<int>(ceil_div(cv, t));
   long long gx = ceil_div(M, (long long)g.rg * 16);  // >= 16 rows per row-group
-  long long cap = 256 / g.gy;
+  long long cap = 1024 / g.gy;   // ~4 blocks per CU: enough bytes in flight for HBM
   if (cap < 1) cap = 1;
   if (gx > cap) gx = cap;
   if (gx < 1) gx = 1;
@@ -152,9 +152,10 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
-// Sum the [gx][C] partials of 64 channels with a 64 x 16 thread block:
-// 16 row groups stream the partials in parallel (fp32), combined in fp64.
-constexpr int kFinCh = 64, kFinGroups = 16;
+// Sum the [gx][C] partials of 32 channels with a 32 x 32 thread block: 32 row
+// groups stream the partials (fp32, 4 independent loads in flight per thread),
+// combined in fp64.  Small blocks so even C = 64 spreads over a few CUs.
+constexpr int kFinCh = 32, kFinGroups = 32;
 
 // Σ over gx partial rows; zero_after: reset the rows read (persistent, reusable stats buffers)
 __device__ __forceinline__ bool sum_partials(const float* __restrict__ p0, const float* __restrict__ p1, int gx, int C,
@@ -162,21 +163,29 @@ __device__ __forceinline__ bool sum_partials(const float* __restrict__ p0, const
   __shared__ double L0[kFinGroups][kFinCh], L1[kFinGroups][kFinCh];
   const int lc = threadIdx.x % kFinCh, grp = threadIdx.x / kFinCh;
   const int c = blockIdx.x * kFinCh + lc;
-  float a = 0.f, b = 0.f;
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
   if (c < C) {
-    for (int i = grp; i < gx; i += kFinGroups) {
-      a += p0[(long long)i * C + c];
-      b += p1[(long long)i * C + c];
+    int i = grp;
+    for (; i + 3 * kFinGroups < gx; i += 4 * kFinGroups) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] += p0[(long long)(i + u * kFinGroups) * C + c];
+        b[u] += p1[(long long)(i + u * kFinGroups) * C + c];
+      }
+    }
+    for (; i < gx; i += kFinGroups) {
+      a[0] += p0[(long long)i * C + c];
+      b[0] += p1[(long long)i * C + c];
     }
     if (zero_after) {
-      for (int i = grp; i < gx; i += kFinGroups) {
-        const_cast<float*>(p0)[(long long)i * C + c] = 0.f;
-        const_cast<float*>(p1)[(long long)i * C + c] = 0.f;
+      for (int r = grp; r < gx; r += kFinGroups) {
+        const_cast<float*>(p0)[(long long)r * C + c] = 0.f;
+        const_cast<float*>(p1)[(long long)r * C + c] = 0.f;
       }
     }
   }
-  L0[grp][lc] = a;
-  L1[grp][lc] = b;
+  L0[grp][lc] = (double)a[0] + (double)a[1] + (double)a[2] + (double)a[3];
+  L1[grp][lc] = (double)b[0] + (double)b[1] + (double)b[2] + (double)b[3];
   __syncthreads();
   if (grp != 0 || c >= C) return false;
   s = 0.0;

@@ -57,6 +57,10 @@ struct ConvArgs {
   int stat_slots;      // fwd: BN-statistics partial rows (power of two: atomics spread; = mtiles: deterministic)
   int ld_dy, ld_dw;    // wgrad v2: row strides of DY and DW in elements (Cout for convolutions)
   int accumulate;      // fwd/dgrad v2: out += result (fan-out gradient accumulation) instead of out = result
+  // strided dgrad (MODE 2), one stride-parity class of DX pixels per launch: pixels
+  // (h0 + SH i, w0 + SW j), i < Hc, j < Wc; their taps kh = kh0 + SH t (t < th), kw = kw0 + SW u (u < tw)
+  // read DY at (q0h + i - t, q0w + j - u)
+  int cls_h0, cls_w0, cls_q0h, cls_q0w, cls_kh0, cls_kw0, cls_Hc, cls_Wc, cls_th, cls_tw;
 };
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p, bool ok) {
@@ -480,7 +484,10 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(ConvArgs a) {
 // LDS rows are 128 B; 16-B chunk c of row r lives at chunk c ^ ((r >> 1) & 7)
 // (the swizzle is applied to the per-lane SOURCE address, the LDS image
 // stays lane-linear), which makes the ds_read_b128 fragment reads of 16 rows
-// conflict-free.  dgrad v2 covers stride 1 (strided dgrad: v1 / MIOpen).
+// conflict-free.  MODE 0 = forward, 1 = stride-1 dgrad, 2 = strided dgrad
+// by stride-parity class: within one class of DX pixels the set of filter
+// taps that reach DY is fixed and the DY offsets are affine again, so each
+// class is a dense implicit GEMM over only its own taps (no zero-tap waste).
 // ============================================================================
 template <int BM, int BN, int MODE, bool STATS, int STAGES>
 __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
@@ -506,14 +513,17 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
   const int GH = MODE == 0 ? a.H : a.OH;
   const int GW = MODE == 0 ? a.W : a.OW;
   const int GC = MODE == 0 ? a.Cin : a.Cout;
-  const int RH = MODE == 0 ? a.OH : a.H;
-  const int RW = MODE == 0 ? a.OW : a.W;
+  const int RH = MODE == 0 ? a.OH : MODE == 1 ? a.H : a.cls_Hc;
+  const int RW = MODE == 0 ? a.OW : MODE == 1 ? a.W : a.cls_Wc;
   const int lrow = lane >> 3;
-  const int ntaps = a.KH * a.KW;                   // <= 32 (host-checked)
+  const int TKW = MODE == 2 ? a.cls_tw : a.KW;      // taps per filter row of the K walk
+  const int ntaps = MODE == 2 ? a.cls_th * a.cls_tw : a.KH * a.KW;   // <= 32 (host-checked)
+  const int DHe = MODE == 2 ? 1 : a.DH, DWe = MODE == 2 ? 1 : a.DW;
 
   // buffer ranges: bounds-checked loads, out-of-range offsets read as zero (host checks < 2 GiB)
   const int bytes_a = (int)((long long)a.N * GH * GW * GC * 2);
-  const int bytes_b = (int)((long long)a.K * a.Ncol * 2);
+  // (MODE 2 walks a subset of the filter taps: the range is the whole filter)
+  const int bytes_b = (int)((long long)(MODE == 2 ? a.KH * a.KW * a.Cout : a.K) * a.Ncol * 2);
 
   // per A row: element offset of tap (0,0) (may be "negative", wraps) + valid-tap bitmask
   unsigned a_off[RA], a_mask[RA];
@@ -527,16 +537,16 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
     const long long t = mm / RW;
     const int oh = static_cast<int>(t % RH);
     const int n = static_cast<int>(t / RH);
-    const int y0 = MODE == 0 ? oh * a.SH - a.PH : oh + a.PH;
-    const int x0 = MODE == 0 ? ow * a.SW - a.PW : ow + a.PW;
+    const int y0 = MODE == 0 ? oh * a.SH - a.PH : MODE == 1 ? oh + a.PH : a.cls_q0h + oh;
+    const int x0 = MODE == 0 ? ow * a.SW - a.PW : MODE == 1 ? ow + a.PW : a.cls_q0w + ow;
     const int ch = 8 * ((lane & 7) ^ ((row >> 1) & 7));
     a_off[i] = (unsigned)((((long long)n * GH + y0) * GW + x0) * GC + ch);
     unsigned mask = 0;
     if (ok) {
       for (int tt = 0; tt < ntaps; ++tt) {
-        const int kh = tt / a.KW, kw = tt - kh * a.KW;
-        const int iy = MODE == 0 ? y0 + kh * a.DH : y0 - kh * a.DH;
-        const int ix = MODE == 0 ? x0 + kw * a.DW : x0 - kw * a.DW;
+        const int kh = tt / TKW, kw = tt - kh * TKW;
+        const int iy = MODE == 0 ? y0 + kh * DHe : y0 - kh * DHe;
+        const int ix = MODE == 0 ? x0 + kw * DWe : x0 - kw * DWe;
         if (iy >= 0 && iy < GH && ix >= 0 && ix < GW) mask |= 1u << tt;
       }
     }
@@ -556,7 +566,7 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
   // scalar K-walk state: tap index, (kh, kw), channel offset c0 within the tap
   int s_t = 0, s_kh = 0, s_kw = 0, s_c0 = 0, s_k0 = 0;
   auto stage = [&](int buf) {
-    const int tap_e = (MODE == 0 ? (s_kh * a.DH * GW + s_kw * a.DW) : -(s_kh * a.DH * GW + s_kw * a.DW)) * GC + s_c0;
+    const int tap_e = (MODE == 0 ? (s_kh * DHe * GW + s_kw * DWe) : -(s_kh * DHe * GW + s_kw * DWe)) * GC + s_c0;
     char* lds = smem_raw + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
@@ -565,7 +575,8 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
       dma16(a.src, bytes_a, lds + (wave + 4 * i) * 1024, voff, 0);
     }
     char* ldsb = lds + BM * ROWB;
-    const int sb = MODE == 0 ? s_k0 * 2 : (s_t * a.Cin * a.Cout + s_c0) * 2;
+    const int wtap = MODE == 2 ? (a.cls_kh0 + a.SH * s_kh) * a.KW + a.cls_kw0 + a.SW * s_kw : s_t;
+    const int sb = MODE == 0 ? s_k0 * 2 : (wtap * a.Cin * a.Cout + s_c0) * 2;
 #pragma unroll
     for (int i = 0; i < RB; ++i)
       dma16(a.wgt, bytes_b, ldsb + (wave + 4 * i) * 1024, b_off[i], sb);
@@ -575,7 +586,7 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
     if (s_c0 == GC) {
       s_c0 = 0;
       ++s_t;
-      if (++s_kw == a.KW) {
+      if (++s_kw == TKW) {
         s_kw = 0;
         ++s_kh;
       }
@@ -609,25 +620,39 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
     const char* As = smem_raw + cur * STAGE;
     cur = cur + 1 == STAGES ? 0 : cur + 1;
     const char* Bs = As + BM * ROWB;
+    // both K halves' fragments in registers; the scheduling groups below issue the first
+    // half's reads, then interleave the second half's reads with the first half's MFMAs
+    bf16x8_t fa[2][TM], fb[2][TN];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      bf16x8_t fa[TM], fb[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * (TM * 16) + i * 16 + fr;
         const int pc = (h * 4 + fq) ^ ((row >> 1) & 7);
-        fa[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(As + row * ROWB + pc * 16));
+        fa[h][i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(As + row * ROWB + pc * 16));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * (TN * 16) + j * 16 + fr;
         const int pc = (h * 4 + fq) ^ ((row >> 1) & 7);
-        fb[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(Bs + row * ROWB + pc * 16));
+        fb[h][j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(Bs + row * ROWB + pc * 16));
       }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fb[j], fa[i], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fb[h][j], fa[h][i], acc[i][j]);
+    {
+      constexpr int R = TM + TN, MF = TM * TN, PER = MF / R > 0 ? MF / R : 1;
+      __builtin_amdgcn_sched_group_barrier(0x100, R, 0);      // half 0 reads
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);  // half 0 MFMAs ...
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);    // ... with one half 1 read each
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * MF, 0); // the rest
     }
   }
 
@@ -647,7 +672,9 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
       float4v v = acc[i][j];
       uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      *reinterpret_cast<uint2*>(smem_raw + pl * LDC + cl * 2) = make_uint2(lo, hi);
+      // 8-B half swap on rows 8..15 of every 16: rows li and li+8 would otherwise share
+      // banks ((LDC/4) % 32 == 4) and the ds_write_b64 would be 2-way
+      *reinterpret_cast<uint2*>(smem_raw + pl * LDC + ((cl * 2) ^ (((pl >> 3) & 1) << 3))) = make_uint2(lo, hi);
     }
   }
   __syncthreads();
@@ -657,7 +684,16 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
     const int n = n0 + c8 * 8;
     if (m < a.M && n < a.Ncol) {
       uint4 v = *reinterpret_cast<const uint4*>(smem_raw + row * LDC + c8 * 16);
-      bf16_t* dst = a.out + m * a.Ncol + n;
+      if ((row >> 3) & 1) v = make_uint4(v.z, v.w, v.x, v.y);
+      long long pix = m;
+      if (MODE == 2) {          // class pixel (n, i, j) -> DX pixel (n, h0 + SH i, w0 + SW j)
+        const int j = static_cast<int>(m % a.cls_Wc);
+        const long long t = m / a.cls_Wc;
+        const int i = static_cast<int>(t % a.cls_Hc);
+        const long long nb = t / a.cls_Hc;
+        pix = (nb * a.H + a.cls_h0 + a.SH * i) * a.W + a.cls_w0 + a.SW * j;
+      }
+      bf16_t* dst = a.out + pix * a.Ncol + n;
       if (a.accumulate) {        // second contribution to a fanned-out activation gradient
         float o[8], c[8];
         load_bf8(dst, o);
@@ -742,7 +778,7 @@ int launch_fd_v2(ConvArgs& a, hipStream_t st) {
   if (nblk > 0x7fffffff) return MDTF_EUNSUPPORTED;
   const size_t stage_bytes = STAGES * (size_t)(BM + BN) * 128, ctile = (size_t)BM * (BN * 2 + 16);
   const size_t lds = stage_bytes > ctile ? stage_bytes : ctile;
-  if (STAGES == 1 && a.K != 64) return MDTF_EINVAL;     // single buffer: one K step only
+  if (STAGES == 1 && a.K > 64) return MDTF_EINVAL;      // single buffer: one K step only
   hipLaunchKernelGGL((conv_fd_v2<BM, BN, MODE, STATS, STAGES>), dim3((unsigned)nblk), dim3(NT), lds, st, a);
   MDTF_LAUNCH_CHECK();
   return 0;
@@ -910,31 +946,38 @@ __global__ void __launch_bounds__(NT) conv_wgrad_v2(ConvArgs a) {
     else
       wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
-    {
-      const int nk = kt + STAGES - 1;
-      if (nk < KT) stage(nk % STAGES);
-    }
     const char* As = smem_raw + cur * STAGE;
     const char* Bs = As + BM * 128;
     cur = cur + 1 == STAGES ? 0 : cur + 1;
+    // all of this step's transposed reads are issued BEFORE the next stage's LDS-DMA: the
+    // compiler makes an LDS read that follows an LDS-DMA wait for it (vmcnt(0)), which would
+    // serialise the DMA with this step's MFMAs
+    bf16x8_t fa[2][TM], fb[2][TN];
 #pragma unroll
     for (int kh2 = 0; kh2 < 2; ++kh2) {
-      bf16x8_t fa[TM], fb[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int col = wm * (TM * 16) + i * 16;           // column within the BM tile
-        fa[i] = frag_tr(As + (col >> 6) * 8192, col & 63, 32 * kh2, lane);
+        fa[kh2][i] = frag_tr(As + (col >> 6) * 8192, col & 63, 32 * kh2, lane);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = wn * (TN * 16) + j * 16;
-        fb[j] = frag_tr(Bs + (col >> 6) * 8192, col & 63, 32 * kh2, lane);
+        fb[kh2][j] = frag_tr(Bs + (col >> 6) * 8192, col & 63, 32 * kh2, lane);
       }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const int nk = kt + STAGES - 1;                      // its buffer was last read in step kt-1
+      if (nk < KT) stage(nk % STAGES);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kh2 = 0; kh2 < 2; ++kh2)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
-    }
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fa[kh2][i], fb[kh2][j], acc[i][j]);
   }
   const int g = lane >> 4, li = lane & 15;
 #pragma unroll
@@ -1125,19 +1168,45 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
                                    int OW, int Cout, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW,
                                    int bm, int bn, int accumulate, hipStream_t st) {
   if (Cout % 64 || Cin % 8) return MDTF_EINVAL;
-  if (SH != 1 || SW != 1 || KH * KW > 32 || (long long)N * OH * OW * Cout * 2 > 0x7fffffffLL)
-    return MDTF_EUNSUPPORTED;
+  if ((long long)N * OH * OW * Cout * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
+  if ((SH != 1 || SW != 1) && (DH != 1 || DW != 1)) return MDTF_EUNSUPPORTED;
+  // <= 32 taps per K walk (per stride-parity class when strided)
+  if (ceil_div(KH, SH) * ceil_div(KW, SW) > 32) return MDTF_EUNSUPPORTED;
   ConvArgs a = make_args(N, H, W, Cin, OH, OW, Cout, KH, KW, SH, SW, PH, PW, DH, DW);
   a.src = (const bf16_t*)dy;
   a.wgt = (const bf16_t*)w;
   a.out = (bf16_t*)dx;
   a.accumulate = accumulate;
-  a.M = (long long)N * H * W;
   a.Ncol = Cin;
-  a.K = KH * KW * Cout;
   const int stages = bm / 1000 ? bm / 1000 : 2;
   bm %= 1000;
-  return dispatch_fd_v2<1, false>(a, bm, bn, stages, st);
+  if (SH == 1 && SW == 1) {
+    a.M = (long long)N * H * W;
+    a.K = KH * KW * Cout;
+    return dispatch_fd_v2<1, false>(a, bm, bn, stages, st);
+  }
+  // strided: one launch per stride-parity class (rh, rw) = ((h + PH) % SH, (w + PW) % SW)
+  for (int rh = 0; rh < SH; ++rh)
+    for (int rw = 0; rw < SW; ++rw) {
+      ConvArgs c = a;
+      c.cls_h0 = ((rh - PH) % SH + SH) % SH;
+      c.cls_w0 = ((rw - PW) % SW + SW) % SW;
+      c.cls_Hc = c.cls_h0 < H ? (H - c.cls_h0 + SH - 1) / SH : 0;
+      c.cls_Wc = c.cls_w0 < W ? (W - c.cls_w0 + SW - 1) / SW : 0;
+      c.cls_kh0 = rh;
+      c.cls_kw0 = rw;
+      c.cls_th = rh < KH ? (KH - rh + SH - 1) / SH : 0;
+      c.cls_tw = rw < KW ? (KW - rw + SW - 1) / SW : 0;
+      c.cls_q0h = (c.cls_h0 + PH - rh) / SH;
+      c.cls_q0w = (c.cls_w0 + PW - rw) / SW;
+      c.M = (long long)N * c.cls_Hc * c.cls_Wc;
+      c.K = c.cls_th * c.cls_tw * Cout;
+      if (c.M == 0 || (c.K == 0 && accumulate)) continue;      // no pixels / nothing to add
+      const int cs = c.K > 64 && stages == 1 ? 2 : stages;
+      const int rc = dispatch_fd_v2<2, false>(c, bm, bn, cs, st);
+      if (rc) return rc;
+    }
+  return 0;
 }
 
 // v2 wgrad (Cin % 64 == 0, Cout % 64 == 0): DW (fp32, HWIO, zeroed or a grad slot) += wgrad(X, DY)

@@ -51,14 +51,14 @@ def _default_tile(ncol):
     return (128, 128) if ncol % 128 == 0 else (128, 64)
 
 
-def v2_ok(pass_, c, co, stride=(1, 1), taps=1):
-    """The BK=64 LDS-DMA kernels: gathered channels % 64 == 0, <= 32 filter taps; dgrad stride 1."""
+def v2_ok(pass_, c, co, stride=(1, 1), taps=1, dil=(1, 1)):
+    """The BK=64 LDS-DMA kernels: gathered channels % 64 == 0, <= 32 filter taps; strided dgrad undilated."""
     if taps > 32:
         return False
     if pass_ == "fwd":
         return c % 64 == 0 and co % 8 == 0
     if pass_ == "dgrad":
-        return co % 64 == 0 and c % 8 == 0 and tuple(stride) == (1, 1)
+        return co % 64 == 0 and c % 8 == 0 and (tuple(stride) == (1, 1) or tuple(dil) == (1, 1))
     if pass_ == "wgrad":
         return c % 64 == 0 and co % 64 == 0
     return False
@@ -79,7 +79,7 @@ def choose(pass_, x_shape, w_shape, stride, pads, dil):
     ent = table().get(shape_key(pass_, x_shape, w_shape, stride, pads, dil))
     if N.deterministic() and pass_ == "wgrad":
         # no split-K atomics, no library algorithm choice: one block per DW tile
-        ver = 2 if v2_ok(pass_, c, co, stride, kh * kw) else 1
+        ver = 2 if v2_ok(pass_, c, co, stride, kh * kw, dil) else 1
         return ("mdtf", 128 if kh * kw * ci >= 128 else 64, 128 if co % 128 == 0 else 64, 1, ver, 2)
     if forced == "auto" and ent is not None:
         if ent["backend"] == "miopen":
@@ -87,11 +87,11 @@ def choose(pass_, x_shape, w_shape, stride, pads, dil):
         return ("mdtf", ent["bm"], ent["bn"], ent.get("splits", 0), ent.get("ver", 1), ent.get("stages", 2))
     if pass_ == "wgrad":
         r = kh * kw * ci
-        ver = 2 if (forced in ("auto", "mdtf2") and v2_ok(pass_, c, co, stride, kh * kw)) else 1
+        ver = 2 if (forced in ("auto", "mdtf2") and v2_ok(pass_, c, co, stride, kh * kw, dil)) else 1
         return ("mdtf", 128 if r >= 128 else 64, 128 if co % 128 == 0 else 64, 0, ver, 2)
     ncol = co if pass_ == "fwd" else ci
     bm, bn = _default_tile(ncol)
-    ver = 2 if (forced in ("auto", "mdtf2") and v2_ok(pass_, c, co, stride, kh * kw)) else 1
+    ver = 2 if (forced in ("auto", "mdtf2") and v2_ok(pass_, c, co, stride, kh * kw, dil)) else 1
     return ("mdtf", bm, bn, 0, ver, 3 if ver == 2 else 2)
 
 

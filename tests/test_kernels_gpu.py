@@ -762,6 +762,35 @@ def test_conv_v2_stages_k64(stages):
     assert _rel(dx, ref) < 1e-2
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,s,h,w,pads", [(3, 2, 15, 14, (1, 1, 1, 1)), (1, 2, 14, 14, (0, 0, 0, 0)),
+                                          (3, 2, 8, 9, (0, 1, 0, 1)), (4, 3, 13, 11, (1, 2, 1, 1)),
+                                          (7, 2, 16, 16, (3, 3, 3, 3))])
+@pytest.mark.parametrize("stages", [1, 2, 3])
+def test_conv_v2_strided_dgrad(k, s, h, w, pads, stages):
+    """Strided dgrad on the v2 kernel, one launch per stride-parity class (classes without taps write
+    zeros), plain and accumulating, vs the fp32 autograd reference."""
+    from mdtf.ops import conv as C
+    torch.manual_seed(k * 100 + h)
+    n, c, co = 2, 72, 128
+    oh = (h + pads[0] + pads[1] - k) // s + 1
+    ow = (w + pads[2] + pads[3] - k) // s + 1
+    wt = (torch.randn(k, k, c, co) / (k * k * c) ** 0.5).bfloat16()
+    dy = torch.randn(n, oh, ow, co).bfloat16()
+    xr = torch.zeros(n, c, h, w, requires_grad=True)
+    yr = torch.nn.functional.conv2d(torch.nn.functional.pad(xr, (pads[2], pads[3], pads[0], pads[1])),
+                                    wt.float().permute(3, 2, 0, 1), stride=s)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    ref = xr.grad.permute(0, 2, 3, 1)
+    dx = C.mdtf_dgrad(dy.to(DEV), wt.to(DEV), (n, h, w, c), (s, s), pads, (1, 1), 64, 64, 2, stages)
+    assert _rel(dx, ref) < 1e-2
+    base = torch.randn(n, h, w, c).bfloat16()
+    out = base.to(DEV).clone()
+    C.mdtf_dgrad(dy.to(DEV), wt.to(DEV), (n, h, w, c), (s, s), pads, (1, 1), 128, 128, 2, stages, out=out,
+                 accumulate=True)
+    assert _rel(out, ref + base.float()) < 1e-2
+
+
 class _TinyRes(object):
     """Fan-out activations as in ResNet: a BN output feeding a conv AND a residual (identity block),
     then a block input feeding two convs (projection shortcut) -- exercises the activation-gradient sinks."""
