@@ -17,6 +17,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mdtf.ops import conv as C  # noqa: E402
+from mdtf.ops import winograd as Wg  # noqa: E402
 from mdtf.ops.padding import conv_geometry  # noqa: E402
 
 
@@ -99,8 +100,8 @@ def main():
     shapes, all_convs = resnet_convs(args.depth, args.batch)
     counts = {s: all_convs.count(s) for s in shapes}
     table = {}
-    lines = ["| pass | shape (N,H,W,C,k,Co,s) | count | miopen ms | best mdtf ms (tile) | TF/s mdtf | choice |",
-             "|---|---|---|---|---|---|---|"]
+    lines = ["| pass | shape (N,H,W,C,k,Co,s) | count | miopen ms | best mdtf ms (tile) | winograd ms | TF/s mdtf |"
+             " choice |", "|---|---|---|---|---|---|---|---|"]
     tot = {"miopen": 0.0, "best": 0.0}
     torch.manual_seed(0)
     if args.strides:
@@ -141,6 +142,12 @@ def main():
                     x, dy, wt.shape, (s, s), pads4, (1, 1), bm[0] if v == 2 else bm, bn, sp, None, v,
                     bm[1] if v == 2 else 2))
             t_lib = timeit(lib, args.reps)
+            t_wino = None
+            if pass_ in ("fwd", "dgrad") and Wg.eligible((kh, kw), (s, s), pads4, (1, 1), c, co):
+                if pass_ == "fwd":
+                    t_wino = timeit(lambda: Wg.winograd_fwd(x, wt, (oh, ow), pads4), args.reps)
+                else:
+                    t_wino = timeit(lambda: Wg.winograd_dgrad(dy, wt, x.shape, pads4), args.reps)
             best = None
             if native_ok:
                 for bm, bn, sp, v in cands:
@@ -150,7 +157,11 @@ def main():
                         continue
                     if best is None or t < best[0]:
                         best = (t, bm, bn, sp, v)
-            if best is not None and best[0] < t_lib:
+            if t_wino is not None and t_wino < t_lib and (best is None or t_wino < best[0]):
+                table[key] = {"backend": "winograd", "ms": round(t_wino, 4), "miopen_ms": round(t_lib, 4),
+                              "mdtf_ms": round(best[0], 4) if best else None}
+                choice = "winograd"
+            elif best is not None and best[0] < t_lib:
                 ent = {"backend": "mdtf", "bm": best[1], "bn": best[2], "splits": best[3], "ver": best[4],
                        "ms": round(best[0], 4), "miopen_ms": round(t_lib, 4)}
                 if best[4] == 2 and pass_ == "wgrad":     # v2 wgrad: bm field carries (rows, stages)
@@ -165,10 +176,11 @@ def main():
                 choice = "miopen"
             k = counts[(n, h, w, c, kh, kw, co, s, pads)]
             tot["miopen"] += k * t_lib
-            tot["best"] += k * min(t_lib, best[0] if best else 1e9)
-            lines.append("| %s | %d,%d,%d,%d,%dx%d,%d,s%d | %d | %.3f | %s | %s | %s |" % (
+            tot["best"] += k * min(t_lib, best[0] if best else 1e9, t_wino or 1e9)
+            lines.append("| %s | %d,%d,%d,%d,%dx%d,%d,s%d | %d | %.3f | %s | %s | %s | %s |" % (
                 pass_, n, h, w, c, kh, kw, co, s, k, t_lib,
                 ("%.3f (%s,%d,%d,v%d)" % best) if best else "n/a",
+                ("%.3f" % t_wino) if t_wino is not None else "-",
                 ("%.0f" % (flops / best[0] / 1e9)) if best else "-", choice))
             print(lines[-1], flush=True)
     lines.append("")

@@ -40,6 +40,9 @@ def main():
         out = torch.zeros(K, N, device=dev)
         fl = 2.0 * M * K * N
         t_lib = timeit(lambda: torch.addmm(out, x.t(), dy, out_dtype=torch.float32, out=out))
+        xt = x.t()
+        t_b16 = timeit(lambda: out.add_(torch.mm(xt, dy)))       # bf16-output GEMM + fp32 accumulate pass
+        t_b16only = timeit(lambda: torch.mm(xt, dy))
         best = None
         x4 = x.view(M, 1, 1, K)
         dy4 = dy.view(M, 1, 1, N)
@@ -58,9 +61,9 @@ def main():
                      stages=best[3])
         ref = (x.t().float() @ dy.float())
         err = float((out.view(K, N) - ref).norm() / ref.norm())
-        print("| %d | %d | %d | %.4f | %.0f | %.4f (%d,%d,s%d,k%d) | %.0f | err %.1e" % (
-            M, K, N, t_lib, fl / t_lib / 1e9, best[0], best[1], best[2], best[3], best[4], fl / best[0] / 1e9, err),
-            flush=True)
+        print("| %d | %d | %d | %.4f | %.0f | %.4f (%d,%d,s%d,k%d) | %.0f | bf16-out %.4f (+add %.4f) | err %.1e" % (
+            M, K, N, t_lib, fl / t_lib / 1e9, best[0], best[1], best[2], best[3], best[4], fl / best[0] / 1e9,
+            t_b16only, t_b16, err), flush=True)
 
 
 if __name__ == "__main__":

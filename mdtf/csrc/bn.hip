@@ -273,9 +273,9 @@ __global__ void __launch_bounds__(1024)
     bn_finalize_bwd(const float* __restrict__ p0, const float* __restrict__ p1, int gx, long long M, int C,
                     const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
                     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ k1,
-                    float* __restrict__ k2, float* __restrict__ k3) {
+                    float* __restrict__ k2, float* __restrict__ k3, int zero_after) {
   double sdz, sdzx;
-  if (!sum_partials(p0, p1, gx, C, sdz, sdzx)) return;
+  if (!sum_partials(p0, p1, gx, C, sdz, sdzx, zero_after != 0)) return;
   const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
   float mu = mean[c], inv = invstd[c];
   float g = gamma ? gamma[c] : 1.f;
@@ -332,6 +332,8 @@ __global__ void __launch_bounds__(kThreads)
 }
 
 inline int ew_grid(long long n8);
+void launch_dx(const void* dy, const void* x, const void* mask, void* dx, void* dres, long long M, int C,
+               const float* k1, const float* k2, const float* k3, int relu, int accum_dres, hipStream_t st);
 
 void launch_apply(const void* x, const void* res, void* y, uint8_t* mask, long long n8, int C, const float* scale,
                   const float* shift, int relu, hipStream_t st) {
@@ -439,7 +441,32 @@ MDTF_EXPORT int mdtf_bn_bwd(const void* dy, const void* x, const void* mask, voi
     hipLaunchKernelGGL((bn_reduce_kernel<true, false>), dim3(g.gx, g.gy), dim3(kThreads), lds, st, (const bf16_t*)dy,
                        (const bf16_t*)x, nullptr, M, C, g.tpr, g.rg, p0, p1);
   hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, p0, p1, g.gx, M, C, gamma, mean,
-                     invstd, dgamma, dbeta, k1, k2, k3);
+                     invstd, dgamma, dbeta, k1, k2, k3, 0);
+  launch_dx(dy, x, mask, dx, dres, M, C, k1, k2, k3, relu, accum_dres, st);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// Backward when the gradient's producer (the v2 conv dgrad epilogue) already emitted
+// Σ g·mask and Σ g·mask·x as [P][C] partials (persistent buffer, re-zeroed here).
+MDTF_EXPORT int mdtf_bn_bwd_stats(const void* dy, const void* x, const void* mask, void* dx, void* dres, long long M,
+                                  int C, const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                                  float* dbeta, int relu, float* psum, float* psq, int P, float* ws, int accum_dres,
+                                  hipStream_t st) {
+  if (C % 8) return MDTF_EINVAL;
+  float* k1 = ws;
+  float* k2 = k1 + C;
+  float* k3 = k2 + C;
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M, C,
+                     gamma, mean, invstd, dgamma, dbeta, k1, k2, k3, 1);
+  launch_dx(dy, x, mask, dx, dres, M, C, k1, k2, k3, relu, accum_dres, st);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+namespace {
+void launch_dx(const void* dy, const void* x, const void* mask, void* dx, void* dres, long long M, int C,
+               const float* k1, const float* k2, const float* k3, int relu, int accum_dres, hipStream_t st) {
   long long n8 = M * C / 8;
   if (relu && dres)
     hipLaunchKernelGGL((bn_dx_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
@@ -453,6 +480,5 @@ MDTF_EXPORT int mdtf_bn_bwd(const void* dy, const void* x, const void* mask, voi
   else
     hipLaunchKernelGGL((bn_dx_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
                        (const bf16_t*)x, nullptr, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3, 0);
-  MDTF_LAUNCH_CHECK();
-  return 0;
 }
+}  // namespace

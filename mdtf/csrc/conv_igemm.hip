@@ -61,6 +61,14 @@ struct ConvArgs {
   // (h0 + SH i, w0 + SW j), i < Hc, j < Wc; their taps kh = kh0 + SH t (t < th), kw = kw0 + SW u (u < tw)
   // read DY at (q0h + i - t, q0w + j - u)
   int cls_h0, cls_w0, cls_q0h, cls_q0w, cls_kh0, cls_kw0, cls_Hc, cls_Wc, cls_th, cls_tw;
+  // dgrad v2 writing the COMPLETE gradient g of a BatchNorm output (its last contribution):
+  // also emit that BN's backward statistics  Σ g·relu_mask, Σ g·relu_mask·x  per channel into
+  // bslots atomic partial rows (saves the BN backward's separate reduction pass over g and x)
+  const bf16_t* bx;      // the BN's input x  [M][Ncol]
+  const uint8_t* bmask;  // its forward ReLU bitmask (1 bit / element) or null
+  float* bsum;           // [bslots][Ncol] (null: off)
+  float* bsq;
+  int bslots;
 };
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p, bool ok) {
@@ -678,13 +686,29 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
     }
   }
   __syncthreads();
-  for (int idx = tid; idx < BM * (BN / 8); idx += NT) {
+  const bool bstat = MODE != 0 && a.bsum != nullptr;
+  float bs0[8], bs1[8];                        // this thread's BN-backward partials (fixed c8 per thread)
+#pragma unroll
+  for (int k = 0; k < 8; ++k) bs0[k] = bs1[k] = 0.f;
+  // every global read of the copy-out (old DX when accumulating, BN input x and ReLU mask for the
+  // statistics) is issued for all of this thread's rows before the first store: one latency, not ITER
+  constexpr int ITER = BM * (BN / 8) / NT;
+  static_assert(ITER * NT == BM * (BN / 8), "copy-out rows per thread");
+  constexpr int PF = ITER < 4 ? ITER : 4;      // rows in flight (register budget of the 256-row tiles)
+  static_assert(ITER % PF == 0, "prefetch groups");
+#pragma unroll
+  for (int g0 = 0; g0 < ITER; g0 += PF) {
+  long long off[PF];
+  uint4 old4[PF], x4[PF];
+  uint32_t mb[PF];
+#pragma unroll
+  for (int it = 0; it < PF; ++it) {
+    const int idx = tid + (g0 + it) * NT;
     const int row = idx / (BN / 8), c8 = idx - row * (BN / 8);
     const long long m = m0 + row;
     const int n = n0 + c8 * 8;
+    off[it] = -1;
     if (m < a.M && n < a.Ncol) {
-      uint4 v = *reinterpret_cast<const uint4*>(smem_raw + row * LDC + c8 * 16);
-      if ((row >> 3) & 1) v = make_uint4(v.z, v.w, v.x, v.y);
       long long pix = m;
       if (MODE == 2) {          // class pixel (n, i, j) -> DX pixel (n, h0 + SH i, w0 + SW j)
         const int j = static_cast<int>(m % a.cls_Wc);
@@ -693,21 +717,79 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
         const long long nb = t / a.cls_Hc;
         pix = (nb * a.H + a.cls_h0 + a.SH * i) * a.W + a.cls_w0 + a.SW * j;
       }
-      bf16_t* dst = a.out + pix * a.Ncol + n;
+      off[it] = pix * a.Ncol + n;
+      if (a.accumulate) old4[it] = *reinterpret_cast<const uint4*>(a.out + off[it]);
+      if (bstat) {
+        x4[it] = *reinterpret_cast<const uint4*>(a.bx + off[it]);
+        mb[it] = a.bmask ? a.bmask[off[it] >> 3] : 0xffu;
+      }
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < PF; ++it) {
+    if (off[it] < 0) continue;
+    const int idx = tid + (g0 + it) * NT;
+    const int row = idx / (BN / 8), c8 = idx - row * (BN / 8);
+    uint4 v = *reinterpret_cast<const uint4*>(smem_raw + row * LDC + c8 * 16);
+    if ((row >> 3) & 1) v = make_uint4(v.z, v.w, v.x, v.y);
+    bf16_t* dst = a.out + off[it];
+    if (a.accumulate || bstat) {
+      float c[8];
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        c[2 * k] = __uint_as_float(w4[k] << 16);
+        c[2 * k + 1] = __uint_as_float(w4[k] & 0xffff0000u);
+      }
       if (a.accumulate) {        // second contribution to a fanned-out activation gradient
-        float o[8], c[8];
-        load_bf8(dst, o);
-        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t o4[4] = {old4[it].x, old4[it].y, old4[it].z, old4[it].w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          c[2 * k] = __uint_as_float(w4[k] << 16);
-          c[2 * k + 1] = __uint_as_float(w4[k] & 0xffff0000u);
+          const float lo = __uint_as_float(o4[k] << 16) + c[2 * k];
+          const float hi = __uint_as_float(o4[k] & 0xffff0000u) + c[2 * k + 1];
+          c[2 * k] = __uint_as_float((uint32_t)f2bf(lo) << 16);      // as stored
+          c[2 * k + 1] = __uint_as_float((uint32_t)f2bf(hi) << 16);
         }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] += c[k];
-        store_bf8(dst, o);
+        store_bf8(dst, c);
       } else {
         *reinterpret_cast<uint4*>(dst) = v;
+      }
+      if (bstat) {
+        const uint32_t xw[4] = {x4[it].x, x4[it].y, x4[it].z, x4[it].w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float xk = (k & 1) ? __uint_as_float(xw[k >> 1] & 0xffff0000u) : __uint_as_float(xw[k >> 1] << 16);
+          const float gk = ((mb[it] >> k) & 1u) ? c[k] : 0.f;
+          bs0[k] += gk;
+          bs1[k] += gk * xk;
+        }
+      }
+    } else {
+      *reinterpret_cast<uint4*>(dst) = v;
+    }
+  }
+  }
+  if (bstat) {
+    static_assert(NT % (BN / 8) == 0, "one channel chunk per thread");
+    __syncthreads();                           // the C tile copy-out is done with the LDS
+    float* red = reinterpret_cast<float*>(smem_raw);   // [NT][16] (16 KiB <= the stage ring)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[tid * 16 + k] = bs0[k];
+      red[tid * 16 + 8 + k] = bs1[k];
+    }
+    __syncthreads();
+    for (int nl = tid; nl < BN; nl += NT) {
+      const int n = n0 + nl, c8 = nl >> 3, k = nl & 7;
+      if (n < a.Ncol) {
+        float sv = 0.f, q = 0.f;
+        for (int t2 = c8; t2 < NT; t2 += BN / 8) {
+          sv += red[t2 * 16 + k];
+          q += red[t2 * 16 + 8 + k];
+        }
+        const long long slot = (long long)(mt % a.bslots) * a.Ncol + n;
+        atomicAdd(a.bsum + slot, sv);
+        atomicAdd(a.bsq + slot, q);
       }
     }
   }
@@ -777,7 +859,8 @@ int launch_fd_v2(ConvArgs& a, hipStream_t st) {
   const long long nblk = (long long)a.mtiles * a.ntiles;
   if (nblk > 0x7fffffff) return MDTF_EUNSUPPORTED;
   const size_t stage_bytes = STAGES * (size_t)(BM + BN) * 128, ctile = (size_t)BM * (BN * 2 + 16);
-  const size_t lds = stage_bytes > ctile ? stage_bytes : ctile;
+  size_t lds = stage_bytes > ctile ? stage_bytes : ctile;
+  if (lds < (size_t)NT * 16 * sizeof(float)) lds = (size_t)NT * 16 * sizeof(float);   // BN-stat reduction
   if (STAGES == 1 && a.K > 64) return MDTF_EINVAL;      // single buffer: one K step only
   hipLaunchKernelGGL((conv_fd_v2<BM, BN, MODE, STATS, STAGES>), dim3((unsigned)nblk), dim3(NT), lds, st, a);
   MDTF_LAUNCH_CHECK();
@@ -1166,7 +1249,8 @@ MDTF_EXPORT int mdtf_conv_fwd_v2(const void* x, const void* wt, void* y, float* 
 // v2 (Cout % 64 == 0): DX = dgrad(DY, W), W in HWIO
 MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int OH,
                                    int OW, int Cout, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW,
-                                   int bm, int bn, int accumulate, hipStream_t st) {
+                                   int bm, int bn, int accumulate, const void* bx, const void* bmask,
+                                   float* bsum, float* bsq, int bslots, hipStream_t st) {
   if (Cout % 64 || Cin % 8) return MDTF_EINVAL;
   if ((long long)N * OH * OW * Cout * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
   if ((SH != 1 || SW != 1) && (DH != 1 || DW != 1)) return MDTF_EUNSUPPORTED;
@@ -1177,6 +1261,11 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
   a.wgt = (const bf16_t*)w;
   a.out = (bf16_t*)dx;
   a.accumulate = accumulate;
+  a.bx = (const bf16_t*)bx;
+  a.bmask = (const uint8_t*)bmask;
+  a.bsum = bsum;
+  a.bsq = bsq;
+  a.bslots = bslots > 0 ? bslots : 1;
   a.Ncol = Cin;
   const int stages = bm / 1000 ? bm / 1000 : 2;
   bm %= 1000;
@@ -1201,7 +1290,8 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
       c.cls_q0w = (c.cls_w0 + PW - rw) / SW;
       c.M = (long long)N * c.cls_Hc * c.cls_Wc;
       c.K = c.cls_th * c.cls_tw * Cout;
-      if (c.M == 0 || (c.K == 0 && accumulate)) continue;      // no pixels / nothing to add
+      // no pixels / nothing to add (unless the BN statistics need every pixel)
+      if (c.M == 0 || (c.K == 0 && accumulate && !bsum)) continue;
       const int cs = c.K > 64 && stages == 1 ? 2 : stages;
       const int rc = dispatch_fd_v2<2, false>(c, bm, bn, cs, st);
       if (rc) return rc;

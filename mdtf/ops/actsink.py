@@ -17,11 +17,26 @@ gradient arrived, so consumers that are not sink-aware stay correct.
 
 
 class ActGradSink(object):
-    __slots__ = ("buf", "count")
+    """``consumers``: sink-aware consumers registered in the forward.  ``stat_req``: what the
+    producing BatchNorm needs for its backward statistics, ``(x, relu_mask)``.  The contributor that
+    completes the sum (the ``consumers``-th) may emit the statistics in its epilogue into ``stats``
+    (the v2 conv dgrad does)."""
+    __slots__ = ("buf", "count", "consumers", "stat_req", "stats")
 
     def __init__(self):
         self.buf = None
         self.count = 0
+        self.consumers = 0
+        self.stat_req = None
+        self.stats = None
+
+    def register(self):
+        self.consumers += 1
+        return self
+
+    def completing(self):
+        """True when the next contribution completes the gradient (every registered consumer)."""
+        return self.count + 1 == self.consumers
 
     def adopt_or_add(self, g):
         """Contribute a materialised gradient tensor."""
@@ -49,6 +64,11 @@ class ActGradSink(object):
             total = total.add_(dy)
         self.buf, self.count = None, 0
         return total
+
+    def take_stats(self):
+        """The emitted BN statistics ``(psum, psq, slots)`` or None (cleared)."""
+        st, self.stats = self.stats, None
+        return st
 
 
 ENABLED = True      # switch for A/B tests (tests/test_kernels_gpu.py)

@@ -8,8 +8,13 @@ N.register("mdtf_bn_workspace_floats", [N.L, N.I], N.L)
 N.register("mdtf_bn_fwd_train", [N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P])
 N.register("mdtf_bn_fwd_eval", [N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.I, N.P, N.P])
 N.register("mdtf_bn_bwd", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P, N.I, N.P])
+N.register("mdtf_bn_bwd_stats", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P, N.P, N.I,
+                                 N.P, N.I, N.P])
 N.register("mdtf_bn_fwd_stats", [N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P,
                                  N.I, N.P, N.P])
+
+
+FUSED_BWD = [0]      # backward passes that took their statistics from the dgrad epilogue (tests)
 
 
 def _check(x):
@@ -29,6 +34,8 @@ class _BNTrain(torch.autograd.Function):
         from . import actsink
         ctx.set_materialize_grads(False)
         ctx.res_sink = actsink.sink_of(residual)       # residual fan-out: write dres into the producer's sink
+        if ctx.res_sink is not None:
+            ctx.res_sink.register()
         x = x.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
@@ -63,13 +70,24 @@ class _BNTrain(torch.autograd.Function):
                      V.grad_sink(beta) if beta is not None else None)
         ctx.like = (gamma, beta)
         ctx.out_sink = actsink.attach(y)             # this output's consumers may accumulate here
+        if ctx.out_sink is not None:
+            # the consumer that completes dy may emit Σ dy·mask, Σ dy·mask·x for this backward
+            ctx.out_sink.stat_req = (x, mask)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mask, g, mean, invstd = ctx.saved_tensors
+        pstats = None
         if ctx.out_sink is not None:
+            pstats = ctx.out_sink.take_stats()
+            if pstats is not None and dy is not None:
+                # part of dy came through plain autograd: the epilogue statistics are incomplete
+                from . import conv as _conv
+                _conv.bwd_stats_release(pstats, False)
+                pstats = None
             dy = ctx.out_sink.take(dy)
+            ctx.out_sink.stat_req = None
         if dy is None:
             return (None,) * 10
         dy = dy.contiguous()
@@ -88,11 +106,21 @@ class _BNTrain(torch.autograd.Function):
         # dgamma/dbeta accumulate straight into the fp32 grad slots when available
         dgamma = sg.grad if sg is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
         dbeta = sb.grad if sb is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
-        ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
-        N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(x), N.ptr(mask if ctx.relu else None), N.ptr(dx), N.ptr(dres), M,
-                                    C, N.ptr(g),
-                                    N.ptr(mean), N.ptr(invstd), N.ptr(dgamma), N.ptr(dbeta), int(ctx.relu), N.ptr(ws),
-                                    accum, N.stream_ptr()), "bn_bwd")
+        if pstats is not None:
+            from . import conv as _conv
+            ws = torch.empty(3 * C, dtype=torch.float32, device=x.device)
+            N.check(N.fn("mdtf_bn_bwd_stats")(N.ptr(dy), N.ptr(x), N.ptr(mask if ctx.relu else None), N.ptr(dx),
+                                              N.ptr(dres), M, C, N.ptr(g), N.ptr(mean), N.ptr(invstd), N.ptr(dgamma),
+                                              N.ptr(dbeta), int(ctx.relu), N.ptr(pstats[0]), N.ptr(pstats[1]),
+                                              int(pstats.shape[1]), N.ptr(ws), accum, N.stream_ptr()), "bn_bwd_stats")
+            _conv.bwd_stats_release(pstats, True)        # the finalize re-zeroed it
+            FUSED_BWD[0] += 1
+        else:
+            ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
+            N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(x), N.ptr(mask if ctx.relu else None), N.ptr(dx), N.ptr(dres), M,
+                                        C, N.ptr(g),
+                                        N.ptr(mean), N.ptr(invstd), N.ptr(dgamma), N.ptr(dbeta), int(ctx.relu),
+                                        N.ptr(ws), accum, N.stream_ptr()), "bn_bwd")
         if rs is not None and dres is not None:
             rs.written(dres)
             dres = None                                  # delivered through the sink

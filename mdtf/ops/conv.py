@@ -16,13 +16,14 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
+from . import winograd
 from ..train import variables as V
 
 N.register("mdtf_conv_fwd", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P])
 N.register("mdtf_conv_dgrad", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
 N.register("mdtf_conv_wgrad", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 N.register("mdtf_conv_fwd_v2", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P])
-N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
+N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P, N.P, N.P, N.I, N.P])
 N.register("mdtf_conv_wgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -76,14 +77,16 @@ def choose(pass_, x_shape, w_shape, stride, pads, dil):
     native_ok = c % 8 == 0 and co % 8 == 0
     if not native_ok or forced == "miopen":
         return ("miopen",)
+    if pass_ in ("fwd", "dgrad") and winograd.enabled() and winograd.eligible(w_shape, stride, pads, dil, c, co):
+        return ("winograd",)                 # the reference's TF_ENABLE_WINOGRAD_NONFUSED toggle
     ent = table().get(shape_key(pass_, x_shape, w_shape, stride, pads, dil))
     if N.deterministic() and pass_ == "wgrad":
         # no split-K atomics, no library algorithm choice: one block per DW tile
         ver = 2 if v2_ok(pass_, c, co, stride, kh * kw, dil) else 1
         return ("mdtf", 128 if kh * kw * ci >= 128 else 64, 128 if co % 128 == 0 else 64, 1, ver, 2)
     if forced == "auto" and ent is not None:
-        if ent["backend"] == "miopen":
-            return ("miopen",)
+        if ent["backend"] in ("miopen", "winograd"):
+            return (ent["backend"],)
         return ("mdtf", ent["bm"], ent["bn"], ent.get("splits", 0), ent.get("ver", 1), ent.get("stages", 2))
     if pass_ == "wgrad":
         r = kh * kw * ci
@@ -180,16 +183,24 @@ def mdtf_fwd(x, w, out_hw, stride, pads, dil, bm, bn, stats=None, ver=1, stages=
     return y
 
 
-def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn, ver=1, stages=2, out=None, accumulate=False):
-    """DX of a conv; v2 can write into ``out`` and accumulate (out += dgrad) in its epilogue."""
+def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn, ver=1, stages=2, out=None, accumulate=False,
+               bn_stats=None):
+    """DX of a conv; v2 can write into ``out`` and accumulate (out += dgrad) in its epilogue.
+
+    ``bn_stats = (x, relu_mask or None, psum, psq, slots)``: DX is the complete gradient of a BatchNorm
+    output; the epilogue also accumulates that BN's backward statistics into ``psum``/``psq``."""
     dx = out if out is not None else torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
     n, h, wd, c = x_shape
     kh, kw, ci, co = w.shape
     geo = [n, h, wd, c, dy.shape[1], dy.shape[2], co, kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1]]
     if ver == 2:
+        bx, bmask, bsum, bsq, bslots = bn_stats if bn_stats is not None else (None, None, None, None, 0)
         N.check(N.fn("mdtf_conv_dgrad_v2")(N.ptr(dy), N.ptr(w), N.ptr(dx), *geo, bm + 1000 * stages, bn,
-                                           int(bool(accumulate)), N.stream_ptr()), "conv_dgrad_v2")
+                                           int(bool(accumulate)), N.ptr(bx), N.ptr(bmask), N.ptr(bsum), N.ptr(bsq),
+                                           int(bslots), N.stream_ptr()), "conv_dgrad_v2")
         return dx
+    if bn_stats is not None:
+        raise ValueError("BN statistics in the dgrad epilogue need the v2 kernel")
     if accumulate:
         raise ValueError("accumulating dgrad needs the v2 kernel")
     N.check(N.fn("mdtf_conv_dgrad")(N.ptr(dy), N.ptr(w), N.ptr(dx), *geo, bm, bn, N.stream_ptr()), "conv_dgrad")
@@ -217,6 +228,7 @@ def _pads_ok(pads):
     return True
 
 
+BWD_STATS = os.environ.get("MDTF_BN_BWD_STATS", "1") != "0"   # BN backward statistics from the dgrad epilogue
 STAT_SLOTS = 64   # atomic partial rows of the fused BN statistics (csrc/conv_igemm.hip kStatSlots)
 _STATS = {}       # device -> [flat fp32 buffer, dirty]: persistent, re-zeroed by the BN finalize kernel
 
@@ -245,12 +257,40 @@ def stats_consumed(device):
         ent[1] = False
 
 
+def stat_slots(mtiles):
+    """Atomic partial rows for epilogue statistics: one per M tile in deterministic mode,
+    else ~8 M tiles per row (64..1024 rows): low contention, small finalize."""
+    if N.deterministic():
+        return mtiles
+    slots = STAT_SLOTS
+    while slots < 1024 and slots * 8 < mtiles:
+        slots *= 2
+    return slots
+
+
+_BSTATS = {}      # (device, C, slots) -> free zeroed [2, slots, C] buffers (BN backward statistics)
+
+
+def bwd_stats_acquire(device, C, slots):
+    pool = _BSTATS.setdefault((device, C, slots), [])
+    return pool.pop() if pool else torch.zeros((2, slots, C), dtype=torch.float32, device=device)
+
+
+def bwd_stats_release(buf, zeroed):
+    """Return a buffer to the pool; ``zeroed``: the BN finalize already re-zeroed it."""
+    if not zeroed:
+        buf.zero_()
+    _BSTATS.setdefault((buf.device, buf.shape[2], buf.shape[1]), []).append(buf)
+
+
 class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, pads, dil, out_hw, want_stats):
         from . import actsink
         ctx.set_materialize_grads(False)      # no zero-filled grads for the (non-differentiable) stats outputs
         ctx.x_sink = actsink.sink_of(x)       # fanned-out input: dgrad accumulates into the producer's sink
+        if ctx.x_sink is not None:
+            ctx.x_sink.register()
         x = x.contiguous()
         w = w.contiguous()
         ch = choose("fwd", x.shape, w.shape, stride, pads, dil)
@@ -258,16 +298,12 @@ class _Conv(torch.autograd.Function):
         if ch[0] == "mdtf":
             if want_stats:
                 co = w.shape[3]
-                mtiles = -(-x.shape[0] * out_hw[0] * out_hw[1] // ch[1])
-                if N.deterministic():       # one partial row per M tile: no atomic reordering
-                    slots = mtiles
-                else:                       # ~8 M tiles per atomic row: low contention, small finalize
-                    slots = STAT_SLOTS
-                    while slots < 1024 and slots * 8 < mtiles:
-                        slots *= 2
+                slots = stat_slots(-(-x.shape[0] * out_hw[0] * out_hw[1] // ch[1]))
                 buf = _stats_buffer(co, x.device, slots)
                 stats = (buf[0], buf[1])
             y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2], stats, ch[4], ch[5])
+        elif ch[0] == "winograd":
+            y = winograd.winograd_fwd(x, w, out_hw, pads)
         else:
             y = miopen_fwd(x, w, stride, pads, dil)
         ctx.save_for_backward(x, w)
@@ -308,11 +344,21 @@ class _Conv(torch.autograd.Function):
                 else:
                     dw = ldw
         xs = ctx.x_sink if need_dx else None
-        if need_dx and not lib_dx:
+        if need_dx and cd[0] == "winograd":
+            dx = winograd.winograd_dgrad(dy, w, x.shape, pads)
+        elif need_dx and not lib_dx:
             if xs is not None and cd[4] == 2:
                 buf, acc = xs.target()
+                bst = None
+                if xs.stat_req is not None and xs.completing() and BWD_STATS and not N.deterministic():
+                    # this dgrad completes the BN output's gradient: emit the BN backward statistics
+                    bx, bmask = xs.stat_req
+                    sbuf = bwd_stats_acquire(x.device, x.shape[3], stat_slots(-(-x.numel() // x.shape[3] // cd[1])))
+                    bst = (bx, bmask, sbuf[0], sbuf[1], sbuf.shape[1])
                 xs.written(mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5], out=buf,
-                                      accumulate=acc))
+                                      accumulate=acc, bn_stats=bst))
+                if bst is not None:
+                    xs.stats = sbuf
                 dx = None
             else:
                 dx = mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5])

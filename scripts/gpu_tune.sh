@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 TAG=$1; PASSES=$2; STRIDES=${3:-}
-timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py tests/test_kernels_property.py -q -m gpu -k "conv" \
+timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py tests/test_kernels_property.py tests/test_winograd.py -q -m gpu -k "${KF:-conv}" \
   > gpurun_out/pytest_conv_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_conv_$TAG.log; exit 1; }
 tail -1 gpurun_out/pytest_conv_$TAG.log
 cp mdtf/ops/conv_table.json gpurun_out/conv_table_$TAG.json

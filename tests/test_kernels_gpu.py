@@ -811,6 +811,49 @@ class _TinyRes(object):
         return tools.dense("logits", x, 16)
 
 
+class _TinyStrided(object):
+    """BN outputs consumed by a strided 3x3 conv, a strided 1x1 projection and stride-1 convs: the
+    BN backward statistics come from stride-1 and stride-parity-class dgrad epilogues."""
+
+    def inference(self, x):
+        from mdtf.layers import tools
+        from mdtf.train import variables as V
+        store = V.get_store()
+        if store.compute_dtype is not None:
+            x = x.to(store.compute_dtype)
+        s = tools.conv_bn("c1", x, 64, 3, 1, relu=True)
+        y = tools.conv_bn("c2", s, 64, 3, 2, relu=True)                     # strided 3x3 dgrad -> c1 BN
+        sc = tools.conv_bn("sc", s, 128, 1, 2, relu=False)                   # strided 1x1 projection -> c1 BN
+        z = tools.conv_bn("c3", y, 128, 1, 1, relu=True, residual=sc)
+        x = ops.global_avg_pool(z)
+        return tools.dense("logits", x, 16)
+
+
+@pytest.mark.parametrize("model", ["res", "strided"])
+def test_bn_backward_stats_from_dgrad_epilogue(model, monkeypatch):
+    """BN backward with Σdy·mask, Σdy·mask·x emitted by the completing v2 dgrad's epilogue == the
+    separate reduction pass; the fused path must actually run."""
+    from mdtf.ops import bn as B, conv as C
+    monkeypatch.setenv("MDTF_CONV", "mdtf2")
+    global _Tiny
+    saved = _Tiny
+    _Tiny = _TinyRes if model == "res" else _TinyStrided
+    try:
+        torch.manual_seed(4)
+        x = torch.randn(16, 12, 12, 64)
+        y = torch.randint(0, 16, (16,))
+        n0 = B.FUSED_BWD[0]
+        lf, gf = _tiny_step(DEV, torch.bfloat16, x, y)
+        assert B.FUSED_BWD[0] - n0 >= 2
+        monkeypatch.setattr(C, "BWD_STATS", False)
+        lo, go = _tiny_step(DEV, torch.bfloat16, x, y)
+    finally:
+        _Tiny = saved
+    assert lf == lo
+    for k in go:
+        assert _rel(gf[k], go[k]) < 1e-2, (k, _rel(gf[k], go[k]))
+
+
 @pytest.mark.parametrize("conv_backend", ["mdtf2", "miopen"])
 def test_fanout_gradient_sinks(conv_backend, monkeypatch):
     """In-place fan-out gradient accumulation == autograd's add (same kernels otherwise), and both ~ fp32 CPU."""
