@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--kernels", default=None, help="native|torch (MDTF_KERNELS)")
     p.add_argument("--bucket_mb", type=int, default=None)
     p.add_argument("--profile_dir", default=None)
+    p.add_argument("--hip_graph", type=int, default=1,
+                   help="1: capture the whole training step in a hipGraph after 2 eager steps (mdtf.train.graph)")
     return p.parse_args()
 
 
@@ -86,7 +88,7 @@ def main():
                   batch_size=args.batch)
     _, loss, _ = tower.process()
     opt = mdtf.train.SyncReplicasOptimizer(base, replicas_to_aggregate=world, total_num_replicas=world,
-                                           mode=args.mode,
+                                           mode=args.mode, hip_graph=bool(args.hip_graph),
                                            bucket_bytes=(args.bucket_mb << 20) if args.bucket_mb else None)
     train_op = opt.apply_gradients(Tower.average_gradients(tower_grads), global_step=gs)
     sess = mdtf.train.MonitoredTrainingSession(is_chief=(rank == 0), checkpoint_dir=None, log_step_count_steps=0,
@@ -136,7 +138,8 @@ def main():
             "config": {"model": "resnet%d_v1.5" % args.depth, "global_batch": args.batch * world, "seq_len": None,
                        "per_gpu_batch": args.batch, "image_size": 224, "parallelism": "dp%d" % world,
                        "grad_sync": args.mode, "optimizer": "momentum-sgd (fused)",
-                       "kernels": os.environ.get("MDTF_KERNELS", "native")},
+                       "kernels": os.environ.get("MDTF_KERNELS", "native"),
+                       "hip_graph": bool(args.hip_graph)},
             "loss_first": float(lv), "loss_last": final_loss,
         }
         print(json.dumps(rec), flush=True)

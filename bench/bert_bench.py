@@ -31,6 +31,7 @@ def parse():
     p.add_argument("--seq", type=int, default=128)
     p.add_argument("--size", default="base")
     p.add_argument("--stock", action="store_true")
+    p.add_argument("--hip_graph", type=int, default=1, help="capture the mdtf training step in a hipGraph")
     return p.parse_args()
 
 
@@ -135,7 +136,7 @@ def main():
         tower = Tower(Net(Bert(args.size, seq_len=args.seq, max_predictions=P)), "tower_0/", tg, raw, gt,
                       BertPretrainingLoss(P), base, batch_size=args.batch)
         _, loss_h, _ = tower.process()
-        opt = mdtf.train.SyncReplicasOptimizer(base, world, world)
+        opt = mdtf.train.SyncReplicasOptimizer(base, world, world, hip_graph=bool(args.hip_graph))
         op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
         sess = mdtf.train.MonitoredTrainingSession(is_chief=rank == 0, log_step_count_steps=0, server=server)
 
@@ -161,6 +162,7 @@ def main():
                           "value": round(world * args.batch * args.steps / el, 2), "unit": "sequences/sec",
                           "n_gpus": world, "ms_per_step": round(1000 * el / args.steps, 3),
                           "per_gpu_batch": args.batch, "impl": "stock-pytorch" if args.stock else "mdtf",
+                          "hip_graph": bool(args.hip_graph) and not args.stock,
                           "dtype": "bf16", "data": "synthetic"}), flush=True)
 
 

@@ -156,6 +156,7 @@ DEFINE_string('mode', '', "Override @current_mode (Train / Eval).")
 DEFINE_integer('epochs', 0, "Override @epoch_num when > 0.")
 DEFINE_integer('save_checkpoint_steps', 0, "Checkpoint every N global steps (0: every save_checkpoint_secs).")
 DEFINE_integer('save_checkpoint_secs', 600, "Checkpoint period in seconds (chief), as MonitoredTrainingSession.")
+DEFINE_boolean('hip_graph', False, "Capture the synchronous training step in a hipGraph and replay it (mdtf.train.graph).")
 
 
 def apply_thread_flags():

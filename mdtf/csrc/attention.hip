@@ -67,6 +67,11 @@ __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
   return x;
 }
 
+// per-step seed: host seed of the call site mixed with the device step counter (hipGraph replay)
+__device__ __forceinline__ uint32_t step_seed(uint32_t seed, const long long* seed_off) {
+  return seed_off ? seed ^ ((uint32_t)(*seed_off) * 0x85EBCA6Bu) : seed;
+}
+
 // keep bit of attention-dropout element (bh, q, k)
 __device__ __forceinline__ bool keep_elem(uint32_t seed, int bh, int q, int k, uint32_t thr) {
   const uint32_t idx = ((uint32_t)bh * S + (uint32_t)q) * S + (uint32_t)k;
@@ -131,7 +136,9 @@ __device__ __forceinline__ bf16x8_t load_frag_global(const bf16_t* p) {
 // ============================================================================ forward
 __global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                                                       bf16_t* __restrict__ out, float* __restrict__ lse_out, int B,
-                                                      int nh, float scale, float p_drop, uint32_t seed) {
+                                                      int nh, float scale, float p_drop, uint32_t seed,
+                                                      const long long* __restrict__ seed_off) {
+  seed = step_seed(seed, seed_off);
   __shared__ __attribute__((aligned(16))) char smem[2 * S * D * 2];
   char* Kimg = smem;
   char* Vimg = smem + S * D * 2;
@@ -269,7 +276,9 @@ constexpr int kBwdLds = 5 * S * D * 2 + 2 * S * S * 2;   // K_A V_A K_T Q_T dO_T
 __global__ void __launch_bounds__(NT) attn_bwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                                                       const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
                                                       const float* __restrict__ lse, bf16_t* __restrict__ dqkv, int B,
-                                                      int nh, float scale, float p_drop, uint32_t seed) {
+                                                      int nh, float scale, float p_drop, uint32_t seed,
+                                                      const long long* __restrict__ seed_off) {
+  seed = step_seed(seed, seed_off);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* KA = smem;
   char* VA = KA + S * D * 2;
@@ -460,11 +469,12 @@ __global__ void __launch_bounds__(NT) attn_bwd_kernel(const bf16_t* __restrict__
 
 // ctx[B*S, H] = attention(qkv[B*S, 3H]); lse [B*nh, S] (fp32) saved for backward
 MDTF_EXPORT int mdtf_attn_fwd(const void* qkv, const float* mask, void* out, float* lse, int B, int seq, int nh,
-                              int dh, float scale, float p_drop, unsigned seed, hipStream_t st) {
+                              int dh, float scale, float p_drop, unsigned seed, const long long* seed_off,
+                              hipStream_t st) {
   if (seq != S || dh != D) return MDTF_EUNSUPPORTED;
   if ((long long)B * S * 3 * nh * D * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
   hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * nh), dim3(NT), 0, st, (const bf16_t*)qkv, mask, (bf16_t*)out, lse, B,
-                     nh, scale, p_drop, (uint32_t)seed);
+                     nh, scale, p_drop, (uint32_t)seed, seed_off);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
@@ -472,12 +482,12 @@ MDTF_EXPORT int mdtf_attn_fwd(const void* qkv, const float* mask, void* out, flo
 // dqkv[B*S, 3H] (every element written) from dout[B*S, H]
 MDTF_EXPORT int mdtf_attn_bwd(const void* qkv, const float* mask, const void* out, const void* dout, const float* lse,
                               void* dqkv, int B, int seq, int nh, int dh, float scale, float p_drop, unsigned seed,
-                              hipStream_t st) {
+                              const long long* seed_off, hipStream_t st) {
   if (seq != S || dh != D) return MDTF_EUNSUPPORTED;
   if ((long long)B * S * 3 * nh * D * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
   hipLaunchKernelGGL(attn_bwd_kernel, dim3(B * nh), dim3(NT), kBwdLds, st, (const bf16_t*)qkv, mask,
                      (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv, B, nh, scale, p_drop,
-                     (uint32_t)seed);
+                     (uint32_t)seed, seed_off);
   MDTF_LAUNCH_CHECK();
   return 0;
 }

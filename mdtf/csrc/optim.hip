@@ -5,7 +5,11 @@
 // writes master/state back and — when a bf16 shadow buffer is given — the
 // bf16 compute copy of the weights (no separate cast kernels before the next
 // forward).  Memory-bound: 3-5 streams of fp32 at HBM rate; grid-stride with
-// ~8 blocks/CU.  Reference ops: tf.train.AdamOptimizer / MomentumOptimizer
+// ~8 blocks/CU.  ``dyn`` (nullable) points at device-resident hyper-parameters
+// {lr, lr_t, grad_scale} that override the scalar arguments: a hipGraph-captured
+// training step bakes kernel arguments, so per-step values (LR schedule, Adam
+// bias correction, backup-worker scale) are refreshed in that buffer instead.
+// Reference ops: tf.train.AdamOptimizer / MomentumOptimizer
 // apply on the PS (distribute_train.py:151-158), l2_loss*wd (distribute_tools.py:64).
 #include "mdtf_common.h"
 
@@ -20,6 +24,14 @@ inline int grid_for(long long n4) {
   return static_cast<int>(b < 2048 ? (b > 0 ? b : 1) : 2048);
 }
 
+__device__ __forceinline__ void load_dyn(const float* dyn, float& lr, float& lr_t, float& gs) {
+  if (dyn) {
+    lr = dyn[0];
+    lr_t = dyn[1];
+    gs = dyn[2];
+  }
+}
+
 __device__ __forceinline__ void store_shadow4(bf16_t* s, long long i, const float4& w) {
   uint32_t lo = static_cast<uint32_t>(f2bf(w.x)) | (static_cast<uint32_t>(f2bf(w.y)) << 16);
   uint32_t hi = static_cast<uint32_t>(f2bf(w.z)) | (static_cast<uint32_t>(f2bf(w.w)) << 16);
@@ -27,7 +39,10 @@ __device__ __forceinline__ void store_shadow4(bf16_t* s, long long i, const floa
 }
 
 __global__ void __launch_bounds__(kThreads) sgd_kernel(long long n, float* __restrict__ w, const float* __restrict__ g,
-                                                      bf16_t* __restrict__ shadow, float lr, float gs, float wd) {
+                                                      bf16_t* __restrict__ shadow, float lr, float gs, float wd,
+                                                      const float* __restrict__ dyn) {
+  float lr_t = lr;
+  load_dyn(dyn, lr, lr_t, gs);
   long long n4 = n >> 2;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     float4 wv = reinterpret_cast<float4*>(w)[i];
@@ -44,7 +59,9 @@ __global__ void __launch_bounds__(kThreads) sgd_kernel(long long n, float* __res
 __global__ void __launch_bounds__(kThreads) momentum_kernel(long long n, float* __restrict__ w,
                                                            const float* __restrict__ g, float* __restrict__ acc,
                                                            bf16_t* __restrict__ shadow, float lr, float mom, float gs,
-                                                           float wd, int nesterov) {
+                                                           float wd, int nesterov, const float* __restrict__ dyn) {
+  float lr_t = lr;
+  load_dyn(dyn, lr, lr_t, gs);
   long long n4 = n >> 2;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     float4 wv = reinterpret_cast<float4*>(w)[i];
@@ -88,7 +105,9 @@ __device__ __forceinline__ float adam1(float& w, float g, float& m, float& v, fl
 __global__ void __launch_bounds__(kThreads) adam_kernel(long long n, float* __restrict__ w, const float* __restrict__ g,
                                                        float* __restrict__ m, float* __restrict__ v,
                                                        bf16_t* __restrict__ shadow, float lr, float lr_t, float b1,
-                                                       float b2, float eps, float gs, float wd, int decoupled) {
+                                                       float b2, float eps, float gs, float wd, int decoupled,
+                                                       const float* __restrict__ dyn) {
+  load_dyn(dyn, lr, lr_t, gs);
   long long n4 = n >> 2;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     float4 wv = reinterpret_cast<float4*>(w)[i];
@@ -110,30 +129,30 @@ __global__ void __launch_bounds__(kThreads) adam_kernel(long long n, float* __re
 
 // n must be a multiple of 4 (flat groups are padded to 64 elements).
 MDTF_EXPORT int mdtf_fused_sgd(long long n, void* w, const void* g, void* shadow, float lr, float gs, float wd,
-                               hipStream_t st) {
+                               const void* dyn, hipStream_t st) {
   if (n % 4) return MDTF_EINVAL;
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4)), dim3(kThreads), 0, st, n, (float*)w, (const float*)g,
-                     (bf16_t*)shadow, lr, gs, wd);
+                     (bf16_t*)shadow, lr, gs, wd, (const float*)dyn);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
 
 MDTF_EXPORT int mdtf_fused_momentum(long long n, void* w, const void* g, void* acc, void* shadow, float lr, float mom,
-                                    float gs, float wd, int nesterov, hipStream_t st) {
+                                    float gs, float wd, int nesterov, const void* dyn, hipStream_t st) {
   if (n % 4) return MDTF_EINVAL;
   hipLaunchKernelGGL(momentum_kernel, dim3(grid_for(n / 4)), dim3(kThreads), 0, st, n, (float*)w, (const float*)g,
-                     (float*)acc, (bf16_t*)shadow, lr, mom, gs, wd, nesterov);
+                     (float*)acc, (bf16_t*)shadow, lr, mom, gs, wd, nesterov, (const float*)dyn);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
 
 MDTF_EXPORT int mdtf_fused_adam(long long n, void* w, const void* g, void* m, void* v, void* shadow, float lr,
-                                float lr_t, float b1, float b2, float eps, float gs, float wd, float unused,
-                                int decoupled, hipStream_t st) {
-  (void)unused;
+                                float lr_t, float b1, float b2, float eps, float gs, float wd, int decoupled,
+                                const void* dyn, hipStream_t st) {
   if (n % 4) return MDTF_EINVAL;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4)), dim3(kThreads), 0, st, n, (float*)w, (const float*)g,
-                     (float*)m, (float*)v, (bf16_t*)shadow, lr, lr_t, b1, b2, eps, gs, wd, decoupled);
+                     (float*)m, (float*)v, (bf16_t*)shadow, lr, lr_t, b1, b2, eps, gs, wd, decoupled,
+                     (const float*)dyn);
   MDTF_LAUNCH_CHECK();
   return 0;
 }

@@ -31,13 +31,20 @@ __device__ __forceinline__ bool drop_keep(uint32_t idx, uint32_t seed, uint32_t 
   return x >= thr;
 }
 
+// per-step seed: the host seed of the call site mixed with the device step counter
+// (hipGraph replays re-use the captured host seed; the counter advances per replay)
+__device__ __forceinline__ uint32_t step_seed(uint32_t seed, const long long* seed_off) {
+  return seed_off ? seed ^ ((uint32_t)(*seed_off) * 0x85EBCA6Bu) : seed;
+}
+
 template <int NV>
 __global__ void __launch_bounds__(kT) ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                                    bf16_t* __restrict__ y, bf16_t* __restrict__ s_out,
                                                    float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                    long long rows, int H, float eps, uint32_t thr, float inv_keep,
-                                                   uint32_t seed) {
+                                                   uint32_t seed, const long long* __restrict__ seed_off) {
+  seed = step_seed(seed, seed_off);
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -102,7 +109,9 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
                                                    const float* __restrict__ rstd, bf16_t* __restrict__ dx,
                                                    bf16_t* __restrict__ dx_branch, float* __restrict__ ws,
                                                    long long rows, int H, int rows_per_block, int beta_first,
-                                                   uint32_t thr, float inv_keep, uint32_t seed) {
+                                                   uint32_t thr, float inv_keep, uint32_t seed,
+                                                   const long long* __restrict__ seed_off) {
+  seed = step_seed(seed, seed_off);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nvec = H / 8;
   float dg[NV][8], db[NV][8];
@@ -313,13 +322,13 @@ static uint32_t drop_thr(float p) {
 // y = LN(dropout_p(x) + res); s = dropout_p(x) + res saved for backward (p = 0: no dropout)
 MDTF_EXPORT int mdtf_ln_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y, void* s,
                             float* mean, float* rstd, long long rows, int H, float eps, float p_drop, unsigned seed,
-                            hipStream_t st) {
+                            const long long* seed_off, hipStream_t st) {
   if (H % 8) return MDTF_EINVAL;
   if (rows * H > 0xffffffffLL && p_drop > 0.f) return MDTF_EUNSUPPORTED;
   const uint32_t thr = drop_thr(p_drop);
   const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   NV_DISPATCH(H, ln_fwd_kernel, dim3(ceil_div(rows, kT / 64)), (const bf16_t*)x, (const bf16_t*)res, gamma, beta,
-              (bf16_t*)y, (bf16_t*)s, mean, rstd, rows, H, eps, thr, inv_keep, (uint32_t)seed);
+              (bf16_t*)y, (bf16_t*)s, mean, rstd, rows, H, eps, thr, inv_keep, (uint32_t)seed, seed_off);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
@@ -348,7 +357,7 @@ MDTF_EXPORT long long mdtf_ln_bwd_ws(long long rows, int H) {
 // dx = d(loss)/d(s); dx_branch (optional) = d(loss)/d(x) through the fused dropout
 MDTF_EXPORT int mdtf_ln_bwd(const void* dy, const void* s, const float* gamma, const float* mean, const float* rstd,
                             void* dx, void* dx_branch, float* dgamma, float* dbeta, float* ws, long long rows, int H,
-                            float p_drop, unsigned seed, hipStream_t st) {
+                            float p_drop, unsigned seed, const long long* seed_off, hipStream_t st) {
   if (H % 8) return MDTF_EINVAL;
   if (rows <= 0) return 0;
   int blocks, rpb;
@@ -358,7 +367,7 @@ MDTF_EXPORT int mdtf_ln_bwd(const void* dy, const void* s, const float* gamma, c
   const uint32_t thr = drop_thr(p_drop);
   const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   NV_DISPATCH(H, ln_bwd_kernel, dim3(blocks), (const bf16_t*)dy, (const bf16_t*)s, gamma, mean, rstd, (bf16_t*)dx,
-              (bf16_t*)dx_branch, ws, rows, H, rpb, beta_first, thr, inv_keep, (uint32_t)seed);
+              (bf16_t*)dx_branch, ws, rows, H, rpb, beta_first, thr, inv_keep, (uint32_t)seed, seed_off);
   MDTF_LAUNCH_CHECK();
   if (beta_first) return mdtf_reduce_partials(ws, blocks, 2 * H, dbeta, st);
   // ws rows are [dgamma(H) | dbeta(H)]: reduce as a [blocks, 2H] matrix when the

@@ -89,7 +89,7 @@ _DETERMINISTIC = os.environ.get("MDTF_DETERMINISTIC", "0") not in ("0", "", "fal
 def check(rc, what):
     if rc != 0:
         raise RuntimeError("mdtf kernel %s failed: %s (code %d)" % (what, _error_string(rc), rc))
-    if _SYNC_CHECK:
+    if _SYNC_CHECK and not torch.cuda.is_current_stream_capturing():
         # debug mode (MDTF_SYNC_CHECK=1): serialize after every native launch so a faulting
         # kernel is named here instead of surfacing at some later synchronization
         import torch

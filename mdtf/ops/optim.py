@@ -10,6 +10,10 @@ folded in.  Reference: the optimizer is ``tf.train.AdamOptimizer(0.001)``
 
 GPU tensors run ``mdtf_fused_{sgd,momentum,adam}`` (``csrc/optim.hip``);
 CPU tensors use the vectorised PyTorch reference below (same math).
+
+``dyn`` (optional) is a device float32 tensor ``[lr, lr_t, grad_scale]`` the
+kernels read instead of their scalar arguments, so a hipGraph-captured step
+(:mod:`mdtf.train.graph`) picks up per-step values without re-capture.
 """
 import math
 
@@ -18,12 +22,12 @@ import torch
 from . import _native
 
 _native.register("mdtf_fused_sgd", [_native.L, _native.P, _native.P, _native.P,
-                                    _native.F, _native.F, _native.F, _native.P])
+                                    _native.F, _native.F, _native.F, _native.P, _native.P])
 _native.register("mdtf_fused_momentum", [_native.L, _native.P, _native.P, _native.P, _native.P,
-                                         _native.F, _native.F, _native.F, _native.F, _native.I, _native.P])
+                                         _native.F, _native.F, _native.F, _native.F, _native.I, _native.P, _native.P])
 _native.register("mdtf_fused_adam", [_native.L, _native.P, _native.P, _native.P, _native.P, _native.P,
                                      _native.F, _native.F, _native.F, _native.F, _native.F, _native.F,
-                                     _native.F, _native.F, _native.I, _native.P])
+                                     _native.F, _native.I, _native.P, _native.P])
 
 
 def _shadow_code(shadow):
@@ -34,14 +38,22 @@ def _native_ok(master):
     return master.is_cuda and _native.mode() != "torch" and _native.use_native(master)
 
 
-def sgd_(master, grad, shadow, lr, grad_scale=1.0, weight_decay=0.0):
+def _dyn_scalars(dyn, lr, lr_t, grad_scale):
+    if dyn is None:
+        return lr, lr_t, grad_scale
+    d = dyn.tolist()
+    return d[0], d[1], d[2]
+
+
+def sgd_(master, grad, shadow, lr, grad_scale=1.0, weight_decay=0.0, dyn=None):
     """``w -= lr * (g*scale + wd*w)``; refresh ``shadow`` if given."""
     if _native_ok(master):
         n = master.numel()
         _native.check(_native.fn("mdtf_fused_sgd")(
             n, _native.ptr(master), _native.ptr(grad), _native.ptr(shadow),
-            float(lr), float(grad_scale), float(weight_decay), _native.stream_ptr()), "fused_sgd")
+            float(lr), float(grad_scale), float(weight_decay), _native.ptr(dyn), _native.stream_ptr()), "fused_sgd")
         return
+    lr, _, grad_scale = _dyn_scalars(dyn, lr, lr, grad_scale)
     g = grad.float() * grad_scale
     if weight_decay:
         g = g + weight_decay * master
@@ -50,15 +62,17 @@ def sgd_(master, grad, shadow, lr, grad_scale=1.0, weight_decay=0.0):
         shadow.copy_(master)
 
 
-def momentum_(master, grad, accum, shadow, lr, momentum, grad_scale=1.0, weight_decay=0.0, nesterov=False):
+def momentum_(master, grad, accum, shadow, lr, momentum, grad_scale=1.0, weight_decay=0.0, nesterov=False,
+              dyn=None):
     """TF MomentumOptimizer: ``a = m*a + g``; ``w -= lr*a`` (nesterov: ``lr*(g + m*a)``)."""
     if _native_ok(master):
         n = master.numel()
         _native.check(_native.fn("mdtf_fused_momentum")(
             n, _native.ptr(master), _native.ptr(grad), _native.ptr(accum), _native.ptr(shadow),
             float(lr), float(momentum), float(grad_scale), float(weight_decay), int(bool(nesterov)),
-            _native.stream_ptr()), "fused_momentum")
+            _native.ptr(dyn), _native.stream_ptr()), "fused_momentum")
         return
+    lr, _, grad_scale = _dyn_scalars(dyn, lr, lr, grad_scale)
     g = grad.float() * grad_scale
     if weight_decay:
         g = g + weight_decay * master
@@ -71,27 +85,30 @@ def momentum_(master, grad, accum, shadow, lr, momentum, grad_scale=1.0, weight_
         shadow.copy_(master)
 
 
+def adam_lr_t(lr, beta1, beta2, step, bias_correction=True):
+    """TF Adam's step size with the bias correction folded in (``step`` counts from 1)."""
+    if not bias_correction:
+        return lr
+    return lr * math.sqrt(1.0 - beta2 ** step) / (1.0 - beta1 ** step)
+
+
 def adam_(master, grad, m, v, shadow, lr, beta1, beta2, epsilon, step, grad_scale=1.0, weight_decay=0.0,
-          decoupled=False, bias_correction=True):
+          decoupled=False, bias_correction=True, dyn=None):
     """Adam (TF form: bias correction folded into lr, eps added outside sqrt).
 
     ``decoupled=True`` gives AdamW/BERT's AdamWeightDecay:
     ``w -= lr * (m_hat/(sqrt(v_hat)+eps) + wd*w)``; otherwise ``wd`` is L2
     (added to the gradient).
     """
-    if bias_correction:
-        bc1 = 1.0 - beta1 ** step
-        bc2 = 1.0 - beta2 ** step
-        lr_t = lr * math.sqrt(bc2) / bc1
-    else:
-        lr_t = lr
+    lr_t = adam_lr_t(lr, beta1, beta2, step, bias_correction)
     if _native_ok(master):
         n = master.numel()
         _native.check(_native.fn("mdtf_fused_adam")(
             n, _native.ptr(master), _native.ptr(grad), _native.ptr(m), _native.ptr(v), _native.ptr(shadow),
             float(lr), float(lr_t), float(beta1), float(beta2), float(epsilon), float(grad_scale),
-            float(weight_decay), 0.0, int(bool(decoupled)), _native.stream_ptr()), "fused_adam")
+            float(weight_decay), int(bool(decoupled)), _native.ptr(dyn), _native.stream_ptr()), "fused_adam")
         return
+    lr, lr_t, grad_scale = _dyn_scalars(dyn, lr, lr_t, grad_scale)
     g = grad.float() * grad_scale
     if weight_decay and not decoupled:
         g = g + weight_decay * master

@@ -12,15 +12,31 @@ import torch.nn.functional as F
 from . import _native as N
 from ..train import variables as V
 
-N.register("mdtf_ln_fwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.F, N.F, N.U, N.P])
-N.register("mdtf_ln_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.F, N.U, N.P])
+N.register("mdtf_ln_fwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.F, N.F, N.U, N.P, N.P])
+N.register("mdtf_ln_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.F, N.U, N.P, N.P])
 N.register("mdtf_ln_bwd_ws", [N.L, N.I], restype=N.L)
 N.register("mdtf_softmax_fwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.L, N.P])
 N.register("mdtf_softmax_bwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.P])
 N.register("mdtf_embed_fwd", [N.P, N.P, N.P, N.L, N.I, N.L, N.P])
 N.register("mdtf_embed_bwd", [N.P, N.P, N.P, N.L, N.I, N.L, N.P])
-N.register("mdtf_attn_fwd", [N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P])
-N.register("mdtf_attn_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P])
+N.register("mdtf_attn_fwd", [N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P, N.P])
+N.register("mdtf_attn_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P, N.P])
+
+
+def effective_seed(seed, device):
+    """The seed the dropout kernels hash with: ``seed ^ (step_counter * 0x85EBCA6B)`` (32-bit)."""
+    from ..train.graph import rng_offset_tensor
+    off = int(rng_offset_tensor(device).item())
+    return (int(seed) ^ ((off * 0x85EBCA6B) & 0xFFFFFFFF)) & 0xFFFFFFFF
+
+
+def _seed_off(p_drop, device):
+    """Device step counter mixed into the dropout hash (advanced by hipGraph replays,
+    see mdtf.train.graph); None without dropout."""
+    if not p_drop:
+        return None
+    from ..train.graph import rng_offset_tensor
+    return rng_offset_tensor(device)
 
 
 def _sink_or_zeros(t, n, device):
@@ -46,7 +62,8 @@ class _LayerNorm(torch.autograd.Function):
         b = beta.detach().float().contiguous()
         r = res.contiguous() if res is not None else None
         N.check(N.fn("mdtf_ln_fwd")(N.ptr(x), N.ptr(r), N.ptr(g), N.ptr(b), N.ptr(y), N.ptr(s), N.ptr(mean),
-                                    N.ptr(rstd), rows, H, float(eps), float(p_drop), seed, N.stream_ptr()), "ln_fwd")
+                                    N.ptr(rstd), rows, H, float(eps), float(p_drop), seed,
+                                    N.ptr(_seed_off(p_drop, x.device)), N.stream_ptr()), "ln_fwd")
         ctx.save_for_backward(s, g, mean, rstd)
         ctx.has_res = res is not None
         ctx.drop = (float(p_drop), seed)
@@ -68,7 +85,8 @@ class _LayerNorm(torch.autograd.Function):
         db = sb.grad if sb is not None else torch.zeros(H, dtype=torch.float32, device=s.device)
         ws = torch.empty(N.fn("mdtf_ln_bwd_ws")(rows, H), dtype=torch.float32, device=s.device)
         N.check(N.fn("mdtf_ln_bwd")(N.ptr(dy), N.ptr(s), N.ptr(g), N.ptr(mean), N.ptr(rstd), N.ptr(ds), N.ptr(dxb),
-                                    N.ptr(dg), N.ptr(db), N.ptr(ws), rows, H, p_drop, seed, N.stream_ptr()),
+                                    N.ptr(dg), N.ptr(db), N.ptr(ws), rows, H, p_drop, seed,
+                                    N.ptr(_seed_off(p_drop, s.device)), N.stream_ptr()),
                 "ln_bwd")
         gamma, beta = ctx.like
         rg = V.grad_marker(gamma) if sg is not None else dg
@@ -205,7 +223,8 @@ class _FusedAttention(torch.autograd.Function):
         m = mask.float().contiguous() if mask is not None else None
         scale = 1.0 / math.sqrt(FUSED_DIM)
         N.check(N.fn("mdtf_attn_fwd")(N.ptr(qkv), N.ptr(m), N.ptr(out), N.ptr(lse), B, S_, nh, FUSED_DIM, scale,
-                                      float(p_drop), seed, N.stream_ptr()), "attn_fwd")
+                                      float(p_drop), seed, N.ptr(_seed_off(p_drop, qkv.device)), N.stream_ptr()),
+                "attn_fwd")
         ctx.save_for_backward(qkv, out, lse)
         ctx.mask = m
         ctx.args = (B, S_, nh, float(p_drop), seed, scale)
@@ -218,7 +237,8 @@ class _FusedAttention(torch.autograd.Function):
         dout = dout.contiguous()
         dqkv = torch.empty_like(qkv)
         N.check(N.fn("mdtf_attn_bwd")(N.ptr(qkv), N.ptr(ctx.mask), N.ptr(out), N.ptr(dout), N.ptr(lse), N.ptr(dqkv),
-                                      B, S_, nh, FUSED_DIM, scale, p_drop, seed, N.stream_ptr()), "attn_bwd")
+                                      B, S_, nh, FUSED_DIM, scale, p_drop, seed, N.ptr(_seed_off(p_drop, qkv.device)),
+                                      N.stream_ptr()), "attn_bwd")
         return dqkv, None, None, None, None, None, None
 
 

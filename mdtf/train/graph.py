@@ -1,0 +1,252 @@
+"""hipGraph capture of a whole synchronous training step.
+
+The reference builds a TF1 graph once and replays it with
+``sess.run([train_op, global_step, loss])`` (``distribute_train.py:183-193``);
+TF's executor, not Python, issues the kernels.  mdtf runs eagerly, so a
+ResNet-50 step costs ~470 kernel launches from Python (autograd + ctypes):
+enough host time that the GPU idles between launches at the start of
+backward.  On MI355X the right tool is a HIP graph, not a tracing compiler:
+the step — forward, autograd backward, the bucketed RCCL reductions fired from
+the gradient hooks, the fused optimizer launches and the PS-shard all-gathers
+— is captured once into a ``torch.cuda.CUDAGraph`` (a hipGraph on ROCm) and
+replayed as a single launch per step.
+
+Protocol (:class:`StepGraph`, driven by :class:`mdtf.train.step.TrainOp`):
+
+1. ``warmup`` eager steps: conv autotune lookups, lazily created optimizer
+   state, RCCL communicator setup, allocator warm-up all happen outside
+   capture.
+2. Capture: the step's inputs are bound to *static* device buffers, the
+   per-step hyper-parameters (LR schedule, Adam bias correction, gradient
+   scale) are read by the optimizer kernels from a device buffer ``dyn``
+   (``csrc/optim.hip``), so the captured kernel arguments never go stale.
+3. Replay: copy the new batch into the static buffers (skipped when the
+   loader hands out the same device tensors, e.g. synthetic data), refresh
+   ``dyn`` if a value changed, ``graph.replay()``.
+
+A step falls back to eager execution when it cannot be replayed exactly: a
+changed input shape, backup workers (``replicas_to_aggregate < N`` needs a
+host-side arrival counter), or a non-CUDA device.  Dropout kernels read a
+device step counter (:func:`rng_offset_tensor`) so replayed masks differ step
+to step.
+
+Enable with ``MDTF_HIP_GRAPH=1``, ``--hip_graph`` (FLAGS) or
+``SyncReplicasOptimizer(..., hip_graph=True)``.
+"""
+import os
+
+import torch
+
+_RNG = {}
+
+
+def env_enabled():
+    return os.environ.get("MDTF_HIP_GRAPH", "0") not in ("0", "", "false", "False")
+
+
+def rng_offset_tensor(device):
+    """Device int64 step counter mixed into dropout seeds (incremented once per captured step)."""
+    key = str(device)
+    t = _RNG.get(key)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int64, device=device)
+        _RNG[key] = t
+    return t
+
+
+def capturing():
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def _leaves(x, out):
+    from .step import Placeholder, SourceOutput
+    if isinstance(x, (Placeholder, SourceOutput)):
+        out.append(x)
+    elif isinstance(x, (list, tuple)):
+        for i in x:
+            _leaves(i, out)
+    elif isinstance(x, dict):
+        for i in x.values():
+            _leaves(i, out)
+    return out
+
+
+class _ClonedOutputs(dict):
+    """Program outputs of a replayed step: the graph's static tensors are cloned on first
+    access, so a fetched ``loss`` keeps its value after the next replay overwrites them."""
+
+    def __init__(self, static):
+        super(_ClonedOutputs, self).__init__()
+        self._static = static
+
+    def __getitem__(self, k):
+        if not dict.__contains__(self, k):
+            v = self._static[k]
+            dict.__setitem__(self, k, v.detach().clone() if isinstance(v, torch.Tensor) else v)
+        return dict.__getitem__(self, k)
+
+    def __contains__(self, k):
+        return k in self._static
+
+    def get(self, k, default=None):
+        return self[k] if k in self._static else default
+
+    def keys(self):
+        return self._static.keys()
+
+
+class StepGraph(object):
+    def __init__(self, op, warmup=2):
+        self.op = op
+        self.warmup = max(int(warmup), 1)
+        self.graph = None
+        self.eager_steps = 0
+        self.replays = 0
+        self.fallbacks = 0
+        self.dyn = None
+        self._dyn_vals = None
+        self._static_src = {}       # id(source) -> (source, tuple of static tensors)
+        self._static_ph = {}        # placeholder -> static tensor
+        self._seen_ptrs = {}        # id(source) -> data_ptr tuple per warm-up step
+        self._outputs = {}          # id(program) -> static output dict
+        self._gs = None
+
+    # ------------------------------------------------------------------
+    def _inputs(self):
+        leaves = []
+        for p in self.op.programs:
+            _leaves(p.inputs, leaves)
+        return leaves
+
+    def _resolve_inputs(self, ctx):
+        """Dequeue this step's inputs into ``ctx`` (the same objects the eager path would use)."""
+        from .step import SourceOutput
+        vals = {}
+        for leaf in self._inputs():
+            v = leaf.evaluate(ctx)
+            if isinstance(leaf, SourceOutput):
+                vals[id(leaf.source)] = (leaf.source, ctx.cache[("src", id(leaf.source))])
+            else:
+                vals[leaf] = v
+        return vals
+
+    def _eligible(self):
+        red = self.op.reducer
+        dev = self.op.space.groups[0].device if self.op.space.groups else None
+        return dev is not None and dev.type == "cuda" and red.R == red.world
+
+    # ------------------------------------------------------------------
+    def run(self, ctx, step):
+        """Run one training step (eager, capture or replay); returns the gradient scale."""
+        if not self._eligible():
+            return self.op._run_step(ctx, step)
+        if self.graph is None:
+            if self.eager_steps < self.warmup:
+                self.eager_steps += 1
+                vals = self._resolve_inputs(ctx)
+                self._note_ptrs(vals)
+                return self.op._run_step(ctx, step)
+            return self._capture(ctx, step)
+        vals = self._resolve_inputs(ctx)
+        if not self._bind(vals):
+            self.fallbacks += 1
+            return self.op._run_step(ctx, step)
+        self._set_dyn(step)
+        self.graph.replay()
+        self.replays += 1
+        for p in self.op.programs:
+            out = _ClonedOutputs(self._outputs[id(p)])
+            ctx.cache[("prog", id(p))] = out
+            p.last_outputs = out
+        return self._gs
+
+    def _note_ptrs(self, vals):
+        for k, v in vals.items():
+            if isinstance(k, int):
+                self._seen_ptrs.setdefault(k, []).append(tuple(t.data_ptr() if isinstance(t, torch.Tensor) else 0
+                                                              for t in v[1]))
+
+    def _persistent(self, key, tensors):
+        """The loader hands out the same device tensors every step (synthetic data)."""
+        seen = self._seen_ptrs.get(key, [])
+        now = tuple(t.data_ptr() if isinstance(t, torch.Tensor) else 0 for t in tensors)
+        return len(seen) >= 1 and all(s == now for s in seen)
+
+    def _bind(self, vals):
+        """Copy this step's inputs into the static buffers; False if a shape changed."""
+        copies = []
+        for k, v in vals.items():
+            if isinstance(k, int):
+                static = self._static_src[k][1]
+                for t, s in zip(v[1], static):
+                    if not isinstance(t, torch.Tensor):
+                        continue
+                    if t.shape != s.shape or t.dtype != s.dtype:
+                        return False
+                    if t.data_ptr() != s.data_ptr():
+                        copies.append((s, t))
+            else:
+                s = self._static_ph[k]
+                if v.shape != s.shape:
+                    return False
+                copies.append((s, v))
+        for s, t in copies:
+            s.copy_(t, non_blocking=True)
+        return True
+
+    def _set_dyn(self, step):
+        op = self.op
+        lr = op.optimizer.learning_rate(step)
+        vals = (float(lr), float(op.optimizer.step_size(lr, op.step_count)), float(self._gs))
+        if vals != self._dyn_vals:
+            host = torch.tensor(vals, dtype=torch.float32).pin_memory()
+            self.dyn.copy_(host, non_blocking=True)
+            self._dyn_vals = vals
+
+    def _capture(self, ctx, step):
+        from .step import RunContext
+        op = self.op
+        dev = op.space.groups[0].device
+        vals = self._resolve_inputs(ctx)
+        feed = {}
+        cache = {}
+        for k, v in vals.items():
+            if isinstance(k, int):
+                src, tensors = v
+                if self._persistent(k, tensors):
+                    static = tensors
+                else:
+                    static = tuple(t.clone() if isinstance(t, torch.Tensor) else t for t in tensors)
+                self._static_src[k] = (src, static)
+                cache[("src", k)] = static
+            else:
+                s = v.clone()
+                self._static_ph[k] = s
+                feed[k] = s
+        # the scale is fixed for a replayable step (all replicas contribute)
+        red = op.reducer
+        self._gs = (1.0 / red.world) * op.grad_scale_extra
+        self.dyn = torch.zeros(3, dtype=torch.float32, device=dev)
+        self._dyn_vals = None
+        self._set_dyn(step)
+        rng = rng_offset_tensor(dev)
+        fd = dict(ctx.feed_dict)
+        fd.update(feed)
+        cap_ctx = RunContext(feed_dict=fd, session=ctx.session)
+        cap_ctx.cache.update(cache)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            rng.add_(1)
+            op._run_step(cap_ctx, step, dyn=self.dyn)
+        self.graph = g
+        for p in op.programs:
+            self._outputs[id(p)] = cap_ctx.cache[("prog", id(p))]
+        # capture records without executing: run this step now
+        g.replay()
+        self.replays += 1
+        for p in op.programs:
+            out = _ClonedOutputs(self._outputs[id(p)])
+            ctx.cache[("prog", id(p))] = out
+            p.last_outputs = out
+        return self._gs

@@ -59,8 +59,14 @@ class Optimizer(object):
         return self.apply_gradients(self.compute_gradients(loss, var_list), global_step, name)
 
     # -- fused update over one UpdateTarget ------------------------------
-    def update(self, target, lr, grad_scale, step):
+    def update(self, target, lr, grad_scale, step, dyn=None):
+        """One fused launch over ``target``.  ``dyn``: optional device tensor
+        ``[lr, lr_t, grad_scale]`` overriding the scalars (hipGraph replay)."""
         raise NotImplementedError
+
+    def step_size(self, lr, step):
+        """The per-step ``lr_t`` the kernel applies (Adam folds its bias correction in)."""
+        return lr
 
     def _wd(self, target):
         return self.weight_decay if target.decay else 0.0
@@ -77,8 +83,8 @@ class GradientDescentOptimizer(Optimizer):
     def __init__(self, learning_rate, use_locking=False, name="GradientDescent", weight_decay=0.0):
         super(GradientDescentOptimizer, self).__init__(learning_rate, use_locking, name, weight_decay)
 
-    def update(self, target, lr, grad_scale, step):
-        K.sgd_(target.master, target.grad, target.shadow, lr, grad_scale, self._wd(target))
+    def update(self, target, lr, grad_scale, step, dyn=None):
+        K.sgd_(target.master, target.grad, target.shadow, lr, grad_scale, self._wd(target), dyn=dyn)
 
 
 class MomentumOptimizer(Optimizer):
@@ -88,9 +94,9 @@ class MomentumOptimizer(Optimizer):
         self.momentum = float(momentum)
         self.use_nesterov = use_nesterov
 
-    def update(self, target, lr, grad_scale, step):
+    def update(self, target, lr, grad_scale, step, dyn=None):
         K.momentum_(target.master, target.grad, target.state("momentum"), target.shadow, lr, self.momentum,
-                    grad_scale, self._wd(target), self.use_nesterov)
+                    grad_scale, self._wd(target), self.use_nesterov, dyn=dyn)
 
     def slot_checkpoint_names(self):
         return [("momentum", "Momentum")]
@@ -104,10 +110,13 @@ class AdamOptimizer(Optimizer):
         self.decoupled = decoupled_weight_decay
         self.bias_correction = bias_correction
 
-    def update(self, target, lr, grad_scale, step):
+    def update(self, target, lr, grad_scale, step, dyn=None):
         K.adam_(target.master, target.grad, target.state("m"), target.state("v"), target.shadow, lr,
                 self.beta1, self.beta2, self.epsilon, step + 1, grad_scale, self._wd(target), self.decoupled,
-                self.bias_correction)
+                self.bias_correction, dyn=dyn)
+
+    def step_size(self, lr, step):
+        return K.adam_lr_t(lr, self.beta1, self.beta2, step + 1, self.bias_correction)
 
     def slot_checkpoint_names(self):
         return [("m", "Adam"), ("v", "Adam_1")]
@@ -138,7 +147,7 @@ class SyncReplicasOptimizer(Optimizer):
 
     def __init__(self, opt, replicas_to_aggregate=None, total_num_replicas=None, variable_averages=None,
                  variables_to_average=None, use_locking=False, name="sync_replicas", mode="allreduce",
-                 bucket_bytes=None, overlap=True):
+                 bucket_bytes=None, overlap=True, hip_graph=None):
         super(SyncReplicasOptimizer, self).__init__(opt._lr, use_locking, name, opt.weight_decay)
         self._opt = opt
         self.replicas_to_aggregate = replicas_to_aggregate
@@ -146,12 +155,16 @@ class SyncReplicasOptimizer(Optimizer):
         self.mode = mode
         self.bucket_bytes = bucket_bytes
         self.overlap = overlap
+        self.hip_graph = hip_graph   # None: MDTF_HIP_GRAPH / --hip_graph decide (mdtf.train.graph)
 
     def learning_rate(self, global_step=0):
         return self._opt.learning_rate(global_step)
 
-    def update(self, target, lr, grad_scale, step):
-        self._opt.update(target, lr, grad_scale, step)
+    def update(self, target, lr, grad_scale, step, dyn=None):
+        self._opt.update(target, lr, grad_scale, step, dyn=dyn)
+
+    def step_size(self, lr, step):
+        return self._opt.step_size(lr, step)
 
     def slot_checkpoint_names(self):
         return self._opt.slot_checkpoint_names()

@@ -266,6 +266,7 @@ class TrainOp(Fetchable):
         self.step_count = 0
         self.grad_scale_extra = 1.0 / max(len(self.programs), 1)
         self.last_contributed = True
+        self.graph = None
         _register(self)
 
     # -- finalisation: flat buffers + reducer ----------------------------
@@ -295,26 +296,50 @@ class TrainOp(Fetchable):
                                    replicas_to_aggregate=R, store=store)
 
     # -- execution ---------------------------------------------------------
+    def _graph_enabled(self):
+        from . import graph as G
+        flag = getattr(self.optimizer, "hip_graph", None)
+        if flag is None:
+            flag = G.env_enabled()
+            if not flag:
+                try:
+                    from ..config.flags import FLAGS
+                    flag = bool(getattr(FLAGS, "hip_graph", False))
+                except Exception:
+                    flag = False
+        return bool(flag) and torch.cuda.is_available()
+
+    def _run_step(self, ctx, step, dyn=None):
+        """forward + backward of every tower program, reduction, fused update (one step)."""
+        red = self.reducer
+        red.begin_step()
+        for prog in self.programs:
+            out = prog.forward(ctx, grad=True)
+            loss = out[self.loss_key]
+            loss.backward()
+        scale = red.end_backward(step) * self.grad_scale_extra
+        lr = self.optimizer.learning_rate(step)
+        with torch.no_grad():
+            for target in red.update_targets():
+                self.optimizer.update(target, lr, scale, self.step_count, dyn=dyn)
+            red.after_update()
+        return scale
+
     def evaluate(self, ctx):
         key = ("train", id(self))
         if key in ctx.cache:
             return None
         if self.space is None:
             self.finalize()
-        red = self.reducer
-        red.begin_step()
         step = self.global_step.value() if self.global_step is not None else self.step_count
-        for prog in self.programs:
-            out = prog.forward(ctx, grad=True)
-            loss = out[self.loss_key]
-            loss.backward()
-        scale = red.end_backward(step) * self.grad_scale_extra
-        self.last_contributed = red.contributed
-        lr = self.optimizer.learning_rate(step)
-        with torch.no_grad():
-            for target in red.update_targets():
-                self.optimizer.update(target, lr, scale, self.step_count)
-            red.after_update()
+        if self.graph is None and self._graph_enabled():
+            from .graph import StepGraph
+            self.graph = StepGraph(self)
+        if self.graph is not None:
+            self.graph.run(ctx, step)
+        else:
+            self._run_step(ctx, step)
+        self.last_contributed = self.reducer.contributed
         self.step_count += 1
         if self.global_step is not None:
             self.global_step.increment()

@@ -630,7 +630,7 @@ def test_fused_attention_fwd_bwd(p_drop):
     s = q @ k.transpose(-1, -2) / dh ** 0.5 + mask[:, None, None, :]
     pr = torch.softmax(s, -1)
     if p_drop:
-        keep = _attn_keep_mask(seed, B, nh, S, p_drop)
+        keep = _attn_keep_mask(T.effective_seed(seed, xg.device), B, nh, S, p_drop)
         pr = pr * keep / (1 - p_drop)
     ref = (pr @ v).transpose(1, 2).reshape(B * S, H)
     ref.backward(dout.bfloat16().float())
@@ -734,7 +734,7 @@ def test_layernorm_fused_dropout():
     rg = r.to(DEV).bfloat16().requires_grad_(True)
     y = T._LayerNorm.apply(xg, rg, g.to(DEV), b.to(DEV), 1e-12, p, seed)
     y.backward(dy.to(DEV).bfloat16())
-    keep = _hash_keep(seed, rows * H, p).view(rows, H).float()
+    keep = _hash_keep(T.effective_seed(seed, xg.device), rows * H, p).view(rows, H).float()
     xc = x.bfloat16().float().requires_grad_(True)
     rc = r.bfloat16().float().requires_grad_(True)
     s = xc * keep / (1 - p) + rc
