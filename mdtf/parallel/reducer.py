@@ -29,6 +29,8 @@ drops them as stale); arrival order comes from an atomic counter in the
 cluster store.  Overlap is disabled in that mode because the mask is only
 known after backward.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -63,7 +65,11 @@ class GradReducer(object):
         if self.R > self.world or self.R < 1:
             raise ValueError("replicas_to_aggregate=%d must be in [1, %d]" % (self.R, self.world))
         self.store = store
-        self.overlap = overlap and self.world > 1 and self.R == self.world
+        # collectives run for world > 1; MDTF_FORCE_COLLECTIVES=1 also issues them on a 1-rank group
+        # (exercises the RCCL + hipGraph capture path on a single GPU)
+        self.collective = self.distributed and (self.world > 1 or
+                                                os.environ.get("MDTF_FORCE_COLLECTIVES", "0") == "1")
+        self.overlap = overlap and self.collective and self.R == self.world
         self.contributed = True
         self.num_contributors = self.world
         self._shards = {}
@@ -122,7 +128,7 @@ class GradReducer(object):
         if b.launched:
             return
         b.launched = True
-        if self.world == 1:
+        if not self.collective:
             return
         g = b.group
         if self.mode == "allreduce":
@@ -153,7 +159,7 @@ class GradReducer(object):
             if b.work is not None:
                 b.work.wait()
                 b.work = None
-        if self.world == 1 and self.mode == "sharded":
+        if not self.collective and self.mode == "sharded":
             for g in self.space.groups:
                 self._shards[id(g)]["grad"].copy_(self._gather_index(g, g.grad))
         return 1.0 / self.num_contributors
@@ -185,7 +191,7 @@ class GradReducer(object):
             for b in g.buckets:
                 part = src[b.shard_offset:b.shard_offset + b.shard_len]
                 dst = dst_full[b.start:b.end]
-                if self.world == 1:
+                if not self.collective:
                     dst.copy_(part)
                 else:
                     works.append(dist.all_gather_into_tensor(dst, part, group=self.pg, async_op=True))

@@ -28,7 +28,7 @@ class _TinyRes(object):
         return tools.dense("logits", x, 16)
 
 
-def _run_resnetish(dev, dt, batches, hip_graph, opt_kind="momentum"):
+def _run_resnetish(dev, dt, batches, hip_graph, opt_kind="momentum", mode="allreduce"):
     from mdtf.models import SoftmaxCrossEntropyLoss
     from mdtf.runtime import Model, Net, Tower
     from mdtf.train import step as S
@@ -50,7 +50,7 @@ def _run_resnetish(dev, dt, batches, hip_graph, opt_kind="momentum"):
     M = type("TinyResModel", (_TinyRes, Model), {})
     t = Tower(Net(M()), "tower_0/", tg, xp, yp, SoftmaxCrossEntropyLoss(), base, batch_size=x0.shape[0])
     _, loss, _ = t.process()
-    opt = mdtf.train.SyncReplicasOptimizer(base, hip_graph=hip_graph)
+    opt = mdtf.train.SyncReplicasOptimizer(base, hip_graph=hip_graph, mode=mode, bucket_bytes=1 << 18)
     op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
     sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
     losses = []
@@ -164,3 +164,36 @@ def test_hip_graph_bert_dropout_advances_per_replay():
     assert int(G.rng_offset_tensor(store.device).item()) - rng0 == 23
     assert len(set(ls[3:])) > 10          # not the same masked step replayed over and over
     assert sum(ls[-5:]) < 0.7 * sum(ls[:5]), ls
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["allreduce", "sharded"])
+def test_hip_graph_captures_rccl_collectives(mode, monkeypatch):
+    """The bucketed RCCL all-reduce (or PS-shard reduce-scatter + all-gather) fired from the gradient hooks
+    is captured into the step graph: a 1-rank nccl group with collectives forced on, eager == replay."""
+    _gpu()
+    import socket
+    import torch.distributed as dist
+    from mdtf.ops import _native
+    monkeypatch.setenv("MDTF_FORCE_COLLECTIVES", "1")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    try:
+        torch.manual_seed(0)
+        batches = [(torch.randn(16, 16, 16, 8), torch.randint(0, 16, (16,))) for _ in range(5)]
+        _native.set_deterministic(True)
+        try:
+            l_e, w_e, op_e = _run_resnetish("cuda", torch.bfloat16, batches, hip_graph=False, mode=mode)
+            l_g, w_g, op = _run_resnetish("cuda", torch.bfloat16, batches, hip_graph=True, mode=mode)
+        finally:
+            _native.set_deterministic(False)
+        assert op_e.reducer.collective and op_e.reducer.overlap and len(op_e.space.buckets) > 1
+        assert op.graph.replays == 3 and op.graph.fallbacks == 0
+        assert l_e == l_g, (l_e, l_g)
+        for k in w_e:
+            assert torch.equal(w_e[k], w_g[k]), k
+    finally:
+        dist.destroy_process_group()
