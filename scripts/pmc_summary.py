@@ -1,0 +1,74 @@
+#!/usr/bin/env python
+"""Summarise the rocprofv3 --pmc passes of scripts/gpu_pmc.sh per kernel.
+
+usage: pmc_summary.py <dir prefix, e.g. gpurun_out/pmc1> [top N]
+
+Per kernel (aggregated over its dispatches in the profiled steps):
+  time      summed dispatch time (serialised by the counter collection)
+  TF/s      SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512 FLOP / time
+  MFMA %    SQ_VALU_MFMA_BUSY_CYCLES / (time x 2.4 GHz x 1024 SIMDs)
+  LDS conf  SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra cycles per LDS-array cycle)
+  HBM GB/s  (FETCH_SIZE + WRITE_SIZE) KiB / time
+  L2 hit    TCC_HIT / (TCC_HIT + TCC_MISS)
+"""
+import collections
+import csv
+import re
+import sys
+
+CLOCK = 2.4e9
+SIMDS = 1024
+
+
+def load(path):
+    per = collections.OrderedDict()
+    for r in csv.DictReader(open(path)):
+        d = per.setdefault(int(r["Dispatch_Id"]), {"name": r["Kernel_Name"],
+                                                   "dur": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return list(per.values())
+
+
+def short(name):
+    n = re.sub(r"\(anonymous namespace\)::", "", name)
+    n = re.sub(r"\(\(ConvArgs\)\)|\(ConvArgs\)", "", n)
+    n = n.replace("void ", "")
+    return n[:70]
+
+
+def main(prefix, top):
+    # each pass is its own run: aggregate per kernel name within a pass, then join the passes by name
+    aggs = []
+    for i in (1, 2, 3):
+        agg = collections.defaultdict(lambda: collections.defaultdict(float))
+        for d in load("%s_p%d/run_counter_collection.csv" % (prefix, i)):
+            a = agg[short(d["name"])]
+            a["calls"] += 1
+            a["dur"] += d["dur"]
+            for k, v in d.items():
+                if k not in ("name", "dur"):
+                    a[k] += v
+        aggs.append(agg)
+    a1, a2, a3 = aggs
+    rows = sorted(a1.items(), key=lambda t: -t[1]["dur"])
+    tot = sum(a["dur"] for _, a in rows)
+    print("| kernel | calls | ms | TF/s | MFMA busy % | LDS bank-conflict % | HBM GB/s (rd+wr) | L2 hit % |")
+    print("|---|---|---|---|---|---|---|---|")
+    for name, a in rows[:top]:
+        b, c = a2.get(name, {}), a3.get(name, {})
+        dur = a["dur"]
+        tf = a["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 / dur / 1e12 if dur else 0
+        mf = 100.0 * a["SQ_VALU_MFMA_BUSY_CYCLES"] / (dur * CLOCK * SIMDS) if dur else 0
+        lds = 100.0 * a["SQ_LDS_BANK_CONFLICT"] / a["SQ_LDS_IDX_ACTIVE"] if a["SQ_LDS_IDX_ACTIVE"] else 0
+        rd = b.get("FETCH_SIZE", 0) * 1024 / b["dur"] / 1e9 if b.get("dur") else 0
+        wr = c.get("WRITE_SIZE", 0) * 1024 / c["dur"] / 1e9 if c.get("dur") else 0
+        hit = c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0)
+        hit = 100.0 * c.get("TCC_HIT_sum", 0) / hit if hit else 0
+        print("| `%s` | %d | %.3f | %.0f | %.1f | %.1f | %.0f + %.0f | %.0f |" % (
+            name, a["calls"], dur * 1e3, tf, mf, lds, rd, wr, hit))
+    print("\nprofiled dispatches (pass 1): %d, total serialized kernel time %.2f ms" % (
+        sum(a["calls"] for _, a in rows), tot * 1e3))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 40)
