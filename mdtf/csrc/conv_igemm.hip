@@ -497,11 +497,14 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(ConvArgs a) {
 // taps that reach DY is fixed and the DY offsets are affine again, so each
 // class is a dense implicit GEMM over only its own taps (no zero-tap waste).
 // ============================================================================
-template <int BM, int BN, int MODE, bool STATS, int STAGES>
-__global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
-  constexpr int WM = 2, WN = 2;
+template <int BM, int BN, int MODE, bool STATS, int STAGES, int NW>
+__global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
+  // NW = 4 waves (2x2) or 8 waves (one 256-row block per CU: 2 waves per SIMD, half the
+  // operand traffic per FLOP of a 128x128 tile; 4x2 or 2x4 waves by the tile's aspect)
+  constexpr int NT = 64 * NW;
+  constexpr int WM = NW == 4 ? 2 : (BM > BN ? 4 : 2), WN = NW / WM;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
-  constexpr int RA = BM / 32, RB = BN / 32;       // DMA instructions per wave per K step
+  constexpr int RA = BM / (8 * NW), RB = BN / (8 * NW);   // DMA instructions per wave per K step
   constexpr int ROWB = 128;                       // bytes per LDS row (64 bf16)
   constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int PER_STAGE = RA + RB;               // LDS-DMA wave-instructions per stage
@@ -537,7 +540,7 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
   unsigned a_off[RA], a_mask[RA];
 #pragma unroll
   for (int i = 0; i < RA; ++i) {
-    const int row = 8 * (wave + 4 * i) + lrow;
+    const int row = 8 * (wave + NW * i) + lrow;
     const long long m = m0 + row;
     const bool ok = m < a.M;
     const long long mm = ok ? m : 0;
@@ -564,7 +567,7 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
   unsigned b_off[RB];
 #pragma unroll
   for (int i = 0; i < RB; ++i) {
-    const int row = 8 * (wave + 4 * i) + lrow;
+    const int row = 8 * (wave + NW * i) + lrow;
     const int n = n0 + row;
     const int ch = 8 * ((lane & 7) ^ ((row >> 1) & 7));
     const long long e = MODE == 0 ? (long long)n * a.K + ch : (long long)n * a.Cout + ch;
@@ -580,14 +583,14 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
     for (int i = 0; i < RA; ++i) {
       const bool ok = (a_mask[i] >> s_t) & 1u;
       const unsigned voff = ok ? (a_off[i] + (unsigned)tap_e) * 2u : OOB;
-      dma16(a.src, bytes_a, lds + (wave + 4 * i) * 1024, voff, 0);
+      dma16(a.src, bytes_a, lds + (wave + NW * i) * 1024, voff, 0);
     }
     char* ldsb = lds + BM * ROWB;
     const int wtap = MODE == 2 ? (a.cls_kh0 + a.SH * s_kh) * a.KW + a.cls_kw0 + a.SW * s_kw : s_t;
     const int sb = MODE == 0 ? s_k0 * 2 : (wtap * a.Cin * a.Cout + s_c0) * 2;
 #pragma unroll
     for (int i = 0; i < RB; ++i)
-      dma16(a.wgt, bytes_b, ldsb + (wave + 4 * i) * 1024, b_off[i], sb);
+      dma16(a.wgt, bytes_b, ldsb + (wave + NW * i) * 1024, b_off[i], sb);
     // advance the K walk by 64
     s_k0 += 64;
     s_c0 += 64;
@@ -852,8 +855,9 @@ __global__ void __launch_bounds__(NT) conv_fd_v2(ConvArgs a) {
   }
 }
 
-template <int BM, int BN, int MODE, bool STATS, int STAGES>
+template <int BM, int BN, int MODE, bool STATS, int STAGES, int NW = 4>
 int launch_fd_v2(ConvArgs& a, hipStream_t st) {
+  constexpr int NT = 64 * NW;
   a.mtiles = static_cast<int>(ceil_div(a.M, BM));
   a.ntiles = static_cast<int>(ceil_div(a.Ncol, BN));
   const long long nblk = (long long)a.mtiles * a.ntiles;
@@ -862,7 +866,8 @@ int launch_fd_v2(ConvArgs& a, hipStream_t st) {
   size_t lds = stage_bytes > ctile ? stage_bytes : ctile;
   if (lds < (size_t)NT * 16 * sizeof(float)) lds = (size_t)NT * 16 * sizeof(float);   // BN-stat reduction
   if (STAGES == 1 && a.K > 64) return MDTF_EINVAL;      // single buffer: one K step only
-  hipLaunchKernelGGL((conv_fd_v2<BM, BN, MODE, STATS, STAGES>), dim3((unsigned)nblk), dim3(NT), lds, st, a);
+  if (lds > 160 * 1024) return MDTF_EUNSUPPORTED;
+  hipLaunchKernelGGL((conv_fd_v2<BM, BN, MODE, STATS, STAGES, NW>), dim3((unsigned)nblk), dim3(NT), lds, st, a);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
@@ -879,8 +884,20 @@ int dispatch_fd_v2s(ConvArgs& a, int bm, int bn, hipStream_t st) {
   return MDTF_EUNSUPPORTED;
 }
 
+// 8-wave tiles (bm code >= 10000): 256 x {256, 128, 64} and 128 x 256, LDS ring <= 160 KiB
+template <int MODE, bool STATS>
+int dispatch_fd_v2w8(ConvArgs& a, int bm, int bn, int stages, hipStream_t st) {
+#define FD8(BM_, BN_, S_) \
+  if (bm == BM_ && bn == BN_ && stages == S_) return launch_fd_v2<BM_, BN_, MODE, STATS, S_, 8>(a, st);
+  FD8(256, 256, 1) FD8(256, 256, 2) FD8(256, 128, 1) FD8(256, 128, 2) FD8(256, 128, 3) FD8(256, 64, 2)
+  FD8(256, 64, 3) FD8(256, 64, 4) FD8(128, 256, 2) FD8(128, 256, 3)
+#undef FD8
+  return MDTF_EUNSUPPORTED;
+}
+
 template <int MODE, bool STATS>
 int dispatch_fd_v2(ConvArgs& a, int bm, int bn, int stages, hipStream_t st) {
+  if (bm >= 10000) return dispatch_fd_v2w8<MODE, STATS>(a, bm % 10000, bn, stages, st);
   if (stages == 1) return dispatch_fd_v2s<MODE, STATS, 1>(a, bm, bn, st);
   if (stages == 2) return dispatch_fd_v2s<MODE, STATS, 2>(a, bm, bn, st);
   if (stages == 3) return dispatch_fd_v2s<MODE, STATS, 3>(a, bm, bn, st);
@@ -1239,8 +1256,9 @@ MDTF_EXPORT int mdtf_conv_fwd_v2(const void* x, const void* wt, void* y, float* 
   a.M = (long long)N * OH * OW;
   a.Ncol = Cout;
   a.K = KH * KW * Cin;
-  const int stages = bm / 1000 ? bm / 1000 : 2;   // bm = stages * 1000 + tile rows
-  bm %= 1000;
+  // bm = 10000 (8 waves) + stages * 1000 + tile rows
+  const int w8 = bm / 10000, stages = (bm % 10000) / 1000 ? (bm % 10000) / 1000 : 2;
+  bm = w8 * 10000 + bm % 1000;
   int rc = stat_sum ? dispatch_fd_v2<0, true>(a, bm, bn, stages, st) : dispatch_fd_v2<0, false>(a, bm, bn, stages, st);
   if (mtiles_out) *mtiles_out = a.mtiles;
   return rc;
@@ -1267,8 +1285,8 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
   a.bsq = bsq;
   a.bslots = bslots > 0 ? bslots : 1;
   a.Ncol = Cin;
-  const int stages = bm / 1000 ? bm / 1000 : 2;
-  bm %= 1000;
+  const int w8 = bm / 10000, stages = (bm % 10000) / 1000 ? (bm % 10000) / 1000 : 2;
+  bm = w8 * 10000 + bm % 1000;
   if (SH == 1 && SW == 1) {
     a.M = (long long)N * H * W;
     a.K = KH * KW * Cout;

@@ -27,7 +27,7 @@ N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P, N.P, 
 N.register("mdtf_conv_wgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-TABLE_PATH = os.path.join(_HERE, "conv_table.json")
+TABLE_PATH = os.environ.get("MDTF_CONV_TABLE") or os.path.join(_HERE, "conv_table.json")
 _TABLE = None
 
 
@@ -162,6 +162,12 @@ def transpose_filter(w):
     return kernels.transpose_brs(w.reshape(1, kh * kw * ci, co), 1, kh * kw * ci, co).view(co, kh * kw * ci)
 
 
+def _v2_code(bm, stages, ver):
+    """C-ABI tile code of the v2 kernels: [10000 if 8 waves] + 1000 * stages + tile rows.
+    ``ver`` 2 = 4-wave tiles, 3 = 8-wave tiles (one 256-row or 256-column block per CU)."""
+    return bm + 1000 * stages + (10000 if ver == 3 else 0)
+
+
 def mdtf_fwd(x, w, out_hw, stride, pads, dil, bm, bn, stats=None, ver=1, stages=2):
     n = x.shape[0]
     co = w.shape[3]
@@ -170,10 +176,10 @@ def mdtf_fwd(x, w, out_hw, stride, pads, dil, bm, bn, stats=None, ver=1, stages=
     s_sum, s_sq = (stats if stats is not None else (None, None))
     slots = s_sum.shape[0] if s_sum is not None else 0
     import ctypes
-    if ver == 2:
+    if ver in (2, 3):
         wt = transpose_filter(w)
         N.check(N.fn("mdtf_conv_fwd_v2")(N.ptr(x), N.ptr(wt), N.ptr(y), N.ptr(s_sum), N.ptr(s_sq), slots,
-                                         *_geo(x, w, out_hw, stride, pads, dil), bm + 1000 * stages, bn,
+                                         *_geo(x, w, out_hw, stride, pads, dil), _v2_code(bm, stages, ver), bn,
                                          ctypes.byref(mt),
                                          N.stream_ptr()), "conv_fwd_v2")
         return y
@@ -193,9 +199,9 @@ def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn, ver=1, stages=2, out=N
     n, h, wd, c = x_shape
     kh, kw, ci, co = w.shape
     geo = [n, h, wd, c, dy.shape[1], dy.shape[2], co, kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1]]
-    if ver == 2:
+    if ver in (2, 3):
         bx, bmask, bsum, bsq, bslots = bn_stats if bn_stats is not None else (None, None, None, None, 0)
-        N.check(N.fn("mdtf_conv_dgrad_v2")(N.ptr(dy), N.ptr(w), N.ptr(dx), *geo, bm + 1000 * stages, bn,
+        N.check(N.fn("mdtf_conv_dgrad_v2")(N.ptr(dy), N.ptr(w), N.ptr(dx), *geo, _v2_code(bm, stages, ver), bn,
                                            int(bool(accumulate)), N.ptr(bx), N.ptr(bmask), N.ptr(bsum), N.ptr(bsq),
                                            int(bslots), N.stream_ptr()), "conv_dgrad_v2")
         return dx
@@ -347,7 +353,7 @@ class _Conv(torch.autograd.Function):
         if need_dx and cd[0] == "winograd":
             dx = winograd.winograd_dgrad(dy, w, x.shape, pads)
         elif need_dx and not lib_dx:
-            if xs is not None and cd[4] == 2:
+            if xs is not None and cd[4] in (2, 3):
                 buf, acc = xs.target()
                 bst = None
                 if xs.stat_req is not None and xs.completing() and BWD_STATS and not N.deterministic():

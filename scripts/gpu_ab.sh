@@ -1,12 +1,14 @@
 #!/bin/bash
-# GPU job: A/B of the BN-backward-statistics fusion (same box), plus the wgrad GEMM micro-bench
+# A/B: ResNet-50 bench with conv table A vs B (alternating, 2 runs each), one box.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-TAG=${1:-ab}
-for v in 1 0 1 0; do
-  MDTF_BN_BWD_STATS=$v timeout -k 10 300 python bench.py --steps 30 --warmup 10 > gpurun_out/bench_${TAG}_$v.log 2>&1 || exit 1
-  echo "BN_BWD_STATS=$v $(tail -1 gpurun_out/bench_${TAG}_$v.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+TAG=${1:-ab}; A=${2:-bench/conv_table_prev.json}; B=${3:-mdtf/ops/conv_table.json}
+for i in 1 2; do
+  for T in A B; do
+    F=$A; [ $T = B ] && F=$B
+    MDTF_CONV_TABLE=$F timeout -k 10 200 python bench.py --steps 30 --warmup 5 > gpurun_out/ab_${TAG}_$T$i.json \
+        2> gpurun_out/ab_${TAG}_$T$i.err || { echo "bench $T failed"; tail -20 gpurun_out/ab_${TAG}_$T$i.err; exit 1; }
+    echo "$T$i $(python -c "import json,sys; d=json.load(open('gpurun_out/ab_${TAG}_$T$i.json')); print(d['value'], d['ms_per_step'])")"
+  done
 done
-timeout -k 10 300 python bench/gemm_micro.py > gpurun_out/gemm_micro_$TAG.log 2>&1 || exit 1
-cat gpurun_out/gemm_micro_$TAG.log

@@ -879,3 +879,50 @@ def test_fanout_gradient_sinks(conv_backend, monkeypatch):
     for k in gc:
         assert _rel(gg[k], go[k]) < 2e-2, (k, _rel(gg[k], go[k]))        # sinks vs autograd adds
         assert _rel(gg[k], gc[k]) < 0.25, (k, _rel(gg[k], gc[k]))        # bf16 path vs fp32 (deep-layer noise)
+
+
+V3_TILES = [(256, 256, 1), (256, 256, 2), (256, 128, 1), (256, 128, 2), (256, 128, 3), (256, 64, 2),
+            (256, 64, 3), (256, 64, 4), (128, 256, 2), (128, 256, 3)]
+
+
+@pytest.mark.parametrize("bm,bn,stages", V3_TILES)
+@pytest.mark.parametrize("geo", [(3, 9, 9, 64, 3, 320, 1), (2, 12, 12, 128, 1, 256, 1), (2, 15, 13, 64, 3, 128, 2)])
+def test_conv_v2_8wave_tiles(bm, bn, stages, geo):
+    """8-wave (512-thread) v2 tiles: forward with the fused BN-statistics epilogue, stride-1 / strided dgrad
+    (plain and accumulating) vs fp32 references; M and N tails, one and many K steps."""
+    from mdtf.ops import conv as C
+    n, h, w, c, k, co, s = geo
+    if stages == 1 and k * k * c > 64:
+        k, s = 1, 1                                   # single-buffer tiles: one K step only
+    if stages == 1:
+        c = 64
+    torch.manual_seed(bm + bn + stages + k)
+    p = k // 2
+    pads = (p, p, p, p)
+    oh = (h + 2 * p - k) // s + 1
+    ow = (w + 2 * p - k) // s + 1
+    x = torch.randn(n, h, w, c).bfloat16()
+    wt = (torch.randn(k, k, c, co) / (k * k * c) ** 0.5).bfloat16()
+    xr = x.float().permute(0, 3, 1, 2)
+    yr = torch.nn.functional.conv2d(xr, wt.float().permute(3, 2, 0, 1), stride=s, padding=p).permute(0, 2, 3, 1)
+    sbuf = torch.zeros(2, 64, co, device=DEV)
+    y = C.mdtf_fwd(x.to(DEV), wt.to(DEV), (oh, ow), (s, s), pads, (1, 1), bm, bn, (sbuf[0], sbuf[1]), 3, stages)
+    assert _rel(y, yr) < 1e-2
+    yf = yr.reshape(-1, co)                 # the statistics come from the fp32 accumulators
+    assert _rel(sbuf[0].sum(0), yf.sum(0)) < 5e-3
+    assert _rel(sbuf[1].sum(0), (yf * yf).sum(0)) < 5e-3
+    if co % 64 or (stages == 1 and k * k * co > 64):
+        return
+    # dgrad: DX [n,h,w,c] from DY [n,oh,ow,co]; Ncol = c
+    dy = torch.randn(n, oh, ow, co).bfloat16()
+    xg = torch.zeros(n, c, h, w, requires_grad=True)
+    yg = torch.nn.functional.conv2d(xg, wt.float().permute(3, 2, 0, 1), stride=s, padding=p)
+    yg.backward(dy.float().permute(0, 3, 1, 2))
+    ref = xg.grad.permute(0, 2, 3, 1)
+    dx = C.mdtf_dgrad(dy.to(DEV), wt.to(DEV), (n, h, w, c), (s, s), pads, (1, 1), bm, bn, 3, stages)
+    assert _rel(dx, ref) < 1e-2
+    base = torch.randn(n, h, w, c).bfloat16()
+    out = base.to(DEV).clone()
+    C.mdtf_dgrad(dy.to(DEV), wt.to(DEV), (n, h, w, c), (s, s), pads, (1, 1), bm, bn, 3, stages, out=out,
+                 accumulate=True)
+    assert _rel(out, ref + base.float()) < 1e-2
