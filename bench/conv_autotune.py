@@ -167,8 +167,10 @@ def main():
                               "mdtf_ms": round(best[0], 4) if best else None}
                 choice = "winograd"
             # a library forward cannot fuse the following BatchNorm's statistics (a separate pass over y),
-            # which the mdtf timing includes: MIOpen must be clearly faster to be chosen for fwd
-            elif best is not None and best[0] < (t_lib / 0.85 if pass_ == "fwd" else t_lib):
+            # which the mdtf timing includes; a library dgrad cannot accumulate into a fanned-out input's
+            # gradient or emit the BN backward statistics in its epilogue (an extra add / reduction pass):
+            # MIOpen must be clearly faster to be chosen for either
+            elif best is not None and best[0] < {"fwd": t_lib / 0.85, "dgrad": t_lib / 0.75}.get(pass_, t_lib):
                 ent = {"backend": "mdtf", "bm": best[1], "bn": best[2], "splits": best[3], "ver": best[4],
                        "ms": round(best[0], 4), "miopen_ms": round(t_lib, 4)}
                 if best[4] == 2 and pass_ == "wgrad":     # v2 wgrad: bm field carries (rows, stages)

@@ -66,10 +66,15 @@ __global__ void __launch_bounds__(kThreads)
 #pragma unroll
   for (int i = 0; i < 8; ++i) s0[i] = s1[i] = 0.f;
   if (c0 < C) {
-    const long long step = (long long)gridDim.x * rg;
-    long long r = (long long)blockIdx.x * rg + rgi;
+    // each block reduces one contiguous range of rows (contiguous streams per block keep HBM at
+    // full rate; a grid-stride sweep does not, bench/ew_probe.hip); row groups interleave inside it
+    const long long span = ceil_div(ceil_div(M, (long long)gridDim.x), (long long)rg) * rg;
+    const long long rbeg = (long long)blockIdx.x * span;
+    const long long rend = rbeg + span < M ? rbeg + span : M;
+    const long long step = rg;
+    long long r = rbeg + rgi;
     // 4 rows per iteration: all loads issued before the first use (bytes in flight)
-    for (; r + 3 * step < M; r += 4 * step) {
+    for (; r + 3 * step < rend; r += 4 * step) {
       // raw 16-B vectors (4 VGPRs each) so every load is in flight before the first use
       uint4 ra[4], rb[4];
       uint32_t vm[4] = {0, 0, 0, 0};
@@ -99,7 +104,7 @@ __global__ void __launch_bounds__(kThreads)
         }
       }
     }
-    for (; r < M; r += step) {
+    for (; r < rend; r += step) {
       const long long off = r * C + c0;
       float va[8];
       load_bf8(a + off, va);
@@ -235,37 +240,76 @@ __global__ void bn_eval_coeffs(int C, const float* __restrict__ gamma, const flo
   shift[c] = (beta ? beta[c] : 0.f) - mmean[c] * g * inv;
 }
 
+__device__ __forceinline__ void unpack8(const uint4& raw, float (&f)[8]) {
+  const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ void load_coef8(const float* __restrict__ p, int c, float (&f)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p + c), b = *reinterpret_cast<const float4*>(p + c + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+// One 8-channel vector of the apply: y = x*scale + shift (+ res) (ReLU) and its ReLU mask byte.
+template <bool HAS_RES, bool RELU>
+__device__ __forceinline__ void apply8(const uint4& xr, const uint4& rr, const float (&sc)[8], const float (&sh)[8],
+                                       bf16_t* __restrict__ y, uint8_t* __restrict__ mask, long long i) {
+  float v[8], r[8];
+  unpack8(xr, v);
+  if (HAS_RES) unpack8(rr, r);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float o = v[k] * sc[k] + sh[k];
+    if (HAS_RES) o += r[k];
+    if (RELU) {
+      o = fmaxf(o, 0.f);
+      bits |= (o > 0.f ? 1u : 0u) << k;
+    }
+    v[k] = o;
+  }
+  store_bf8(y + i * 8, v);
+  if (RELU && mask) mask[i] = static_cast<uint8_t>(bits);   // 1 bit per element: the backward's ReLU mask
+}
+
+// Each block streams one contiguous chunk of kVpt*256 8-channel vectors (thread t: vectors
+// base + u*256), loads first, then math and stores.  Contiguous chunks per block reach ~5.6 TB/s
+// on MI355X where a grid-stride sweep of the same kernel stays at ~4.1-4.5 TB/s
+// (bench/ew_probe.hip).  With C | 2048 (every power-of-two C <= 2048) a thread's vectors share
+// their 8 channels, so the coefficients are loaded once.
+constexpr int kVpt = 4;
+
 template <bool HAS_RES, bool RELU>
 __global__ void __launch_bounds__(kThreads)
     bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
                     uint8_t* __restrict__ mask, long long n8, int C, const float* __restrict__ scale,
                     const float* __restrict__ shift) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
-    long long off = i * 8;
-    int c = static_cast<int>(off % C);
-    float v[8];
-    load_bf8(x + off, v);
-    float4 s0 = *reinterpret_cast<const float4*>(scale + c);
-    float4 s1 = *reinterpret_cast<const float4*>(scale + c + 4);
-    float4 h0 = *reinterpret_cast<const float4*>(shift + c);
-    float4 h1 = *reinterpret_cast<const float4*>(shift + c + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    float r[8];
-    if (HAS_RES) load_bf8(res + off, r);
-    uint32_t bits = 0;
+  const long long base = (long long)blockIdx.x * (kThreads * kVpt) + threadIdx.x;
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  uint4 xr[kVpt], rr[kVpt];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float o = v[k] * sc[k] + sh[k];
-      if (HAS_RES) o += r[k];
-      if (RELU) {
-        o = fmaxf(o, 0.f);
-        bits |= (o > 0.f ? 1u : 0u) << k;
-      }
-      v[k] = o;
+  for (int u = 0; u < kVpt; ++u) {
+    const long long i = base + u * kThreads;
+    xr[u] = i < n8 ? *reinterpret_cast<const uint4*>(x + i * 8) : z4;
+    rr[u] = (HAS_RES && i < n8) ? *reinterpret_cast<const uint4*>(res + i * 8) : z4;
+  }
+  const bool fixed = (kThreads * 8) % C == 0;
+  float sc[8], sh[8];
+  load_coef8(scale, static_cast<int>((base * 8) % C), sc);
+  load_coef8(shift, static_cast<int>((base * 8) % C), sh);
+#pragma unroll
+  for (int u = 0; u < kVpt; ++u) {
+    const long long i = base + u * kThreads;
+    if (i >= n8) break;
+    if (!fixed) {
+      load_coef8(scale, static_cast<int>((i * 8) % C), sc);
+      load_coef8(shift, static_cast<int>((i * 8) % C), sh);
     }
-    store_bf8(y + off, v);
-    if (RELU && mask) mask[i] = static_cast<uint8_t>(bits);   // 1 bit per element: the backward's ReLU mask
+    apply8<HAS_RES, RELU>(xr[u], rr[u], sc, sh, y, mask, i);
   }
 }
 
@@ -291,43 +335,72 @@ __global__ void __launch_bounds__(1024)
   k3[c] = a * (-db * invM + mu * inv * dg * invM);
 }
 
+// One 8-channel vector of the BN backward: dz = dy (ReLU-masked), d(res) = dz, dx = k1*dz + k2*x + k3.
+template <bool RELU, bool WRITE_DRES>
+__device__ __forceinline__ void dx8(const uint4& gr, const uint4& xr, uint32_t m8, const uint4& orr,
+                                    const float (&A)[8], const float (&B)[8], const float (&E)[8],
+                                    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long i, int accum_dres) {
+  float g[8], xv[8];
+  unpack8(gr, g);
+  unpack8(xr, xv);
+  if (RELU) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = ((m8 >> k) & 1u) ? g[k] : 0.f;
+  }
+  if (WRITE_DRES) {
+    if (accum_dres) {          // fan-out: add to the other consumer's gradient already there
+      float o[8];
+      unpack8(orr, o);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] += g[k];
+      store_bf8(dres + i * 8, o);
+    } else {
+      store_bf8(dres + i * 8, g);
+    }
+  }
+  float o[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = A[k] * g[k] + B[k] * xv[k] + E[k];
+  store_bf8(dx + i * 8, o);
+}
+
+// Same chunked structure as bn_apply_kernel (k1..k3 loaded once when C | 2048).
 template <bool RELU, bool WRITE_DRES>
 __global__ void __launch_bounds__(kThreads)
     bn_dx_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const uint8_t* __restrict__ mk,
                  bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long n8, int C, const float* __restrict__ k1,
                  const float* __restrict__ k2, const float* __restrict__ k3, int accum_dres) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
-    long long off = i * 8;
-    int c = static_cast<int>(off % C);
-    float g[8], xv[8];
-    load_bf8(dy + off, g);
-    load_bf8(x + off, xv);
-    if (RELU) {
-      const uint32_t m8 = mk[i];
+  const long long base = (long long)blockIdx.x * (kThreads * kVpt) + threadIdx.x;
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  const bool acc = WRITE_DRES && accum_dres;
+  uint4 gr[kVpt], xr[kVpt], orr[kVpt];
+  uint32_t m8[kVpt];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) g[k] = ((m8 >> k) & 1u) ? g[k] : 0.f;
+  for (int u = 0; u < kVpt; ++u) {
+    const long long i = base + u * kThreads;
+    const bool ok = i < n8;
+    gr[u] = ok ? *reinterpret_cast<const uint4*>(dy + i * 8) : z4;
+    xr[u] = ok ? *reinterpret_cast<const uint4*>(x + i * 8) : z4;
+    m8[u] = (RELU && ok) ? mk[i] : 0xffu;
+    orr[u] = (acc && ok) ? *reinterpret_cast<const uint4*>(dres + i * 8) : z4;
+  }
+  const bool fixed = (kThreads * 8) % C == 0;
+  float A[8], B[8], E[8];
+  const int c0 = static_cast<int>((base * 8) % C);
+  load_coef8(k1, c0, A);
+  load_coef8(k2, c0, B);
+  load_coef8(k3, c0, E);
+#pragma unroll
+  for (int u = 0; u < kVpt; ++u) {
+    const long long i = base + u * kThreads;
+    if (i >= n8) break;
+    if (!fixed) {
+      const int c = static_cast<int>((i * 8) % C);
+      load_coef8(k1, c, A);
+      load_coef8(k2, c, B);
+      load_coef8(k3, c, E);
     }
-    if (WRITE_DRES) {
-      if (accum_dres) {          // fan-out: add to the other consumer's gradient already there
-        float o[8];
-        load_bf8(dres + off, o);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] += g[k];
-        store_bf8(dres + off, o);
-      } else {
-        store_bf8(dres + off, g);
-      }
-    }
-    float4 a0 = *reinterpret_cast<const float4*>(k1 + c), a1 = *reinterpret_cast<const float4*>(k1 + c + 4);
-    float4 b0 = *reinterpret_cast<const float4*>(k2 + c), b1 = *reinterpret_cast<const float4*>(k2 + c + 4);
-    float4 e0 = *reinterpret_cast<const float4*>(k3 + c), e1 = *reinterpret_cast<const float4*>(k3 + c + 4);
-    const float A[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const float B[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-    const float E[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-    float o[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = A[k] * g[k] + B[k] * xv[k] + E[k];
-    store_bf8(dx + off, o);
+    dx8<RELU, WRITE_DRES>(gr[u], xr[u], m8[u], orr[u], A, B, E, dx, dres, i, accum_dres);
   }
 }
 
@@ -354,9 +427,10 @@ void launch_apply(const void* x, const void* res, void* y, uint8_t* mask, long l
                        nullptr, n8, C, scale, shift);
 }
 
+// one block per contiguous chunk of kVpt * kThreads vectors
 inline int ew_grid(long long n8) {
-  long long b = ceil_div(n8, kThreads);
-  return static_cast<int>(b < 4096 ? (b > 0 ? b : 1) : 4096);
+  long long b = ceil_div(n8, (long long)kThreads * kVpt);
+  return static_cast<int>(b > 0 ? b : 1);
 }
 
 }  // namespace
