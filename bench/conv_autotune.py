@@ -53,6 +53,7 @@ def resnet_convs(depth=50, batch=256, image=224, width=64):
 
 
 WG2_TILES = ((128, 128, 2), (128, 128, 3), (128, 64, 2), (64, 128, 2), (64, 64, 3))
+WG3_TILES = ((256, 256, 2), (256, 128, 2), (256, 128, 3), (128, 256, 2), (128, 256, 3), (128, 128, 3))   # 8 waves
 # (bm, bn, stages): LDS = stages * (bm + bn) * 128 B <= 160 KiB
 V2_TILES = ((128, 128, 2), (128, 128, 3), (128, 128, 4), (128, 64, 3), (128, 64, 4), (256, 128, 2), (256, 128, 3),
             (256, 64, 3), (64, 128, 2), (64, 128, 3), (64, 128, 4), (64, 64, 4),
@@ -143,9 +144,10 @@ def main():
                          for sp in (0, 256, 2048)]
                 if C.v2_ok("wgrad", c, co, (s, s), kh * kw):
                     cands += [((bm, st), bn, sp, 2) for bm, bn, st in WG2_TILES for sp in (0, 256, 2048)]
+                    cands += [((bm, st), bn, sp, 3) for bm, bn, st in WG3_TILES for sp in (0, 128, 1024)]
                 mk = lambda bm, bn, sp, v: (lambda: C.mdtf_wgrad(  # noqa
-                    x, dy, wt.shape, (s, s), pads4, (1, 1), bm[0] if v == 2 else bm, bn, sp, None, v,
-                    bm[1] if v == 2 else 2))
+                    x, dy, wt.shape, (s, s), pads4, (1, 1), bm[0] if v >= 2 else bm, bn, sp, None, v,
+                    bm[1] if v >= 2 else 2))
             t_lib = timeit(lib, args.reps)
             t_wino = None
             if pass_ in ("fwd", "dgrad") and Wg.eligible((kh, kw), (s, s), pads4, (1, 1), c, co):
@@ -173,7 +175,7 @@ def main():
             elif best is not None and best[0] < {"fwd": t_lib / 0.85, "dgrad": t_lib / 0.75}.get(pass_, t_lib):
                 ent = {"backend": "mdtf", "bm": best[1], "bn": best[2], "splits": best[3], "ver": best[4],
                        "ms": round(best[0], 4), "miopen_ms": round(t_lib, 4)}
-                if best[4] == 2 and pass_ == "wgrad":     # v2 wgrad: bm field carries (rows, stages)
+                if best[4] >= 2 and pass_ == "wgrad":     # v2 wgrad: bm field carries (rows, stages)
                     ent["bm"], ent["stages"] = best[1]
                 elif best[4] in (2, 3):                   # v2 fwd/dgrad: the third field is the pipeline depth
                     ent["stages"], ent["splits"] = best[3], 0

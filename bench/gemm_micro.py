@@ -46,23 +46,25 @@ def main():
         best = None
         x4 = x.view(M, 1, 1, K)
         dy4 = dy.view(M, 1, 1, N)
-        for bm, bn, st in ((128, 128, 2), (128, 128, 3), (64, 128, 2), (128, 64, 2), (64, 64, 3)):
-            for sp in (0, 8, 16, 32, 64):
+        for bm, bn, st, v in ((128, 128, 2, 2), (128, 128, 3, 2), (64, 128, 2, 2), (128, 64, 2, 2), (64, 64, 3, 2),
+                              (256, 256, 2, 3), (256, 128, 2, 3), (256, 128, 3, 3), (128, 256, 2, 3),
+                              (128, 256, 3, 3), (128, 128, 3, 3)):
+            for sp in (0, 4, 8, 16, 32, 64):
                 try:
                     t = timeit(lambda: C.mdtf_wgrad(x4, dy4, (1, 1, K, N), (1, 1), (0, 0, 0, 0), (1, 1), bm, bn, sp,
-                                                    out=out, ver=2, stages=st))
+                                                    out=out, ver=v, stages=st))
                 except RuntimeError:
                     continue
                 if best is None or t < best[0]:
-                    best = (t, bm, bn, st, sp)
+                    best = (t, bm, bn, st, sp, v)
         # numerics spot check
         out.zero_()
-        C.mdtf_wgrad(x4, dy4, (1, 1, K, N), (1, 1), (0, 0, 0, 0), (1, 1), best[1], best[2], best[4], out=out, ver=2,
-                     stages=best[3])
+        C.mdtf_wgrad(x4, dy4, (1, 1, K, N), (1, 1), (0, 0, 0, 0), (1, 1), best[1], best[2], best[4], out=out,
+                     ver=best[5], stages=best[3])
         ref = (x.t().float() @ dy.float())
         err = float((out.view(K, N) - ref).norm() / ref.norm())
-        print("| %d | %d | %d | %.4f | %.0f | %.4f (%d,%d,s%d,k%d) | %.0f | bf16-out %.4f (+add %.4f) | err %.1e" % (
-            M, K, N, t_lib, fl / t_lib / 1e9, best[0], best[1], best[2], best[3], best[4], fl / best[0] / 1e9,
+        print("| %d | %d | %d | %.4f | %.0f | %.4f (%d,%d,s%d,k%d,v%d) | %.0f | bf16-out %.4f (+add %.4f) | err %.1e" % (
+            M, K, N, t_lib, fl / t_lib / 1e9, best[0], best[1], best[2], best[3], best[4], best[5], fl / best[0] / 1e9,
             t_b16only, t_b16, err), flush=True)
 
 

@@ -932,12 +932,14 @@ __device__ __forceinline__ bf16x8_t frag_tr(const char* img, int col0, int kbase
   return __builtin_bit_cast(bf16x8_t, f);
 }
 
-template <int BM, int BN, int STAGES>
-__global__ void __launch_bounds__(NT) conv_wgrad_v2(ConvArgs a) {
-  constexpr int WM = 2, WN = 2;
+template <int BM, int BN, int STAGES, int NW>
+__global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
+  // NW = 4 (2x2 waves) or 8 (one 256-row/col block per CU, 4x2 or 2x4 waves by aspect)
+  constexpr int WM = NW == 4 ? 2 : (BM > BN ? 4 : 2), WN = NW / WM;
+  constexpr int U = 8 / NW;                       // 8-row DMA blocks per wave per 64-pixel step
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int HA = BM / 64, HB = BN / 64;       // 64-column half-images per operand
-  constexpr int IA = HA * 2, IB = HB * 2;         // DMA instructions per wave per stage
+  constexpr int IA = HA * U, IB = HB * U;         // DMA instructions per wave per stage
   constexpr int STAGE = (BM + BN) * 128;
   constexpr int PER_STAGE = IA + IB;
   constexpr unsigned OOB = 0x80000000u;
@@ -977,14 +979,16 @@ __global__ void __launch_bounds__(NT) conv_wgrad_v2(ConvArgs a) {
     h_dy[h] = kh * a.DH - a.PH;
     h_dx[h] = kw * a.DW - a.PW;
   }
-  // this lane's two pixel rows per step: k = 8*wave + (lane>>3) and k + 32
+  // this lane's U pixel rows per step: k = 8*wave + (lane>>3) (+ 8*NW*u)
   const int krow0 = 8 * wave + (lane >> 3);
-  const int gch[2] = {((lane & 7) ^ trswz(krow0)) * 8, ((lane & 7) ^ trswz(krow0 + 32)) * 8};
-  int p_ow[2], p_oh[2], p_n[2];
-  long long p_m[2];
+  int gch[U];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const long long m = (long long)kt_begin * 64 + krow0 + 32 * u;
+  for (int u = 0; u < U; ++u) gch[u] = ((lane & 7) ^ trswz(krow0 + 8 * NW * u)) * 8;
+  int p_ow[U], p_oh[U], p_n[U];
+  long long p_m[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long m = (long long)kt_begin * 64 + krow0 + 8 * NW * u;
     p_m[u] = m;
     p_ow[u] = static_cast<int>(m % a.OW);
     const long long t = m / a.OW;
@@ -996,7 +1000,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_v2(ConvArgs a) {
   auto stage = [&](int buf) {
     char* lds = smem_raw + buf * STAGE;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) {
       const bool mok = p_m[u] < Mpix;
       const int iy0 = p_oh[u] * a.SH, ix0 = p_ow[u] * a.SW;
       // A halves: X[n, iy, ix, c + chunk]
@@ -1006,8 +1010,8 @@ __global__ void __launch_bounds__(NT) conv_wgrad_v2(ConvArgs a) {
         const bool ok = mok && h_ok[h] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
         const unsigned voff =
             ok ? (unsigned)((((p_n[u] * a.H + iy) * a.W + ix) * a.Cin + h_c[h] + gch[u]) * 2) : OOB;
-        // instruction slot: half h, row block (wave + 4u) -> LDS rows 8*(wave+4u) ..
-        dma16(a.src, bytes_x, lds + h * 8192 + (wave + 4 * u) * 1024, voff, 0);
+        // instruction slot: half h, row block (wave + NW u) -> LDS rows 8*(wave+NW u) ..
+        dma16(a.src, bytes_x, lds + h * 8192 + (wave + NW * u) * 1024, voff, 0);
       }
       // B halves: DY[m, n0 + 64h + chunk]
       char* ldsb = lds + BM * 128;
@@ -1015,7 +1019,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_v2(ConvArgs a) {
       for (int h = 0; h < HB; ++h) {
         const int co = n0 + 64 * h;
         const unsigned voff = (mok && co < a.Cout) ? (unsigned)((p_m[u] * a.ld_dy + co + gch[u]) * 2) : OOB;
-        dma16(a.dy, bytes_dy, ldsb + h * 8192 + (wave + 4 * u) * 1024, voff, 0);
+        dma16(a.dy, bytes_dy, ldsb + h * 8192 + (wave + NW * u) * 1024, voff, 0);
       }
       // advance this row by 64 pixels
       p_m[u] += 64;
@@ -1094,7 +1098,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_v2(ConvArgs a) {
     }
 }
 
-template <int BM, int BN, int STAGES>
+template <int BM, int BN, int STAGES, int NW = 4>
 int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
   const int R = a.KH * a.KW * a.Cin;
   a.mtiles = static_cast<int>(ceil_div(R, BM));
@@ -1102,13 +1106,16 @@ int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
   const int kt_total = static_cast<int>(ceil_div(a.M, 64));
   if (splits < 1) {
     const int tiles = a.mtiles * a.ntiles;
-    splits = (1024 + tiles - 1) / tiles;
+    const int target = NW == 8 ? 512 : 1024;      // ~2 (8-wave) / ~4 (4-wave) blocks per CU
+    splits = (target + tiles - 1) / tiles;
   }
   if (splits > kt_total) splits = kt_total;
   a.ksplit_steps = (kt_total + splits - 1) / splits;
   splits = (kt_total + a.ksplit_steps - 1) / a.ksplit_steps;
   const size_t lds = STAGES * (size_t)(BM + BN) * 128;
-  hipLaunchKernelGGL((conv_wgrad_v2<BM, BN, STAGES>), dim3(a.mtiles * a.ntiles * splits), dim3(NT), lds, st, a);
+  if (lds > 160 * 1024) return MDTF_EUNSUPPORTED;
+  hipLaunchKernelGGL((conv_wgrad_v2<BM, BN, STAGES, NW>), dim3(a.mtiles * a.ntiles * splits), dim3(64 * NW), lds, st,
+                     a);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
@@ -1160,6 +1167,19 @@ int launch_wgrad(ConvArgs& a, int splits, hipStream_t st) {
   hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN>), dim3(a.mtiles * a.ntiles * splits), dim3(NT), lds, st, a);
   MDTF_LAUNCH_CHECK();
   return 0;
+}
+
+// v2 wgrad tile table; w8: 8-wave (512-thread) tiles
+int dispatch_wgrad_v2(ConvArgs& a, int bm, int bn, int stages, int w8, int splits, hipStream_t st) {
+#define WG2(BM_, BN_, S_, NW_) \
+  if (bm == BM_ && bn == BN_ && stages == S_ && (NW_ == 8) == (w8 != 0)) \
+    return launch_wgrad_v2<BM_, BN_, S_, NW_>(a, splits, st);
+  WG2(128, 128, 2, 4) WG2(128, 128, 3, 4) WG2(128, 64, 2, 4) WG2(128, 64, 3, 4) WG2(64, 128, 2, 4)
+  WG2(64, 128, 3, 4) WG2(64, 64, 2, 4) WG2(64, 64, 3, 4) WG2(64, 64, 4, 4)
+  WG2(256, 256, 2, 8) WG2(256, 128, 2, 8) WG2(256, 128, 3, 8) WG2(128, 256, 2, 8) WG2(128, 256, 3, 8)
+  WG2(128, 128, 2, 8) WG2(128, 128, 3, 8) WG2(128, 128, 4, 8)
+#undef WG2
+  return MDTF_EUNSUPPORTED;
 }
 
 ConvArgs make_args(int N, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int SH, int SW, int PH,
@@ -1332,14 +1352,9 @@ MDTF_EXPORT int mdtf_conv_wgrad_v2(const void* x, const void* dy, float* dw, int
   a.ld_dy = a.ld_dw = Cout;
   a.M = (long long)N * OH * OW;
   a.Ncol = Cout;
-  const int stages = bm / 1000 ? bm / 1000 : 2;
+  const int w8 = bm / 10000, stages = (bm % 10000) / 1000 ? (bm % 10000) / 1000 : 2;
   bm %= 1000;
-#define WG2(BM_, BN_, S_) \
-  if (bm == BM_ && bn == BN_ && stages == S_) return launch_wgrad_v2<BM_, BN_, S_>(a, splits, st);
-  WG2(128, 128, 2) WG2(128, 128, 3) WG2(128, 64, 2) WG2(128, 64, 3) WG2(64, 128, 2) WG2(64, 128, 3)
-  WG2(64, 64, 2) WG2(64, 64, 3) WG2(64, 64, 4)
-#undef WG2
-  return MDTF_EUNSUPPORTED;
+  return dispatch_wgrad_v2(a, bm, bn, stages, w8, splits, st);
 }
 
 // dW[K][N] (fp32, row stride ld_dw) += X[M][K]^T DY[M][N] (DY row stride ld_dy): the dense-layer
@@ -1356,10 +1371,5 @@ MDTF_EXPORT int mdtf_gemm_wgrad(const void* x, const void* dy, float* dw, long l
   a.ld_dw = ld_dw;
   a.M = M;
   a.Ncol = N;
-#define WG2(BM_, BN_, S_) \
-  if (bm == BM_ && bn == BN_ && stages == S_) return launch_wgrad_v2<BM_, BN_, S_>(a, splits, st);
-  WG2(128, 128, 2) WG2(128, 128, 3) WG2(128, 64, 2) WG2(128, 64, 3) WG2(64, 128, 2) WG2(64, 128, 3)
-  WG2(64, 64, 2) WG2(64, 64, 3) WG2(64, 64, 4)
-#undef WG2
-  return MDTF_EUNSUPPORTED;
+  return dispatch_wgrad_v2(a, bm % 10000, bn, stages, bm / 10000, splits, st);
 }

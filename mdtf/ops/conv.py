@@ -218,10 +218,11 @@ def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=
     dw = torch.zeros(w_shape, dtype=torch.float32, device=x.device) if out is None else out
     n, h, wd, c = x.shape
     kh, kw, ci, co = w_shape
-    if ver == 2:
+    if ver in (2, 3):
         N.check(N.fn("mdtf_conv_wgrad_v2")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co,
                                            kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
-                                           bm + 1000 * stages, bn, int(splits), N.stream_ptr()), "conv_wgrad_v2")
+                                           _v2_code(bm, stages, ver), bn, int(splits), N.stream_ptr()),
+                "conv_wgrad_v2")
         return dw
     N.check(N.fn("mdtf_conv_wgrad")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co, kh,
                                     kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1], bm, bn, int(splits),

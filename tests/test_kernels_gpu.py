@@ -926,3 +926,27 @@ def test_conv_v2_8wave_tiles(bm, bn, stages, geo):
     C.mdtf_dgrad(dy.to(DEV), wt.to(DEV), (n, h, w, c), (s, s), pads, (1, 1), bm, bn, 3, stages, out=out,
                  accumulate=True)
     assert _rel(out, ref + base.float()) < 1e-2
+
+
+@pytest.mark.parametrize("bm,bn,stages", [(256, 256, 2), (256, 128, 2), (256, 128, 3), (128, 256, 2), (128, 256, 3),
+                                          (128, 128, 3)])
+@pytest.mark.parametrize("geo", [(3, 9, 9, 64, 3, 320, 1), (2, 12, 12, 192, 1, 256, 1), (2, 15, 13, 64, 3, 128, 2)])
+def test_conv_wgrad_8wave_tiles(bm, bn, stages, geo):
+    """8-wave v2 weight-gradient tiles (split-K fp32 atomics) vs the fp32 autograd reference: R and Cout
+    tails, pixel tails, strided 3x3."""
+    from mdtf.ops import conv as C
+    n, h, w, c, k, co, s = geo
+    torch.manual_seed(bm * 3 + bn + stages + k)
+    p = k // 2
+    pads = (p, p, p, p)
+    x = torch.randn(n, h, w, c).bfloat16()
+    wt = (torch.randn(k, k, c, co) / (k * k * c) ** 0.5).bfloat16()
+    wr = wt.float().permute(3, 2, 0, 1).requires_grad_(True)
+    yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wr, stride=s, padding=p)
+    dy = torch.randn(yr.shape).bfloat16()
+    yr.backward(dy.float())
+    ref = wr.grad.permute(2, 3, 1, 0)                         # HWIO
+    for sp in (0, 3):
+        dw = C.mdtf_wgrad(x.to(DEV), dy.permute(0, 2, 3, 1).contiguous().to(DEV), wt.shape, (s, s), pads, (1, 1),
+                          bm, bn, sp, ver=3, stages=stages)
+        assert _rel(dw, ref) < 1e-2, sp
