@@ -69,6 +69,10 @@ struct ConvArgs {
   float* bsum;           // [bslots][Ncol] (null: off)
   float* bsq;
   int bslots;
+  // wgrad v2 split-K: per-split partial tiles stored to slab[split][R][Cout] (plain stores) and summed
+  // into DW by one reduction pass, instead of fp32 atomics into DW (null: atomics)
+  float* slab;
+  int slab_cap;          // splits the slab has room for
 };
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p, bool ok) {
@@ -1084,6 +1088,7 @@ __global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fa[kh2][i], fb[kh2][j], acc[i][j]);
   }
   const int g = lane >> 4, li = lane & 15;
+  float* slab = a.slab ? a.slab + (long long)split * R * a.Cout : nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1093,9 +1098,46 @@ __global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int r = r0 + wm * (TM * 16) + i * 16 + 4 * g + rr;
-        if (r < R) atomicAdd(a.dw + (long long)r * a.ld_dw + co, acc[i][j][rr]);
+        if (r >= R) continue;
+        if (slab)
+          slab[(long long)r * a.Cout + co] = acc[i][j][rr];
+        else
+          atomicAdd(a.dw + (long long)r * a.ld_dw + co, acc[i][j][rr]);
       }
     }
+}
+
+// DW[r][c] (row stride ld) += sum_s slab[s][r][c]  (slab rows dense, C % 4 == 0); 4 splits in flight
+__global__ void __launch_bounds__(256) wgrad_slab_reduce(const float* __restrict__ slab, int splits, long long RC,
+                                                         int C, long long ld, float* __restrict__ dw) {
+  const long long q = blockIdx.x * 256LL + threadIdx.x;     // float4 index
+  if (q * 4 >= RC) return;
+  const float4* s4 = reinterpret_cast<const float4*>(slab);
+  const long long st = RC / 4;
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  int sp = 0;
+  for (; sp + 3 < splits; sp += 4) {
+    const float4 a = s4[q + sp * st], b = s4[q + (sp + 1) * st], c = s4[q + (sp + 2) * st], d = s4[q + (sp + 3) * st];
+    t.x += (a.x + b.x) + (c.x + d.x);
+    t.y += (a.y + b.y) + (c.y + d.y);
+    t.z += (a.z + b.z) + (c.z + d.z);
+    t.w += (a.w + b.w) + (c.w + d.w);
+  }
+  for (; sp < splits; ++sp) {
+    const float4 a = s4[q + sp * st];
+    t.x += a.x;
+    t.y += a.y;
+    t.z += a.z;
+    t.w += a.w;
+  }
+  const long long e = q * 4, r = e / C, c = e - r * C;
+  float4* o = reinterpret_cast<float4*>(dw + r * ld + c);
+  float4 v = *o;
+  v.x += t.x;
+  v.y += t.y;
+  v.z += t.z;
+  v.w += t.w;
+  *o = v;
 }
 
 template <int BM, int BN, int STAGES, int NW = 4>
@@ -1114,9 +1156,17 @@ int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
   splits = (kt_total + a.ksplit_steps - 1) / a.ksplit_steps;
   const size_t lds = STAGES * (size_t)(BM + BN) * 128;
   if (lds > 160 * 1024) return MDTF_EUNSUPPORTED;
+  ConvArgs b = a;
+  if (a.slab && (splits < 2 || splits > a.slab_cap || (a.ld_dw % 4) || (a.Cout % 4))) b.slab = nullptr;
   hipLaunchKernelGGL((conv_wgrad_v2<BM, BN, STAGES, NW>), dim3(a.mtiles * a.ntiles * splits), dim3(64 * NW), lds, st,
-                     a);
+                     b);
   MDTF_LAUNCH_CHECK();
+  if (b.slab) {
+    const long long RC = (long long)R * a.Cout;
+    hipLaunchKernelGGL(wgrad_slab_reduce, dim3((unsigned)ceil_div(RC / 4, 256)), dim3(256), 0, st, b.slab, splits, RC,
+                       a.Cout, (long long)a.ld_dw, a.dw);
+    MDTF_LAUNCH_CHECK();
+  }
   return 0;
 }
 
@@ -1341,7 +1391,7 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
 // bm encodes stages * 1000 + tile rows
 MDTF_EXPORT int mdtf_conv_wgrad_v2(const void* x, const void* dy, float* dw, int N, int H, int W, int Cin, int OH,
                                    int OW, int Cout, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW,
-                                   int bm, int bn, int splits, hipStream_t st) {
+                                   int bm, int bn, int splits, float* slab, int slab_cap, hipStream_t st) {
   if (Cin % 64 || Cout % 64) return MDTF_EINVAL;
   if ((long long)N * H * W * Cin * 2 > 0x7fffffffLL || (long long)N * OH * OW * Cout * 2 > 0x7fffffffLL)
     return MDTF_EUNSUPPORTED;
@@ -1352,6 +1402,8 @@ MDTF_EXPORT int mdtf_conv_wgrad_v2(const void* x, const void* dy, float* dw, int
   a.ld_dy = a.ld_dw = Cout;
   a.M = (long long)N * OH * OW;
   a.Ncol = Cout;
+  a.slab = slab;
+  a.slab_cap = slab_cap;
   const int w8 = bm / 10000, stages = (bm % 10000) / 1000 ? (bm % 10000) / 1000 : 2;
   bm %= 1000;
   return dispatch_wgrad_v2(a, bm, bn, stages, w8, splits, st);
@@ -1360,7 +1412,8 @@ MDTF_EXPORT int mdtf_conv_wgrad_v2(const void* x, const void* dy, float* dw, int
 // dW[K][N] (fp32, row stride ld_dw) += X[M][K]^T DY[M][N] (DY row stride ld_dy): the dense-layer
 // weight gradient on the v2 wgrad kernel (a 1x1 convolution over M "pixels").  K % 64 == 0, N % 64 == 0.
 MDTF_EXPORT int mdtf_gemm_wgrad(const void* x, const void* dy, float* dw, long long M, int K, int N, int ld_dy,
-                                int ld_dw, int bm, int bn, int stages, int splits, hipStream_t st) {
+                                int ld_dw, int bm, int bn, int stages, int splits, float* slab, int slab_cap,
+                                hipStream_t st) {
   if (K % 64 || N % 64 || ld_dy % 8 || M > 0x7fffffff) return MDTF_EINVAL;
   if (M * K * 2 > 0x7fffffffLL || M * (long long)ld_dy * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
   ConvArgs a = make_args((int)M, 1, 1, K, 1, 1, N, 1, 1, 1, 1, 0, 0, 1, 1);
@@ -1371,5 +1424,7 @@ MDTF_EXPORT int mdtf_gemm_wgrad(const void* x, const void* dy, float* dw, long l
   a.ld_dw = ld_dw;
   a.M = M;
   a.Ncol = N;
+  a.slab = slab;
+  a.slab_cap = slab_cap;
   return dispatch_wgrad_v2(a, bm % 10000, bn, stages, bm / 10000, splits, st);
 }

@@ -24,7 +24,36 @@ N.register("mdtf_conv_dgrad", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
 N.register("mdtf_conv_wgrad", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 N.register("mdtf_conv_fwd_v2", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P])
 N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P, N.P, N.P, N.I, N.P])
-N.register("mdtf_conv_wgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
+N.register("mdtf_conv_wgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.I, N.P])
+
+# split-K weight gradients: per-split partial slabs + one reduction pass (plain stores) instead of fp32
+# atomics into DW.  Measured on MI355X (scripts/gpu_envab.sh): +0.4 % BERT-base (dense GEMM weight
+# gradients), -0.3 % ResNet-50 (conv tiles were autotuned with atomics) -> default: dense layers only.
+# MDTF_WGRAD_SLAB = dense (default) | 1 (conv too) | 0 (atomics everywhere)
+_SLAB_MODE = os.environ.get("MDTF_WGRAD_SLAB", "dense")
+WGRAD_SLAB = _SLAB_MODE not in ("0", "", "false", "dense")
+DENSE_WGRAD_SLAB = _SLAB_MODE not in ("0", "", "false")
+
+
+def wgrad_splits(M, R, Cout, bm, bn, ver, splits):
+    """The split count launch_wgrad_v2 (csrc/conv_igemm.hip) will use."""
+    kt_total = -(-M // 64)
+    tiles = -(-R // bm) * -(-Cout // bn)
+    if splits < 1:
+        splits = -(-(512 if ver == 3 else 1024) // tiles)
+    splits = max(1, min(splits, kt_total))
+    ks = -(-kt_total // splits)
+    return -(-kt_total // ks)
+
+
+def wgrad_slab(M, R, Cout, bm, bn, ver, splits, device, dense=False):
+    """(slab tensor or None, capacity) for one v2 weight-gradient launch."""
+    if not (DENSE_WGRAD_SLAB if dense else WGRAD_SLAB) or N.deterministic():
+        return None, 0
+    sp = wgrad_splits(M, R, Cout, bm, bn, ver, splits)
+    if sp < 2:
+        return None, 0
+    return torch.empty(sp * R * Cout, dtype=torch.float32, device=device), sp
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 TABLE_PATH = os.environ.get("MDTF_CONV_TABLE") or os.path.join(_HERE, "conv_table.json")
@@ -219,10 +248,11 @@ def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=
     n, h, wd, c = x.shape
     kh, kw, ci, co = w_shape
     if ver in (2, 3):
+        slab, cap = wgrad_slab(n * dy.shape[1] * dy.shape[2], kh * kw * ci, co, bm, bn, ver, int(splits), x.device)
         N.check(N.fn("mdtf_conv_wgrad_v2")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co,
                                            kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
-                                           _v2_code(bm, stages, ver), bn, int(splits), N.stream_ptr()),
-                "conv_wgrad_v2")
+                                           _v2_code(bm, stages, ver), bn, int(splits), N.ptr(slab), cap,
+                                           N.stream_ptr()), "conv_wgrad_v2")
         return dw
     N.check(N.fn("mdtf_conv_wgrad")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co, kh,
                                     kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1], bm, bn, int(splits),

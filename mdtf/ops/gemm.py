@@ -23,7 +23,7 @@ from ..train import variables as V
 _ACT = {None: 0, "relu": 1, "gelu": 2}
 _fp32_out_ok = None      # does this torch build accept addmm(out_dtype=float32, out=...)?
 
-N.register("mdtf_gemm_wgrad", [N.P, N.P, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.P])
+N.register("mdtf_gemm_wgrad", [N.P, N.P, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.P, N.I, N.P])
 
 
 def wgrad_into(out, x, d):
@@ -39,8 +39,10 @@ def wgrad_into(out, x, d):
             and x.dtype == torch.bfloat16 and d.dtype == torch.bfloat16 and out.dtype == torch.float32):
         splits = 1 if N.deterministic() else (8 if K * Nn <= 768 * 768 else 0)
         bm, bn = (128, 128) if M < 4096 else (64, 128)
+        from . import conv as C
+        slab, cap = C.wgrad_slab(M, K, Nn, bm, bn, 2, splits, x.device, dense=True)
         rc = N.fn("mdtf_gemm_wgrad")(N.ptr(x), N.ptr(d), N.ptr(out), M, K, Nn, d.stride(0), out.stride(0), bm, bn, 2,
-                                     splits, N.stream_ptr())
+                                     splits, N.ptr(slab), cap, N.stream_ptr())
         if rc == 0:
             return
     _accum_mm(out, x.t(), d)

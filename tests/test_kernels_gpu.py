@@ -931,10 +931,12 @@ def test_conv_v2_8wave_tiles(bm, bn, stages, geo):
 @pytest.mark.parametrize("bm,bn,stages", [(256, 256, 2), (256, 128, 2), (256, 128, 3), (128, 256, 2), (128, 256, 3),
                                           (128, 128, 3)])
 @pytest.mark.parametrize("geo", [(3, 9, 9, 64, 3, 320, 1), (2, 12, 12, 192, 1, 256, 1), (2, 15, 13, 64, 3, 128, 2)])
-def test_conv_wgrad_8wave_tiles(bm, bn, stages, geo):
+@pytest.mark.parametrize("slab", [True, False])
+def test_conv_wgrad_8wave_tiles(bm, bn, stages, geo, slab, monkeypatch):
     """8-wave v2 weight-gradient tiles (split-K fp32 atomics) vs the fp32 autograd reference: R and Cout
     tails, pixel tails, strided 3x3."""
     from mdtf.ops import conv as C
+    monkeypatch.setattr(C, "WGRAD_SLAB", slab)      # split-K partial slabs + reduction, or fp32 atomics
     n, h, w, c, k, co, s = geo
     torch.manual_seed(bm * 3 + bn + stages + k)
     p = k // 2
