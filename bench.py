@@ -43,6 +43,7 @@ def parse():
     p.add_argument("--profile_dir", default=None)
     p.add_argument("--hip_graph", type=int, default=1,
                    help="1: capture the whole training step in a hipGraph after 2 eager steps (mdtf.train.graph)")
+    p.add_argument("--image_size", type=int, default=224, help="image side (CPU tests of the launch path use 32-64)")
     return p.parse_args()
 
 
@@ -77,8 +78,8 @@ def main():
     store.compute_dtype = torch.bfloat16 if dev.type == "cuda" else None
     store.generator.manual_seed(1234)
 
-    loader = SyntheticDataLoader(shape=(224, 224, 3), num_classes=1000, dtype=torch.bfloat16 if dev.type == "cuda"
-                                 else torch.float32, seed=rank)
+    loader = SyntheticDataLoader(shape=(args.image_size, args.image_size, 3), num_classes=1000,
+                                 dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32, seed=rank)
     loader.batch_size = args.batch
     raw, gt = loader.load_train_batch()
     base = mdtf.train.MomentumOptimizer(0.1 * args.batch * world / 256.0, momentum=0.9, weight_decay=5e-5)
@@ -134,9 +135,11 @@ def main():
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(ips / (base_ips * world), 4) if base_ips else None,
             "baseline": "stock PyTorch-ROCm comparator, %.2f img/s/GPU x %d" % (base_ips, world) if base_ips else None,
-            "dtype": "bf16", "data": "synthetic (random 224x224x3 NHWC images, random labels; random-init weights)",
+            "dtype": "bf16" if dev.type == "cuda" else "fp32",
+            "data": "synthetic (random %dx%dx3 NHWC images, random labels; random-init weights)" % (
+                args.image_size, args.image_size),
             "config": {"model": "resnet%d_v1.5" % args.depth, "global_batch": args.batch * world, "seq_len": None,
-                       "per_gpu_batch": args.batch, "image_size": 224, "parallelism": "dp%d" % world,
+                       "per_gpu_batch": args.batch, "image_size": args.image_size, "parallelism": "dp%d" % world,
                        "grad_sync": args.mode, "optimizer": "momentum-sgd (fused)",
                        "kernels": os.environ.get("MDTF_KERNELS", "native"),
                        "hip_graph": bool(args.hip_graph)},
@@ -145,7 +148,11 @@ def main():
         print(json.dumps(rec), flush=True)
     sess.close()
     if distributed:
+        # the captured step graph holds RCCL collectives: sess.close() released it; now the communicator
+        S.release_graphs()
+        dist.barrier(group=pg)
         server.shutdown()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

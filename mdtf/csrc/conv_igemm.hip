@@ -779,11 +779,14 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   if (bstat) {
     static_assert(NT % (BN / 8) == 0, "one channel chunk per thread");
     __syncthreads();                           // the C tile copy-out is done with the LDS
-    float* red = reinterpret_cast<float*>(smem_raw);   // [NT][16] (16 KiB <= the stage ring)
+    // [16][NT + 8] floats: the per-k rows are written lane-contiguously and the +8 row pad puts the
+    // reads of 8 channels x 8 threads on 64 distinct banks (a [NT][16] layout was 16-way conflicted)
+    constexpr int LDR = NT + 8;
+    float* red = reinterpret_cast<float*>(smem_raw);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      red[tid * 16 + k] = bs0[k];
-      red[tid * 16 + 8 + k] = bs1[k];
+      red[k * LDR + tid] = bs0[k];
+      red[(8 + k) * LDR + tid] = bs1[k];
     }
     __syncthreads();
     for (int nl = tid; nl < BN; nl += NT) {
@@ -791,8 +794,8 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
       if (n < a.Ncol) {
         float sv = 0.f, q = 0.f;
         for (int t2 = c8; t2 < NT; t2 += BN / 8) {
-          sv += red[t2 * 16 + k];
-          q += red[t2 * 16 + 8 + k];
+          sv += red[k * LDR + t2];
+          q += red[(8 + k) * LDR + t2];
         }
         const long long slot = (long long)(mt % a.bslots) * a.Ncol + n;
         atomicAdd(a.bsum + slot, sv);
@@ -868,7 +871,7 @@ int launch_fd_v2(ConvArgs& a, hipStream_t st) {
   if (nblk > 0x7fffffff) return MDTF_EUNSUPPORTED;
   const size_t stage_bytes = STAGES * (size_t)(BM + BN) * 128, ctile = (size_t)BM * (BN * 2 + 16);
   size_t lds = stage_bytes > ctile ? stage_bytes : ctile;
-  if (lds < (size_t)NT * 16 * sizeof(float)) lds = (size_t)NT * 16 * sizeof(float);   // BN-stat reduction
+  if (lds < (size_t)(NT + 8) * 16 * sizeof(float)) lds = (size_t)(NT + 8) * 16 * sizeof(float);   // BN-stat reduction
   if (STAGES == 1 && a.K > 64) return MDTF_EINVAL;      // single buffer: one K step only
   if (lds > 160 * 1024) return MDTF_EUNSUPPORTED;
   hipLaunchKernelGGL((conv_fd_v2<BM, BN, MODE, STATS, STAGES, NW>), dim3((unsigned)nblk), dim3(NT), lds, st, a);

@@ -194,94 +194,96 @@ struct PoolGeo {
   int N, H, W, C, OH, OW, KH, KW, SH, SW, PT, PL;
 };
 
-__global__ void maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ arg,
-                            PoolGeo g) {
+// Max pooling, one 8-channel vector per thread and one contiguous chunk of vectors per block
+// (index math in IDX = int when the tensor has < 2^31 vectors: 64-bit divisions per element made
+// the grid-stride version run at ~2 TB/s).
+template <typename IDX>
+__global__ void __launch_bounds__(kT) maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                  uint8_t* __restrict__ arg, PoolGeo g, IDX total) {
+  const IDX i = (IDX)blockIdx.x * kT + threadIdx.x;
+  if (i >= total) return;
   const int cv = g.C / 8;
-  long long total = (long long)g.N * g.OH * g.OW * cv;
-  GRID_STRIDE(i, total) {
-    int c8 = static_cast<int>(i % cv);
-    long long p = i / cv;
-    int ow = static_cast<int>(p % g.OW);
-    p /= g.OW;
-    int oh = static_cast<int>(p % g.OH);
-    int n = static_cast<int>(p / g.OH);
-    float best[8];
-    uint8_t bi[8];
+  const int c8 = static_cast<int>(i % cv);
+  IDX p = i / cv;
+  const int ow = static_cast<int>(p % g.OW);
+  p /= g.OW;
+  const int oh = static_cast<int>(p % g.OH);
+  const IDX n = p / g.OH;
+  float best[8];
+  uint8_t bi[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      best[k] = -INFINITY;
-      bi[k] = 0;
-    }
-    for (int kh = 0; kh < g.KH; ++kh) {
-      int h = oh * g.SH - g.PT + kh;
-      if (h < 0 || h >= g.H) continue;
-      for (int kw = 0; kw < g.KW; ++kw) {
-        int w = ow * g.SW - g.PL + kw;
-        if (w < 0 || w >= g.W) continue;
-        float v[8];
-        load_bf8(x + (((long long)n * g.H + h) * g.W + w) * g.C + c8 * 8, v);
-        uint8_t idx = static_cast<uint8_t>(kh * g.KW + kw);
+  for (int k = 0; k < 8; ++k) {
+    best[k] = -INFINITY;
+    bi[k] = 0;
+  }
+  for (int kh = 0; kh < g.KH; ++kh) {
+    const int h = oh * g.SH - g.PT + kh;
+    if (h < 0 || h >= g.H) continue;
+    for (int kw = 0; kw < g.KW; ++kw) {
+      const int w = ow * g.SW - g.PL + kw;
+      if (w < 0 || w >= g.W) continue;
+      float v[8];
+      load_bf8(x + ((long long)((n * g.H + h) * g.W + w)) * g.C + c8 * 8, v);
+      const uint8_t idx = static_cast<uint8_t>(kh * g.KW + kw);
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (v[k] > best[k]) {
-            best[k] = v[k];
-            bi[k] = idx;
-          }
-      }
+      for (int k = 0; k < 8; ++k)
+        if (v[k] > best[k]) {
+          best[k] = v[k];
+          bi[k] = idx;
+        }
     }
-    long long o = (((long long)n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8;
-    store_bf8(y + o, best);
-    if (arg) {
-      uint2 packed;
-      packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
-      packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
-      *reinterpret_cast<uint2*>(arg + o) = packed;
-    }
+  }
+  const long long o = (long long)i * 8;
+  store_bf8(y + o, best);
+  if (arg) {
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *reinterpret_cast<uint2*>(arg + o) = packed;
   }
 }
 
-// gather form: each input pixel collects dy from every window whose argmax it is
-__global__ void maxpool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
-                            PoolGeo g) {
+// gather form: each input vector collects dy from every window whose argmax it is
+template <typename IDX>
+__global__ void __launch_bounds__(kT) maxpool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                  bf16_t* __restrict__ dx, PoolGeo g, IDX total) {
+  const IDX i = (IDX)blockIdx.x * kT + threadIdx.x;
+  if (i >= total) return;
   const int cv = g.C / 8;
-  long long total = (long long)g.N * g.H * g.W * cv;
-  GRID_STRIDE(i, total) {
-    int c8 = static_cast<int>(i % cv);
-    long long p = i / cv;
-    int w = static_cast<int>(p % g.W);
-    p /= g.W;
-    int h = static_cast<int>(p % g.H);
-    int n = static_cast<int>(p / g.H);
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int oh0 = (h + g.PT - g.KH + 1 + g.SH - 1);
-    oh0 = oh0 < 0 ? 0 : oh0 / g.SH;
-    int oh1 = (h + g.PT) / g.SH;
-    int ow0 = (w + g.PL - g.KW + 1 + g.SW - 1);
-    ow0 = ow0 < 0 ? 0 : ow0 / g.SW;
-    int ow1 = (w + g.PL) / g.SW;
-    if (oh1 >= g.OH) oh1 = g.OH - 1;
-    if (ow1 >= g.OW) ow1 = g.OW - 1;
-    for (int oh = oh0; oh <= oh1; ++oh) {
-      int kh = h - (oh * g.SH - g.PT);
-      if (kh < 0 || kh >= g.KH) continue;
-      for (int ow = ow0; ow <= ow1; ++ow) {
-        int kw = w - (ow * g.SW - g.PL);
-        if (kw < 0 || kw >= g.KW) continue;
-        long long o = (((long long)n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8;
-        uint2 packed = *reinterpret_cast<const uint2*>(arg + o);
-        uint8_t id[8] = {(uint8_t)(packed.x), (uint8_t)(packed.x >> 8), (uint8_t)(packed.x >> 16),
-                         (uint8_t)(packed.x >> 24), (uint8_t)(packed.y), (uint8_t)(packed.y >> 8),
-                         (uint8_t)(packed.y >> 16), (uint8_t)(packed.y >> 24)};
-        float gv[8];
-        load_bf8(dy + o, gv);
-        uint8_t me = static_cast<uint8_t>(kh * g.KW + kw);
+  const int c8 = static_cast<int>(i % cv);
+  IDX p = i / cv;
+  const int w = static_cast<int>(p % g.W);
+  p /= g.W;
+  const int h = static_cast<int>(p % g.H);
+  const IDX n = p / g.H;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int oh0 = h + g.PT - g.KH + 1 + g.SH - 1;
+  oh0 = oh0 < 0 ? 0 : oh0 / g.SH;
+  int oh1 = (h + g.PT) / g.SH;
+  int ow0 = w + g.PL - g.KW + 1 + g.SW - 1;
+  ow0 = ow0 < 0 ? 0 : ow0 / g.SW;
+  int ow1 = (w + g.PL) / g.SW;
+  if (oh1 >= g.OH) oh1 = g.OH - 1;
+  if (ow1 >= g.OW) ow1 = g.OW - 1;
+  for (int oh = oh0; oh <= oh1; ++oh) {
+    const int kh = h - (oh * g.SH - g.PT);
+    if (kh < 0 || kh >= g.KH) continue;
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int kw = w - (ow * g.SW - g.PL);
+      if (kw < 0 || kw >= g.KW) continue;
+      const long long o = (long long)((n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8;
+      const uint2 packed = *reinterpret_cast<const uint2*>(arg + o);
+      const uint32_t me = static_cast<uint32_t>(kh * g.KW + kw);
+      float gv[8];
+      load_bf8(dy + o, gv);
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (id[k] == me) acc[k] += gv[k];
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t id = ((k < 4 ? packed.x : packed.y) >> (8 * (k & 3))) & 0xffu;
+        if (id == me) acc[k] += gv[k];
       }
     }
-    store_bf8(dx + (((long long)n * g.H + h) * g.W + w) * g.C + c8 * 8, acc);
   }
+  store_bf8(dx + (long long)i * 8, acc);
 }
 
 __device__ __forceinline__ int win_count(const PoolGeo& g, int oh, int ow) {
@@ -619,10 +621,15 @@ MDTF_EXPORT int mdtf_pool_fwd(int is_max, const void* x, void* y, void* argmax, 
   if (C % 8 || KH * KW > 255) return MDTF_EINVAL;
   PoolGeo g{N, H, W, C, OH, OW, KH, KW, SH, SW, PT, PL};
   long long work = (long long)N * OH * OW * (C / 8);
-  if (is_max)
-    hipLaunchKernelGGL(maxpool_fwd, dim3(grid_cap(work)), dim3(kT), 0, st, (const bf16_t*)x, (bf16_t*)y,
-                       (uint8_t*)argmax, g);
-  else
+  if (is_max) {
+    const dim3 grid((unsigned)ceil_div(work, kT));
+    if (work < 0x7fffffffLL && (long long)N * H * W * C < 0x7fffffffLL)
+      hipLaunchKernelGGL(maxpool_fwd<int>, grid, dim3(kT), 0, st, (const bf16_t*)x, (bf16_t*)y, (uint8_t*)argmax, g,
+                         (int)work);
+    else
+      hipLaunchKernelGGL(maxpool_fwd<long long>, grid, dim3(kT), 0, st, (const bf16_t*)x, (bf16_t*)y,
+                         (uint8_t*)argmax, g, work);
+  } else
     hipLaunchKernelGGL(avgpool_fwd, dim3(grid_cap(work)), dim3(kT), 0, st, (const bf16_t*)x, (bf16_t*)y, g);
   MDTF_LAUNCH_CHECK();
   return 0;
@@ -633,10 +640,15 @@ MDTF_EXPORT int mdtf_pool_bwd(int is_max, const void* dy, const void* argmax, vo
   if (C % 8) return MDTF_EINVAL;
   PoolGeo g{N, H, W, C, OH, OW, KH, KW, SH, SW, PT, PL};
   long long work = (long long)N * H * W * (C / 8);
-  if (is_max)
-    hipLaunchKernelGGL(maxpool_bwd, dim3(grid_cap(work)), dim3(kT), 0, st, (const bf16_t*)dy,
-                       (const uint8_t*)argmax, (bf16_t*)dx, g);
-  else
+  if (is_max) {
+    const dim3 grid((unsigned)ceil_div(work, kT));
+    if (work < 0x7fffffffLL && (long long)N * H * W * C < 0x7fffffffLL)
+      hipLaunchKernelGGL(maxpool_bwd<int>, grid, dim3(kT), 0, st, (const bf16_t*)dy, (const uint8_t*)argmax,
+                         (bf16_t*)dx, g, (int)work);
+    else
+      hipLaunchKernelGGL(maxpool_bwd<long long>, grid, dim3(kT), 0, st, (const bf16_t*)dy, (const uint8_t*)argmax,
+                         (bf16_t*)dx, g, work);
+  } else
     hipLaunchKernelGGL(avgpool_bwd, dim3(grid_cap(work)), dim3(kT), 0, st, (const bf16_t*)dy, (bf16_t*)dx, g);
   MDTF_LAUNCH_CHECK();
   return 0;

@@ -105,10 +105,19 @@ class _Pool(torch.autograd.Function):
         ctx.is_max = is_max
         if is_max:
             ctx.save_for_backward(arg)
+        # fanned-out output (a ResNet stem pool feeds conv1 AND the projection shortcut): the
+        # consumers' dgrads accumulate in place instead of autograd adding their gradients
+        from . import actsink
+        ctx.set_materialize_grads(False)
+        ctx.out_sink = actsink.attach(y)
         return y
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.out_sink is not None:
+            dy = ctx.out_sink.take(dy)
+        if dy is None:
+            return None, None, None, None, None, None
         dy = dy.contiguous()
         geo = ctx.geo
         arg = ctx.saved_tensors[0] if ctx.is_max else None

@@ -111,6 +111,18 @@ class StepGraph(object):
         self._outputs = {}          # id(program) -> static output dict
         self._gs = None
 
+    def release(self):
+        """Drop the captured graph, its static buffers and outputs (synchronizes the device)."""
+        if self.graph is not None:
+            torch.cuda.synchronize()
+            self.graph.reset()
+            self.graph = None
+        self._static_src.clear()
+        self._static_ph.clear()
+        self._outputs.clear()
+        self.dyn = None
+        self.eager_steps = 0
+
     # ------------------------------------------------------------------
     def _inputs(self):
         leaves = []

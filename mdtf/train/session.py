@@ -261,6 +261,8 @@ class MonitoredSession(Session):
             h.end(self)
         if torch.cuda.is_available():
             torch.cuda.synchronize()
+        from . import step as step_mod
+        step_mod.release_graphs()            # captured steps hold collectives of the current process group
 
     def __exit__(self, exc_type, exc, tb):
         if exc_type is None:

@@ -325,6 +325,13 @@ class TrainOp(Fetchable):
             red.after_update()
         return scale
 
+    def release_graph(self):
+        """Free the captured step graph (and its private memory pool).  Must run before the
+        process group it captured collectives of is destroyed; the next step re-captures."""
+        if self.graph is not None:
+            self.graph.release()
+            self.graph = None
+
     def evaluate(self, ctx):
         key = ("train", id(self))
         if key in ctx.cache:
@@ -358,5 +365,11 @@ def train_ops():
     return list(_TRAIN_OPS)
 
 
+def release_graphs():
+    for op in _TRAIN_OPS:
+        op.release_graph()
+
+
 def reset():
+    release_graphs()
     del _TRAIN_OPS[:]

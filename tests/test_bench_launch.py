@@ -1,0 +1,43 @@
+"""The driver's multi-GPU launch of bench.py, rehearsed on the CPU.
+
+The round-end driver runs ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N
+--master-addr 127.0.0.1 --master-port P bench.py --gpus N ...`` (one rank per GPU over RCCL).
+The same command with 2 ranks on gloo (no GPU here) walks the whole path: Server.from_env, the
+bucketed gradient reduction in both sync modes, the MAX-over-ranks timing and rank 0's JSON line.
+Tiny images keep ResNet-50 cheap on the CPU.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("mode", ["allreduce", "sharded"])
+def test_bench_torchrun_two_ranks(mode):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--batch", "2", "--image_size", "32", "--mode", mode]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("MDTF_HIP_GRAPH", None)
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]          # rank 0 only
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["config"]["global_batch"] == 4 and rec["config"]["parallelism"] == "dp2"
+    assert rec["config"]["grad_sync"] == mode
+    assert rec["value"] > 0 and rec["ms_per_step"] > 0
+    assert rec["loss_last"] == rec["loss_last"]           # finite

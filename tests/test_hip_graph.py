@@ -196,4 +196,6 @@ def test_hip_graph_captures_rccl_collectives(mode, monkeypatch):
         for k in w_e:
             assert torch.equal(w_e[k], w_g[k]), k
     finally:
+        from mdtf.train import step as S
+        S.release_graphs()                 # the captured RCCL collectives go before their communicator
         dist.destroy_process_group()
