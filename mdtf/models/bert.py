@@ -125,12 +125,17 @@ class Bert(Model):
     def _layer(self, x, amask, B, S_, H, nh, dh):
         with V.variable_scope("attention"):
             with V.variable_scope("self"):
-                ws, bs = [], []
-                for nm in ("query", "key", "value"):
+                ws, bs = {}, {}
+                # created value, key, query: the flat parameter space lays variables out in reverse
+                # creation order, so the three biases (and their fp32 gradient slots) end up adjacent
+                # in q|k|v order -- one fused bias view / one column-sum for the fused projection
+                for nm in ("value", "key", "query"):
                     with V.variable_scope(nm):
-                        ws.append(V.get_variable("kernel", [H, H], initializer=_init()))
-                        bs.append(V.get_variable("bias", [H], initializer=V.constant_initializer(0.0)))
-                qkv = ops.dense_multi(x.reshape(-1, H), ws, bs)                               # one GEMM
+                        ws[nm] = V.get_variable("kernel", [H, H], initializer=_init())
+                        bs[nm] = V.get_variable("bias", [H], initializer=V.constant_initializer(0.0))
+                order = ("query", "key", "value")
+                qkv = ops.dense_multi(x, [ws[n] for n in order], [bs[n] for n in order])   # one GEMM
+                qkv = qkv.reshape(-1, 3 * H)
                 drop = self.dropout if S.is_training() else 0.0
                 ctx = T.fused_attention(qkv, B, S_, nh, amask, drop).reshape(B, S_, H)
             with V.variable_scope("output"):

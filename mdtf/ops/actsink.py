@@ -14,6 +14,8 @@ The producer's backward (called with ``None`` once all consumers are done)
 takes the summed gradient from the sink. It also adds whatever ordinary autograd
 gradient arrived, so consumers that are not sink-aware stay correct.
 """
+import os
+
 
 
 class ActGradSink(object):
@@ -71,7 +73,7 @@ class ActGradSink(object):
         return st
 
 
-ENABLED = True      # switch for A/B tests (tests/test_kernels_gpu.py)
+ENABLED = os.environ.get("MDTF_ACT_SINKS", "1") != "0"      # switch for A/B tests and benches
 
 
 def attach(t):

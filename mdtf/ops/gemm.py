@@ -78,17 +78,42 @@ def _act_bwd(dy, saved, act):
     return dx
 
 
+def _adjacent(ts):
+    """One 1-D view over tensors that lie back to back in memory (e.g. neighbouring slots of the
+    flat parameter / gradient buffers), else None."""
+    t0 = ts[0]
+    if t0 is None or any(t is None or t.dim() != 1 or t.dtype != t0.dtype or not t.is_contiguous() for t in ts):
+        return None
+    off = t0.data_ptr()
+    for t in ts:
+        if t.data_ptr() != off:
+            return None
+        off += t.numel() * t.element_size()
+    return t0.as_strided((sum(t.numel() for t in ts),), (1,))
+
+
 class _Dense(torch.autograd.Function):
-    """y = act(x @ [W_1 | ... | W_n] + [b_1 | ... | b_n]); ``trans``: W given as [N, K]."""
+    """y = act(x @ [W_1 | ... | W_n] + [b_1 | ... | b_n]); ``trans``: W given as [N, K].
+
+    ``x_sink``: the activation-gradient sink of a fanned-out input (a LayerNorm output that also
+    feeds the next residual): dx is accumulated into it by the GEMM itself (beta = 1) instead of
+    autograd adding two gradient tensors."""
 
     @staticmethod
-    def forward(ctx, x, act, trans, nw, *wb):
+    def forward(ctx, x, act, trans, nw, x_sink, x_shape, *wb):
         ws, bs = wb[:nw], wb[nw:]
         w = ws[0] if nw == 1 else torch.cat(ws, 1)
         if trans:
             w = w.t()
         has_b = bs[0] is not None
-        b = (bs[0] if nw == 1 else torch.cat(bs, 0)).to(x.dtype) if has_b else None
+        if has_b:
+            b = bs[0] if nw == 1 else _adjacent(bs)
+            b = (b if b is not None else torch.cat(bs, 0)).to(x.dtype)
+        else:
+            b = None
+        ctx.x_sink, ctx.x_shape = x_sink, x_shape
+        if x_sink is not None:
+            x_sink.register()
         pre = torch.addmm(b, x, w) if has_b else torch.mm(x, w)
         if act == 0:
             y, saved = pre, None
@@ -108,7 +133,19 @@ class _Dense(torch.autograd.Function):
         x, w, saved = ctx.saved_tensors
         dy = dy.contiguous()
         dpre = dy if ctx.act == 0 else _act_bwd(dy, saved, ctx.act)
-        dx = torch.mm(dpre, w.t()) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            xs = ctx.x_sink
+            if xs is None:
+                dx = torch.mm(dpre, w.t())
+            else:
+                buf, acc = xs.target()
+                if acc:                        # second contribution: C += dpre @ w^T inside the GEMM
+                    b2 = buf.view(-1, w.shape[0])
+                    torch.addmm(b2, dpre, w.t(), out=b2)
+                    xs.written(buf)
+                else:
+                    xs.written(torch.mm(dpre, w.t()).view(ctx.x_shape))
         ws, bs = ctx.like[:ctx.nw], ctx.like[ctx.nw:]
         gws, gbs = [], []
         col = 0
@@ -122,15 +159,21 @@ class _Dense(torch.autograd.Function):
                 else:
                     wgrad_into(sink.grad, x, d)
                 gws.append(V.grad_marker(ws[j]))
-            elif ctx.needs_input_grad[4 + j]:
+            elif ctx.needs_input_grad[6 + j]:
                 g = torch.mm(d.t(), x) if ctx.trans else torch.mm(x.t(), d)
                 gws.append(g.to(ws[j].dtype))
             else:
                 gws.append(None)
         if ctx.has_b:
+            fused = None
+            if ctx.nw > 1 and all(sk is not None for sk in ctx.bsinks):
+                fused = _adjacent([sk.grad for sk in ctx.bsinks])     # q|k|v slots back to back
             if ctx.nw == 1 and ctx.bsinks[0] is not None:
                 kernels.colsum_into(dpre, ctx.bsinks[0].grad)
                 gbs.append(V.grad_marker(bs[0]))
+            elif fused is not None:
+                kernels.colsum_into(dpre, fused)
+                gbs = [V.grad_marker(b) for b in bs]
             else:
                 tot = kernels.colsum(dpre)
                 col = 0
@@ -144,7 +187,7 @@ class _Dense(torch.autograd.Function):
                         gbs.append(part.to(bs[j].dtype))
         else:
             gbs = [None] * ctx.nw
-        return (dx, None, None, None) + tuple(gws) + tuple(gbs)
+        return (dx, None, None, None, None, None) + tuple(gws) + tuple(gbs)
 
 
 def matmul(a, b):
@@ -164,10 +207,11 @@ def dense(x, w, b=None, act=None):
 def dense_multi(x, ws, bs, act=None):
     """One GEMM for several weight matrices sharing input ``x`` (outputs concatenated)."""
     _check(x, "dense")
+    from . import actsink
     shp = x.shape
     x2 = x.reshape(-1, shp[-1])
     ws = [w.to(x.dtype) if w.dtype != x.dtype else w for w in ws]
-    y = _Dense.apply(x2, _ACT[act], False, len(ws), *ws, *bs)
+    y = _Dense.apply(x2, _ACT[act], False, len(ws), actsink.sink_of(x), tuple(shp), *ws, *bs)
     return y.reshape(*shp[:-1], y.shape[-1])
 
 
@@ -176,5 +220,5 @@ def dense_transposed(x, w, b=None):
     _check(x, "dense")
     shp = x.shape
     w = w.to(x.dtype) if w.dtype != x.dtype else w
-    y = _Dense.apply(x.reshape(-1, shp[-1]), 0, True, 1, w, b)
+    y = _Dense.apply(x.reshape(-1, shp[-1]), 0, True, 1, None, tuple(shp), w, b)
     return y.reshape(*shp[:-1], y.shape[-1])

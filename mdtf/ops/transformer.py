@@ -51,6 +51,14 @@ class _LayerNorm(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, res, gamma, beta, eps, p_drop, seed):
+        from . import actsink
+        ctx.set_materialize_grads(False)
+        # the residual is usually the previous LayerNorm's output, which also feeds a dense layer:
+        # hand d(residual) to its sink (the dense dgrad then accumulates in its GEMM).  Only with
+        # dropout: without it dx and d(residual) are one tensor that autograd still passes on.
+        ctx.res_sink = actsink.sink_of(res) if (res is not None and p_drop > 0) else None
+        if ctx.res_sink is not None:
+            ctx.res_sink.register()
         x = x.contiguous()
         H = x.shape[-1]
         rows = x.numel() // H
@@ -69,11 +77,16 @@ class _LayerNorm(torch.autograd.Function):
         ctx.drop = (float(p_drop), seed)
         ctx.sinks = (V.grad_sink(gamma), V.grad_sink(beta))
         ctx.like = (gamma, beta)
+        ctx.out_sink = actsink.attach(y)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         s, g, mean, rstd = ctx.saved_tensors
+        if ctx.out_sink is not None:
+            dy = ctx.out_sink.take(dy)
+        if dy is None:
+            return None, None, None, None, None, None, None
         dy = dy.contiguous()
         H = s.shape[-1]
         rows = s.numel() // H
@@ -92,7 +105,11 @@ class _LayerNorm(torch.autograd.Function):
         rg = V.grad_marker(gamma) if sg is not None else dg
         rb = V.grad_marker(beta) if sb is not None else db
         dx = dxb if dxb is not None else ds
-        return dx, (ds if ctx.has_res else None), rg, rb, None, None, None
+        dres = ds if ctx.has_res else None
+        if ctx.res_sink is not None:
+            ctx.res_sink.adopt_or_add(ds.view(s.shape))
+            dres = None
+        return dx, dres, rg, rb, None, None, None
 
 
 def layer_norm(x, gamma, beta, eps=1e-12, residual=None, dropout=0.0):

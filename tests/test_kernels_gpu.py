@@ -511,7 +511,7 @@ def test_bert_tiny_train_step_gpu():
     assert ls[-1] < 0.5 * ls[0], ls
 
 
-def _bert_step(dev, dt, raw, gt, seq=32, heads_dim=None):
+def _bert_step(dev, dt, raw, gt, seq=32, heads_dim=None, dropout=0.0):
     import mdtf
     from mdtf.models import Bert, BertPretrainingLoss
     from mdtf.runtime import Net, Tower
@@ -527,7 +527,7 @@ def _bert_step(dev, dt, raw, gt, seq=32, heads_dim=None):
     gp = mdtf.placeholder(torch.int64, [None, gt.shape[1]])
     opt = mdtf.train.GradientDescentOptimizer(0.1)
     tg = []
-    model = Bert("tiny", vocab_size=512, seq_len=seq, max_predictions=5, dropout=0.0)
+    model = Bert("tiny", vocab_size=512, seq_len=seq, max_predictions=5, dropout=dropout)
     if heads_dim:                      # tiny width, but head dim 64 (2 heads) so the fused kernel applies
         model.heads = model.H // heads_dim
     t = Tower(Net(model), "tower_0/", tg, rp, gp, BertPretrainingLoss(5), opt, batch_size=raw.shape[0])
@@ -661,6 +661,30 @@ def test_bert_fused_vs_unfused_attention_path(monkeypatch):
         if k.endswith("key/bias"):
             continue
         assert _rel(gf[k], gu[k]) < 0.1, (k, _rel(gf[k], gu[k]))
+
+
+def test_bert_activation_sinks_match_autograd(monkeypatch):
+    """BERT step with dropout: LayerNorm outputs as gradient sinks (d(residual) handed to the sink, the
+    next dense layer's dgrad accumulating into it inside its GEMM, fused q|k|v bias column sum) == the
+    same step with plain autograd gradient adds."""
+    from mdtf.models import SyntheticBertLoader
+    from mdtf.ops import actsink
+    from mdtf.train import variables as V
+    V.get_store().device = torch.device("cpu")
+    ld = SyntheticBertLoader(seq_len=128, max_predictions=5, vocab=512, seed=5)
+    ld.batch_size = 4
+    raw, gt = ld._make()
+    out = {}
+    for enabled in (True, False):
+        monkeypatch.setattr(actsink, "ENABLED", enabled)
+        torch.manual_seed(11)                        # same dropout masks in both runs
+        out[enabled] = _bert_step(DEV, torch.bfloat16, raw, gt, seq=128, heads_dim=64, dropout=0.1)
+    (ls, gs), (la, ga) = out[True], out[False]
+    assert abs(ls - la) / la < 1e-3
+    for k in ga:
+        if k.endswith("key/bias"):                   # zero up to rounding (softmax is shift invariant)
+            continue
+        assert _rel(gs[k], ga[k]) < 2e-2, (k, _rel(gs[k], ga[k]))
 
 
 def test_deterministic_mode_bitwise_repeatable():
