@@ -267,6 +267,7 @@ def _pads_ok(pads):
 
 BWD_STATS = os.environ.get("MDTF_BN_BWD_STATS", "1") != "0"   # BN backward statistics from the dgrad epilogue
 STAT_SLOTS = 64   # atomic partial rows of the fused BN statistics (csrc/conv_igemm.hip kStatSlots)
+MAX_STAT_SLOTS = int(os.environ.get("MDTF_BN_MAX_SLOTS", "128"))   # cap of the adaptive slot count (A/B: 128 beat 1024 by 0.4%)
 _STATS = {}       # device -> [flat fp32 buffer, dirty]: persistent, re-zeroed by the BN finalize kernel
 
 
@@ -296,11 +297,11 @@ def stats_consumed(device):
 
 def stat_slots(mtiles):
     """Atomic partial rows for epilogue statistics: one per M tile in deterministic mode,
-    else ~8 M tiles per row (64..1024 rows): low contention, small finalize."""
+    else ~8 M tiles per row (64..MAX_STAT_SLOTS rows): low contention, small finalize."""
     if N.deterministic():
         return mtiles
     slots = STAT_SLOTS
-    while slots < 1024 and slots * 8 < mtiles:
+    while slots < MAX_STAT_SLOTS and slots * 8 < mtiles:
         slots *= 2
     return slots
 
