@@ -306,6 +306,32 @@ def stat_slots(mtiles):
     return slots
 
 
+# Weight gradients on a side stream: a conv's wgrad does not feed the rest of backward (only the flat
+# gradient buffer), so it runs on its own HIP stream beside the dgrad -> BN-backward chain and fills
+# the CUs that chain's memory-bound and small kernels leave idle.  Captured hipGraphs keep the two
+# streams as concurrent branches.  The gradient buffer is read only after join_side_streams()
+# (bucket all-reduce launch, end of backward).  Measured on ResNet-50 (scripts/gpu_envab.sh): -0.3 %
+# (the chain's kernels already keep HBM busy), so it is opt-in: MDTF_WGRAD_STREAM=1.
+WGRAD_STREAM = os.environ.get("MDTF_WGRAD_STREAM", "0") == "1"
+_SIDE = {}        # device -> side stream
+_PENDING = set()  # devices with side-stream work the main stream has not joined yet
+
+
+def _side_stream(device):
+    s = _SIDE.get(device)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _SIDE[device] = s
+    return s
+
+
+def join_side_streams():
+    """Make the current stream wait for every weight gradient issued on the side streams."""
+    for dev in list(_PENDING):
+        torch.cuda.current_stream(dev).wait_stream(_SIDE[dev])
+    _PENDING.clear()
+
+
 _BSTATS = {}      # (device, C, slots) -> free zeroed [2, slots, C] buffers (BN backward statistics)
 
 
@@ -406,8 +432,18 @@ class _Conv(torch.autograd.Function):
         if need_dw and not lib_dw:
             if sink is not None:
                 # fp32 atomics of the wgrad kernel accumulate into the flat gradient buffer
-                mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], out=sink.grad, ver=cw[4],
-                           stages=cw[5])
+                if WGRAD_STREAM and x.is_cuda:
+                    side = _side_stream(x.device)
+                    side.wait_stream(torch.cuda.current_stream(x.device))
+                    with torch.cuda.stream(side):
+                        mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], out=sink.grad,
+                                   ver=cw[4], stages=cw[5])
+                    x.record_stream(side)
+                    dy.record_stream(side)
+                    _PENDING.add(x.device)
+                else:
+                    mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], out=sink.grad, ver=cw[4],
+                               stages=cw[5])
                 dw = V.grad_marker(w)
             else:
                 dw = mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], ver=cw[4], stages=cw[5])

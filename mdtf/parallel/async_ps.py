@@ -238,6 +238,8 @@ class AsyncWorker(object):
             self.space.zero_grad()
             out = loss_h.forward(ctx, grad=True)
             out["loss"].backward()
+            from ..ops import conv as _conv
+            _conv.join_side_streams()
             self._exchange("push")
             self.steps_done += 1
             step = self.store.add(gs_key, 1)

@@ -130,6 +130,8 @@ class GradReducer(object):
         b.launched = True
         if not self.collective:
             return
+        from ..ops import conv as _conv
+        _conv.join_side_streams()          # side-stream weight gradients of this bucket are in
         g = b.group
         if self.mode == "allreduce":
             b.work = dist.all_reduce(g.grad[b.start:b.end], group=self.pg, async_op=True)
@@ -139,6 +141,8 @@ class GradReducer(object):
 
     def end_backward(self, step=0):
         """Finish all reductions; returns the gradient scale (1/contributors)."""
+        from ..ops import conv as _conv
+        _conv.join_side_streams()          # every weight gradient is in the flat buffer
         if self.world > 1 and self.R < self.world:
             order = self.store.add("mdtf/sync_replicas/%d" % step, 1)
             self.contributed = order <= self.R
