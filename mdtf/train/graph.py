@@ -54,10 +54,6 @@ def rng_offset_tensor(device):
     return t
 
 
-def capturing():
-    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
-
-
 def _leaves(x, out):
     from .step import Placeholder, SourceOutput
     if isinstance(x, (Placeholder, SourceOutput)):
