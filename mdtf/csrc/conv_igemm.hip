@@ -939,7 +939,7 @@ __device__ __forceinline__ bf16x8_t frag_tr(const char* img, int col0, int kbase
   return __builtin_bit_cast(bf16x8_t, f);
 }
 
-template <int BM, int BN, int STAGES, int NW>
+template <int BM, int BN, int STAGES, int NW, bool PIPE>
 __global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
   // NW = 4 (2x2 waves) or 8 (one 256-row/col block per CU, 4x2 or 2x4 waves by aspect)
   constexpr int WM = NW == 4 ? 2 : (BM > BN ? 4 : 2), WN = NW / WM;
@@ -971,6 +971,7 @@ __global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
 
   const int bytes_x = (int)((long long)a.N * a.H * a.W * a.Cin * 2);
   const int bytes_dy = (int)((Mpix - 1) * a.ld_dy * 2 + a.Cout * 2);
+  const i32x4_t rsrc_x = buffer_rsrc(a.src, bytes_x), rsrc_dy = buffer_rsrc(a.dy, bytes_dy);
 
   // A half h: rows r0 + 64h .. +63 lie in one tap (Cin % 64 == 0)
   int h_dy[HA], h_dx[HA], h_c[HA];
@@ -1018,7 +1019,10 @@ __global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
         const unsigned voff =
             ok ? (unsigned)((((p_n[u] * a.H + iy) * a.W + ix) * a.Cin + h_c[h] + gch[u]) * 2) : OOB;
         // instruction slot: half h, row block (wave + NW u) -> LDS rows 8*(wave+NW u) ..
-        dma16(a.src, bytes_x, lds + h * 8192 + (wave + NW * u) * 1024, voff, 0);
+        if constexpr (PIPE)
+          dma16_asm(rsrc_x, lds + h * 8192 + (wave + NW * u) * 1024, voff);
+        else
+          dma16(a.src, bytes_x, lds + h * 8192 + (wave + NW * u) * 1024, voff, 0);
       }
       // B halves: DY[m, n0 + 64h + chunk]
       char* ldsb = lds + BM * 128;
@@ -1026,7 +1030,10 @@ __global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
       for (int h = 0; h < HB; ++h) {
         const int co = n0 + 64 * h;
         const unsigned voff = (mok && co < a.Cout) ? (unsigned)((p_m[u] * a.ld_dy + co + gch[u]) * 2) : OOB;
-        dma16(a.dy, bytes_dy, ldsb + h * 8192 + (wave + NW * u) * 1024, voff, 0);
+        if constexpr (PIPE)
+          dma16_asm(rsrc_dy, ldsb + h * 8192 + (wave + NW * u) * 1024, voff);
+        else
+          dma16(a.dy, bytes_dy, ldsb + h * 8192 + (wave + NW * u) * 1024, voff, 0);
       }
       // advance this row by 64 pixels
       p_m[u] += 64;
@@ -1047,6 +1054,87 @@ __global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
     for (int j = 0; j < TN; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
   const int KT = kt_end - kt_begin;
+  if constexpr (PIPE) {
+    // Software-pipelined variant: the k-step is split in halves.  The second half's fragments
+    // are read while the first half's MFMAs run, and the next step's first-half fragments
+    // while the second half's MFMAs run, so LDS reads hide under MFMAs.  The DMA for step
+    // kt + STAGES goes out right after the mid-step barrier that frees its buffer: every
+    // buffer is in flight from the prologue on, and each lands one step ahead of its use.
+    // The DMAs are inline asm (dma16_asm), so the compiler adds no vmcnt(0) before LDS reads;
+    // the counted waits below and the barriers order them.
+    bf16x8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+    auto read_half = [&](bf16x8_t (&fa)[TM], bf16x8_t (&fb)[TN], int buf, int kh2) {
+      const char* As = smem_raw + buf * STAGE;
+      const char* Bs = As + BM * 128;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wm * (TM * 16) + i * 16;
+        fa[i] = frag_tr(As + (col >> 6) * 8192, col & 63, 32 * kh2, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * (TN * 16) + j * 16;
+        fb[j] = frag_tr(Bs + (col >> 6) * 8192, col & 63, 32 * kh2, lane);
+      }
+    };
+    // wait until at most n stages (newest first) are still in flight
+    auto wait_stages = [&](int n) {
+      if (n <= 0)
+        wait_vmcnt<0>();
+      else if (n == 1)
+        wait_vmcnt<PER_STAGE>();
+      else if (n == 2)
+        wait_vmcnt<2 * PER_STAGE>();
+      else
+        wait_vmcnt<3 * PER_STAGE>();
+    };
+    // interleave this half's fragment reads with the other half's MFMAs (both in one block)
+    constexpr int NRD = 2 * (TM + TN), NMF = TM * TN, NIL = NRD < NMF ? NRD : NMF;
+    auto interleave = [&]() {
+#pragma unroll
+      for (int q = 0; q < NIL; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one LDS read
+      }
+      if constexpr (NRD > NIL) __builtin_amdgcn_sched_group_barrier(0x100, NRD - NIL, 0);
+      if constexpr (NMF > NIL) __builtin_amdgcn_sched_group_barrier(0x008, NMF - NIL, 0);
+    };
+    const int pro = KT < STAGES ? KT : STAGES;
+    for (int s = 0; s < pro; ++s) stage(s);
+    wait_stages(pro - 1);
+    asm volatile("s_barrier" ::: "memory");
+    read_half(fa0, fb0, 0, 0);
+    int cur = 0;
+    for (int kt = 0; kt < KT; ++kt) {
+      __builtin_amdgcn_sched_barrier(0);
+      read_half(fa1, fb1, cur, 1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fa0[i], fb0[j], acc[i][j]);
+      interleave();
+      __builtin_amdgcn_sched_barrier(0);
+      const int nxt = cur + 1 == STAGES ? 0 : cur + 1;
+      if (kt + 1 < KT) {
+        // issued so far: steps 0 .. min(KT-1, kt-1+STAGES); wait for step kt+1
+        const int newer = (KT - 2 - kt) < (STAGES - 2) ? (KT - 2 - kt) : (STAGES - 2);
+        wait_stages(newer);
+      }
+      // this wave's second-half reads are complete, so after the barrier no wave reads `cur`
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (kt + STAGES < KT) stage(cur);
+      __builtin_amdgcn_sched_barrier(0);
+      // the next step's first-half fragments (a harmless stale read after the last step)
+      read_half(fa0, fb0, nxt, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fa1[i], fb1[j], acc[i][j]);
+      interleave();
+      cur = nxt;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  } else {
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < KT) stage(s);
@@ -1089,6 +1177,7 @@ __global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fa[kh2][i], fb[kh2][j], acc[i][j]);
+  }
   }
   const int g = lane >> 4, li = lane & 15;
   float* slab = a.slab ? a.slab + (long long)split * R * a.Cout : nullptr;
@@ -1143,7 +1232,7 @@ __global__ void __launch_bounds__(256) wgrad_slab_reduce(const float* __restrict
   *o = v;
 }
 
-template <int BM, int BN, int STAGES, int NW = 4>
+template <int BM, int BN, int STAGES, int NW = 4, bool PIPE = false>
 int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
   const int R = a.KH * a.KW * a.Cin;
   a.mtiles = static_cast<int>(ceil_div(R, BM));
@@ -1161,8 +1250,8 @@ int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
   if (lds > 160 * 1024) return MDTF_EUNSUPPORTED;
   ConvArgs b = a;
   if (a.slab && (splits < 2 || splits > a.slab_cap || (a.ld_dw % 4) || (a.Cout % 4))) b.slab = nullptr;
-  hipLaunchKernelGGL((conv_wgrad_v2<BM, BN, STAGES, NW>), dim3(a.mtiles * a.ntiles * splits), dim3(64 * NW), lds, st,
-                     b);
+  hipLaunchKernelGGL((conv_wgrad_v2<BM, BN, STAGES, NW, PIPE>), dim3(a.mtiles * a.ntiles * splits), dim3(64 * NW), lds,
+                     st, b);
   MDTF_LAUNCH_CHECK();
   if (b.slab) {
     const long long RC = (long long)R * a.Cout;
@@ -1224,9 +1313,15 @@ int launch_wgrad(ConvArgs& a, int splits, hipStream_t st) {
 
 // v2 wgrad tile table; w8: 8-wave (512-thread) tiles
 int dispatch_wgrad_v2(ConvArgs& a, int bm, int bn, int stages, int w8, int splits, hipStream_t st) {
+  // MDTF_WGRAD_PIPE=0 selects the non-pipelined main loop (A/B switch)
+  static const bool pipe = [] {
+    const char* e = getenv("MDTF_WGRAD_PIPE");
+    return !(e && e[0] == '0');
+  }();
 #define WG2(BM_, BN_, S_, NW_) \
   if (bm == BM_ && bn == BN_ && stages == S_ && (NW_ == 8) == (w8 != 0)) \
-    return launch_wgrad_v2<BM_, BN_, S_, NW_>(a, splits, st);
+    return pipe ? launch_wgrad_v2<BM_, BN_, S_, NW_, true>(a, splits, st) \
+                : launch_wgrad_v2<BM_, BN_, S_, NW_, false>(a, splits, st);
   WG2(128, 128, 2, 4) WG2(128, 128, 3, 4) WG2(128, 64, 2, 4) WG2(128, 64, 3, 4) WG2(64, 128, 2, 4)
   WG2(64, 128, 3, 4) WG2(64, 64, 2, 4) WG2(64, 64, 3, 4) WG2(64, 64, 4, 4)
   WG2(256, 256, 2, 8) WG2(256, 128, 2, 8) WG2(256, 128, 3, 8) WG2(128, 256, 2, 8) WG2(128, 256, 3, 8)

@@ -78,6 +78,26 @@ __device__ __forceinline__ void dma16(const void* base, int nbytes, char* lds, u
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
 }
 
+// Same transfer, issued from inline asm so the compiler does not see an LDS write: it then
+// inserts no vmcnt(0) in front of later LDS reads (it cannot prove they miss the DMA target).
+// The caller owns the ordering: a counted wait_vmcnt<N>() plus an asm s_barrier with a "memory"
+// clobber (which LDS reads cannot move across) before any wave reads the target.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4_t buffer_rsrc(const void* base, int nbytes) {
+  const unsigned long long p = reinterpret_cast<unsigned long long>(base);
+  i32x4_t r;
+  r.x = static_cast<int>(p & 0xffffffffu);
+  r.y = static_cast<int>((p >> 32) & 0xffffu);
+  r.z = nbytes;
+  r.w = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void dma16_asm(i32x4_t rsrc, const char* lds, unsigned voff) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(
+      static_cast<unsigned>(reinterpret_cast<unsigned long long>((__attribute__((address_space(3))) const char*)lds)));
+  asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "{m0}"(m0) : "memory");
+}
+
 // s_waitcnt vmcnt(N) leaving lgkm/exp counters alone (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14)
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
