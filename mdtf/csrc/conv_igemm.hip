@@ -69,6 +69,9 @@ struct ConvArgs {
   float* bsum;           // [bslots][Ncol] (null: off)
   float* bsq;
   int bslots;
+  // wgrad (4-wave tiles): also add the column sums of DY (a dense layer's bias gradient) into
+  // dbias[Cout]; the first row-tile's blocks sum their B fragments with an all-ones MFMA (null: off)
+  float* dbias;
   // wgrad v2 split-K: per-split partial tiles stored to slab[split][R][Cout] (plain stores) and summed
   // into DW by one reduction pass, instead of fp32 atomics into DW (null: atomics)
   float* slab;
@@ -1052,6 +1055,22 @@ __global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+  // fused bias gradient: C = ones(16x32) x B-fragment puts each column's sum in every row
+  constexpr bool CAN_BIAS = NW == 4;          // the 8-wave tiles have no registers to spare
+  const bool do_bias = CAN_BIAS && a.dbias != nullptr && mt == 0 && wm == 0;
+  float4v accb[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) accb[j] = float4v{0.f, 0.f, 0.f, 0.f};
+  const bf16x8_t ones = __builtin_bit_cast(
+      bf16x8_t, short8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
+  auto bias_mfma = [&](const bf16x8_t (&fb)[TN]) {
+    if constexpr (CAN_BIAS) {
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) accb[j] = mfma(ones, fb[j], accb[j]);
+      }
+    }
+  };
 
   const int KT = kt_end - kt_begin;
   if constexpr (PIPE) {
@@ -1114,6 +1133,7 @@ __global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fa0[i], fb0[j], acc[i][j]);
       interleave();
       __builtin_amdgcn_sched_barrier(0);
+      bias_mfma(fb0);
       const int nxt = cur + 1 == STAGES ? 0 : cur + 1;
       if (kt + 1 < KT) {
         // issued so far: steps 0 .. min(KT-1, kt-1+STAGES); wait for step kt+1
@@ -1131,6 +1151,8 @@ __global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fa1[i], fb1[j], acc[i][j]);
       interleave();
+      __builtin_amdgcn_sched_barrier(0);
+      bias_mfma(fb1);
       cur = nxt;
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -1177,9 +1199,18 @@ __global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fa[kh2][i], fb[kh2][j], acc[i][j]);
+    bias_mfma(fb[0]);
+    bias_mfma(fb[1]);
   }
   }
   const int g = lane >> 4, li = lane & 15;
+  if (CAN_BIAS && do_bias && g == 0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int co = n0 + wn * (TN * 16) + j * 16 + li;
+      if (co < a.Cout) atomicAdd(a.dbias + co, accb[j][0]);
+    }
+  }
   float* slab = a.slab ? a.slab + (long long)split * R * a.Cout : nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -1509,9 +1540,11 @@ MDTF_EXPORT int mdtf_conv_wgrad_v2(const void* x, const void* dy, float* dw, int
 
 // dW[K][N] (fp32, row stride ld_dw) += X[M][K]^T DY[M][N] (DY row stride ld_dy): the dense-layer
 // weight gradient on the v2 wgrad kernel (a 1x1 convolution over M "pixels").  K % 64 == 0, N % 64 == 0.
+// dbias (optional, fp32 [N]): += column sums of dy (4-wave tiles only; else MDTF_EUNSUPPORTED)
 MDTF_EXPORT int mdtf_gemm_wgrad(const void* x, const void* dy, float* dw, long long M, int K, int N, int ld_dy,
                                 int ld_dw, int bm, int bn, int stages, int splits, float* slab, int slab_cap,
-                                hipStream_t st) {
+                                float* dbias, hipStream_t st) {
+  if (dbias && bm >= 10000) return MDTF_EUNSUPPORTED;
   if (K % 64 || N % 64 || ld_dy % 8 || M > 0x7fffffff) return MDTF_EINVAL;
   if (M * K * 2 > 0x7fffffffLL || M * (long long)ld_dy * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
   ConvArgs a = make_args((int)M, 1, 1, K, 1, 1, N, 1, 1, 1, 1, 0, 0, 1, 1);
@@ -1524,5 +1557,6 @@ MDTF_EXPORT int mdtf_gemm_wgrad(const void* x, const void* dy, float* dw, long l
   a.Ncol = N;
   a.slab = slab;
   a.slab_cap = slab_cap;
+  a.dbias = dbias;
   return dispatch_wgrad_v2(a, bm % 10000, bn, stages, bm / 10000, splits, st);
 }

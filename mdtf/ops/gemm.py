@@ -6,14 +6,17 @@ pre-activation for backward) is the mdtf activation kernel.  Several weight
 matrices that share an input (BERT's query/key/value) run as one GEMM on the
 column-concatenated weights.
 
-Backward: ``dx = dpre @ W^T`` (bf16), and the weight gradient is computed by
-hipBLASLt *directly into the variable's fp32 gradient slot* with
-``C += A^T B`` (bf16 inputs, fp32 accumulate/output), so no bf16 weight
-gradient is materialised and no separate cast/accumulate kernel runs; the
-bias gradient is the two-stage column-sum kernel, also accumulating into the
-fp32 slot.  (The library GEMM is used for these plain GEMMs; everything
-between them is mdtf kernels.)
+Backward: ``dx = dpre @ W^T`` (bf16, hipBLASLt; accumulated inside the GEMM into a
+fanned-out input's gradient sink), and the weight gradient is the mdtf weight-gradient
+kernel (``csrc/conv_igemm.hip`` conv_wgrad_v2 run as a 1x1 convolution) writing
+*directly into the variable's fp32 gradient slot*.  The same kernel adds the bias
+gradient (the column sums of ``dpre``) from the B fragments it already holds, with an
+all-ones MFMA, so no bf16 weight gradient is materialised and no column-sum kernel runs.
+Shapes the kernel does not take fall back to hipBLASLt ``C += A^T B`` (bf16 inputs, fp32
+output) and the two-stage column-sum kernel.
 """
+import os
+
 import torch
 
 from . import _native as N
@@ -22,16 +25,20 @@ from ..train import variables as V
 
 _ACT = {None: 0, "relu": 1, "gelu": 2}
 _fp32_out_ok = None      # does this torch build accept addmm(out_dtype=float32, out=...)?
+# bias gradients summed inside the weight-gradient kernel (MDTF_FUSED_BIAS_GRAD=0: separate column sums)
+FUSED_BIAS_GRAD = os.environ.get("MDTF_FUSED_BIAS_GRAD", "1") != "0"
 
-N.register("mdtf_gemm_wgrad", [N.P, N.P, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.P, N.I, N.P])
+N.register("mdtf_gemm_wgrad", [N.P, N.P, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.P, N.I, N.P, N.P])
 
 
-def wgrad_into(out, x, d):
+def wgrad_into(out, x, d, dbias=None):
     """``out[K][N] += x[M][K]^T d[M][N]`` in fp32 (``d`` may be a column slice).
 
     The mdtf weight-gradient kernel where it applies (K, N multiples of 64 -- it beats
     the library's fp32-output GEMM on the BERT shapes, bench/gemm_micro.py), else
-    hipBLASLt.  Deterministic mode uses the unsplit kernel.
+    hipBLASLt.  Deterministic mode uses the unsplit kernel.  ``dbias`` (fp32 [N]): the
+    kernel also adds the column sums of ``d`` (the layer's bias gradient) into it, from the
+    B fragments it already holds; returns True when it did (else the caller sums them).
     """
     M, K = x.shape
     Nn = d.shape[1]
@@ -41,11 +48,13 @@ def wgrad_into(out, x, d):
         bm, bn = (128, 128) if M < 4096 else (64, 128)
         from . import conv as C
         slab, cap = C.wgrad_slab(M, K, Nn, bm, bn, 2, splits, x.device, dense=True)
+        fuse = dbias is not None and FUSED_BIAS_GRAD and dbias.is_contiguous() and dbias.dtype == torch.float32
         rc = N.fn("mdtf_gemm_wgrad")(N.ptr(x), N.ptr(d), N.ptr(out), M, K, Nn, d.stride(0), out.stride(0), bm, bn, 2,
-                                     splits, N.ptr(slab), cap, N.stream_ptr())
+                                     splits, N.ptr(slab), cap, N.ptr(dbias) if fuse else None, N.stream_ptr())
         if rc == 0:
-            return
+            return fuse
     _accum_mm(out, x.t(), d)
+    return False
 
 
 def _accum_mm(out, a, b):
@@ -148,6 +157,7 @@ class _Dense(torch.autograd.Function):
                     xs.written(torch.mm(dpre, w.t()).view(ctx.x_shape))
         ws, bs = ctx.like[:ctx.nw], ctx.like[ctx.nw:]
         gws, gbs = [], []
+        bias_done = [False] * ctx.nw
         col = 0
         for j, n in enumerate(ctx.widths):
             d = dpre[:, col:col + n] if ctx.nw > 1 else dpre
@@ -157,14 +167,31 @@ class _Dense(torch.autograd.Function):
                 if ctx.trans:
                     _accum_mm(sink.grad, d.t(), x)
                 else:
-                    wgrad_into(sink.grad, x, d)
+                    bsink = ctx.bsinks[j] if ctx.has_b else None
+                    if wgrad_into(sink.grad, x, d, bsink.grad if bsink is not None else None):
+                        bias_done[j] = True
                 gws.append(V.grad_marker(ws[j]))
             elif ctx.needs_input_grad[6 + j]:
                 g = torch.mm(d.t(), x) if ctx.trans else torch.mm(x.t(), d)
                 gws.append(g.to(ws[j].dtype))
             else:
                 gws.append(None)
-        if ctx.has_b:
+        if ctx.has_b and all(bias_done):
+            gbs = [V.grad_marker(b) for b in bs]    # summed inside the weight-gradient kernel
+        elif ctx.has_b and any(bias_done):
+            tot = kernels.colsum(dpre)
+            col = 0
+            for j, n in enumerate(ctx.widths):
+                part = tot[col:col + n]
+                col += n
+                if bias_done[j]:
+                    gbs.append(V.grad_marker(bs[j]))
+                elif ctx.bsinks[j] is not None:
+                    ctx.bsinks[j].grad.add_(part)
+                    gbs.append(V.grad_marker(bs[j]))
+                else:
+                    gbs.append(part.to(bs[j].dtype))
+        elif ctx.has_b:
             fused = None
             if ctx.nw > 1 and all(sk is not None for sk in ctx.bsinks):
                 fused = _adjacent([sk.grad for sk in ctx.bsinks])     # q|k|v slots back to back

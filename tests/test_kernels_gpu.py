@@ -733,6 +733,26 @@ def test_gemm_wgrad_into_strided(M, K, N, col0, ld):
     assert _rel(out, ref) < 1e-4
 
 
+@pytest.mark.parametrize("M,K,N,col0,ld,det", [(8192, 768, 768, 768, 2304, False), (8192, 768, 3072, 0, 3072, False),
+                                               (1000, 128, 192, 0, 192, False), (2048, 192, 128, 64, 256, True)])
+def test_gemm_wgrad_fused_bias(M, K, N, col0, ld, det):
+    """The weight-gradient kernel also adds the column sums of d (the bias gradient) into dbias."""
+    from mdtf.ops import _native, gemm
+    torch.manual_seed(37)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    d = torch.randn(M, ld, device=DEV).bfloat16()[:, col0:col0 + N]
+    out = torch.full((K, N), 0.25, device=DEV)
+    db = torch.full((N,), -1.0, device=DEV)
+    _native.set_deterministic(det)
+    try:
+        fused = gemm.wgrad_into(out, x, d, db)
+    finally:
+        _native.set_deterministic(False)
+    assert fused
+    assert _rel(out, x.float().t() @ d.float() + 0.25) < 1e-4
+    assert _rel(db, d.float().sum(0) - 1.0) < 1e-4
+
+
 def _hash_keep(seed, n, p):
     import numpy as np
     idx = np.arange(n, dtype=np.uint64).astype(np.uint32)
