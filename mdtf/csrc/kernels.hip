@@ -431,6 +431,53 @@ __global__ void xent_fwd(const T* __restrict__ logits, const long long* __restri
   }
 }
 
+// one 256-thread block per row: a single online pass (running max, rescaled exp-sum) over
+// 4-byte bf16 pairs (rows of an even vocabulary are 4-byte aligned), then a (max, sum)
+// reduction across the block; the label's logit is read by thread 0
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mn));
+  m = mn;
+}
+
+__global__ void __launch_bounds__(256) xent_fwd_row_bf16(const bf16_t* __restrict__ logits,
+                                                         const long long* __restrict__ labels, int K,
+                                                         float* __restrict__ loss, float* __restrict__ lse) {
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const bf16_t* p = logits + (long long)row * K;
+  const uint32_t* p2 = reinterpret_cast<const uint32_t*>(p);
+  const int K2 = K >> 1;
+  float m = -INFINITY, s = 0.f;
+  for (int k = tid; k < K2; k += 256) {
+    const uint32_t w = p2[k];
+    const float a = __uint_as_float(w << 16), b = __uint_as_float(w & 0xffff0000u);
+    const float mx = fmaxf(a, b);
+    if (mx > m) {
+      s = (m == -INFINITY ? 0.f : s * __expf(m - mx));
+      m = mx;
+    }
+    s += __expf(a - m) + __expf(b - m);
+  }
+  if ((K & 1) && tid == 0) lse_merge(m, s, bf2f(p[K - 1]), 1.f);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lse_merge(m, s, __shfl_xor(m, o, 64), __shfl_xor(s, o, 64));
+  __shared__ float sm[4], ss[4];
+  if ((tid & 63) == 0) {
+    sm[tid >> 6] = m;
+    ss[tid >> 6] = s;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float M = sm[0], S = ss[0];
+    for (int w = 1; w < 4; ++w) lse_merge(M, S, sm[w], ss[w]);
+    const float l = M + __logf(S);
+    const long long lab = labels[row];
+    const float xl = (lab >= 0 && lab < K) ? bf2f(p[lab]) : 0.f;
+    lse[row] = l;
+    loss[row] = l - xl;
+  }
+}
+
 template <typename T>
 __global__ void xent_bwd(const T* __restrict__ logits, const long long* __restrict__ labels,
                          const float* __restrict__ lse, const float* __restrict__ dloss, T* __restrict__ dlogits,
@@ -672,7 +719,9 @@ MDTF_EXPORT int mdtf_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hip
 MDTF_EXPORT int mdtf_xent_fwd(const void* logits, int is_bf16, const long long* labels, int N, int K, float* loss,
                               float* lse, hipStream_t st) {
   dim3 grid(ceil_div(N, 4));
-  if (is_bf16)
+  if (is_bf16 && K >= 2048 && (reinterpret_cast<uintptr_t>(logits) & 3) == 0 && (K & 1) == 0)
+    hipLaunchKernelGGL(xent_fwd_row_bf16, dim3(N), dim3(256), 0, st, (const bf16_t*)logits, labels, K, loss, lse);
+  else if (is_bf16)
     hipLaunchKernelGGL(xent_fwd<bf16_t>, grid, dim3(kT), 0, st, (const bf16_t*)logits, labels, N, K, loss, lse);
   else
     hipLaunchKernelGGL(xent_fwd<float>, grid, dim3(kT), 0, st, (const float*)logits, labels, N, K, loss, lse);

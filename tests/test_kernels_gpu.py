@@ -100,11 +100,13 @@ def test_global_avg_pool():
     assert _rel(xg.grad, xc.grad) < 1e-2
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_softmax_xent(dtype):
+@pytest.mark.parametrize("dtype,N,K", [(torch.bfloat16, 37, 1000), (torch.float32, 37, 1000),
+                                       (torch.bfloat16, 300, 30522), (torch.bfloat16, 5, 4096)])
+def test_softmax_xent(dtype, N, K):
+    """K >= 2048 bf16 rows take the one-block-per-row online-softmax kernel."""
     torch.manual_seed(2)
-    logits = torch.randn(37, 1000) * 3
-    labels = torch.randint(0, 1000, (37,))
+    logits = torch.randn(N, K) * 3
+    labels = torch.randint(0, K, (N,))
     lg = logits.to(DEV).to(dtype).requires_grad_(True)
     lc = logits.to(dtype).float().requires_grad_(True)
     l = ops.sparse_softmax_cross_entropy_with_logits(labels.to(DEV), lg)
