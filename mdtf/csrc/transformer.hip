@@ -90,9 +90,15 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const bf16_t* __restrict__ x
     const int c = (lane + i * 64);
     if (c < nvec) {
       if (s_out) store_bf8(s_out + row * H + c * 8, v[i]);
+      const float4 g0 = *reinterpret_cast<const float4*>(gamma + c * 8);
+      const float4 g1 = *reinterpret_cast<const float4*>(gamma + c * 8 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(beta + c * 8);
+      const float4 b1 = *reinterpret_cast<const float4*>(beta + c * 8 + 4);
+      const float gk[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bk[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
       float o[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = (v[i][k] - mean) * rstd * gamma[c * 8 + k] + beta[c * 8 + k];
+      for (int k = 0; k < 8; ++k) o[k] = (v[i][k] - mean) * rstd * gk[k] + bk[k];
       store_bf8(y + row * H + c * 8, o);
     }
   }
@@ -121,7 +127,29 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
     for (int k = 0; k < 8; ++k) dg[i][k] = db[i][k] = 0.f;
   const long long r0 = (long long)blockIdx.x * rows_per_block;
   const long long r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
-  for (long long row = r0 + wave; row < r1; row += kT / 64) {
+  // gamma in registers for the whole block
+  float gm[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    if (c < nvec) {
+      const float4 g0 = *reinterpret_cast<const float4*>(gamma + c * 8);
+      const float4 g1 = *reinterpret_cast<const float4*>(gamma + c * 8 + 4);
+      gm[i][0] = g0.x; gm[i][1] = g0.y; gm[i][2] = g0.z; gm[i][3] = g0.w;
+      gm[i][4] = g1.x; gm[i][5] = g1.y; gm[i][6] = g1.z; gm[i][7] = g1.w;
+    }
+  }
+  auto load_row = [&](long long row, uint4 (&gr)[NV], uint4 (&sr)[NV]) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + i * 64;
+      if (c < nvec) {
+        gr[i] = *reinterpret_cast<const uint4*>(dy + row * H + c * 8);
+        sr[i] = *reinterpret_cast<const uint4*>(s + row * H + c * 8);
+      }
+    }
+  };
+  auto do_row = [&](long long row, const uint4 (&gr)[NV], const uint4 (&sr)[NV]) {
     const float mu = mean[row], rs = rstd[row];
     float g[NV][8], xh[NV][8];
     float a = 0.f, b = 0.f;
@@ -129,15 +157,16 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
     for (int i = 0; i < NV; ++i) {
       const int c = lane + i * 64;
       if (c < nvec) {
-        float sv[8];
-        load_bf8(dy + row * H + c * 8, g[i]);
-        load_bf8(s + row * H + c * 8, sv);
+        const uint32_t gw[4] = {gr[i].x, gr[i].y, gr[i].z, gr[i].w};
+        const uint32_t sw[4] = {sr[i].x, sr[i].y, sr[i].z, sr[i].w};
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          xh[i][k] = (sv[k] - mu) * rs;
+          g[i][k] = __uint_as_float(k & 1 ? gw[k >> 1] & 0xffff0000u : gw[k >> 1] << 16);
+          const float sv = __uint_as_float(k & 1 ? sw[k >> 1] & 0xffff0000u : sw[k >> 1] << 16);
+          xh[i][k] = (sv - mu) * rs;
           dg[i][k] += g[i][k] * xh[i][k];
           db[i][k] += g[i][k];
-          const float gg = g[i][k] * gamma[c * 8 + k];
+          const float gg = g[i][k] * gm[i][k];
           a += gg;
           b += gg * xh[i][k];
         }
@@ -151,7 +180,7 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
       if (c < nvec) {
         float o[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = rs * (g[i][k] * gamma[c * 8 + k] - a - xh[i][k] * b);
+        for (int k = 0; k < 8; ++k) o[k] = rs * (g[i][k] * gm[i][k] - a - xh[i][k] * b);
         store_bf8(dx + row * H + c * 8, o);
         if (dx_branch) {     // gradient of the dropped-out branch input
 #pragma unroll
@@ -161,6 +190,16 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
         }
       }
     }
+  };
+  // two rows per wave per iteration, both rows' loads in flight before either is reduced
+  constexpr int W = kT / 64;
+  for (long long row = r0 + wave; row < r1; row += 2 * W) {
+    uint4 ga[NV], sa[NV], gb[NV], sb[NV];
+    const bool two = row + W < r1;
+    load_row(row, ga, sa);
+    if (two) load_row(row + W, gb, sb);
+    do_row(row, ga, sa);
+    if (two) do_row(row + W, gb, sb);
   }
   // combine the 4 waves through LDS; block partials -> ws[block][2][H] (plain stores)
   __shared__ float L[2][kT / 64][64 * 8];   // one 512-column slab per pass over NV
