@@ -79,12 +79,12 @@ __device__ __forceinline__ bool keep_elem(uint32_t seed, int bh, int q, int k, u
 }
 
 // DMA a [128 rows][64 cols] bf16 slice (row r at elements row0 + r * ld) into a 16 KiB image
-template <class SW>
+template <class SW, int NWV = 4>
 __device__ __forceinline__ void load_head(const bf16_t* t, int tbytes, long long row0, int ld, char* img, int wave,
                                           int lane) {
 #pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    const int j = wave + 4 * jj;                  // 8-row block
+  for (int jj = 0; jj < 16 / NWV; ++jj) {
+    const int j = wave + NWV * jj;                // 8-row block
     const int r = 8 * j + (lane >> 3);
     const int c = SW::f(r, lane & 7);             // logical chunk this lane's LDS slot holds
     const unsigned voff = (unsigned)((row0 + (long long)r * ld + c * 8) * 2);
@@ -273,11 +273,16 @@ __global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__
 // ============================================================================ backward
 constexpr int kBwdLds = 5 * S * D * 2 + 2 * S * S * 2;   // K_A V_A K_T Q_T dO_T | P dS  = 144 KiB
 
-__global__ void __launch_bounds__(NT) attn_bwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+// BW waves per workgroup (8: 16 queries / keys per wave; twice the waves per CU of the 4-wave
+// version at the same 144 KiB of LDS, which allows one workgroup per CU)
+template <int BW>
+__global__ void __launch_bounds__(64 * BW) attn_bwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                                                       const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
                                                       const float* __restrict__ lse, bf16_t* __restrict__ dqkv, int B,
                                                       int nh, float scale, float p_drop, uint32_t seed,
                                                       const long long* __restrict__ seed_off) {
+  constexpr int QPW = S / BW, NQT = QPW / 16;     // rows per wave, 16-row tiles per wave
+  static_assert(NQT >= 1 && NQT * 16 * BW == S, "waves");
   seed = step_seed(seed, seed_off);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* KA = smem;
@@ -297,18 +302,18 @@ __global__ void __launch_bounds__(NT) attn_bwd_kernel(const bf16_t* __restrict__
   const int tbytes = (int)((long long)B * S * ld * 2);
   const int obytes = (int)((long long)B * S * H * 2);
 
-  load_head<SwzA>(qkv, tbytes, row0 + H + h * D, ld, KA, wave, lane);
-  load_head<SwzA>(qkv, tbytes, row0 + 2 * H + h * D, ld, VA, wave, lane);
-  load_head<SwzT>(qkv, tbytes, row0 + H + h * D, ld, KT, wave, lane);
-  load_head<SwzT>(qkv, tbytes, row0 + h * D, ld, QT, wave, lane);
-  load_head<SwzT>(dout, obytes, orow0 + h * D, H, OT, wave, lane);
+  load_head<SwzA, BW>(qkv, tbytes, row0 + H + h * D, ld, KA, wave, lane);
+  load_head<SwzA, BW>(qkv, tbytes, row0 + 2 * H + h * D, ld, VA, wave, lane);
+  load_head<SwzT, BW>(qkv, tbytes, row0 + H + h * D, ld, KT, wave, lane);
+  load_head<SwzT, BW>(qkv, tbytes, row0 + h * D, ld, QT, wave, lane);
+  load_head<SwzT, BW>(dout, obytes, orow0 + h * D, H, OT, wave, lane);
 
   // phase-1 register operands: Q and dO fragments (B operands), D = rowsum(dO * O), lse, mask
-  bf16x8_t qf[2][2], of[2][2];
-  float Dq[2], lq[2];
+  bf16x8_t qf[NQT][2], of[NQT][2];
+  float Dq[NQT], lq[NQT];
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = 32 * wave + 16 * qt + li;
+  for (int qt = 0; qt < NQT; ++qt) {
+    const int q = QPW * wave + 16 * qt + li;
     float part = 0.f;
 #pragma unroll
     for (int ds = 0; ds < 2; ++ds) {
@@ -346,11 +351,11 @@ __global__ void __launch_bounds__(NT) attn_bwd_kernel(const bf16_t* __restrict__
   const uint32_t thr = p_drop > 0.f ? (uint32_t)fminf(p_drop * 4294967296.f, 4294967295.f) : 0u;
   const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   {
-    float4v sacc[8][2], pacc[8][2];
+    float4v sacc[8][NQT], pacc[8][NQT];
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) sacc[kt][qt] = pacc[kt][qt] = float4v{0.f, 0.f, 0.f, 0.f};
+      for (int qt = 0; qt < NQT; ++qt) sacc[kt][qt] = pacc[kt][qt] = float4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ds = 0; ds < 2; ++ds)
 #pragma unroll
@@ -358,14 +363,14 @@ __global__ void __launch_bounds__(NT) attn_bwd_kernel(const bf16_t* __restrict__
         const bf16x8_t kf = row_frag<SwzA>(KA, kt * 16, 4 * ds, lane);
         const bf16x8_t vf = row_frag<SwzA>(VA, kt * 16, 4 * ds, lane);
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
+        for (int qt = 0; qt < NQT; ++qt) {
           sacc[kt][qt] = mfma(kf, qf[qt][ds], sacc[kt][qt]);
           pacc[kt][qt] = mfma(vf, of[qt][ds], pacc[kt][qt]);
         }
       }
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int q = 32 * wave + 16 * qt + li;
+    for (int qt = 0; qt < NQT; ++qt) {
+      const int q = QPW * wave + 16 * qt + li;
 #pragma unroll
       for (int kt = 0; kt < 8; ++kt) {
         float pd[4], dsv[4];
@@ -394,33 +399,33 @@ __global__ void __launch_bounds__(NT) attn_bwd_kernel(const bf16_t* __restrict__
 
   // ---- phase 2a: dV^T[d][k] = dO^T P_drop, dK^T[d][k] = scale Q^T dS for keys 32w .. 32w+31
   {
-    float4v vacc[4][2], kacc[4][2];
+    float4v vacc[4][NQT], kacc[4][NQT];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) vacc[dt][kt] = kacc[dt][kt] = float4v{0.f, 0.f, 0.f, 0.f};
+      for (int kt = 0; kt < NQT; ++kt) vacc[dt][kt] = kacc[dt][kt] = float4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {          // 32 queries per step
-      bf16x8_t pf[2], sf[2];
+      bf16x8_t pf[NQT], sf[NQT];
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        pf[kt] = tr_frag<Swz256, 256>(PI, 32 * ks, 32 * wave + 16 * kt, lane);
-        sf[kt] = tr_frag<Swz256, 256>(SI, 32 * ks, 32 * wave + 16 * kt, lane);
+      for (int kt = 0; kt < NQT; ++kt) {
+        pf[kt] = tr_frag<Swz256, 256>(PI, 32 * ks, QPW * wave + 16 * kt, lane);
+        sf[kt] = tr_frag<Swz256, 256>(SI, 32 * ks, QPW * wave + 16 * kt, lane);
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const bf16x8_t df = tr_frag<SwzT, 128>(OT, 32 * ks, dt * 16, lane);
         const bf16x8_t qq = tr_frag<SwzT, 128>(QT, 32 * ks, dt * 16, lane);
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
+        for (int kt = 0; kt < NQT; ++kt) {
           vacc[dt][kt] = mfma(df, pf[kt], vacc[dt][kt]);
           kacc[dt][kt] = mfma(qq, sf[kt], kacc[dt][kt]);
         }
       }
     }
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const int k = 32 * wave + 16 * kt + li;
+    for (int kt = 0; kt < NQT; ++kt) {
+      const int k = QPW * wave + 16 * kt + li;
       bf16_t* rowp = dqkv + row0 + (long long)k * ld + h * D;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -434,26 +439,26 @@ __global__ void __launch_bounds__(NT) attn_bwd_kernel(const bf16_t* __restrict__
   }
   // ---- phase 2b: dQ^T[d][q] = scale K^T dS^T for this wave's queries
   {
-    float4v qacc[4][2];
+    float4v qacc[4][NQT];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) qacc[dt][qt] = float4v{0.f, 0.f, 0.f, 0.f};
+      for (int qt = 0; qt < NQT; ++qt) qacc[dt][qt] = float4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {          // 32 keys per step
-      bf16x8_t sf[2];
+      bf16x8_t sf[NQT];
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) sf[qt] = row_frag256<Swz256>(SI, 32 * wave + 16 * qt, 4 * ks, lane);
+      for (int qt = 0; qt < NQT; ++qt) sf[qt] = row_frag256<Swz256>(SI, QPW * wave + 16 * qt, 4 * ks, lane);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const bf16x8_t kf = tr_frag<SwzT, 128>(KT, 32 * ks, dt * 16, lane);
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) qacc[dt][qt] = mfma(kf, sf[qt], qacc[dt][qt]);
+        for (int qt = 0; qt < NQT; ++qt) qacc[dt][qt] = mfma(kf, sf[qt], qacc[dt][qt]);
       }
     }
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int q = 32 * wave + 16 * qt + li;
+    for (int qt = 0; qt < NQT; ++qt) {
+      const int q = QPW * wave + 16 * qt + li;
       bf16_t* rowp = dqkv + row0 + (long long)q * ld + h * D;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -485,7 +490,19 @@ MDTF_EXPORT int mdtf_attn_bwd(const void* qkv, const float* mask, const void* ou
                               const long long* seed_off, hipStream_t st) {
   if (seq != S || dh != D) return MDTF_EUNSUPPORTED;
   if ((long long)B * S * 3 * nh * D * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(B * nh), dim3(NT), kBwdLds, st, (const bf16_t*)qkv, mask,
+  // MDTF_ATTN_BWD_WAVES=4: the 4-wave workgroup (A/B switch)
+  static const bool w4 = [] {
+    const char* e = getenv("MDTF_ATTN_BWD_WAVES");
+    return e && e[0] == '4';
+  }();
+  if (w4) {
+    hipLaunchKernelGGL(attn_bwd_kernel<4>, dim3(B * nh), dim3(256), kBwdLds, st, (const bf16_t*)qkv, mask,
+                       (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv, B, nh, scale, p_drop,
+                       (uint32_t)seed, seed_off);
+    MDTF_LAUNCH_CHECK();
+    return 0;
+  }
+  hipLaunchKernelGGL(attn_bwd_kernel<8>, dim3(B * nh), dim3(512), kBwdLds, st, (const bf16_t*)qkv, mask,
                      (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv, B, nh, scale, p_drop,
                      (uint32_t)seed, seed_off);
   MDTF_LAUNCH_CHECK();
