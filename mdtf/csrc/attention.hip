@@ -134,7 +134,10 @@ __device__ __forceinline__ bf16x8_t load_frag_global(const bf16_t* p) {
 }
 
 // ============================================================================ forward
-__global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+// MINW: minimum waves per SIMD the register allocation must allow (2: at most 256 registers, so
+// two 4-wave workgroups share a CU; 1: the allocator may use up to 512)
+template <int MINW>
+__global__ void __launch_bounds__(NT, MINW) attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                                                       bf16_t* __restrict__ out, float* __restrict__ lse_out, int B,
                                                       int nh, float scale, float p_drop, uint32_t seed,
                                                       const long long* __restrict__ seed_off) {
@@ -478,8 +481,17 @@ MDTF_EXPORT int mdtf_attn_fwd(const void* qkv, const float* mask, void* out, flo
                               hipStream_t st) {
   if (seq != S || dh != D) return MDTF_EUNSUPPORTED;
   if ((long long)B * S * 3 * nh * D * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * nh), dim3(NT), 0, st, (const bf16_t*)qkv, mask, (bf16_t*)out, lse, B,
-                     nh, scale, p_drop, (uint32_t)seed, seed_off);
+  // MDTF_ATTN_FWD_MINW=1: no register cap (A/B switch)
+  static const bool w1 = [] {
+    const char* e = getenv("MDTF_ATTN_FWD_MINW");
+    return e && e[0] == '1';
+  }();
+  if (w1)
+    hipLaunchKernelGGL(attn_fwd_kernel<1>, dim3(B * nh), dim3(NT), 0, st, (const bf16_t*)qkv, mask, (bf16_t*)out, lse,
+                       B, nh, scale, p_drop, (uint32_t)seed, seed_off);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<2>, dim3(B * nh), dim3(NT), 0, st, (const bf16_t*)qkv, mask, (bf16_t*)out, lse,
+                       B, nh, scale, p_drop, (uint32_t)seed, seed_off);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
