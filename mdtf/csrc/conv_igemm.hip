@@ -942,8 +942,17 @@ __device__ __forceinline__ bf16x8_t frag_tr(const char* img, int col0, int kbase
   return __builtin_bit_cast(bf16x8_t, f);
 }
 
+// register budget: as many waves per SIMD as the LDS ring lets blocks be resident
+template <int BM, int BN, int STAGES, int NW>
+constexpr int wgrad_min_waves() {
+  constexpr int blocks = (160 * 1024) / (STAGES * (BM + BN) * 128);
+  constexpr int w = blocks * NW / 4;
+  return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
+
 template <int BM, int BN, int STAGES, int NW, bool PIPE>
-__global__ void __launch_bounds__(64 * NW) conv_wgrad_v2(ConvArgs a) {
+__global__ void __launch_bounds__(64 * NW, (wgrad_min_waves<BM, BN, STAGES, NW>()))
+    conv_wgrad_v2(ConvArgs a) {
   // NW = 4 (2x2 waves) or 8 (one 256-row/col block per CU, 4x2 or 2x4 waves by aspect)
   constexpr int WM = NW == 4 ? 2 : (BM > BN ? 4 : 2), WN = NW / WM;
   constexpr int U = 8 / NW;                       // 8-row DMA blocks per wave per 64-pixel step

@@ -22,7 +22,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(os.path.dirname(_HERE), "csrc", "build")
-LIB_PATH = os.path.join(LIB_DIR, "libmdtf_kernels.so")
+# MDTF_KERNELS_LIB: load another build of the kernel library (A/B of two builds on one box)
+LIB_PATH = os.environ.get("MDTF_KERNELS_LIB") or os.path.join(LIB_DIR, "libmdtf_kernels.so")
 
 _lib = None
 _load_error = None
