@@ -21,6 +21,7 @@ import torch
 
 from . import _native as N
 from . import kernels
+from . import tunable
 from ..train import variables as V
 
 _ACT = {None: 0, "relu": 1, "gelu": 2}
@@ -110,6 +111,7 @@ class _Dense(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, act, trans, nw, x_sink, x_shape, *wb):
+        tunable.ensure(x.device)
         ws, bs = wb[:nw], wb[nw:]
         w = ws[0] if nw == 1 else torch.cat(ws, 1)
         if trans:

@@ -1,0 +1,45 @@
+"""Pre-tuned hipBLASLt / rocBLAS solution choices for the library GEMMs (PyTorch TunableOp).
+
+The dense layers' plain GEMMs (BERT's QKV / output / FFN projections, the tied MLM decoder) go to
+the vendor libraries through ``torch.mm`` / ``torch.addmm``.  The library heuristics do not pick
+the fastest solution for every shape. ``tunableop_gfx950.csv`` holds the choices timed on an
+MI355X with this image's PyTorch / HIP / hipBLASLt / rocBLAS (``scripts/gpu_tunableop.sh``).
+They are loaded read-only before the first GEMM, so a captured step graph replays the tuned
+kernels (BERT-base: +3.5% seq/s in an alternating A/B).
+
+The file's validator rows (library versions, GPU arch) are checked by PyTorch; shapes that are not
+in the file keep the default heuristic.  ``MDTF_TUNABLEOP=0`` turns this off; a user's own
+``PYTORCH_TUNABLEOP_*`` settings take precedence.
+"""
+import os
+import tempfile
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+TABLE = os.path.join(_HERE, "tunableop_gfx950.csv")
+_done = set()
+
+
+def ensure(device):
+    """Load the tuned GEMM table once per process (no-op off gfx950 / on CPU / when disabled)."""
+    if device.type != "cuda" or "loaded" in _done or "skip" in _done:
+        return "loaded" in _done
+    if (os.environ.get("MDTF_TUNABLEOP", "1") in ("0", "", "false")
+            or any(k.startswith("PYTORCH_TUNABLEOP") for k in os.environ) or not os.path.exists(TABLE)):
+        _done.add("skip")
+        return False
+    arch = getattr(torch.cuda.get_device_properties(device), "gcnArchName", "")
+    if not arch.startswith("gfx950"):
+        _done.add("skip")
+        return False
+    import torch.cuda.tunable as T
+    T.enable(True)
+    T.tuning_enable(False)
+    # anything the runtime writes back goes to a scratch file, never over the shipped table
+    T.set_filename(os.path.join(tempfile.gettempdir(), "mdtf_tunableop_%d.csv" % os.getpid()))
+    ok = T.read_file(TABLE)
+    _done.add("loaded" if ok else "skip")
+    if not ok:
+        T.enable(False)
+    return bool(ok)
