@@ -191,15 +191,16 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
       }
     }
   };
-  // two rows per wave per iteration, both rows' loads in flight before either is reduced
-  constexpr int W = kT / 64;
-  for (long long row = r0 + wave; row < r1; row += 2 * W) {
-    uint4 ga[NV], sa[NV], gb[NV], sb[NV];
-    const bool two = row + W < r1;
-    load_row(row, ga, sa);
-    if (two) load_row(row + W, gb, sb);
-    do_row(row, ga, sa);
-    if (two) do_row(row + W, gb, sb);
+  // RIF rows per wave per iteration, all their loads in flight before the first is reduced
+  constexpr int W = kT / 64, RIF = NV <= 2 ? 4 : 1;
+  for (long long row = r0 + wave; row < r1; row += RIF * W) {
+    uint4 gr[RIF][NV], sr[RIF][NV];
+#pragma unroll
+    for (int j = 0; j < RIF; ++j)
+      if (row + j * W < r1) load_row(row + j * W, gr[j], sr[j]);
+#pragma unroll
+    for (int j = 0; j < RIF; ++j)
+      if (row + j * W < r1) do_row(row + j * W, gr[j], sr[j]);
   }
   // combine the 4 waves through LDS; block partials -> ws[block][2][H] (plain stores)
   __shared__ float L[2][kT / 64][64 * 8];   // one 512-column slab per pass over NV
@@ -376,8 +377,8 @@ extern "C" int mdtf_reduce_partials(const float* ws, int B, int C, float* out, h
 extern "C" int mdtf_reduce_partials_strided(const float* ws, int B, int C, long long ld, float* out, hipStream_t st);
 
 static void ln_bwd_geometry(long long rows, int* blocks, int* rpb) {
-  long long b = ceil_div(rows, 8);          // >= 2 rows per wave
-  if (b > 1024) b = 1024;
+  long long b = ceil_div(rows, 16);         // >= 4 rows per wave (all in flight together)
+  if (b > 512) b = 512;
   if (b < 1) b = 1;
   *rpb = static_cast<int>(ceil_div(rows, b));
   *blocks = static_cast<int>(ceil_div(rows, *rpb));
