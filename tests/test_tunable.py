@@ -38,3 +38,17 @@ def test_tuned_gemm_numerics():
     y = torch.addmm(b, x, w)                       # a shape the table covers
     ref = x.float() @ w.float() + b.float()
     assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
+def test_user_tunableop_settings_take_precedence(monkeypatch):
+    """A user's own PYTORCH_TUNABLEOP_* environment (or MDTF_TUNABLEOP=0) leaves TunableOp alone."""
+    class _Dev(object):
+        type = "cuda"
+    for env in ({"PYTORCH_TUNABLEOP_ENABLED": "1"}, {"MDTF_TUNABLEOP": "0"}):
+        monkeypatch.setattr(tunable, "_done", set())
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        assert tunable.ensure(_Dev()) is False
+        assert "skip" in tunable._done
+        for k in env:
+            monkeypatch.delenv(k)
