@@ -32,6 +32,8 @@ def parse():
     p.add_argument("--size", default="base")
     p.add_argument("--stock", action="store_true")
     p.add_argument("--hip_graph", type=int, default=1, help="capture the mdtf training step in a hipGraph")
+    p.add_argument("--trace_ops", default=None,
+                   help="after the warm-up, profile one step with Python stacks (use --hip_graph 0) into this dir")
     return p.parse_args()
 
 
@@ -145,6 +147,24 @@ def main():
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize()
+    if args.trace_ops and rank == 0:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+            run()
+            torch.cuda.synchronize()
+        os.makedirs(args.trace_ops, exist_ok=True)
+        with open(os.path.join(args.trace_ops, "ops_by_shape.txt"), "w") as f:
+            f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=80,
+                                                                       max_name_column_width=40,
+                                                                       max_shapes_column_width=80))
+        with open(os.path.join(args.trace_ops, "ops_parents.txt"), "w") as f:
+            for e in prof.events():
+                if e.name in ("aten::add_", "aten::add", "aten::fill_", "aten::copy_", "aten::cat"):
+                    chain, p = [], e.cpu_parent
+                    while p is not None and len(chain) < 4:
+                        chain.append(p.name)
+                        p = p.cpu_parent
+                    f.write("%s %s <- %s\n" % (e.name, str(e.input_shapes)[:80], " < ".join(chain)))
     if world > 1:
         dist.barrier(group=pg)
     t0 = time.perf_counter()

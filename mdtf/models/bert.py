@@ -17,6 +17,7 @@ input_mask | masked_lm_positions; ``ground_truth`` int64 ``[B, P + 1]`` =
 masked_lm_ids | next_sentence_label.
 """
 import math
+import os
 
 import torch
 
@@ -38,13 +39,20 @@ def _init(std=0.02):
     return V.truncated_normal_initializer(stddev=std)
 
 
+_DENSE_VIEW = os.environ.get("MDTF_BERT_DENSE_VIEW", "0") == "1"
+
+
 def _dense(name, x, out, act=None):
     with V.variable_scope(name):
         w = V.get_variable("kernel", [x.shape[-1], out], initializer=_init())
         b = V.get_variable("bias", [out], initializer=V.constant_initializer(0.0))
-    shp = x.shape
-    y = ops.dense(x.reshape(-1, shp[-1]), w, b, act=act)
-    return y.reshape(*shp[:-1], out)
+    # x goes in unreshaped: a reshaped view would hide the activation-gradient sink attached to a
+    # LayerNorm output, and autograd would then add this layer's dx to the residual's separately
+    # (MDTF_BERT_DENSE_VIEW=1 restores the view, for A/B runs)
+    if _DENSE_VIEW:
+        shp = x.shape
+        return ops.dense(x.reshape(-1, shp[-1]), w, b, act=act).reshape(*shp[:-1], out)
+    return ops.dense(x, w, b, act=act)
 
 
 def _ln(name, x, residual=None, eps=1e-12, dropout=0.0):
