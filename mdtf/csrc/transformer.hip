@@ -335,6 +335,39 @@ __global__ void embed_bwd_kernel(const bf16_t* __restrict__ dy, const long long*
   }
 }
 
+// Tiny tables (token types: 2 rows) would take ~n fp32 atomics per element on one or two rows.
+// Instead each block sums a run of kSmallTok tokens per (row, 8-column vector) in registers
+// (thread = vector) and adds its partials once.
+constexpr int kSmallVocab = 4, kSmallTok = 64;
+__global__ void embed_bwd_small_kernel(const bf16_t* __restrict__ dy, const long long* __restrict__ ids,
+                                       float* __restrict__ dtable, long long n, int H, int vocab) {
+  const int v8 = threadIdx.x;
+  if (v8 * 8 >= H) return;
+  const long long t0 = (long long)blockIdx.x * kSmallTok;
+  const long long t1 = t0 + kSmallTok < n ? t0 + kSmallTok : n;
+  float acc[kSmallVocab][8];
+#pragma unroll
+  for (int r = 0; r < kSmallVocab; ++r)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[r][k] = 0.f;
+  for (long long t = t0; t < t1; ++t) {
+    const long long id = ids[t];
+    if (id < 0 || id >= vocab) continue;
+    float g[8];
+    load_bf8(dy + t * H + v8 * 8, g);
+#pragma unroll
+    for (int r = 0; r < kSmallVocab; ++r)
+      if (r == id) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[r][k] += g[k];
+      }
+  }
+  for (int r = 0; r < vocab; ++r)
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (acc[r][k] != 0.f) atomicAdd(dtable + (long long)r * H + v8 * 8 + k, acc[r][k]);
+}
+
 inline int gcap(long long work) {
   long long b = ceil_div(work, kT);
   return static_cast<int>(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -447,6 +480,13 @@ MDTF_EXPORT int mdtf_embed_fwd(const void* table, const long long* ids, void* ou
 
 MDTF_EXPORT int mdtf_embed_bwd(const void* dy, const long long* ids, float* dtable, long long n, int H,
                                long long vocab, hipStream_t st) {
+  if (vocab <= kSmallVocab && H % 8 == 0 && H / 8 <= 1024 && n > 0) {
+    const int threads = static_cast<int>(ceil_div(H / 8, 64) * 64);
+    hipLaunchKernelGGL(embed_bwd_small_kernel, dim3((unsigned)ceil_div(n, kSmallTok)), dim3(threads), 0, st,
+                       (const bf16_t*)dy, ids, dtable, n, H, static_cast<int>(vocab));
+    MDTF_LAUNCH_CHECK();
+    return 0;
+  }
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(gcap(n * H)), dim3(kT), 0, st, (const bf16_t*)dy, ids, dtable, n, H,
                      vocab);
   MDTF_LAUNCH_CHECK();

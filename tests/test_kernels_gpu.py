@@ -473,16 +473,18 @@ def test_masked_softmax_kernel(cols):
     assert _rel(outs[DEV][1], outs["cpu"][1]) < 2e-2
 
 
-def test_embedding_kernel():
+@pytest.mark.parametrize("vocab,B,S,H", [(100, 7, 9, 64), (2, 64, 128, 768), (3, 5, 33, 1024)])
+def test_embedding_kernel(vocab, B, S, H):
+    """vocab <= 4 (token types) takes the per-block partial-sum backward instead of per-element atomics."""
     from mdtf.ops import transformer as T
     torch.manual_seed(13)
-    table = torch.randn(100, 64)
-    ids = torch.randint(0, 100, (7, 9))
+    table = torch.randn(vocab, H)
+    ids = torch.randint(0, vocab, (B, S))
     outs = {}
     for dev, dt in ((DEV, torch.bfloat16), ("cpu", torch.float32)):
         tt = table.to(dev).to(dt).requires_grad_(True)
         y = T.embedding_lookup(tt, ids.to(dev))
-        y.backward(torch.randn(7, 9, 64, generator=torch.Generator().manual_seed(4)).to(dev).to(dt))
+        y.backward(torch.randn(B, S, H, generator=torch.Generator().manual_seed(4)).to(dev).to(dt))
         outs[dev] = (y.detach(), tt.grad)
     assert _rel(outs[DEV][0], outs["cpu"][0]) < 1e-2
     assert _rel(outs[DEV][1], outs["cpu"][1]) < 2e-2
