@@ -34,6 +34,7 @@ Enable with ``MDTF_HIP_GRAPH=1``, ``--hip_graph`` (FLAGS) or
 ``SyncReplicasOptimizer(..., hip_graph=True)``.
 """
 import os
+import time
 
 import torch
 
@@ -52,6 +53,19 @@ def rng_offset_tensor(device):
         t = torch.zeros(1, dtype=torch.int64, device=device)
         _RNG[key] = t
     return t
+
+
+def _drain_comm_watchdog():
+    """Let the RCCL process group's watchdog thread retire the (completed) work of the eager warm-up
+    steps before capture begins.  It polls every ~100 ms and queries each work's completion event;
+    a query that lands while this thread is capturing races the capture, which intermittently aborted
+    the process in the RCCL capture test.  Capture happens once per step graph, so the wait is paid once."""
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+            time.sleep(0.5)
+    except (RuntimeError, ValueError):
+        pass
 
 
 def _leaves(x, out):
@@ -243,6 +257,7 @@ class StepGraph(object):
         cap_ctx = RunContext(feed_dict=fd, session=ctx.session)
         cap_ctx.cache.update(cache)
         torch.cuda.synchronize(dev)
+        _drain_comm_watchdog()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             rng.add_(1)
