@@ -47,8 +47,20 @@ def parse():
     return p.parse_args()
 
 
+def _ensure_ranks(args):
+    """--gpus N is honoured: under torchrun WORLD_SIZE must equal N, otherwise N ranks are spawned
+    (mdtf/utils/launch.py; loaded by path so nothing imports torch or touches the GPU first)."""
+    import importlib.util
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("_mdtf_launch", os.path.join(here, "mdtf", "utils", "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod.ensure_ranks(args.gpus, os.path.abspath(__file__))
+
+
 def main():
     args = parse()
+    _ensure_ranks(args)
     if args.kernels:
         os.environ["MDTF_KERNELS"] = args.kernels
     import torch
@@ -130,7 +142,8 @@ def main():
         base_ips = BASELINE_IMAGES_PER_SEC_PER_GPU
         rec = {
             "metric": "images/sec (whole node) ResNet-50 sync-SGD at 1/2/4/8 MI355X; scaling efficiency",
-            "value": round(ips, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+            "value": round(ips, 2), "unit": "images/sec", "n_gpus": world,
+            "per_gpu_images_per_sec": round(ips / world, 2), "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(ips / (base_ips * world), 4) if base_ips else None,
@@ -142,7 +155,7 @@ def main():
                        "per_gpu_batch": args.batch, "image_size": args.image_size, "parallelism": "dp%d" % world,
                        "grad_sync": args.mode, "optimizer": "momentum-sgd (fused)",
                        "kernels": os.environ.get("MDTF_KERNELS", "native"),
-                       "hip_graph": bool(args.hip_graph)},
+                       "hip_graph": bool(args.hip_graph) and dev.type == "cuda"},
             "loss_first": float(lv), "loss_last": final_loss,
         }
         print(json.dumps(rec), flush=True)

@@ -31,6 +31,7 @@ def parse():
     p.add_argument("--seq", type=int, default=128)
     p.add_argument("--size", default="base")
     p.add_argument("--stock", action="store_true")
+    p.add_argument("--mode", default="allreduce", choices=["allreduce", "sharded"])
     p.add_argument("--hip_graph", type=int, default=1, help="capture the mdtf training step in a hipGraph")
     p.add_argument("--trace_ops", default=None,
                    help="after the warm-up, profile one step with Python stacks (use --hip_graph 0) into this dir")
@@ -86,6 +87,8 @@ class StockBert(nn.Module):
 
 def main():
     args = parse()
+    from mdtf.utils.launch import ensure_ranks
+    ensure_ranks(args.gpus, os.path.abspath(__file__))     # --gpus N: N ranks or a non-zero exit
     distributed = int(os.environ.get("WORLD_SIZE", "1")) > 1
     if distributed:
         from mdtf.cluster import Server
@@ -95,8 +98,12 @@ def main():
     else:
         server, rank, world, pg = None, 0, 1, None
     lr = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", lr)
-    torch.cuda.set_device(dev)
+    gpu = torch.cuda.is_available()
+    dev = torch.device("cuda", lr) if gpu else torch.device("cpu")      # cpu: gloo rehearsal of the launch
+    if gpu:
+        torch.cuda.set_device(dev)
+    if args.stock and not gpu:
+        raise SystemExit("--stock needs a GPU")
     from mdtf.models import Bert, BertPretrainingLoss, SyntheticBertLoader
     from mdtf.models.bert import CONFIGS
     P = 20
@@ -129,7 +136,7 @@ def main():
         from mdtf.train import variables as V
         store = V.get_store()
         store.device = dev
-        store.compute_dtype = torch.bfloat16
+        store.compute_dtype = torch.bfloat16 if gpu else None
         ld = SyntheticBertLoader(args.seq, P, seed=rank)
         ld.batch_size = args.batch
         raw, gt = ld.load_train_batch()
@@ -138,15 +145,20 @@ def main():
         tower = Tower(Net(Bert(args.size, seq_len=args.seq, max_predictions=P)), "tower_0/", tg, raw, gt,
                       BertPretrainingLoss(P), base, batch_size=args.batch)
         _, loss_h, _ = tower.process()
-        opt = mdtf.train.SyncReplicasOptimizer(base, world, world, hip_graph=bool(args.hip_graph))
+        opt = mdtf.train.SyncReplicasOptimizer(base, world, world, hip_graph=bool(args.hip_graph) and gpu,
+                                               mode=args.mode)
         op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
         sess = mdtf.train.MonitoredTrainingSession(is_chief=rank == 0, log_step_count_steps=0, server=server)
 
         def run():
             sess.run(op)
+    def sync():
+        if gpu:
+            torch.cuda.synchronize()
+
     for _ in range(args.warmup):
         run()
-    torch.cuda.synchronize()
+    sync()
     if args.trace_ops and rank == 0:
         from torch.profiler import ProfilerActivity, profile
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
@@ -167,10 +179,11 @@ def main():
                     f.write("%s %s <- %s\n" % (e.name, str(e.input_shapes)[:80], " < ".join(chain)))
     if world > 1:
         dist.barrier(group=pg)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier(group=pg)
     el = torch.tensor([time.perf_counter() - t0], device=dev)
@@ -178,12 +191,30 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX, group=pg)
     el = float(el)
     if rank == 0:
+        sps = world * args.batch * args.steps / el
         print(json.dumps({"metric": "sequences/sec BERT-%s pretraining seq%d" % (args.size, args.seq),
-                          "value": round(world * args.batch * args.steps / el, 2), "unit": "sequences/sec",
-                          "n_gpus": world, "ms_per_step": round(1000 * el / args.steps, 3),
-                          "per_gpu_batch": args.batch, "impl": "stock-pytorch" if args.stock else "mdtf",
-                          "hip_graph": bool(args.hip_graph) and not args.stock,
-                          "dtype": "bf16", "data": "synthetic"}), flush=True)
+                          "value": round(sps, 2), "unit": "sequences/sec", "n_gpus": world,
+                          "per_gpu_sequences_per_sec": round(sps / world, 2), "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3),
+                          "higher_is_better": True, "scaling": "weak",
+                          "impl": "stock-pytorch" if args.stock else "mdtf",
+                          "hip_graph": bool(args.hip_graph) and not args.stock and gpu,
+                          "dtype": "bf16" if gpu else "fp32",
+                          "data": "synthetic (random token ids, random-init weights)",
+                          "config": {"model": "bert-%s" % args.size, "global_batch": world * args.batch,
+                                     "per_gpu_batch": args.batch, "seq_len": args.seq,
+                                     "parallelism": "dp%d" % world,
+                                     "grad_sync": "ddp" if args.stock else args.mode,
+                                     "optimizer": "torch AdamW" if args.stock else "AdamWeightDecay (fused)"}}),
+              flush=True)
+    if not args.stock:
+        sess.close()
+    if distributed:
+        from mdtf.train import step as S_
+        S_.release_graphs()
+        dist.barrier(group=pg)
+        server.shutdown()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

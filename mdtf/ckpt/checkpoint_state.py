@@ -15,8 +15,12 @@ def _q(s):
 
 
 def write_state(directory, model_checkpoint_path, all_paths):
+    # TF convention: paths are stored relative to the save directory, whether the caller passed
+    # them relative to the working directory ("ck/model.ckpt-1") or absolute.
+    base = os.path.abspath(directory)
+
     def rel(p):
-        return os.path.relpath(p, directory) if os.path.isabs(p) else p
+        return os.path.relpath(os.path.abspath(p), base)
     lines = ["model_checkpoint_path: %s" % _q(rel(model_checkpoint_path))]
     lines += ["all_model_checkpoint_paths: %s" % _q(rel(p)) for p in all_paths]
     tmp = os.path.join(directory, STATE_FILE + ".tmp")

@@ -134,6 +134,9 @@ class Server(object):
             self.job_name, self.task_index, "/%d" % self.local_rank if self.layout.gpu_num > 1 else ""))
         # surface RCCL errors / dead peers as exceptions instead of silent hangs
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        # flight recorder on: hipGraph capture waits until the RCCL watchdog has retired every eager
+        # work (train/graph.py _drain_comm_watchdog reads the recorder's active entries)
+        os.environ.setdefault("TORCH_FR_BUFFER_SIZE", "2000")
         timeout = datetime.timedelta(seconds=self.store_timeout_s)
         if self._torchrun:
             backend = self.backend or ("nccl" if torch.cuda.is_available() else "gloo")

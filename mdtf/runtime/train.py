@@ -121,14 +121,10 @@ class Train(object):
         fault = FaultInjectionHook.from_env(self.job_name, self.task_index)
         if fault is not None:
             hooks.append(fault)
-        ckpt_kwargs = {}
-        if ps_mode == "sharded" and num_replicas > 1 and self.model_dir:
-            # collective save: every replica runs the checkpoint hook on the same steps
-            hooks.append(H.CheckpointSaverHook(self.model_dir, save_steps=save_steps or 1000))
-            ckpt_kwargs = dict(save_checkpoint_secs=None, save_checkpoint_steps=None)
-        else:
-            ckpt_kwargs = dict(save_checkpoint_secs=save_secs if not save_steps else None,
-                               save_checkpoint_steps=save_steps)
+        # sharded replicas save collectively: the session factory then puts a step-triggered
+        # checkpoint hook on every replica (session.MonitoredTrainingSession)
+        ckpt_kwargs = dict(save_checkpoint_secs=save_secs if not save_steps else None,
+                           save_checkpoint_steps=save_steps)
         with SESS.MonitoredTrainingSession(master=server.target, is_chief=is_chief,
                                            checkpoint_dir=self.model_dir or None,
                                            scaffold=SESS.Scaffold(init_op=SESS.global_variables_initializer(),

@@ -39,6 +39,7 @@ import time
 import torch
 
 _RNG = {}
+LAST_DRAIN = [None]     # how the last capture drained the RCCL watchdog: "recorder" | "fallback" (tests)
 
 
 def env_enabled():
@@ -55,17 +56,51 @@ def rng_offset_tensor(device):
     return t
 
 
-def _drain_comm_watchdog():
-    """Let the RCCL process group's watchdog thread retire the (completed) work of the eager warm-up
-    steps before capture begins.  It polls every ~100 ms and queries each work's completion event;
-    a query that lands while this thread is capturing races the capture, which intermittently aborted
-    the process in the RCCL capture test.  Capture happens once per step graph, so the wait is paid once."""
+def _active_comm_works():
+    """RCCL works the process groups' watchdog threads still hold (flight-recorder entries not yet
+    retired), or None when the recorder is unavailable or disabled."""
+    try:
+        import json
+        from torch._C._distributed_c10d import _dump_nccl_trace_json
+        d = json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=True))
+        every = json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=False))
+    except (ImportError, RuntimeError, ValueError, TypeError):
+        return None
+    if not every.get("entries"):
+        return None                       # recorder disabled (buffer size 0) or nothing ever issued
+    return len(d.get("entries", []))
+
+
+def _drain_comm_watchdog(timeout_s=60.0):
+    """Wait, on a state and not on a clock, until the RCCL watchdog has retired every eager work.
+
+    A ProcessGroupNCCL watchdog thread polls the completion event of each work issued OUTSIDE graph
+    capture until it retires it (works issued during capture are never handed to it).  A poll that
+    lands while this thread is capturing raced the capture and intermittently aborted the process
+    (the RCCL capture test).  So: drain the device and the warm-up works, then read the flight
+    recorder's active entries (``TORCH_FR_BUFFER_SIZE`` is set by :class:`mdtf.cluster.Server`) until
+    none are left — after that the watchdog has nothing to query during capture.  Without a
+    recorder the old bounded wait is the fallback."""
     try:
         import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
-            time.sleep(0.5)
+        if not (dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"):
+            return
     except (RuntimeError, ValueError):
-        pass
+        return
+    torch.cuda.synchronize()
+    n = _active_comm_works()
+    if n is None:
+        LAST_DRAIN[0] = "fallback"
+        time.sleep(0.5)
+        return
+    LAST_DRAIN[0] = "recorder"
+    deadline = time.time() + timeout_s
+    while n:
+        if time.time() > deadline:
+            raise RuntimeError("RCCL watchdog still holds %d completed works after %.0f s; refusing to capture"
+                               % (n, timeout_s))
+        time.sleep(0.005)
+        n = _active_comm_works()
 
 
 def _leaves(x, out):

@@ -101,7 +101,9 @@ class Saver(object):
         if write_state:
             d = os.path.dirname(prefix) or "."
             st = CS.read_state(d)
-            paths = [p for p in (st["all_model_checkpoint_paths"] if st else []) if p != prefix] + [prefix]
+            same = os.path.abspath(prefix)
+            paths = [p for p in (st["all_model_checkpoint_paths"] if st else [])
+                     if os.path.abspath(p) != same] + [prefix]
             if self.max_to_keep and len(paths) > self.max_to_keep:
                 for old in paths[:-self.max_to_keep]:
                     for f in glob.glob(old + ".index") + glob.glob(old + ".data-*"):

@@ -272,14 +272,48 @@ class MonitoredSession(Session):
         return False
 
 
+COLLECTIVE_SAVE_STEPS = 1000
+
+
+def _collective_save(server=None):
+    """True when a checkpoint save is a collective over the worker replicas (sharded mode, world > 1)."""
+    if not any(getattr(op.optimizer, "mode", None) == "sharded" for op in S.train_ops()):
+        return False
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    srv = server
+    if srv is None:
+        from ..cluster import server as srv_mod
+        srv = srv_mod.current()
+    pg = srv.worker_group if srv is not None and srv.worker_group is not None else None
+    return dist.get_world_size(pg) > 1
+
+
 def MonitoredTrainingSession(master="", is_chief=True, checkpoint_dir=None, scaffold=None, hooks=None,
                              chief_only_hooks=None, save_checkpoint_secs=600, save_summaries_steps=100,
                              save_summaries_secs=None, config=None, stop_grace_period_secs=120,
                              log_step_count_steps=100, max_wait_secs=7200, save_checkpoint_steps=None,
                              summary_dir=None, server=None):
-    """TF1's MonitoredTrainingSession factory with the same default hooks."""
+    """TF1's MonitoredTrainingSession factory with the same default hooks.
+
+    Sharded mode (``SyncReplicasOptimizer(mode='sharded')``, the PS-shard data-parallel path) with more
+    than one replica makes ``Saver.save`` a collective: the optimizer shards and the fp32 masters are
+    all-gathered.  TF's chief-only, time-triggered checkpoint hook would hang there (the other replicas
+    never join) or fire on different steps per replica, so in that case the hook is installed on EVERY
+    replica and triggered by step count (``save_checkpoint_steps``, else :data:`COLLECTIVE_SAVE_STEPS`).
+    """
     scaffold = scaffold or Scaffold()
     all_hooks = list(hooks or [])
+    collective = _collective_save(server)
+    if (collective and checkpoint_dir and (save_checkpoint_secs or save_checkpoint_steps)
+            and not any(isinstance(h, H.CheckpointSaverHook) for h in all_hooks)):
+        steps = save_checkpoint_steps or COLLECTIVE_SAVE_STEPS
+        if not save_checkpoint_steps:
+            logger.warn("sharded replicas save collectively: save_checkpoint_secs=%s replaced by a step trigger "
+                        "every %d steps on every replica" % (save_checkpoint_secs, steps))
+        all_hooks.append(H.CheckpointSaverHook(checkpoint_dir, save_steps=steps, scaffold=scaffold))
+        save_checkpoint_secs = save_checkpoint_steps = None
     if is_chief:
         all_hooks += list(chief_only_hooks or [])
         summary_dir = summary_dir or checkpoint_dir

@@ -77,3 +77,35 @@ def single_process_reference(world, steps, batch=4):
     for _ in range(steps):
         sess.run(op, feed_dict={x_ph: xs, y_ph: ys})
     return {v.name: v.master.tolist() for v in V.get_store().trainable_variables()}
+
+
+def sharded_ckpt_worker(rank, world, port, steps, out_dir, save_steps=None):
+    """Sharded-mode replicas with the factory's default (time-triggered) checkpoint settings:
+    the collective save must run on every replica at the same steps (session.py)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    import mdtf
+    from mdtf.cluster import Server
+    from mdtf.train import hooks as H
+    server = Server.from_env(backend="gloo")
+    batch = 4
+    Lin, MSE, xs, ys, x_ph, y_ph, Tower, Net = _linear_setup(rank, world, batch)
+    base = mdtf.train.AdamOptimizer(0.01)
+    tg = []
+    tower = Tower(Net(Lin()), "tower_0/", tg, x_ph, y_ph, MSE(), base, batch_size=batch)
+    tower.process()
+    opt = mdtf.train.SyncReplicasOptimizer(base, replicas_to_aggregate=world, total_num_replicas=world,
+                                           mode="sharded")
+    gs = mdtf.train.get_or_create_global_step()
+    op = opt.apply_gradients(Tower.average_gradients(tg), global_step=gs)
+    md = os.path.join(out_dir, "model")
+    kw = {} if save_steps is None else dict(save_checkpoint_steps=save_steps)
+    lo, hi = rank * batch, (rank + 1) * batch
+    with mdtf.train.MonitoredTrainingSession(is_chief=rank == 0, checkpoint_dir=md, log_step_count_steps=0,
+                                             hooks=[H.StopAtStepHook(last_step=steps)], server=server,
+                                             **kw) as sess:
+        while not sess.should_stop():
+            sess.run(op, feed_dict={x_ph: xs[lo:hi], y_ph: ys[lo:hi]})
+    with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
+        json.dump({"step": gs.value()}, f)
+    server.shutdown()

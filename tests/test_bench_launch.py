@@ -41,3 +41,43 @@ def test_bench_torchrun_two_ranks(mode):
     assert rec["config"]["grad_sync"] == mode
     assert rec["value"] > 0 and rec["ms_per_step"] > 0
     assert rec["loss_last"] == rec["loss_last"]           # finite
+
+
+def _one_json(out):
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]          # rank 0 only
+    return json.loads(lines[0])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("mode", ["allreduce", "sharded"])
+def test_bench_gpus_flag_self_launches_eight_ranks(mode):
+    """``python bench.py --gpus 8`` without torchrun spawns 8 ranks (here gloo on the CPU) and
+    reports them; it used to ignore --gpus and time one process."""
+    cmd = [sys.executable, "bench.py", "--gpus", "8", "--steps", "2", "--warmup", "1", "--batch", "1",
+           "--image_size", "32", "--mode", mode]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("MDTF_HIP_GRAPH", None)
+    rec = _one_json(subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=1200))
+    assert rec["n_gpus"] == 8 and rec["config"]["parallelism"] == "dp8"
+    assert rec["config"]["global_batch"] == 8 and rec["config"]["grad_sync"] == mode
+    assert rec["per_gpu_images_per_sec"] == pytest.approx(rec["value"] / 8, abs=0.01)
+
+
+@pytest.mark.slow
+def test_bench_world_size_mismatch_exits_nonzero():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0")
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "4"], cwd=ROOT, env=env, capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode != 0 and "launch mismatch" in out.stderr
+
+
+@pytest.mark.slow
+def test_bert_bench_eight_ranks_cpu():
+    cmd = [sys.executable, "bench/bert_bench.py", "--gpus", "8", "--size", "tiny", "--batch", "2", "--seq", "32",
+           "--steps", "2", "--warmup", "1", "--mode", "sharded"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    rec = _one_json(subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900))
+    assert rec["n_gpus"] == 8 and rec["config"]["global_batch"] == 16 and rec["impl"] == "mdtf"
+    assert rec["config"]["grad_sync"] == "sharded" and rec["value"] > 0

@@ -160,3 +160,30 @@ def test_heartbeat_detects_silent_peer():
     time.sleep(1.0)
     c.stop()
     assert failed == []
+
+
+@pytest.mark.parametrize("save_steps", [None, 2])
+def test_sharded_collective_checkpoint_through_monitored_session(save_steps, tmp_path):
+    """Saving in sharded mode all-gathers the optimizer shards; the default chief-only, 600 s
+    hook would hang the chief at the first save.  Every replica now saves on the same steps."""
+    sys.path.insert(0, os.path.dirname(__file__))
+    import dist_helpers
+    from mdtf.train.saver import latest_checkpoint
+    from mdtf.ckpt.tensor_bundle import BundleReader
+    port = free_port()
+    ctx = mp.start_processes(dist_helpers.sharded_ckpt_worker, args=(2, port, 5, str(tmp_path), save_steps),
+                             nprocs=2, join=False, start_method="spawn")
+    import time
+    deadline = time.time() + 180
+    while not ctx.join(timeout=5):
+        if time.time() > deadline:
+            for p in ctx.processes:
+                p.kill()
+            pytest.fail("sharded replicas hung in the collective checkpoint save")
+    ck = latest_checkpoint(str(tmp_path / "model"))
+    assert ck and ck.endswith("model.ckpt-5")
+    r = BundleReader(ck)
+    assert "dense/w/Adam" in r and int(r.get_tensor("global_step").item()) == 5
+    if save_steps == 2:
+        import glob
+        assert os.path.exists(str(tmp_path / "model" / "model.ckpt-4.index"))

@@ -237,3 +237,44 @@ def test_device_setter_round_robin():
         for i in range(5):
             V.get_variable("v%d" % i, [1])
     assert [V.get_store().vars["v%d" % i].ps_task for i in range(5)] == [0, 1, 0, 1, 0]
+
+
+def test_checkpoint_relative_model_dir_resume_and_cleanup(tmp_path, monkeypatch):
+    """--model_dir=ck (relative): the state file stores paths relative to ck/, resume finds the
+    latest checkpoint, and max_to_keep deletes the old shards (checkpoint_state.py)."""
+    import glob
+    import os
+    monkeypatch.chdir(tmp_path)
+
+    def build():
+        V.reset_default_graph()
+        S.reset()
+        loader = SyntheticDataLoader(shape=(28, 28, 1), num_classes=10)
+        loader.batch_size = 4
+        raw, gt = loader.load_train_batch()
+        opt = mdtf.train.MomentumOptimizer(0.01, 0.9)
+        gs = mdtf.train.get_or_create_global_step()
+        tg = []
+        tower = Tower(Net(LeNet()), "tower_0/", tg, raw, gt, SoftmaxCrossEntropyLoss(), opt, batch_size=4)
+        tower.process()
+        return opt.apply_gradients(Tower.average_gradients(tg), global_step=gs), gs
+    train_op, gs = build()
+    saver = mdtf.train.Saver(max_to_keep=2)
+    scaffold = mdtf.train.Scaffold(saver=saver)
+    with mdtf.train.MonitoredTrainingSession(checkpoint_dir="ck", hooks=[H.StopAtStepHook(last_step=8)],
+                                             scaffold=scaffold, log_step_count_steps=0, save_checkpoint_secs=None,
+                                             save_checkpoint_steps=2) as sess:
+        while not sess.should_stop():
+            sess.run(train_op)
+    txt = open(os.path.join("ck", "checkpoint")).read()
+    assert 'model_checkpoint_path: "model.ckpt-8"' in txt and "ck/" not in txt
+    assert sorted(os.path.basename(p) for p in glob.glob("ck/*.index")) == ["model.ckpt-6.index",
+                                                                          "model.ckpt-8.index"]
+    assert mdtf.train.latest_checkpoint("ck").endswith("model.ckpt-8")
+    w_saved = V.get_store().vars["fc2/weights"].master.clone()
+    train_op, gs = build()
+    with mdtf.train.MonitoredTrainingSession(checkpoint_dir="ck", hooks=[H.StopAtStepHook(last_step=8)],
+                                             log_step_count_steps=0, save_checkpoint_secs=None):
+        pass
+    assert gs.value() == 8
+    assert torch.equal(V.get_store().vars["fc2/weights"].master, w_saved)

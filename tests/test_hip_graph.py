@@ -176,6 +176,7 @@ def test_hip_graph_captures_rccl_collectives(mode, monkeypatch):
     import torch.distributed as dist
     from mdtf.ops import _native
     monkeypatch.setenv("MDTF_FORCE_COLLECTIVES", "1")
+    monkeypatch.setenv("TORCH_FR_BUFFER_SIZE", "2000")          # capture drains the watchdog by state
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
@@ -192,6 +193,8 @@ def test_hip_graph_captures_rccl_collectives(mode, monkeypatch):
             _native.set_deterministic(False)
         assert op_e.reducer.collective and op_e.reducer.overlap and len(op_e.space.buckets) > 1
         assert op.graph.replays == 3 and op.graph.fallbacks == 0
+        from mdtf.train import graph as G
+        assert G.LAST_DRAIN[0] == "recorder", G.LAST_DRAIN
         assert l_e == l_g, (l_e, l_g)
         for k in w_e:
             assert torch.equal(w_e[k], w_g[k]), k
