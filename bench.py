@@ -39,7 +39,9 @@ def parse():
     p.add_argument("--depth", type=int, default=50)
     p.add_argument("--mode", default="allreduce", choices=["allreduce", "sharded"])
     p.add_argument("--kernels", default=None, help="native|torch (MDTF_KERNELS)")
-    p.add_argument("--bucket_mb", type=int, default=None)
+    p.add_argument("--bucket_mb", type=int, default=None, help="gradient bucket MiB (default MDTF_BUCKET_MB or 32)")
+    p.add_argument("--comm_dtype", default=None, choices=["fp32", "bf16"],
+                   help="gradient wire dtype of the RCCL reductions (default MDTF_COMM_DTYPE or fp32)")
     p.add_argument("--profile_dir", default=None)
     p.add_argument("--hip_graph", type=int, default=1,
                    help="1: capture the whole training step in a hipGraph after 2 eager steps (mdtf.train.graph)")
@@ -102,7 +104,8 @@ def main():
     _, loss, _ = tower.process()
     opt = mdtf.train.SyncReplicasOptimizer(base, replicas_to_aggregate=world, total_num_replicas=world,
                                            mode=args.mode, hip_graph=bool(args.hip_graph),
-                                           bucket_bytes=(args.bucket_mb << 20) if args.bucket_mb else None)
+                                           bucket_bytes=(args.bucket_mb << 20) if args.bucket_mb else None,
+                                           comm_dtype=args.comm_dtype)
     train_op = opt.apply_gradients(Tower.average_gradients(tower_grads), global_step=gs)
     sess = mdtf.train.MonitoredTrainingSession(is_chief=(rank == 0), checkpoint_dir=None, log_step_count_steps=0,
                                                server=server)
@@ -153,7 +156,9 @@ def main():
                 args.image_size, args.image_size),
             "config": {"model": "resnet%d_v1.5" % args.depth, "global_batch": args.batch * world, "seq_len": None,
                        "per_gpu_batch": args.batch, "image_size": args.image_size, "parallelism": "dp%d" % world,
-                       "grad_sync": args.mode, "optimizer": "momentum-sgd (fused)",
+                       "grad_sync": args.mode,
+                       "comm_dtype": "bf16" if str(opt.comm_dtype or os.environ.get("MDTF_COMM_DTYPE", "fp32")).startswith("bf") else "fp32",
+                       "optimizer": "momentum-sgd (fused)",
                        "kernels": os.environ.get("MDTF_KERNELS", "native"),
                        "hip_graph": bool(args.hip_graph) and dev.type == "cuda"},
             "loss_first": float(lv), "loss_last": final_loss,

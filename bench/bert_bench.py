@@ -33,6 +33,8 @@ def parse():
     p.add_argument("--stock", action="store_true")
     p.add_argument("--mode", default="allreduce", choices=["allreduce", "sharded"])
     p.add_argument("--hip_graph", type=int, default=1, help="capture the mdtf training step in a hipGraph")
+    p.add_argument("--comm_dtype", default=None, choices=["fp32", "bf16"], help="gradient wire dtype")
+    p.add_argument("--bucket_mb", type=int, default=None, help="gradient bucket MiB")
     p.add_argument("--trace_ops", default=None,
                    help="after the warm-up, profile one step with Python stacks (use --hip_graph 0) into this dir")
     return p.parse_args()
@@ -146,7 +148,8 @@ def main():
                       BertPretrainingLoss(P), base, batch_size=args.batch)
         _, loss_h, _ = tower.process()
         opt = mdtf.train.SyncReplicasOptimizer(base, world, world, hip_graph=bool(args.hip_graph) and gpu,
-                                               mode=args.mode)
+                                               mode=args.mode, comm_dtype=args.comm_dtype,
+                                               bucket_bytes=(args.bucket_mb << 20) if args.bucket_mb else None)
         op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
         sess = mdtf.train.MonitoredTrainingSession(is_chief=rank == 0, log_step_count_steps=0, server=server)
 

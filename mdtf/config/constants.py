@@ -11,6 +11,14 @@ MIN_FRACTION_OF_EXAMPLE_IN_QUEUE = 0.05
 # backward on ResNet-50 (~100 MB of fp32 grads -> ~4 buckets).
 DEFAULT_BUCKET_BYTES = 32 << 20
 
+
+def bucket_bytes():
+    """Bucket size in bytes: ``MDTF_BUCKET_MB`` if set, else DEFAULT_BUCKET_BYTES
+    (``bench/collectives.py`` sweeps 4-256 MiB on a node to choose it)."""
+    import os
+    mb = os.environ.get("MDTF_BUCKET_MB")
+    return int(float(mb) * (1 << 20)) if mb else DEFAULT_BUCKET_BYTES
+
 # Rendezvous defaults.
 DEFAULT_PORT = 29500
 STORE_TIMEOUT_S = 600

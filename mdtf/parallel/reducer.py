@@ -23,11 +23,24 @@ Two modes:
     traffic ≈ the all-reduce's, the PS-CPU bottleneck and the separate
     parameter pull are gone.
 
+Wire dtype (``comm_dtype``): fp32 (default) or bf16.  In bf16 mode each bucket's
+fp32 gradients are cast into a persistent bf16 wire buffer, the collective runs
+on half the bytes (xGMI rings are per-link bandwidth bound, so a bucket's
+all-reduce / reduce-scatter time halves), and the result is widened back into
+the fp32 gradient (allreduce) or the fp32 shard gradient the optimizer reads
+(sharded).  Master weights and optimizer state stay fp32; only the summands on
+the wire are rounded (relative error ~N * 2^-9 of the summed gradient, tested
+in ``tests/test_distributed.py``).
+
 Backup workers (``replicas_to_aggregate`` R < N): gradients of the first R
 replicas to finish backward are aggregated, the rest contribute zeros (TF
 drops them as stale); arrival order comes from an atomic counter in the
-cluster store.  Overlap is disabled in that mode because the mask is only
-known after backward.
+cluster store, taken once the replica's backward has completed on its device.
+Overlap is disabled in that mode because the mask is only known after backward.
+Unlike TF's accumulators, stragglers are NOT skipped in time: every replica
+still joins every collective (its contribution zeroed), so a slow replica
+delays the step; backup workers here reproduce the gradient math (exactly R
+contributions per step), not the latency hiding.
 """
 import os
 
@@ -52,10 +65,25 @@ class UpdateTarget(object):
         return self.group.state_buffer("%s/%s" % (self.key, name), self.numel)
 
 
+def resolve_comm_dtype(comm_dtype=None):
+    """``comm_dtype`` argument, else ``MDTF_COMM_DTYPE`` (fp32 | bf16); -> torch dtype."""
+    name = comm_dtype if comm_dtype is not None else os.environ.get("MDTF_COMM_DTYPE", "fp32")
+    if isinstance(name, torch.dtype):
+        name = {torch.float32: "fp32", torch.bfloat16: "bf16"}.get(name, str(name))
+    name = str(name).lower()
+    if name in ("fp32", "float32", "float"):
+        return torch.float32
+    if name in ("bf16", "bfloat16"):
+        return torch.bfloat16
+    raise ValueError("comm_dtype must be fp32 or bf16, got %r" % (comm_dtype,))
+
+
 class GradReducer(object):
     def __init__(self, space, process_group=None, mode="allreduce", overlap=True,
-                 replicas_to_aggregate=None, store=None):
+                 replicas_to_aggregate=None, store=None, comm_dtype=None):
         self.space = space
+        self.comm_dtype = resolve_comm_dtype(comm_dtype)
+        self._wire = {}                    # bucket index -> (bf16 full buffer, bf16 shard buffer or None)
         self.pg = process_group
         self.mode = mode
         self.distributed = dist.is_available() and dist.is_initialized()
@@ -133,17 +161,50 @@ class GradReducer(object):
         from ..ops import conv as _conv
         _conv.join_side_streams()          # side-stream weight gradients of this bucket are in
         g = b.group
+        if self.comm_dtype != torch.float32:
+            wire, wshard = self._wire_buffers(b)
+            wire.copy_(g.grad[b.start:b.end])          # fp32 -> bf16 on the compute stream
+            if self.mode == "allreduce":
+                b.work = dist.all_reduce(wire, group=self.pg, async_op=True)
+            else:
+                b.work = dist.reduce_scatter_tensor(wshard, wire, group=self.pg, async_op=True)
+            return
         if self.mode == "allreduce":
             b.work = dist.all_reduce(g.grad[b.start:b.end], group=self.pg, async_op=True)
         else:
             out = self._shards[id(g)]["grad"][b.shard_offset:b.shard_offset + b.shard_len]
             b.work = dist.reduce_scatter_tensor(out, g.grad[b.start:b.end], group=self.pg, async_op=True)
 
+    def _wire_buffers(self, b):
+        """Persistent (graph-capture safe) bf16 wire buffers of one bucket."""
+        ent = self._wire.get(id(b))
+        if ent is None:
+            g = b.group
+            wire = torch.empty(b.numel, dtype=self.comm_dtype, device=g.device)
+            wshard = (torch.empty(b.shard_len, dtype=self.comm_dtype, device=g.device)
+                      if self.mode == "sharded" else None)
+            ent = (wire, wshard)
+            self._wire[id(b)] = ent
+        return ent
+
+    def _widen(self, b):
+        """bf16 wire result -> the fp32 gradient the optimizer reads."""
+        wire, wshard = self._wire[id(b)]
+        g = b.group
+        if self.mode == "allreduce":
+            g.grad[b.start:b.end].copy_(wire)
+        else:
+            self._shards[id(g)]["grad"][b.shard_offset:b.shard_offset + b.shard_len].copy_(wshard)
+
     def end_backward(self, step=0):
         """Finish all reductions; returns the gradient scale (1/contributors)."""
         from ..ops import conv as _conv
         _conv.join_side_streams()          # every weight gradient is in the flat buffer
         if self.world > 1 and self.R < self.world:
+            # the ticket is taken after this replica's backward has COMPLETED on the device (not
+            # merely been enqueued), so "first R" means first R to finish computing
+            if self.space.device is not None and torch.device(self.space.device).type == "cuda":
+                torch.cuda.current_stream(self.space.device).synchronize()
             order = self.store.add("mdtf/sync_replicas/%d" % step, 1)
             self.contributed = order <= self.R
             if not self.contributed:
@@ -163,6 +224,8 @@ class GradReducer(object):
             if b.work is not None:
                 b.work.wait()
                 b.work = None
+                if self.comm_dtype != torch.float32:
+                    self._widen(b)
         if not self.collective and self.mode == "sharded":
             for g in self.space.groups:
                 self._shards[id(g)]["grad"].copy_(self._gather_index(g, g.grad))

@@ -143,11 +143,13 @@ class SyncReplicasOptimizer(Optimizer):
     overlapped bucketed all-reduce; ``mode='sharded'`` makes every rank the
     parameter server of 1/N of each bucket (reduce-scatter + local fused update
     + all-gather) — the MI355X-native form of PS variable sharding.
+    ``bucket_bytes`` (default ``MDTF_BUCKET_MB`` or 32 MiB of fp32 gradients) sets the
+    collective granularity; ``comm_dtype='bf16'`` halves the bytes on the wire.
     """
 
     def __init__(self, opt, replicas_to_aggregate=None, total_num_replicas=None, variable_averages=None,
                  variables_to_average=None, use_locking=False, name="sync_replicas", mode="allreduce",
-                 bucket_bytes=None, overlap=True, hip_graph=None):
+                 bucket_bytes=None, overlap=True, hip_graph=None, comm_dtype=None):
         super(SyncReplicasOptimizer, self).__init__(opt._lr, use_locking, name, opt.weight_decay)
         self._opt = opt
         self.replicas_to_aggregate = replicas_to_aggregate
@@ -156,6 +158,8 @@ class SyncReplicasOptimizer(Optimizer):
         self.bucket_bytes = bucket_bytes
         self.overlap = overlap
         self.hip_graph = hip_graph   # None: MDTF_HIP_GRAPH / --hip_graph decide (mdtf.train.graph)
+        # gradient wire dtype: None -> MDTF_COMM_DTYPE (fp32 default) | "bf16" (mdtf.parallel.reducer)
+        self.comm_dtype = comm_dtype
 
     def learning_rate(self, global_step=0):
         return self._opt.learning_rate(global_step)

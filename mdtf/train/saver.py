@@ -28,6 +28,27 @@ def latest_checkpoint(checkpoint_dir):
     return CS.latest_checkpoint(checkpoint_dir)
 
 
+class TensorDictReader(object):
+    """BundleReader look-alike over an in-memory ``{name: tensor}`` dict."""
+
+    def __init__(self, tensors):
+        self.tensors = tensors
+
+    def __contains__(self, name):
+        return name in self.tensors
+
+    def keys(self):
+        return list(self.tensors)
+
+    def get_tensor(self, name):
+        return self.tensors[name]
+
+
+def read_all(save_path):
+    r = BundleReader(save_path)
+    return {k: r.get_tensor(k) for k in r.keys()}
+
+
 def _is_writer():
     import torch.distributed as dist
     from ..cluster import server as srv_mod
@@ -112,8 +133,10 @@ class Saver(object):
             CS.write_state(d, prefix, paths)
         return prefix
 
-    def restore(self, sess, save_path):
-        r = BundleReader(save_path)
+    def restore(self, sess, save_path, reader=None):
+        """``reader``: any object with ``in`` / ``get_tensor`` (e.g. :class:`TensorDictReader` of tensors
+        the chief read and broadcast when ``save_path`` is not visible on this replica)."""
+        r = reader if reader is not None else BundleReader(save_path)
         store = V.get_store()
         missing = []
         with torch.no_grad():

@@ -181,7 +181,17 @@ class MonitoredSession(Session):
         restored = False
         if ckpt:
             saver = self.scaffold.saver or Saver()
-            saver.restore(self, ckpt)
+            reader = None
+            if multi and not self._visible_everywhere(ckpt, pg):
+                # node-local model_dir: only the chief can read the files; it broadcasts the
+                # tensors and every replica restores from them (its own shard in sharded mode)
+                from .saver import TensorDictReader, read_all
+                box = [read_all(ckpt) if self.is_chief else None]
+                src = dist.get_global_rank(pg, 0) if pg is not dist.group.WORLD else 0
+                dist.broadcast_object_list(box, src=src, group=pg)
+                reader = TensorDictReader(box[0])
+                logger.info("checkpoint %s is not visible on every replica: restoring from the chief's copy" % ckpt)
+            saver.restore(self, ckpt, reader=reader)
             self.restored_from = ckpt
             restored = True
             logger.info("Restored from checkpoint %s (global_step %d)" % (ckpt, V.get_global_step().value()))
@@ -199,6 +209,16 @@ class MonitoredSession(Session):
         for op in ops:
             op.space.refresh_shadows()
             op.reducer.load_shards_from_master()
+
+    @staticmethod
+    def _visible_everywhere(ckpt, pg):
+        """All-reduce(MIN) of 'this replica sees <ckpt>.index' over the group."""
+        import os
+        import torch.distributed as dist
+        dev = V.get_store().device if dist.get_backend(pg) == "nccl" else "cpu"
+        seen = torch.tensor([1 if os.path.exists(ckpt + ".index") else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(seen, op=dist.ReduceOp.MIN, group=pg)
+        return bool(seen.item())
 
     def _broadcast_state(self, pg):
         """Chief (group rank 0) → every replica."""

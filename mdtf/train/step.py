@@ -282,7 +282,7 @@ class TrainOp(Fetchable):
         world = dist.get_world_size(process_group) if distributed else 1
         opt = self.optimizer
         mode = getattr(opt, "mode", "allreduce")
-        bucket_bytes = getattr(opt, "bucket_bytes", None) or constants.DEFAULT_BUCKET_BYTES
+        bucket_bytes = getattr(opt, "bucket_bytes", None) or constants.bucket_bytes()
         overlap = getattr(opt, "overlap", True) and len(self.programs) <= 1
         self.space = FlatParamSpace(self.variables, vstore.device, vstore.compute_dtype, bucket_bytes,
                                     pad_to=world if mode == "sharded" else 1)
@@ -293,7 +293,8 @@ class TrainOp(Fetchable):
             # replicas are counted in towers (one per rank)
             pass
         self.reducer = GradReducer(self.space, process_group, mode=mode, overlap=overlap,
-                                   replicas_to_aggregate=R, store=store)
+                                   replicas_to_aggregate=R, store=store,
+                                   comm_dtype=getattr(opt, "comm_dtype", None))
 
     # -- execution ---------------------------------------------------------
     def _graph_enabled(self):

@@ -29,7 +29,7 @@ def _linear_setup(rank, world, batch, seed=0):
     return Lin, MSE, xs, ys, x_ph, y_ph, Tower, Net
 
 
-def sync_worker(rank, world, port, mode, steps, out_dir, replicas=None, batch=4):
+def sync_worker(rank, world, port, mode, steps, out_dir, replicas=None, batch=4, comm_dtype=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
     import mdtf
@@ -42,7 +42,8 @@ def sync_worker(rank, world, port, mode, steps, out_dir, replicas=None, batch=4)
     tower = Tower(Net(Lin()), "tower_0/", tg, x_ph, y_ph, MSE(), base, batch_size=batch)
     _, loss, _ = tower.process()
     opt = mdtf.train.SyncReplicasOptimizer(base, replicas_to_aggregate=replicas or world, total_num_replicas=world,
-                                           mode=mode, bucket_bytes=64)     # tiny buckets: several per group
+                                           mode=mode, bucket_bytes=64,     # tiny buckets: several per group
+                                           comm_dtype=comm_dtype)
     gs = mdtf.train.get_or_create_global_step()
     op = opt.apply_gradients(Tower.average_gradients(tg), global_step=gs)
     hook = opt.make_session_run_hook(rank == 0)
@@ -108,4 +109,39 @@ def sharded_ckpt_worker(rank, world, port, steps, out_dir, save_steps=None):
             sess.run(op, feed_dict={x_ph: xs[lo:hi], y_ph: ys[lo:hi]})
     with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
         json.dump({"step": gs.value()}, f)
+    server.shutdown()
+
+
+def hidden_ckpt_restore_worker(rank, world, port, out_dir):
+    """Resume in sharded mode where only the chief can see model_dir (node-local disk): rank 1's
+    os.path.exists is blinded to the checkpoint files, so the chief must read and broadcast them."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    md = os.path.join(out_dir, "model")
+    if rank != 0:
+        real = os.path.exists
+        os.path.exists = lambda p: False if str(p).startswith(md) else real(p)
+    import mdtf
+    from mdtf.cluster import Server
+    from mdtf.train import variables as V
+    server = Server.from_env(backend="gloo")
+    batch = 4
+    Lin, MSE, xs, ys, x_ph, y_ph, Tower, Net = _linear_setup(rank, world, batch)
+    base = mdtf.train.AdamOptimizer(0.01)
+    tg = []
+    tower = Tower(Net(Lin()), "tower_0/", tg, x_ph, y_ph, MSE(), base, batch_size=batch)
+    tower.process()
+    opt = mdtf.train.SyncReplicasOptimizer(base, world, world, mode="sharded")
+    gs = mdtf.train.get_or_create_global_step()
+    op = opt.apply_gradients(Tower.average_gradients(tg), global_step=gs)
+    sess = mdtf.train.MonitoredTrainingSession(is_chief=rank == 0, checkpoint_dir=md if rank == 0 else None,
+                                               log_step_count_steps=0, server=server, save_checkpoint_secs=None)
+    step = gs.value()
+    op.reducer.gather_full_master()
+    w = {v.name: v.master.tolist() for v in V.get_store().trainable_variables()}
+    # this replica's Adam shard, gathered back to full size
+    m = op.reducer.gather_full_state(None, "m")[0].tolist()
+    with open(os.path.join(out_dir, "resume%d.json" % rank), "w") as f:
+        json.dump({"step": step, "weights": w, "adam_m": m, "restored": sess.restored_from}, f)
+    sess.close()
     server.shutdown()

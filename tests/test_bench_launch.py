@@ -81,3 +81,28 @@ def test_bert_bench_eight_ranks_cpu():
     rec = _one_json(subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900))
     assert rec["n_gpus"] == 8 and rec["config"]["global_batch"] == 16 and rec["impl"] == "mdtf"
     assert rec["config"]["grad_sync"] == "sharded" and rec["value"] > 0
+
+
+@pytest.mark.slow
+def test_collectives_sweep_runs_on_gloo():
+    """bench/collectives.py (the bucket-size sweep for an 8-GPU node) runs end to end on 4 gloo ranks."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench/collectives.py",
+           "--sizes_mb", "1,2", "--iters", "2", "--warmup", "1"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    recs = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(recs) >= 2 * 2 * 3            # 2 dtypes x 2 sizes x 3 collectives
+    assert all(r["busbw_GBps"] > 0 for r in recs)
+
+
+@pytest.mark.slow
+def test_bench_bf16_wire_two_ranks():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--batch", "2", "--image_size", "32", "--comm_dtype", "bf16",
+           "--bucket_mb", "8"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["n_gpus"] == 2 and rec["config"]["comm_dtype"] == "bf16"

@@ -21,11 +21,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.slow
 
 
-def _run(world, mode, steps, tmp_path, replicas=None):
+def _run(world, mode, steps, tmp_path, replicas=None, comm_dtype=None):
     sys.path.insert(0, os.path.dirname(__file__))
     import dist_helpers
     port = free_port()
-    mp.start_processes(dist_helpers.sync_worker, args=(world, port, mode, steps, str(tmp_path), replicas),
+    mp.start_processes(dist_helpers.sync_worker, args=(world, port, mode, steps, str(tmp_path), replicas, 4,
+                                                       comm_dtype),
                        nprocs=world, join=True, start_method="spawn")
     return [json.load(open(os.path.join(str(tmp_path), "rank%d.json" % r))) for r in range(world)]
 
@@ -41,6 +42,38 @@ def test_sync_dp_equals_single_process(mode, world, tmp_path):
         assert r["step"] == 5
         for name, vals in ref.items():
             assert torch.allclose(torch.tensor(r["weights"][name]), torch.tensor(vals), atol=1e-5), (mode, name)
+
+
+@pytest.mark.parametrize("mode", ["allreduce", "sharded"])
+def test_bf16_wire_dtype_matches_fp32_within_tolerance(mode, tmp_path):
+    """comm_dtype='bf16': gradients cross the wire in bf16 (half the bytes), masters stay fp32.
+    Stated tolerance: after 5 momentum steps every weight is within 2e-2 relative (of the
+    largest weight of the tensor) of single-process fp32 training."""
+    sys.path.insert(0, os.path.dirname(__file__))
+    import dist_helpers
+    res = _run(2, mode, 5, tmp_path, comm_dtype="bf16")
+    ref = dist_helpers.single_process_reference(2, 5)
+    for r in res:
+        for name, vals in ref.items():
+            a, b = torch.tensor(r["weights"][name]), torch.tensor(vals)
+            assert (a - b).abs().max() <= 2e-2 * b.abs().max() + 1e-4, (mode, name)
+    # all replicas agree bit-for-bit (everyone widens the same reduced bf16 values)
+    for r in res[1:]:
+        for k in res[0]["weights"]:
+            assert r["weights"][k] == res[0]["weights"][k]
+
+
+def test_comm_dtype_resolution(monkeypatch):
+    from mdtf.parallel.reducer import resolve_comm_dtype
+    from mdtf.config import constants
+    assert resolve_comm_dtype() == torch.float32
+    assert resolve_comm_dtype("bf16") == torch.bfloat16
+    monkeypatch.setenv("MDTF_COMM_DTYPE", "bfloat16")
+    assert resolve_comm_dtype() == torch.bfloat16
+    with pytest.raises(ValueError):
+        resolve_comm_dtype("fp8")
+    monkeypatch.setenv("MDTF_BUCKET_MB", "64")
+    assert constants.bucket_bytes() == 64 << 20
 
 
 def test_backup_workers_aggregate_r_of_n(tmp_path):
@@ -187,3 +220,26 @@ def test_sharded_collective_checkpoint_through_monitored_session(save_steps, tmp
     if save_steps == 2:
         import glob
         assert os.path.exists(str(tmp_path / "model" / "model.ckpt-4.index"))
+
+
+def test_restore_when_checkpoint_visible_only_on_chief(tmp_path):
+    """a node-local model_dir.  The chief reads the bundle and broadcasts it; every
+    replica (sharded mode: its own Adam shard) resumes from the same state."""
+    sys.path.insert(0, os.path.dirname(__file__))
+    import dist_helpers
+    from mdtf.ckpt.tensor_bundle import BundleReader
+    from mdtf.train.saver import latest_checkpoint
+    mp.start_processes(dist_helpers.sharded_ckpt_worker, args=(2, free_port(), 3, str(tmp_path), None),
+                       nprocs=2, join=True, start_method="spawn")
+    ck = latest_checkpoint(str(tmp_path / "model"))
+    assert ck and ck.endswith("model.ckpt-3")
+    mp.start_processes(dist_helpers.hidden_ckpt_restore_worker, args=(2, free_port(), str(tmp_path)),
+                       nprocs=2, join=True, start_method="spawn")
+    res = [json.load(open(str(tmp_path / ("resume%d.json" % r)))) for r in range(2)]
+    r = BundleReader(ck)
+    for rec in res:
+        assert rec["step"] == 3 and rec["restored"] == ck
+        for name, vals in rec["weights"].items():
+            assert torch.allclose(torch.tensor(vals), r.get_tensor(name).float().reshape(torch.tensor(vals).shape))
+    assert res[0]["adam_m"] == res[1]["adam_m"]
+    assert any(abs(x) > 0 for x in res[0]["adam_m"])
