@@ -63,6 +63,24 @@ V3_TILES = ((256, 256, 2), (256, 128, 2), (256, 128, 3), (256, 64, 3), (256, 64,
             (256, 256, 1), (256, 128, 1))
 
 
+def ws_tiles(pass_, c, co, kh, kw, s):
+    """Weight-stationary kernel tiles (csrc/conv_ws.hip) valid for this conv pass."""
+    if not C.ws_ok(pass_, c, co, (s, s), kh, kw):
+        return []
+    red, ncol = (c, co) if pass_ == "fwd" else (co, c)
+    kt = kh * kw * red
+    out = []
+    for tp in (2, 4):
+        for nw in (4, 8):
+            for cg in (1, 2, 4):
+                if nw % cg or ncol % (64 * cg) or cg * kt * 128 > 160 * 1024:
+                    continue
+                for d in (2, 3, 4, 6):
+                    if C.ws_depth_ok(kt, d):
+                        out.append((tp, nw, cg, d))
+    return out
+
+
 def _stats(co, bm, M):
     """Statistics buffer as conv_bn uses it (slot count as in ops/conv.py)."""
     import torch
@@ -127,17 +145,28 @@ def main():
                 if C.v2_ok("fwd", c, co, (s, s), kh * kw):
                     cands += [(bm, bn, st, 2) for bm, bn, st in V2_TILES]
                     cands += [(bm, bn, st, 3) for bm, bn, st in V3_TILES]
+                cands += [(t, 0, 0, 4) for t in ws_tiles("fwd", c, co, kh, kw, s)]
+                wtt = C.transpose_filter(wt)
+
                 # training always runs conv -> BN: time the forward with its fused statistics epilogue
-                mk = lambda bm, bn, sp, v: (lambda st=_stats(co, bm, n * oh * ow): C.mdtf_fwd(  # noqa
-                    x, wt, (oh, ow), (s, s), pads4, (1, 1), bm, bn, st, v, sp))
+                def mk(bm, bn, sp, v):
+                    if v == 4:
+                        st = _stats(co, 128, n * oh * ow)
+                        return lambda: C.ws_fwd(x, wtt, kh, kw, (oh, ow), (s, s), pads4, (1, 1), bm, st)
+                    st = _stats(co, bm, n * oh * ow)
+                    return lambda: C.mdtf_fwd(x, wt, (oh, ow), (s, s), pads4, (1, 1), bm, bn, st, v, sp)
             elif pass_ == "dgrad":
                 lib = lambda: C.miopen_bwd(x, wt, dy, (s, s), pads4, (1, 1), True, False)  # noqa: E731
                 cands = [(bm, bn, 0, 1) for bm, bn in ((128, 128), (128, 64), (64, 64), (256, 64))]
                 if C.v2_ok("dgrad", c, co, (s, s), kh * kw):
                     cands += [(bm, bn, st, 2) for bm, bn, st in V2_TILES]
                     cands += [(bm, bn, st, 3) for bm, bn, st in V3_TILES]
-                mk = lambda bm, bn, sp, v: (lambda: C.mdtf_dgrad(dy, wt, x.shape, (s, s), pads4, (1, 1), bm, bn,  # noqa
-                                                               v, sp))
+                cands += [(t, 0, 0, 4) for t in ws_tiles("dgrad", c, co, kh, kw, s)]
+
+                def mk(bm, bn, sp, v):
+                    if v == 4:
+                        return lambda: C.ws_dgrad(dy, wt, x.shape, pads4, (1, 1), bm)
+                    return lambda: C.mdtf_dgrad(dy, wt, x.shape, (s, s), pads4, (1, 1), bm, bn, v, sp)
             else:
                 lib = lambda: C.miopen_bwd(x, wt, dy, (s, s), pads4, (1, 1), False, True)  # noqa: E731
                 cands = [(bm, bn, sp, 1) for bm, bn in ((128, 128), (64, 64), (128, 64), (64, 128))
@@ -175,7 +204,10 @@ def main():
             elif best is not None and best[0] < {"fwd": t_lib / 0.85, "dgrad": t_lib / 0.75}.get(pass_, t_lib):
                 ent = {"backend": "mdtf", "bm": best[1], "bn": best[2], "splits": best[3], "ver": best[4],
                        "ms": round(best[0], 4), "miopen_ms": round(t_lib, 4)}
-                if best[4] >= 2 and pass_ == "wgrad":     # v2 wgrad: bm field carries (rows, stages)
+                if best[4] == 4:                          # weight-stationary kernel: tile in "ws"
+                    ent = {"backend": "mdtf", "ver": 4, "ws": list(best[1]), "ms": round(best[0], 4),
+                           "miopen_ms": round(t_lib, 4)}
+                elif best[4] >= 2 and pass_ == "wgrad":   # v2 wgrad: bm field carries (rows, stages)
                     ent["bm"], ent["stages"] = best[1]
                 elif best[4] in (2, 3):                   # v2 fwd/dgrad: the third field is the pipeline depth
                     ent["stages"], ent["splits"] = best[3], 0
@@ -190,7 +222,7 @@ def main():
             tot["best"] += k * min(t_lib, best[0] if best else 1e9, t_wino or 1e9)
             lines.append("| %s | %d,%d,%d,%d,%dx%d,%d,s%d | %d | %.3f | %s | %s | %s | %s |" % (
                 pass_, n, h, w, c, kh, kw, co, s, k, t_lib,
-                ("%.3f (%s,%d,%d,v%d)" % best) if best else "n/a",
+                ("%.3f (%s,%s,%s,v%d)" % best) if best else "n/a",
                 ("%.3f" % t_wino) if t_wino is not None else "-",
                 ("%.0f" % (flops / best[0] / 1e9)) if best else "-", choice))
             print(lines[-1], flush=True)

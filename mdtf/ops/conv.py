@@ -95,7 +95,8 @@ def v2_ok(pass_, c, co, stride=(1, 1), taps=1, dil=(1, 1)):
 
 
 def choose(pass_, x_shape, w_shape, stride, pads, dil):
-    """-> ('mdtf', bm, bn, splits, version, stages) or ('miopen',).
+    """-> ('mdtf', bm, bn, splits, version, stages), ('ws', (tp, nw, cg, d)) (the weight-stationary
+    kernel, csrc/conv_ws.hip), ('winograd',) or ('miopen',).
 
     ``MDTF_CONV``: ``auto`` (table, else defaults), ``mdtf`` (v1 kernels),
     ``mdtf2`` (v2 kernels where the channels allow, else v1), ``miopen``.
@@ -116,6 +117,10 @@ def choose(pass_, x_shape, w_shape, stride, pads, dil):
     if forced == "auto" and ent is not None:
         if ent["backend"] in ("miopen", "winograd"):
             return (ent["backend"],)
+        if ent.get("ver") == 4:
+            if N.deterministic():                # cross-block statistics atomics: use the v2 kernels
+                return ("mdtf", 128, 128 if (co if pass_ == "fwd" else c) % 128 == 0 else 64, 0, 2, 2)
+            return ("ws", tuple(ent["ws"]))
         return ("mdtf", ent["bm"], ent["bn"], ent.get("splits", 0), ent.get("ver", 1), ent.get("stages", 2))
     if pass_ == "wgrad":
         r = kh * kw * ci
@@ -239,6 +244,74 @@ def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn, ver=1, stages=2, out=N
     if accumulate:
         raise ValueError("accumulating dgrad needs the v2 kernel")
     N.check(N.fn("mdtf_conv_dgrad")(N.ptr(dy), N.ptr(w), N.ptr(dx), *geo, bm, bn, N.stream_ptr()), "conv_dgrad")
+    return dx
+
+
+N.register("mdtf_conv_ws", [N.P, N.P, N.P] + [N.I] * 16 + [N.I, N.I] +
+           [N.P, N.P, N.I, N.P, N.P, N.P, N.P, N.I, N.I, N.P])
+
+
+def ws_ok(pass_, c, co, stride, kh, kw, dil=(1, 1)):
+    """Shapes the weight-stationary kernel (csrc/conv_ws.hip) takes: the reduced channels % 32,
+    output channels % 64, the block's filter slice (64 output channels x K) <= 144 KiB of LDS;
+    dgrad stride 1 only."""
+    if pass_ == "fwd":
+        red, ncol = c, co
+    elif pass_ == "dgrad":
+        if tuple(stride) != (1, 1):
+            return False
+        red, ncol = co, c
+    else:
+        return False
+    return red % 32 == 0 and ncol % 64 == 0 and kh * kw <= 32 and 64 * kh * kw * red * 2 <= 160 * 1024
+
+
+def ws_depth_ok(k_total, d):
+    """Load-ring depths the kernel instantiates for a reduction of ``k_total`` (csrc/conv_ws.hip
+    dispatch_ws_d): K = 64 -> 2 or 4, K = 128 -> 4, longer K -> 3, 4 or 6 dividing K / 32."""
+    ks = k_total // 32
+    if ks in (1, 2):
+        return d in (2, 4)
+    if ks == 3:
+        return d == 3
+    if ks == 4:
+        return d == 4
+    return ks > 4 and d in (3, 4, 6) and ks % d == 0
+
+
+def _ws_code(tp, nw, cg, d=4):
+    """C-ABI tile code of csrc/conv_ws.hip: pixel subtiles, waves, channel groups, load-ring depth."""
+    return tp + 10 * nw + 100 * cg + 1000 * d
+
+
+def ws_fwd(x, wt, kh, kw, out_hw, stride, pads, dil, tile, stats=None, grid_cap=0):
+    """Y = conv(X, W) on the weight-stationary kernel; ``wt`` = Wt[co][(kh,kw,ci)]
+    (:func:`transpose_filter`).  ``tile`` = (tp, nw, cg[, d])."""
+    n, h, wd, c = x.shape
+    co = wt.shape[0]
+    y = torch.empty((n, out_hw[0], out_hw[1], co), dtype=x.dtype, device=x.device)
+    s_sum, s_sq = stats if stats is not None else (None, None)
+    slots = s_sum.shape[0] if s_sum is not None else 0
+    N.check(N.fn("mdtf_conv_ws")(N.ptr(x), N.ptr(wt), N.ptr(y), n, h, wd, c, out_hw[0], out_hw[1], co, kh, kw,
+                                 stride[0], stride[1], pads[0], pads[2], dil[0], dil[1], 0, _ws_code(*tile),
+                                 int(grid_cap), N.ptr(s_sum), N.ptr(s_sq), slots, N.ptr(None), N.ptr(None),
+                                 N.ptr(None), N.ptr(None), 0, 0, N.stream_ptr()), "conv_ws_fwd")
+    return y
+
+
+def ws_dgrad(dy, w, x_shape, pads, dil, tile, out=None, accumulate=False, bn_stats=None, grid_cap=0):
+    """DX of a stride-1 conv on the weight-stationary kernel (the filter used flipped, HWIO as is).
+    ``bn_stats = (x, relu_mask or None, psum, psq, slots)`` as in :func:`mdtf_dgrad`."""
+    n, h, wd, ci = x_shape
+    kh, kw, _, co = w.shape
+    dx = out if out is not None else torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
+    ph = (kh - 1) * dil[0] - pads[0]
+    pw = (kw - 1) * dil[1] - pads[2]
+    bx, bmask, bsum, bsq, bslots = bn_stats if bn_stats is not None else (None, None, None, None, 0)
+    N.check(N.fn("mdtf_conv_ws")(N.ptr(dy), N.ptr(w), N.ptr(dx), n, dy.shape[1], dy.shape[2], co, h, wd, ci, kh, kw,
+                                 1, 1, ph, pw, dil[0], dil[1], 1, _ws_code(*tile), int(grid_cap), N.ptr(None),
+                                 N.ptr(None), 0, N.ptr(bx), N.ptr(bmask), N.ptr(bsum), N.ptr(bsq), int(bslots),
+                                 int(bool(accumulate)), N.stream_ptr()), "conv_ws_dgrad")
     return dx
 
 
@@ -366,6 +439,11 @@ class _Conv(torch.autograd.Function):
                 buf = _stats_buffer(co, x.device, slots)
                 stats = (buf[0], buf[1])
             y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2], stats, ch[4], ch[5])
+        elif ch[0] == "ws":
+            if want_stats:
+                buf = _stats_buffer(w.shape[3], x.device, STAT_SLOTS)
+                stats = (buf[0], buf[1])
+            y = ws_fwd(x, transpose_filter(w), w.shape[0], w.shape[1], out_hw, stride, pads, dil, ch[1], stats)
         elif ch[0] == "winograd":
             y = winograd.winograd_fwd(x, w, out_hw, pads)
         else:
@@ -410,6 +488,21 @@ class _Conv(torch.autograd.Function):
         xs = ctx.x_sink if need_dx else None
         if need_dx and cd[0] == "winograd":
             dx = winograd.winograd_dgrad(dy, w, x.shape, pads)
+        elif need_dx and cd[0] == "ws":
+            tile = cd[1]
+            if xs is not None:
+                buf, acc = xs.target()
+                bst = None
+                if xs.stat_req is not None and xs.completing() and BWD_STATS:
+                    bx, bmask = xs.stat_req
+                    sbuf = bwd_stats_acquire(x.device, x.shape[3], STAT_SLOTS)
+                    bst = (bx, bmask, sbuf[0], sbuf[1], sbuf.shape[1])
+                    tile = (2,) + tuple(tile[1:])      # the statistics epilogue's register budget
+                xs.written(ws_dgrad(dy, w, x.shape, pads, dil, tile, out=buf, accumulate=acc, bn_stats=bst))
+                if bst is not None:
+                    xs.stats = sbuf
+            else:
+                dx = ws_dgrad(dy, w, x.shape, pads, dil, tile)
         elif need_dx and not lib_dx:
             if xs is not None and cd[4] in (2, 3):
                 buf, acc = xs.target()

@@ -1000,3 +1000,68 @@ def test_conv_wgrad_8wave_tiles(bm, bn, stages, geo, slab, monkeypatch):
         dw = C.mdtf_wgrad(x.to(DEV), dy.permute(0, 2, 3, 1).contiguous().to(DEV), wt.shape, (s, s), pads, (1, 1),
                           bm, bn, sp, ver=3, stages=stages)
         assert _rel(dw, ref) < 1e-2, sp
+
+
+WS_TILES = [(4, 8, 1, 4), (4, 8, 2, 6), (4, 4, 1, 4), (2, 8, 1, 8), (2, 4, 2, 4), (4, 8, 4, 4)]
+
+
+@pytest.mark.parametrize("tile", WS_TILES)
+@pytest.mark.parametrize("geo", [(3, 9, 9, 64, 1, 256, 1), (2, 12, 11, 128, 3, 128, 1), (2, 15, 13, 64, 3, 64, 2),
+                                 (4, 7, 7, 256, 1, 512, 2), (2, 6, 9, 96, 1, 128, 1)])
+def test_conv_weight_stationary(tile, geo):
+    """csrc/conv_ws.hip: forward (any stride, padded 3x3) with the fused BN-statistics epilogue, stride-1
+    dgrad (flipped filter) plain / accumulating / with the BN-backward statistics, vs fp32 references;
+    pixel tails, channel groups, persistent tile loops."""
+    from mdtf.ops import conv as C
+    n, h, w, c, k, co, s = geo
+    tp, nw, cg, d = tile
+    if co % (64 * cg) or (c % (64 * cg) and s == 1) or 64 * cg * k * k * max(c, co) * 2 > 160 * 1024:
+        cg = 1
+        tile = (tp, nw, 1, d)
+    kf, kd = k * k * c, k * k * co                           # forward / dgrad reduction lengths
+    pick = lambda kt: d if C.ws_depth_ok(kt, d) else next(x for x in (4, 3, 6, 2) if C.ws_depth_ok(kt, x))  # noqa
+    tile = (tp, nw, cg, pick(kf))
+    torch.manual_seed(sum(geo) + tp * nw * cg)
+    p = k // 2
+    pads = (p, p, p, p)
+    oh = (h + 2 * p - k) // s + 1
+    ow = (w + 2 * p - k) // s + 1
+    x = torch.randn(n, h, w, c).bfloat16()
+    wt = (torch.randn(k, k, c, co) / (k * k * c) ** 0.5).bfloat16()
+    xr = x.float().permute(0, 3, 1, 2)
+    yr = torch.nn.functional.conv2d(xr, wt.float().permute(3, 2, 0, 1), stride=s, padding=p).permute(0, 2, 3, 1)
+    assert C.ws_ok("fwd", c, co, (s, s), k, k)
+    for cap in (0, 3):                                       # default persistent grid and a tiny one (long loops)
+        sbuf = torch.zeros(2, 8, co, device=DEV)
+        y = C.ws_fwd(x.to(DEV), C.transpose_filter(wt.to(DEV)), k, k, (oh, ow), (s, s), pads, (1, 1), tile,
+                     (sbuf[0], sbuf[1]), grid_cap=cap)
+        assert _rel(y, yr) < 1e-2, cap
+        yf = yr.reshape(-1, co)
+        assert _rel(sbuf[0].sum(0), yf.sum(0)) < 5e-3
+        assert _rel(sbuf[1].sum(0), (yf * yf).sum(0)) < 5e-3
+    if s != 1 or c % (64 * cg):
+        return
+    dy = torch.randn(n, oh, ow, co).bfloat16()
+    xg = torch.zeros(n, c, h, w, requires_grad=True)
+    yg = torch.nn.functional.conv2d(xg, wt.float().permute(3, 2, 0, 1), stride=s, padding=p)
+    yg.backward(dy.float().permute(0, 3, 1, 2))
+    ref = xg.grad.permute(0, 2, 3, 1)
+    assert C.ws_ok("dgrad", c, co, (s, s), k, k)
+    tile = (tp, nw, cg, pick(kd))
+    dx = C.ws_dgrad(dy.to(DEV), wt.to(DEV), (n, h, w, c), pads, (1, 1), tile)
+    assert _rel(dx, ref) < 1e-2
+    base = torch.randn(n, h, w, c).bfloat16()
+    out = base.to(DEV).clone()
+    C.ws_dgrad(dy.to(DEV), wt.to(DEV), (n, h, w, c), pads, (1, 1), tile, out=out, accumulate=True, grid_cap=5)
+    assert _rel(out, ref + base.float()) < 1e-2
+    # BN-backward statistics of the stored gradient: sum g*mask, sum g*mask*x
+    bx = torch.randn(n, h, w, c).bfloat16()
+    mbits = torch.rand(n * h * w * c) > 0.4
+    packed = (mbits.view(-1, 8).to(torch.int32) << torch.arange(8)).sum(1).to(torch.uint8)
+    bsum = torch.zeros(2, 4, c, device=DEV)
+    tile_b = (2, nw, cg, tile[3])                          # BN-statistics epilogues: 2-subtile tiles
+    gd = C.ws_dgrad(dy.to(DEV), wt.to(DEV), (n, h, w, c), pads, (1, 1), tile_b,
+                    bn_stats=(bx.to(DEV), packed.to(DEV), bsum[0], bsum[1], 4))
+    gm = gd.float().cpu().reshape(-1, c) * mbits.view(-1, c).float()
+    assert _rel(bsum[0].sum(0), gm.sum(0)) < 5e-3
+    assert _rel(bsum[1].sum(0), (gm * bx.float().reshape(-1, c)).sum(0)) < 5e-3
