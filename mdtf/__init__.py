@@ -21,3 +21,4 @@ from .train.step import placeholder  # noqa: F401
 from .cluster import ClusterSpec, Server  # noqa: F401
 from . import app  # noqa: F401
 from . import estimator  # noqa: F401
+from . import errors  # noqa: F401

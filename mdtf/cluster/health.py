@@ -17,7 +17,8 @@ the only recovery path.  Here:
 * :class:`FaultInjectionHook` — a SessionRunHook that kills (or hangs) the
   process of one chosen task at a given global step, driven by environment
   variables (``MDTF_FAULT_STEP``, ``MDTF_FAULT_TASK=worker:1``,
-  ``MDTF_FAULT_MODE=exit|hang``); it only fires on the first attempt
+  ``MDTF_FAULT_MODE=exit|hang|abort|unavailable``; abort/unavailable raise the TF error in-process,
+  which the MonitoredSession recovers from without a restart); it only fires on the first attempt
   (``MDTF_RESTART_ATTEMPT=0``) so a restarted job runs clean.
 * :func:`supervise` — runs a set of task commands, and when any of them fails,
   stops the rest and restarts the whole set (up to ``max_restarts`` times)
@@ -153,6 +154,12 @@ class FaultInjectionHook(H.SessionRunHook):
         if not self.armed or V.get_global_step().value() < self.step:
             return
         logger.error("injected fault at global step %d (%s)" % (V.get_global_step().value(), self.mode))
+        if self.mode in ("abort", "unavailable"):
+            # in-process recoverable fault: the MonitoredSession re-creates itself from the checkpoint
+            from .. import errors
+            self.armed = False
+            cls = errors.AbortedError if self.mode == "abort" else errors.UnavailableError
+            raise cls(message="injected %s at global step %d" % (self.mode, V.get_global_step().value()))
         if self.mode == "hang":
             while True:
                 time.sleep(3600)

@@ -16,6 +16,14 @@ Creation protocol (TF1 semantics):
   4. hooks: ``begin`` → create → ``after_create_session``.
 ``close`` runs ``end`` on every hook (the checkpoint hook saves a final
 checkpoint) and is safe to call twice.
+
+Recovery (TF's ``_RecoverableSession``): a ``run`` that raises ``mdtf.errors.AbortedError`` /
+``UnavailableError`` (or a transient store failure, ``mdtf.errors.as_recoverable``) re-creates the
+session in this process — captured step graphs released, the latest checkpoint restored (else the
+chief's broadcast state), hooks' ``after_create_session`` called again — and retries the step, up to
+``max_recoveries`` times.  With several replicas every one of them must see the error (a collective
+restore); a single replica's failure is handled one level up, by the job supervisor's restart
+(``mdtf.cluster.health.supervise``).
 """
 import os
 import time
@@ -128,8 +136,11 @@ class Session(object):
 
 class MonitoredSession(Session):
     def __init__(self, hooks=None, is_chief=True, checkpoint_dir=None, scaffold=None, server=None,
-                 stop_grace_period_secs=120):
+                 stop_grace_period_secs=120, max_recoveries=None):
         super(MonitoredSession, self).__init__()
+        self.max_recoveries = int(os.environ.get("MDTF_MAX_RECOVERIES", "3")) if max_recoveries is None \
+            else int(max_recoveries)
+        self.recoveries = 0
         self._hooks = list(hooks or [])
         self.is_chief = is_chief
         self.checkpoint_dir = checkpoint_dir
@@ -242,6 +253,30 @@ class MonitoredSession(Session):
 
     # -- running -----------------------------------------------------------
     def run(self, fetches, feed_dict=None, options=None, run_metadata=None):
+        from .. import errors
+        while True:
+            try:
+                return self._run_once(fetches, feed_dict)
+            except Exception as e:  # noqa: BLE001 - classified below
+                err = errors.as_recoverable(e)
+                if err is None or self.recoveries >= self.max_recoveries:
+                    raise
+                self.recoveries += 1
+                logger.warn("session run failed with %s (%s); re-creating the session (recovery %d of %d)" % (
+                    type(err).__name__, err, self.recoveries, self.max_recoveries))
+                self._recreate()
+
+    def _recreate(self):
+        """Drop per-session device state and create again: restore the latest checkpoint, re-broadcast."""
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        S.release_graphs()
+        self.restored_from = None
+        self._create()
+        for h in self._hooks:
+            h.after_create_session(self, None)
+
+    def _run_once(self, fetches, feed_dict=None):
         if self._stop:
             raise RuntimeError("Run called even after should_stop requested.")
         args = H.SessionRunArgs(fetches, feed_dict)
@@ -314,7 +349,7 @@ def MonitoredTrainingSession(master="", is_chief=True, checkpoint_dir=None, scaf
                              chief_only_hooks=None, save_checkpoint_secs=600, save_summaries_steps=100,
                              save_summaries_secs=None, config=None, stop_grace_period_secs=120,
                              log_step_count_steps=100, max_wait_secs=7200, save_checkpoint_steps=None,
-                             summary_dir=None, server=None):
+                             summary_dir=None, server=None, max_recoveries=None):
     """TF1's MonitoredTrainingSession factory with the same default hooks.
 
     Sharded mode (``SyncReplicasOptimizer(mode='sharded')``, the PS-shard data-parallel path) with more
@@ -346,4 +381,5 @@ def MonitoredTrainingSession(master="", is_chief=True, checkpoint_dir=None, scaf
             all_hooks.append(H.CheckpointSaverHook(
                 checkpoint_dir, save_secs=save_checkpoint_secs if not save_checkpoint_steps else None,
                 save_steps=save_checkpoint_steps, scaffold=scaffold))
-    return MonitoredSession(all_hooks, is_chief, checkpoint_dir, scaffold, server, stop_grace_period_secs)
+    return MonitoredSession(all_hooks, is_chief, checkpoint_dir, scaffold, server, stop_grace_period_secs,
+                            max_recoveries=max_recoveries)

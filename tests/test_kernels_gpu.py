@@ -296,7 +296,7 @@ def test_conv_transpose_hip(monkeypatch):
     assert _rel(wg.grad, wc.grad) < 2e-2
 
 
-def _one_step(dev, dtype, x, y, depth=50):
+def _one_step(dev, dtype, x, y, depth=50, blocks=None, grads=False):
     import mdtf
     from mdtf.models import ResNet, SoftmaxCrossEntropyLoss
     from mdtf.runtime import Net, Tower
@@ -312,13 +312,17 @@ def _one_step(dev, dtype, x, y, depth=50):
     yp = mdtf.placeholder(torch.int64, [None])
     opt = mdtf.train.GradientDescentOptimizer(0.1)
     tg = []
-    tower = Tower(Net(ResNet(depth, num_classes=16, zero_init_residual=False)), "tower_0/", tg, xp, yp,
-                  SoftmaxCrossEntropyLoss(), opt, batch_size=x.shape[0])
+    model = ResNet(depth, num_classes=16, zero_init_residual=False)
+    if blocks is not None:
+        model.blocks = blocks                    # a shallower net of the same bottleneck / BN / kernel structure
+    tower = Tower(Net(model), "tower_0/", tg, xp, yp, SoftmaxCrossEntropyLoss(), opt, batch_size=x.shape[0])
     _, loss, _ = tower.process()
     op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
     sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
     before = {v.name: v.master.detach().float().cpu().clone() for v in store.trainable_variables()}
     _, lv = sess.run([op, loss], feed_dict={xp: x, yp: y})
+    if grads:
+        return float(lv), {v.name: v.grad.detach().float().cpu().clone() for v in store.trainable_variables()}
     after = {v.name: v.master.detach().float().cpu().clone() for v in store.trainable_variables()}
     return float(lv), before, after
 
@@ -340,6 +344,31 @@ def test_resnet50_step_loss_matches_cpu_fp32_reference():
         assert torch.equal(b_cpu[name], b_gpu[name]), name          # identical init
     n = "resnet_v1_50/logits/kernel"
     assert _rel(a_gpu[n] - b_gpu[n], a_cpu[n] - b_cpu[n]) < 0.35
+
+
+def test_resnet_stage1_every_gradient_matches_cpu_fp32(monkeypatch):
+    """Every gradient tensor (each conv weight, BN gamma/beta, the dense layer) of a ResNet-v1.5 with
+    the full stage 1 (3 bottleneck units incl. the projection shortcut) and the first stage-2 unit
+    (strided 3x3, strided projection), batch 16: GPU bf16 (mdtf kernels) vs the fp32 CPU engine, next
+    to the same step on stock PyTorch bf16 ops (MDTF_KERNELS=torch: MIOpen / hipBLASLt) as the measure
+    of what bf16 itself costs.  Each mdtf gradient must be within 5 % of fp32, or no worse than 1.25x
+    the stock bf16 error for tensors where bf16 alone exceeds that (BN parameters of layers followed by
+    another BN get gradients that nearly cancel over the batch)."""
+    torch.manual_seed(5)
+    x = torch.randn(16, 64, 64, 3)
+    y = torch.randint(0, 16, (16,))
+    l_cpu, g_cpu = _one_step("cpu", None, x, y, blocks=[3, 1], grads=True)
+    l_gpu, g_gpu = _one_step(DEV, torch.bfloat16, x, y, blocks=[3, 1], grads=True)
+    monkeypatch.setenv("MDTF_KERNELS", "torch")
+    l_stk, g_stk = _one_step(DEV, torch.bfloat16, x, y, blocks=[3, 1], grads=True)
+    monkeypatch.setenv("MDTF_KERNELS", "native")
+    assert abs(l_cpu - l_gpu) / abs(l_cpu) < 5e-3, (l_cpu, l_gpu)
+    errs = {k: (_rel(g_gpu[k], g_cpu[k]), _rel(g_stk[k], g_cpu[k])) for k in g_cpu}
+    worst = sorted(errs.items(), key=lambda kv: -kv[1][0])[:8]
+    print("worst relative gradient errors (mdtf, stock bf16):", worst)
+    assert len(errs) > 40
+    for k, (e, e_stock) in errs.items():
+        assert e < max(0.05, 1.25 * e_stock), (k, e, e_stock)
 
 
 class _Tiny(object):
