@@ -327,23 +327,24 @@ def _one_step(dev, dtype, x, y, depth=50, blocks=None, grads=False):
     return float(lv), before, after
 
 
-def test_resnet50_step_loss_matches_cpu_fp32_reference():
-    """ResNet-50 training forward (fused conv+BN, pooling, dense, xent) vs the fp32 CPU engine.
-
-    Per-weight gradients of a random-init 50-layer net at batch 16 are too
-    sensitive to bf16 rounding to compare elementwise; the exact-gradient check
-    is ``test_engine_step_matches_cpu_fp32_reference`` on a shallower net.
-    """
+def test_resnet50_step_loss_matches_cpu_fp32_reference(monkeypatch):
+    """ResNet-50 training step (fused conv+BN, pooling, dense, xent) vs the fp32 CPU engine: the loss
+    within 1.5 %, and EVERY gradient tensor within max(5 %, 1.25 x the error of the same step on stock
+    PyTorch bf16 ops) -- at batch 16 a random-init 50-layer net's deep gradients differ from fp32 by tens
+    of percent under any bf16 implementation, so stock bf16 is the yardstick."""
     torch.manual_seed(9)
     x = torch.randn(16, 64, 64, 3)
     y = torch.randint(0, 16, (16,))
-    l_cpu, b_cpu, a_cpu = _one_step("cpu", None, x, y)
-    l_gpu, b_gpu, a_gpu = _one_step(DEV, torch.bfloat16, x, y)
-    assert abs(l_cpu - l_gpu) / abs(l_cpu) < 2e-2, (l_cpu, l_gpu)
-    for name in a_cpu:
-        assert torch.equal(b_cpu[name], b_gpu[name]), name          # identical init
-    n = "resnet_v1_50/logits/kernel"
-    assert _rel(a_gpu[n] - b_gpu[n], a_cpu[n] - b_cpu[n]) < 0.35
+    l_cpu, g_cpu = _one_step("cpu", None, x, y, grads=True)
+    l_gpu, g_gpu = _one_step(DEV, torch.bfloat16, x, y, grads=True)
+    monkeypatch.setenv("MDTF_KERNELS", "torch")
+    l_stk, g_stk = _one_step(DEV, torch.bfloat16, x, y, grads=True)
+    monkeypatch.setenv("MDTF_KERNELS", "native")
+    assert abs(l_cpu - l_gpu) / abs(l_cpu) < 1.5e-2, (l_cpu, l_gpu, l_stk)
+    assert len(g_cpu) > 150
+    for k in g_cpu:
+        e, e_stock = _rel(g_gpu[k], g_cpu[k]), _rel(g_stk[k], g_cpu[k])
+        assert e < max(0.05, 1.25 * e_stock), (k, e, e_stock)
 
 
 def test_resnet_stage1_every_gradient_matches_cpu_fp32(monkeypatch):
@@ -424,9 +425,13 @@ def test_engine_step_matches_cpu_fp32_reference(conv_backend, monkeypatch):
     y = torch.randint(0, 16, (32,))
     lc, gc = _tiny_step("cpu", None, x, y)
     lg, gg = _tiny_step(DEV, torch.bfloat16, x, y)
+    monkeypatch.setenv("MDTF_KERNELS", "torch")
+    _, gs = _tiny_step(DEV, torch.bfloat16, x, y)
+    monkeypatch.setenv("MDTF_KERNELS", "native")
     assert abs(lc - lg) / lc < 5e-3
     for k in gc:
-        assert _rel(gg[k], gc[k]) < 0.15, (k, _rel(gg[k], gc[k]))
+        e, e_stock = _rel(gg[k], gc[k]), _rel(gs[k], gc[k])
+        assert e < max(0.05, 1.5 * e_stock), (k, e, e_stock)    # (was: every gradient within 15 %)
 
 
 @pytest.mark.parametrize("shape,k,s,co,relu,res", [((8, 14, 14, 64), 3, 1, 64, True, False),
