@@ -42,7 +42,8 @@ struct WsArgs {
   const bf16_t* src;     // gathered operand [N][H][W][C]
   const bf16_t* wgt;     // filter (layout by wmode)
   bf16_t* out;           // [M][Ncol]
-  int N, H, W, C;        // src dims; C % 32 == 0
+  int N, H, W, C;        // src dims; C % 32 == 0 (the reduction elements per filter tap)
+  int cs;                // elements between neighbouring src pixels (C, or 4 for the packed stem input)
   int OH, OW, Ncol;      // output pixel grid, output channels (Ncol % (64*CG) == 0)
   int KH, KW, SH, SW, PH, PW, DH, DW;
   int Cw;                // wmode 1: channels of W's last axis (the conv's Cout == C); wmode 0: unused
@@ -148,7 +149,7 @@ __global__ void __launch_bounds__(64 * NW, 2) conv_ws_kernel(WsArgs a) {
   const int n0 = (cb * CG + cg) * 64;                  // this wave's first output channel
   const char* wfr = lds + (size_t)cg * KS * 4 * 1024 + lane * 16;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(a.src), (short)0, (int)((long long)a.N * a.H * a.W * a.C * 2), 0x00020000);
+      const_cast<bf16_t*>(a.src), (short)0, (int)((long long)a.N * a.H * a.W * a.cs * 2), 0x00020000);
   const int tstride = a.pgroups * PS;
   const int ntaps = a.KH * a.KW;
 
@@ -169,7 +170,7 @@ __global__ void __launch_bounds__(64 * NW, 2) conv_ws_kernel(WsArgs a) {
         const int q = (int)((__umulhi((unsigned)p, a.mow) + (unsigned)p) >> a.sow), ow = p - q * a.OW;
         const int n = (int)((__umulhi((unsigned)q, a.mohh) + (unsigned)q) >> a.sohh), oh = q - n * a.OH;
         const int y0 = oh * a.SH - a.PH, x0 = ow * a.SW - a.PW;
-        base = ((n * a.H + y0) * a.W + x0) * a.C;
+        base = ((n * a.H + y0) * a.W + x0) * a.cs;
         // separable validity: rows kh with 0 <= y0 + kh*DH < H, columns likewise
         unsigned rows = 0, cols = 0;
         for (int kh = 0; kh < a.KH; ++kh) rows |= (unsigned)((unsigned)(y0 + kh * a.DH) < (unsigned)a.H) << kh;
@@ -194,7 +195,7 @@ __global__ void __launch_bounds__(64 * NW, 2) conv_ws_kernel(WsArgs a) {
       tap = k / a.C;
       const int c0 = k - tap * a.C;
       const int kh = tap / a.KW, kw = tap - kh * a.KW;
-      toff = (kh * a.DH * a.W + kw * a.DW) * a.C + c0 + 8 * g;
+      toff = (kh * a.DH * a.W + kw * a.DW) * a.cs + c0 + 8 * g;
     }
 #pragma unroll
     for (int j = 0; j < TP; ++j) {
@@ -501,12 +502,13 @@ MDTF_EXPORT void mdtf_conv_ws_debug(int mode) { ws_debug = mode; }
 // 4 k-steps of loads in flight.  grid_cap: persistent blocks (0: 256 x
 // blocks per CU).  ssum/ssq: forward BN statistics ([sslots][Ncol] partial rows, or null);
 // bx/bmask/bsum/bsq: BN-backward statistics of the stored gradient (dgrad); accumulate: out += conv.
-MDTF_EXPORT int mdtf_conv_ws(const void* src, const void* wgt, void* out, int N, int H, int W, int C, int OH, int OW,
-                             int Ncol, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW, int wmode,
-                             int tile, int grid_cap, float* ssum, float* ssq, int sslots, const void* bx,
-                             const void* bmask, float* bsum, float* bsq, int bslots, int accumulate,
-                             hipStream_t st) {
+namespace {
+int conv_ws_impl(const void* src, const void* wgt, void* out, int N, int H, int W, int C, int cs, int OH, int OW,
+                 int Ncol, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW, int wmode, int tile,
+                 int grid_cap, float* ssum, float* ssq, int sslots, const void* bx, const void* bmask, float* bsum,
+                 float* bsq, int bslots, int accumulate, hipStream_t st) {
   WsArgs a{};
+  a.cs = cs;
   a.src = (const bf16_t*)src;
   a.wgt = (const bf16_t*)wgt;
   a.out = (bf16_t*)out;
@@ -521,13 +523,13 @@ MDTF_EXPORT int mdtf_conv_ws(const void* src, const void* wgt, void* out, int N,
   a.bx = (const bf16_t*)bx; a.bmask = (const uint8_t*)bmask; a.bsum = bsum; a.bsq = bsq;
   a.bslots = bslots > 0 ? bslots : 1;
   a.accumulate = accumulate;
-  a.direct = (KH == 1 && KW == 1 && SH == 1 && SW == 1 && PH == 0 && PW == 0 && OH == H && OW == W) ? 1 : 0;
+  a.direct = (KH == 1 && KW == 1 && SH == 1 && SW == 1 && PH == 0 && PW == 0 && OH == H && OW == W && cs == C) ? 1 : 0;
   magic_div((unsigned)OW, a.mow, a.sow);
   magic_div((unsigned)OH, a.mohh, a.sohh);
   const int tp = tile % 10, nw = (tile / 10) % 10, cg = (tile / 100) % 10, d = tile / 1000;
   if (C % 32 || cg < 1 || Ncol % (64 * cg) || KH * KW > 32 || a.M <= 0) return MDTF_EINVAL;
   if (wmode == 1 && (SH != 1 || SW != 1)) return MDTF_EINVAL;
-  if ((long long)N * H * W * C * 2 >= 0x80000000LL) return MDTF_EUNSUPPORTED;   // 32-bit buffer offsets
+  if ((long long)N * H * W * cs * 2 >= 0x80000000LL) return MDTF_EUNSUPPORTED;  // 32-bit buffer offsets
   if (a.M + 16LL * 8 * 64 >= 0x7fffffffLL) return MDTF_EUNSUPPORTED;           // 32-bit pixel indices
   if (nw % cg) return MDTF_EINVAL;
   a.dbg = ws_debug;
@@ -537,4 +539,62 @@ MDTF_EXPORT int mdtf_conv_ws(const void* src, const void* wgt, void* out, int N,
   if (bstat) return accumulate ? dispatch_ws<4>(a, tp, nw, cg, d, grid_cap, st)
                                : dispatch_ws<3>(a, tp, nw, cg, d, grid_cap, st);
   return accumulate ? dispatch_ws<2>(a, tp, nw, cg, d, grid_cap, st) : dispatch_ws<0>(a, tp, nw, cg, d, grid_cap, st);
+}
+}  // namespace
+
+MDTF_EXPORT int mdtf_conv_ws(const void* src, const void* wgt, void* out, int N, int H, int W, int C, int OH, int OW,
+                             int Ncol, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW, int wmode,
+                             int tile, int grid_cap, float* ssum, float* ssq, int sslots, const void* bx,
+                             const void* bmask, float* bsum, float* bsq, int bslots, int accumulate,
+                             hipStream_t st) {
+  return conv_ws_impl(src, wgt, out, N, H, W, C, C, OH, OW, Ncol, KH, KW, SH, SW, PH, PW, DH, DW, wmode, tile,
+                      grid_cap, ssum, ssq, sslots, bx, bmask, bsum, bsq, bslots, accumulate, st);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Stem convolution (Cin <= 4, KW <= 8: ResNet's 7x7/2 on RGB).  The input is repacked once into a
+// zero-haloed 4-channel image x4[N][H+pt+pb][W+pl+pr][4] (8 B per pixel), so the KW taps x 4
+// channels of one filter row are 32 contiguous, 16-B aligned elements for every output pixel
+// (stride 2 keeps 2*ow*8 B aligned).  The forward is then the weight-stationary GEMM with one
+// 32-deep k-step per filter row (rows padded to a multiple of 4 with zero weights), reading its B
+// fragments straight from x4: no im2col, no library call.
+// ---------------------------------------------------------------------------------------------
+namespace {
+__global__ void __launch_bounds__(256) stem_pack4(const bf16_t* __restrict__ x, uint2* __restrict__ x4, int N, int H,
+                                                  int W, int C, int pt, int pl, int H4, int W4) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)N * H4 * W4;
+  if (i >= total) return;
+  const int xw = (int)(i % W4);
+  const long long q = i / W4;
+  const int yh = (int)(q % H4);
+  const int n = (int)(q / H4);
+  const int ih = yh - pt, iw = xw - pl;
+  uint32_t v[4] = {0u, 0u, 0u, 0u};
+  if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
+    const bf16_t* p = x + (((long long)n * H + ih) * W + iw) * C;
+    for (int c = 0; c < C; ++c) v[c] = p[c];
+  }
+  x4[i] = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+}
+}  // namespace
+
+MDTF_EXPORT int mdtf_stem_pack4(const void* x, void* x4, int N, int H, int W, int C, int pt, int pl, int H4, int W4,
+                                hipStream_t st) {
+  if (C < 1 || C > 4) return MDTF_EINVAL;
+  const long long total = (long long)N * H4 * W4;
+  hipLaunchKernelGGL(stem_pack4, dim3((unsigned)ceil_div(total, 256LL)), dim3(256), 0, st, (const bf16_t*)x,
+                     (uint2*)x4, N, H, W, C, pt, pl, H4, W4);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// y = conv(x, W) for the stem: x4 from mdtf_stem_pack4 ([N][H4][W4][4]), wt = [Ncol][KHp][32] filter rows
+// (tap kw, channel c at element 4 kw + c; zero rows/taps past KH / KW), KHp % 4 == 0.
+MDTF_EXPORT int mdtf_conv_ws_stem(const void* x4, const void* wt, void* out, int N, int H4, int W4, int OH, int OW,
+                                  int Ncol, int KHp, int SH, int SW, int tile, float* ssum, float* ssq, int sslots,
+                                  hipStream_t st) {
+  if ((OH - 1) * SH + KHp > H4 + 3 || (OW - 1) * SW + 8 > W4) return MDTF_EINVAL;   // rows / taps stay in x4
+  return conv_ws_impl(x4, wt, out, N, H4, W4, 32, 4, OH, OW, Ncol, KHp, 1, SH, SW, 0, 0, 1, 1, 0, tile, 0, ssum,
+                      ssq, sslots, nullptr, nullptr, nullptr, nullptr, 0, 0, st);
 }

@@ -105,6 +105,8 @@ def choose(pass_, x_shape, w_shape, stride, pads, dil):
     kh, kw, ci, co = w_shape
     forced = os.environ.get("MDTF_CONV", "auto")
     native_ok = c % 8 == 0 and co % 8 == 0
+    if pass_ == "fwd" and not native_ok and stem_ok(x_shape, w_shape, dil):
+        return ("stem",)
     if not native_ok or forced == "miopen":
         return ("miopen",)
     if pass_ in ("fwd", "dgrad") and winograd.enabled() and winograd.eligible(w_shape, stride, pads, dil, c, co):
@@ -264,6 +266,42 @@ def ws_ok(pass_, c, co, stride, kh, kw, dil=(1, 1)):
     else:
         return False
     return red % 32 == 0 and ncol % 64 == 0 and kh * kw <= 32 and 64 * kh * kw * red * 2 <= 160 * 1024
+
+
+N.register("mdtf_stem_pack4", [N.P, N.P] + [N.I] * 8 + [N.P])
+N.register("mdtf_conv_ws_stem", [N.P, N.P, N.P] + [N.I] * 10 + [N.P, N.P, N.I, N.P])
+STEM = os.environ.get("MDTF_STEM", "mdtf")          # mdtf: hand-written stem forward | miopen
+STEM_TILE = (4, 4, 1, 4)          # bench/stem_ws_probe.py: 0.329 ms vs MIOpen 0.487 (batch 256)
+
+
+def stem_ok(x_shape, w_shape, dil):
+    """Few-channel stems (Cin <= 4, KW <= 8, undilated): csrc/conv_ws.hip mdtf_conv_ws_stem."""
+    kh, kw, ci, co = w_shape
+    return (STEM != "miopen" and ci <= 4 and kw <= 8 and co % 64 == 0 and tuple(dil) == (1, 1)
+            and os.environ.get("MDTF_CONV", "auto") != "miopen")
+
+
+def stem_fwd(x, w, out_hw, stride, pads, stats=None, tile=None):
+    """Stem forward: repack x into a zero-haloed 4-channel image (one kernel), then the weight-stationary
+    GEMM with one 32-deep k-step per filter row (filter rows packed [co][row][kw*4 + c], zero-padded)."""
+    n, h, wd, c = x.shape
+    kh, kw, ci, co = w.shape
+    pt, pb, pl, pr = pads
+    khp = -(-kh // 4) * 4
+    h4 = max(h + pt + pb, (out_hw[0] - 1) * stride[0] + khp)
+    w4 = max(wd + pl + pr, (out_hw[1] - 1) * stride[1] + 8)
+    x4 = torch.empty((n, h4, w4, 4), dtype=x.dtype, device=x.device)
+    N.check(N.fn("mdtf_stem_pack4")(N.ptr(x), N.ptr(x4), n, h, wd, c, pt, pl, h4, w4, N.stream_ptr()), "stem_pack4")
+    wp = torch.zeros((khp, 8, 4, co), dtype=x.dtype, device=x.device)
+    wp[:kh, :kw, :ci].copy_(w)
+    wt = wp.view(khp * 32, co).t().contiguous()              # [co][row][kw*4 + c]
+    y = torch.empty((n, out_hw[0], out_hw[1], co), dtype=x.dtype, device=x.device)
+    s_sum, s_sq = stats if stats is not None else (None, None)
+    slots = s_sum.shape[0] if s_sum is not None else 0
+    N.check(N.fn("mdtf_conv_ws_stem")(N.ptr(x4), N.ptr(wt), N.ptr(y), n, h4, w4, out_hw[0], out_hw[1], co, khp,
+                                      stride[0], stride[1], _ws_code(*(tile or STEM_TILE)), N.ptr(s_sum), N.ptr(s_sq),
+                                      slots, N.stream_ptr()), "conv_ws_stem")
+    return y
 
 
 def ws_depth_ok(k_total, d):
@@ -439,6 +477,11 @@ class _Conv(torch.autograd.Function):
                 buf = _stats_buffer(co, x.device, slots)
                 stats = (buf[0], buf[1])
             y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2], stats, ch[4], ch[5])
+        elif ch[0] == "stem":
+            if want_stats:
+                buf = _stats_buffer(w.shape[3], x.device, STAT_SLOTS)
+                stats = (buf[0], buf[1])
+            y = stem_fwd(x, w, out_hw, stride, pads, stats)
         elif ch[0] == "ws":
             if want_stats:
                 buf = _stats_buffer(w.shape[3], x.device, STAT_SLOTS)

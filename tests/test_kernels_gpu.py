@@ -1099,3 +1099,27 @@ def test_conv_weight_stationary(tile, geo):
     gm = gd.float().cpu().reshape(-1, c) * mbits.view(-1, c).float()
     assert _rel(bsum[0].sum(0), gm.sum(0)) < 5e-3
     assert _rel(bsum[1].sum(0), (gm * bx.float().reshape(-1, c)).sum(0)) < 5e-3
+
+
+@pytest.mark.parametrize("geo", [(2, 30, 31, 3, 7, 64, 2, 3), (3, 17, 16, 1, 5, 128, 1, 2), (2, 24, 24, 4, 3, 64, 2, 1),
+                                 (1, 224, 224, 3, 7, 64, 2, 3)])
+def test_stem_conv_forward(geo):
+    """Few-channel stem forward (repack to a haloed 4-channel image + weight-stationary GEMM) with the fused
+    BN-statistics epilogue vs the fp32 reference; ResNet's 7x7/2 RGB stem included."""
+    from mdtf.ops import conv as C
+    n, h, w, c, k, co, s, p = geo
+    torch.manual_seed(sum(geo))
+    x = torch.randn(n, h, w, c).bfloat16()
+    wt = (torch.randn(k, k, c, co) / (k * k * c) ** 0.5).bfloat16()
+    oh = (h + 2 * p - k) // s + 1
+    ow = (w + 2 * p - k) // s + 1
+    assert C.choose("fwd", x.shape, wt.shape, (s, s), (p, p, p, p), (1, 1)) == ("stem",)
+    yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wt.float().permute(3, 2, 0, 1), stride=s,
+                                    padding=p).permute(0, 2, 3, 1)
+    sbuf = torch.zeros(2, 8, co, device=DEV)
+    y = C.stem_fwd(x.to(DEV), wt.to(DEV), (oh, ow), (s, s), (p, p, p, p), (sbuf[0], sbuf[1]))
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 1e-2
+    yf = yr.reshape(-1, co)
+    assert _rel(sbuf[0].sum(0), yf.sum(0)) < 5e-3
+    assert _rel(sbuf[1].sum(0), (yf * yf).sum(0)) < 5e-3
