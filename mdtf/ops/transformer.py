@@ -5,6 +5,7 @@ gradients accumulate straight into the variables' fp32 grad slots when
 available).  CPU path: PyTorch reference implementations.
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -226,6 +227,15 @@ def attention(q, k, v, mask=None, dropout=0.0):
 
 
 FUSED_SEQ, FUSED_DIM = 128, 64      # shapes csrc/attention.hip is built for
+N.register("mdtf_attn_fwd_flash", [N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P, N.P])
+N.register("mdtf_attn_bwd_flash", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P, N.P])
+# MDTF_ATTN_FLASH=1: the tiled kernels (csrc/attention_flash.hip) at S = 128 too (A/B)
+FLASH_ALWAYS = os.environ.get("MDTF_ATTN_FLASH", "0") == "1"
+
+
+def flash_ok(seq, dh):
+    """Shapes of the tiled kernels: any S % 128 == 0, head dim 64 or 128."""
+    return seq % 128 == 0 and seq >= 128 and dh in (64, 128)
 
 
 class _FusedAttention(torch.autograd.Function):
@@ -234,25 +244,34 @@ class _FusedAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, mask, B, S_, nh, p_drop, seed):
         qkv = qkv.contiguous()
-        H = nh * FUSED_DIM
+        dh = qkv.shape[-1] // 3 // nh
+        H = nh * dh
         out = torch.empty((B * S_, H), dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty((B * nh, S_), dtype=torch.float32, device=qkv.device)
         m = mask.float().contiguous() if mask is not None else None
-        scale = 1.0 / math.sqrt(FUSED_DIM)
-        N.check(N.fn("mdtf_attn_fwd")(N.ptr(qkv), N.ptr(m), N.ptr(out), N.ptr(lse), B, S_, nh, FUSED_DIM, scale,
-                                      float(p_drop), seed, N.ptr(_seed_off(p_drop, qkv.device)), N.stream_ptr()),
-                "attn_fwd")
+        scale = 1.0 / math.sqrt(dh)
+        ctx.flash = FLASH_ALWAYS or not (S_ == FUSED_SEQ and dh == FUSED_DIM)
+        name = "mdtf_attn_fwd_flash" if ctx.flash else "mdtf_attn_fwd"
+        N.check(N.fn(name)(N.ptr(qkv), N.ptr(m), N.ptr(out), N.ptr(lse), B, S_, nh, dh, scale,
+                           float(p_drop), seed, N.ptr(_seed_off(p_drop, qkv.device)), N.stream_ptr()), name)
         ctx.save_for_backward(qkv, out, lse)
         ctx.mask = m
-        ctx.args = (B, S_, nh, float(p_drop), seed, scale)
+        ctx.args = (B, S_, nh, float(p_drop), seed, scale, dh)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         qkv, out, lse = ctx.saved_tensors
-        B, S_, nh, p_drop, seed, scale = ctx.args
+        B, S_, nh, p_drop, seed, scale, dh = ctx.args
         dout = dout.contiguous()
         dqkv = torch.empty_like(qkv)
+        if ctx.flash:
+            ws = torch.empty((B * nh * S_,), dtype=torch.float32, device=qkv.device)
+            N.check(N.fn("mdtf_attn_bwd_flash")(N.ptr(qkv), N.ptr(ctx.mask), N.ptr(out), N.ptr(dout), N.ptr(lse),
+                                                N.ptr(dqkv), N.ptr(ws), B, S_, nh, dh, scale, p_drop, seed,
+                                                N.ptr(_seed_off(p_drop, qkv.device)), N.stream_ptr()),
+                    "attn_bwd_flash")
+            return dqkv, None, None, None, None, None, None
         N.check(N.fn("mdtf_attn_bwd")(N.ptr(qkv), N.ptr(ctx.mask), N.ptr(out), N.ptr(dout), N.ptr(lse), N.ptr(dqkv),
                                       B, S_, nh, FUSED_DIM, scale, p_drop, seed, N.ptr(_seed_off(p_drop, qkv.device)),
                                       N.stream_ptr()), "attn_bwd")
@@ -263,14 +282,17 @@ def fused_attention(qkv, batch, seq, heads, mask=None, dropout=0.0):
     """Self-attention from the fused projection ``qkv`` [B*S, 3H] (q | k | v, heads
     contiguous inside each) to the context [B*S, H].
 
-    GPU, S = 128, head dim 64: one fused HIP kernel per direction
-    (``csrc/attention.hip``); otherwise the unfused matmul/softmax path.
+    GPU, S = 128, head dim 64: one fused HIP kernel per direction (``csrc/attention.hip``);
+    any other S % 128 == 0 with head dim 64 / 128 (BERT phase-2 seq 512, BERT-large heads):
+    the tiled online-softmax kernels (``csrc/attention_flash.hip``); otherwise the unfused
+    matmul/softmax path.
     ``mask``: additive [B, S] key mask (0 keep, -10000 drop) or None.
     """
     H3 = qkv.shape[-1]
     H = H3 // 3
     dh = H // heads
-    if N.use_native(qkv) and seq == FUSED_SEQ and dh == FUSED_DIM and qkv.dtype == torch.bfloat16:
+    if N.use_native(qkv) and qkv.dtype == torch.bfloat16 and ((seq == FUSED_SEQ and dh == FUSED_DIM)
+                                                              or flash_ok(seq, dh)):
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if dropout else 0
         return _FusedAttention.apply(qkv.reshape(batch * seq, H3), mask, batch, seq, heads, float(dropout), seed)
     q, k, v = qkv.reshape(batch, seq, 3, heads, dh).unbind(2)

@@ -648,10 +648,14 @@ def _attn_keep_mask(seed, B, nh, S, p):
 
 
 @pytest.mark.parametrize("p_drop", [0.0, 0.1])
-def test_fused_attention_fwd_bwd(p_drop):
+@pytest.mark.parametrize("B,S,nh,dh,flash", [(3, 128, 4, 64, False), (3, 128, 4, 64, True), (2, 384, 3, 64, True),
+                                              (1, 512, 2, 64, True), (2, 256, 2, 128, True), (1, 512, 2, 128, True)])
+def test_fused_attention_fwd_bwd(p_drop, B, S, nh, dh, flash, monkeypatch):
+    """Fused attention (S = 128 whole-sequence kernels, or the tiled online-softmax kernels for any
+    S % 128 == 0 and head dim 64 / 128) forward and backward vs fp32 with the same dropout bits."""
     from mdtf.ops import transformer as T
-    torch.manual_seed(21)
-    B, S, nh, dh = 3, 128, 4, 64
+    monkeypatch.setattr(T, "FLASH_ALWAYS", flash)
+    torch.manual_seed(21 + S + dh)
     H = nh * dh
     qkv = torch.randn(B * S, 3 * H) * 0.5
     mask = (torch.rand(B, S) < 0.15).float() * -10000.0
