@@ -60,11 +60,19 @@ def parent(a):
             r = json.load(f)
         rates.append(r["steps"] * r["batch"] / max(r["seconds"], 1e-9))
     value = sum(rates)
+    ps_stats = []
+    for p in range(a.num_ps):
+        fn = os.path.join(out, "ps%d.json" % p)
+        if os.path.exists(fn):
+            with open(fn) as f:
+                ps_stats.append(json.load(f))
     print(json.dumps({
         "metric": "images/sec ResNet-%d async parameter-server, %d ps + %d workers, one node" % (
             a.depth, a.num_ps, a.num_workers),
         "value": round(value, 2), "unit": "images/sec", "n_gpus": 0 if a.cpu else a.num_ps + a.num_workers,
         "higher_is_better": True, "per_worker": [round(x, 2) for x in rates], "wall_s": round(wall, 1),
+        "ps": [{k: r[k] for k in ("ps", "updates", "mean_staleness", "max_staleness", "apply_s", "idle_s", "wall_s",
+                                  "store_wait_s", "wire")} for r in ps_stats],
         "dtype": "bf16" if not a.cpu else "fp32", "data": "synthetic", "config": {
             "model": "resnet%d_v1.5" % a.depth, "per_worker_batch": a.batch, "image": a.image,
             "parallelism": "async-ps %dps+%dw" % (a.num_ps, a.num_workers)}}), flush=True)

@@ -56,6 +56,7 @@ def wgrad_slab(M, R, Cout, bm, bn, ver, splits, device, dense=False):
     return torch.empty(sp * R * Cout, dtype=torch.float32, device=device), sp
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+TUNED_BATCH = 256        # the batch bench/conv_autotune.py tuned conv_table.json at
 TABLE_PATH = os.environ.get("MDTF_CONV_TABLE") or os.path.join(_HERE, "conv_table.json")
 _TABLE = None
 
@@ -112,6 +113,10 @@ def choose(pass_, x_shape, w_shape, stride, pads, dil):
     if pass_ in ("fwd", "dgrad") and winograd.enabled() and winograd.eligible(w_shape, stride, pads, dil, c, co):
         return ("winograd",)                 # the reference's TF_ENABLE_WINOGRAD_NONFUSED toggle
     ent = table().get(shape_key(pass_, x_shape, w_shape, stride, pads, dil))
+    if ent is None and n != TUNED_BATCH:
+        # batch-agnostic lookup: the same conv at the tuned batch (ResNet-50/101/152 share their conv
+        # shapes; e.g. the async-PS ResNet-152 at batch 64 takes the batch-256 choices)
+        ent = table().get(shape_key(pass_, (TUNED_BATCH, h, w, c), w_shape, stride, pads, dil))
     if N.deterministic() and pass_ == "wgrad":
         # no split-K atomics, no library algorithm choice: one block per DW tile
         ver = 2 if v2_ok(pass_, c, co, stride, kh * kw, dil) else 1

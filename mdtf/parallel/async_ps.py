@@ -15,14 +15,25 @@ MI355X design:
 * workers run forward/backward on their own GPU and exchange with every PS by
   point-to-point RCCL send/recv over xGMI (gloo on CPU): push fp32 gradients,
   receive the updated compute weights (bf16 shadow, or fp32 for fp32 groups);
-* a PS applies each worker's gradient as soon as it arrives (no aggregation,
-  no barrier) with the fused optimizer kernel; request order is the arrival
-  order recorded by an atomic ticket counter in the cluster store;
+* the data plane never touches the cluster store: every PS keeps one posted
+  receive of a 2-word request header ``[kind, version]`` per worker and polls
+  them; a ``push`` header is followed by the worker's gradients (bf16 on the
+  wire: half the bytes, widened into the fp32 gradient the optimizer reads),
+  received into per-worker buffers so several workers' payloads stream in
+  concurrently, and applied in completion order (no aggregation, no barrier)
+  with the fused optimizer kernel; the reply is the PS version + the refreshed
+  compute weights;
+* workers overlap: the push of step t and its reply travel while forward and
+  backward of step t+1 run on the weights already held (the reply lands in a
+  staging copy, swapped in before the next push) -- one step of built-in
+  staleness, the classic async-PS trade;
 * staleness (PS version at apply time minus the version the gradient was
-  computed from) is measured per update and reported;
-* ``global_step`` counts applied worker updates (store counter); workers stop
-  at ``total_step`` and send a "done" ticket; PS tasks exit when every worker
-  is done (the reference's done-queue, ``distribute_train.py:86-90``);
+  computed from) is measured per update and reported, with the PS's busy /
+  idle split;
+* ``global_step`` = updates applied by PS 0 (every push reaches every PS),
+  returned in each reply; workers stop at ``total_step`` and send a ``done``
+  header; PS tasks exit when every worker is done (the reference's done-queue,
+  ``distribute_train.py:86-90``);
 * the chief pulls the fp32 masters from every PS and writes a sharded
   tensor-bundle checkpoint (one data file per PS task — the TF layout).
 """
@@ -73,22 +84,32 @@ def _varspec(variables):
              "decay": bool(v.apply_weight_decay), "ps": int(v.ps_task or 0)} for v in variables]
 
 
-def _ticket(store, ps, msg):
-    n = store.add("%s/ps%d/n" % (_PREFIX, ps), 1)
-    store.set("%s/ps%d/t/%d" % (_PREFIX, ps, n), msg)
+K_PULL, K_PUSH, K_DONE, K_MASTER = 0, 1, 2, 3
+WIRE = torch.bfloat16            # gradient wire dtype (MDTF_ASYNC_WIRE=fp32 for full-precision pushes)
+
+
+def _wire_dtype():
+    import os
+    return torch.float32 if os.environ.get("MDTF_ASYNC_WIRE", "bf16") == "fp32" else WIRE
+
+
+def _hdr(device):
+    return torch.zeros(2, dtype=torch.int64, device=device)
 
 
 # ---------------------------------------------------------------------------
 # parameter-server side
 # ---------------------------------------------------------------------------
 def run_parameter_server(op, server):
-    """PS role of the Train operator in async mode."""
+    """PS role of the Train operator in async mode: a store-free request loop over all workers."""
     from ..runtime.train import configure_store_for
+    import os
     store = server.store
     ps = server.task_index
     num_ps = server.layout.num_ps
     vstore = configure_store_for(server)
     device = vstore.device
+    cdev = device if device.type == "cuda" else torch.device("cpu")
     spec = json.loads(store.get("%s/varspec" % _PREFIX).decode())
     variables = []
     for s in spec:
@@ -106,47 +127,113 @@ def run_parameter_server(op, server):
         dist.recv(g.master, src=chief)
     space.refresh_shadows()
     optimizer = op.optimizer
-    version = 0
-    done = 0
-    n = 0
-    num_workers = server.layout.num_worker_ranks
-    stale_sum, stale_max, updates = 0, 0, 0
-    vt = torch.zeros(1, dtype=torch.int64, device=device if device.type == "cuda" else "cpu")
+    wire = _wire_dtype()
+    workers = [server.layout.rank_of("worker", w, r) for w in range(server.layout.num_workers)
+               for r in range(server.layout.towers_per_worker)]
+    hdr = {w: _hdr(cdev) for w in workers}
+    gbuf = {}                             # worker -> per-group wire buffers (payloads of several workers in flight)
+    vt = torch.zeros(1, dtype=torch.int64, device=cdev)
+    st = {"version": 0, "done": 0, "stale_sum": 0, "stale_max": 0, "updates": 0, "apply": 0.0, "idle": 0.0}
     t0 = time.time()
-    while done < num_workers:
-        n += 1
-        key = "%s/ps%d/t/%d" % (_PREFIX, ps, n)
-        store.wait([key])
-        rank_s, kind, wver = store.get(key).decode().split(":")
-        store.delete_key(key)
-        r = int(rank_s)
-        if kind == "done":
-            done += 1
-            continue
-        if kind == "push":
-            for g in groups:
-                dist.recv(g.grad, src=r)
-            lr = optimizer.learning_rate(version)
-            with torch.no_grad():
-                for g in groups:
-                    optimizer.update(UpdateTarget(g, g.master, g.grad, g.shadow, "full"), lr, 1.0, version)
-            stale = version - int(wver)
-            stale_sum += stale
-            stale_max = max(stale_max, stale)
-            updates += 1
-            version += 1
-        if kind == "master":
-            for g in groups:
-                dist.send(g.master, dst=r)
-            continue
-        vt.fill_(version)
-        dist.send(vt, dst=r)
+
+    def bufs(w):
+        if w not in gbuf:
+            gbuf[w] = [torch.empty(g.numel, dtype=wire if g.shadow is not None else torch.float32, device=device)
+                       for g in groups]
+        return gbuf[w]
+
+    def reply(w):
+        vt.fill_(st["version"])
+        dist.send(vt, dst=w)
         for g in groups:
-            dist.send(g.shadow if g.shadow is not None else g.master, dst=r)
+            dist.send(g.shadow if g.shadow is not None else g.master, dst=w)
+
+    def apply(w, wver):
+        ta = time.time()
+        lr = optimizer.learning_rate(st["version"])
+        with torch.no_grad():
+            for g, buf in zip(groups, gbuf[w]):
+                g.grad.copy_(buf)             # bf16 wire -> the fp32 gradient the optimizer reads
+                optimizer.update(UpdateTarget(g, g.master, g.grad, g.shadow, "full"), lr, 1.0, st["version"])
+        stale = st["version"] - wver
+        st["stale_sum"] += stale
+        st["stale_max"] = max(st["stale_max"], stale)
+        st["updates"] += 1
+        st["version"] += 1
+        reply(w)
+        st["apply"] += time.time() - ta
+
+    def serve(w, kind, wver):
+        """Handle a non-push request; returns False when the worker is done."""
+        if kind == K_DONE:
+            st["done"] += 1
+            return False
+        if kind == K_MASTER:
+            for g in groups:
+                dist.send(g.master, dst=w)
+        else:
+            reply(w)
+        return True
+
+    if dist.get_backend() == "nccl":
+        # RCCL: one posted header receive per worker, polled; a push's payload receives stay in flight
+        # while other workers' requests are served and earlier pushes are applied
+        req = {w: dist.irecv(hdr[w], src=w) for w in workers}
+        inflight = {}
+        while st["done"] < len(workers):
+            progressed = False
+            for w in workers:
+                r = req.get(w)
+                if r is None or not r.is_completed():
+                    continue
+                progressed = True
+                r.wait()
+                kind, wver = int(hdr[w][0].item()), int(hdr[w][1].item())
+                if kind == K_PUSH:
+                    inflight[w] = ([dist.irecv(b, src=w) for b in bufs(w)], wver)
+                    req[w] = None                 # re-posted once the update is applied
+                    continue
+                req[w] = dist.irecv(hdr[w], src=w) if serve(w, kind, wver) else None
+            for w in list(inflight):
+                reqs, wver = inflight[w]
+                if not all(x.is_completed() for x in reqs):
+                    continue
+                progressed = True
+                for x in reqs:
+                    x.wait()
+                del inflight[w]
+                apply(w, wver)
+                req[w] = dist.irecv(hdr[w], src=w)
+            if not progressed:
+                ti = time.time()
+                time.sleep(0.0002)
+                st["idle"] += time.time() - ti
+    else:
+        # gloo: requests are served in arrival order with any-source header receives
+        any_hdr = _hdr(cdev)
+        while st["done"] < len(workers):
+            ti = time.time()
+            w = dist.recv(any_hdr, src=None)
+            st["idle"] += time.time() - ti
+            kind, wver = int(any_hdr[0].item()), int(any_hdr[1].item())
+            if kind == K_PUSH:
+                for b in bufs(w):
+                    dist.recv(b, src=w)
+                apply(w, wver)
+            else:
+                serve(w, kind, wver)
+    updates = st["updates"]
+    stale_sum, stale_max = st["stale_sum"], st["stale_max"]
+    t_apply, t_idle = st["apply"], st["idle"]
     dt = time.time() - t0
     stats = {"ps": ps, "updates": updates, "mean_staleness": stale_sum / max(updates, 1), "max_staleness": stale_max,
-             "updates_per_sec": updates / max(dt, 1e-9)}
+             "updates_per_sec": updates / max(dt, 1e-9), "apply_s": round(t_apply, 3), "idle_s": round(t_idle, 3),
+             "wall_s": round(dt, 3), "store_wait_s": 0.0, "wire": str(wire).replace("torch.", "")}
     store.set("%s/ps%d/stats" % (_PREFIX, ps), json.dumps(stats))
+    out_dir = os.environ.get("MDTF_BENCH_OUT")
+    if out_dir:
+        with open(os.path.join(out_dir, "ps%d.json" % ps), "w") as f:
+            json.dump(stats, f)
     logger.info("async PS %d: %s" % (ps, stats))
     server.signal_done()
     return stats
@@ -177,33 +264,60 @@ class AsyncWorker(object):
         self.by_ps = _groups_by_ps(self.space.groups, self.num_ps)
         self.version = [0] * self.num_ps
         dev = vstore.device
-        self._vt = [torch.zeros(1, dtype=torch.int64, device=dev if dev.type == "cuda" else "cpu")
-                    for _ in range(self.num_ps)]
+        cdev = dev if dev.type == "cuda" else torch.device("cpu")
+        self._vt = [torch.zeros(1, dtype=torch.int64, device=cdev) for _ in range(self.num_ps)]
+        self._h = [_hdr(cdev) for _ in range(self.num_ps)]
+        wire = _wire_dtype()
+        self._wire = {id(g): torch.empty(g.numel, dtype=wire if g.shadow is not None else torch.float32, device=dev)
+                      for g in self.space.groups}
+        self._stage = {id(g): torch.empty(g.numel, dtype=g.shadow.dtype if g.shadow is not None else torch.float32,
+                                          device=dev) for g in self.space.groups}
         self.steps_done = 0
 
-    def _exchange(self, kind):
-        reqs = []
-        for p in range(self.num_ps):
-            _ticket(self.store, p, "%d:%s:%d" % (self.rank, kind, self.version[p]))
+    def _send_hdr(self, kind):
         for p, pr in enumerate(self.ps_ranks):
-            if kind == "push":
-                for g in self.by_ps[p]:
-                    reqs.append(dist.isend(g.grad, dst=pr))
+            self._h[p][0] = kind
+            self._h[p][1] = self.version[p]
+            dist.send(self._h[p], dst=pr)
+
+    def _post_reply(self, into_staging):
+        """Receive requests for every PS's reply (version + compute weights)."""
+        reqs = []
+        for p, pr in enumerate(self.ps_ranks):
             reqs.append(dist.irecv(self._vt[p], src=pr))
             for g in self.by_ps[p]:
-                reqs.append(dist.irecv(g.shadow if g.shadow is not None else g.master, src=pr))
+                dst = self._stage[id(g)] if into_staging else (g.shadow if g.shadow is not None else g.master)
+                reqs.append(dist.irecv(dst, src=pr))
+        return reqs
+
+    def _finish_reply(self, reqs, from_staging):
         for r in reqs:
             r.wait()
         for p in range(self.num_ps):
             self.version[p] = int(self._vt[p].item())
+        if from_staging:
+            for g in self.space.groups:
+                (g.shadow if g.shadow is not None else g.master).copy_(self._stage[id(g)])
+
+    def _push(self):
+        """Cast this step's gradients onto the wire buffers and send them (header first) to every PS."""
+        self._send_hdr(K_PUSH)
         for g in self.space.groups:
-            if g.shadow is not None:
-                pass  # the bf16 compute weights were received directly; fp32 masters stay on the PS
+            self._wire[id(g)].copy_(g.grad)
+        reqs = []
+        for p, pr in enumerate(self.ps_ranks):
+            for g in self.by_ps[p]:
+                reqs.append(dist.isend(self._wire[id(g)], dst=pr))
+        return reqs
+
+    def _exchange(self, kind):
+        """Blocking request/reply (initial pull)."""
+        self._send_hdr(kind)
+        self._finish_reply(self._post_reply(False), False)
 
     def pull_masters(self):
         """Chief: fetch the authoritative fp32 masters from every PS (checkpointing)."""
-        for p in range(self.num_ps):
-            _ticket(self.store, p, "%d:master:0" % self.rank)
+        self._send_hdr(K_MASTER)
         for p, pr in enumerate(self.ps_ranks):
             for g in self.by_ps[p]:
                 dist.recv(g.master, src=pr)
@@ -218,8 +332,7 @@ class AsyncWorker(object):
             for p, pr in enumerate(self.ps_ranks):
                 for g in self.by_ps[p]:
                     dist.send(g.master, dst=pr)
-        self._exchange("pull")
-        gs_key = "%s/global_step" % _PREFIX
+        self._exchange(K_PULL)
         loss_h = self.tower.program
         t0 = time.time()
         window = t0
@@ -227,6 +340,8 @@ class AsyncWorker(object):
         import os
         bench_warmup = int(os.environ.get("MDTF_BENCH_WARMUP", "0"))
         t_bench = None
+        pending = None                    # (push send requests, reply receive requests) of the previous step
+        step = 0
         while True:
             if self.steps_done == bench_warmup and t_bench is None:
                 if V.get_store().device.type == "cuda":
@@ -236,22 +351,35 @@ class AsyncWorker(object):
             for v in self.vars:
                 v.uses = 0
             self.space.zero_grad()
+            # forward/backward of this step overlaps the previous push and its reply (into staging)
             out = loss_h.forward(ctx, grad=True)
             out["loss"].backward()
             from ..ops import conv as _conv
             _conv.join_side_streams()
-            self._exchange("push")
+            if pending is not None:
+                for r in pending[0]:
+                    r.wait()
+                self._finish_reply(pending[1], True)
+            step = self.version[0]            # updates applied by PS 0 == the global step
+            if step >= self.total_step:
+                pending = None
+                break
+            pending = (self._push(), self._post_reply(True))
             self.steps_done += 1
-            step = self.store.add(gs_key, 1)
             last = out["loss"]
-            if step % 10 == 0:
+            if self.steps_done % 10 == 0:
                 lv = float(last)
                 now = time.time()
                 logger.info("async step %d (local %d), loss = %.8f (%.1f examples/sec local)" % (
                     step, self.steps_done, lv, 10 * self.op.batch_size / max(now - window, 1e-9)))
                 window = now
-            if step >= self.total_step:
-                break
+            if step + 1 >= self.total_step:
+                for r in pending[0]:
+                    r.wait()
+                self._finish_reply(pending[1], True)
+                pending = None
+                if self.version[0] >= self.total_step:
+                    break
         if V.get_store().device.type == "cuda":
             torch.cuda.synchronize()
         out_dir = os.environ.get("MDTF_BENCH_OUT")
@@ -262,11 +390,10 @@ class AsyncWorker(object):
                            "staleness": getattr(self, "staleness", None)}, f)
         if is_chief and self.op.model_dir:
             self.pull_masters()
-            V.get_or_create_global_step().assign(self.store.add(gs_key, 0))
+            V.get_or_create_global_step().assign(self.version[0])
             Saver(sharded=True, save_optimizer_state=False).save(None, "%s/model.ckpt" % self.op.model_dir.rstrip("/"),
                                                                  global_step=V.get_global_step())
-        for p in range(self.num_ps):
-            _ticket(self.store, p, "%d:done:0" % self.rank)
+        self._send_hdr(K_DONE)
         self.last_loss = last
         server.signal_done()
         if post_fn is not None:

@@ -106,3 +106,18 @@ def test_bench_bf16_wire_two_ranks():
     assert out.returncode == 0, out.stderr[-2000:]
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["n_gpus"] == 2 and rec["config"]["comm_dtype"] == "bf16"
+
+
+@pytest.mark.slow
+def test_async_ps_bench_two_ps_six_workers_cpu():
+    """BASELINE config 5's topology (2 ps + 6 workers, one process each) on gloo: every worker reports its
+    throughput, every PS its staleness and busy/idle split; the data plane never waits on the store."""
+    cmd = [sys.executable, "bench/async_ps_bench.py", "--cpu", "--num_ps", "2", "--num_workers", "6", "--depth", "50",
+           "--image", "32", "--batch", "2", "--steps", "2", "--warmup", "1", "--timeout_s", "500"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=560)
+    assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-2000:])
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert len(rec["per_worker"]) == 6 and all(r > 0 for r in rec["per_worker"])
+    assert len(rec["ps"]) == 2
+    for ps in rec["ps"]:
+        assert ps["updates"] >= 18 and ps["store_wait_s"] == 0.0 and ps["mean_staleness"] >= 0

@@ -278,3 +278,12 @@ def test_checkpoint_relative_model_dir_resume_and_cleanup(tmp_path, monkeypatch)
         pass
     assert gs.value() == 8
     assert torch.equal(V.get_store().vars["fc2/weights"].master, w_saved)
+
+
+def test_conv_table_lookup_is_batch_agnostic():
+    """Shapes at other batches (ResNet-152 async PS at batch 64) take the batch-256 tuned entries."""
+    from mdtf.ops import conv as C
+    w = (1, 1, 64, 256)
+    a = C.choose("fwd", (256, 56, 56, 64), w, (1, 1), (0, 0, 0, 0), (1, 1))
+    b = C.choose("fwd", (64, 56, 56, 64), w, (1, 1), (0, 0, 0, 0), (1, 1))
+    assert a == b
