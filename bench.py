@@ -46,7 +46,30 @@ def parse():
     p.add_argument("--hip_graph", type=int, default=1,
                    help="1: capture the whole training step in a hipGraph after 2 eager steps (mdtf.train.graph)")
     p.add_argument("--image_size", type=int, default=224, help="image side (CPU tests of the launch path use 32-64)")
+    p.add_argument("--bert", type=int, default=-1,
+                   help="also measure BERT-base (bench/bert_bench.py, a child process run before the ResNet job) and "
+                        "attach it under extra.bert_base; -1: on for the default 1-GPU run")
     return p.parse_args()
+
+
+def _bert_child(args):
+    """BASELINE config 4 on 1 GPU, measured by bench/bert_bench.py in a child process (before this process
+    touches the GPU) so the driver's bench run also records it; None if skipped or failed."""
+    import subprocess
+    want = args.bert if args.bert >= 0 else int(args.gpus == 1 and args.image_size == 224
+                                                   and "RANK" not in os.environ)
+    if not want:
+        return None
+    here = os.path.dirname(os.path.abspath(__file__))
+    cmd = [sys.executable, os.path.join(here, "bench", "bert_bench.py"), "--steps", "20", "--warmup", "5"]
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=400)
+        line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+        rec = json.loads(line)
+        return {k: rec.get(k) for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "vs_baseline",
+                                        "baseline", "config") if k in rec}
+    except Exception as e:  # noqa: BLE001 - the ResNet measurement must not depend on it
+        return {"error": "%s: %s" % (type(e).__name__, str(e)[:200])}
 
 
 def _ensure_ranks(args):
@@ -63,6 +86,7 @@ def _ensure_ranks(args):
 def main():
     args = parse()
     _ensure_ranks(args)
+    bert = _bert_child(args)
     if args.kernels:
         os.environ["MDTF_KERNELS"] = args.kernels
     import torch
@@ -163,6 +187,8 @@ def main():
                        "hip_graph": bool(args.hip_graph) and dev.type == "cuda"},
             "loss_first": float(lv), "loss_last": final_loss,
         }
+        if bert is not None:
+            rec["extra"] = {"bert_base": bert}
         print(json.dumps(rec), flush=True)
     sess.close()
     if distributed:

@@ -87,6 +87,11 @@ class StockBert(nn.Module):
         return h @ self.word.weight.t() + self.obias, self.nsp(pooled)
 
 
+# stock PyTorch-ROCm comparator (this script with --stock: SDPA flash attention, torch AdamW, DDP) on one
+# MI355X at the default config (BERT-base, seq 128, batch 64): README / profiles/rocprof_bert_base_stock_r1_summary.txt
+STOCK_SEQ128_PER_GPU = 3319.0
+
+
 def main():
     args = parse()
     from mdtf.utils.launch import ensure_ranks
@@ -200,6 +205,11 @@ def main():
                           "per_gpu_sequences_per_sec": round(sps / world, 2), "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3),
                           "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": (round(sps / (STOCK_SEQ128_PER_GPU * world), 4)
+                                          if (args.size, args.seq, args.batch) == ("base", 128, 64) and not args.stock
+                                          else None),
+                          "baseline": "stock PyTorch-ROCm comparator, %.0f seq/s/GPU x %d" % (
+                              STOCK_SEQ128_PER_GPU, world),
                           "impl": "stock-pytorch" if args.stock else "mdtf",
                           "hip_graph": bool(args.hip_graph) and not args.stock and gpu,
                           "dtype": "bf16" if gpu else "fp32",

@@ -1,4 +1,5 @@
-"""Dense / matmul on the GPU: hipBLASLt GEMMs with fp32 weight-gradient sinks.
+"""Dense / matmul on the GPU: hand-written MFMA kernels where they win, hipBLASLt GEMMs elsewhere,
+fp32 weight-gradient sinks.
 
 Forward: ``y = act(x @ W + b)`` — the GEMM and the bias run as ONE hipBLASLt
 call (``addmm``'s bias epilogue); GELU/ReLU (which must keep the
@@ -6,8 +7,8 @@ pre-activation for backward) is the mdtf activation kernel.  Several weight
 matrices that share an input (BERT's query/key/value) run as one GEMM on the
 column-concatenated weights.
 
-Backward: ``dx = dpre @ W^T`` (bf16, hipBLASLt; accumulated inside the GEMM into a
-fanned-out input's gradient sink), and the weight gradient is the mdtf weight-gradient
+Backward: ``dx = dpre @ W^T`` (bf16; the mdtf v2 dgrad kernel for the shapes of ``DGRAD_TILES``, else
+hipBLASLt; accumulated inside the GEMM into a fanned-out input's gradient sink), and the weight gradient is the mdtf weight-gradient
 kernel (``csrc/conv_igemm.hip`` conv_wgrad_v2 run as a 1x1 convolution) writing
 *directly into the variable's fp32 gradient slot*.  The same kernel adds the bias
 gradient (the column sums of ``dpre``) from the B fragments it already holds, with an
@@ -56,6 +57,31 @@ def wgrad_into(out, x, d, dbias=None):
             return fuse
     _accum_mm(out, x.t(), d)
     return False
+
+
+# data gradient dx[M][K] = dpre[M][N] W[K][N]^T on the hand-written MFMA kernel (csrc/conv_igemm.hip's v2
+# dgrad, a 1x1 convolution over M pixels) where it beats hipBLASLt (bench/gemm_hand_probe.py on MI355X,
+# BERT-base shapes, ms mdtf / hipBLASLt): K 768 x N 2304 0.047 / 0.055, 768 x 768 0.027 / 0.033,
+# 768 x 3072 0.055 / 0.064, M 1280 768 x 768 0.019 / 0.026; K 3072 x N 768 stays on hipBLASLt (0.064 / 0.053)
+DGRAD_TILES = {(768, 2304): (128, 128, 2, 2), (768, 768): (128, 256, 2, 3), (768, 3072): (128, 128, 2, 2),
+               (1024, 1024): (128, 256, 2, 3), (1024, 3072): (128, 128, 2, 2), (1024, 4096): (128, 128, 2, 2)}
+HAND_DGRAD = os.environ.get("MDTF_DENSE_DGRAD", "mdtf") != "hipblaslt"
+
+
+def _hand_dgrad(dpre, w, out=None, accumulate=False):
+    """dx = dpre @ w^T on the v2 dgrad kernel, or None when the shape is not in DGRAD_TILES."""
+    M, Nn = dpre.shape
+    K = w.shape[0]
+    tile = DGRAD_TILES.get((K, Nn)) if HAND_DGRAD else None
+    if tile is None or dpre.dtype != torch.bfloat16 or not dpre.is_cuda or not w.is_contiguous():
+        return None
+    if M < 512:
+        tile = (64, 128, 3, 2)
+    from . import conv as C
+    bm, bn, st, ver = tile
+    return C.mdtf_dgrad(dpre.view(1, 1, M, Nn), w.view(1, 1, K, Nn), (1, 1, M, K), (1, 1), (0, 0, 0, 0), (1, 1), bm,
+                        bn, ver, st, out=out.view(1, 1, M, K) if out is not None else None,
+                        accumulate=accumulate).view(M, K)
 
 
 def _accum_mm(out, a, b):
@@ -147,16 +173,21 @@ class _Dense(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             xs = ctx.x_sink
+            hand = not ctx.trans
             if xs is None:
-                dx = torch.mm(dpre, w.t())
+                dx = _hand_dgrad(dpre, w) if hand else None
+                if dx is None:
+                    dx = torch.mm(dpre, w.t())
             else:
                 buf, acc = xs.target()
                 if acc:                        # second contribution: C += dpre @ w^T inside the GEMM
                     b2 = buf.view(-1, w.shape[0])
-                    torch.addmm(b2, dpre, w.t(), out=b2)
+                    if not hand or _hand_dgrad(dpre, w, out=b2, accumulate=True) is None:
+                        torch.addmm(b2, dpre, w.t(), out=b2)
                     xs.written(buf)
                 else:
-                    xs.written(torch.mm(dpre, w.t()).view(ctx.x_shape))
+                    d2 = _hand_dgrad(dpre, w) if hand else None
+                    xs.written((d2 if d2 is not None else torch.mm(dpre, w.t())).view(ctx.x_shape))
         ws, bs = ctx.like[:ctx.nw], ctx.like[ctx.nw:]
         gws, gbs = [], []
         bias_done = [False] * ctx.nw

@@ -1127,3 +1127,21 @@ def test_stem_conv_forward(geo):
     yf = yr.reshape(-1, co)
     assert _rel(sbuf[0].sum(0), yf.sum(0)) < 5e-3
     assert _rel(sbuf[1].sum(0), (yf * yf).sum(0)) < 5e-3
+
+
+@pytest.mark.parametrize("M,K,N", [(1000, 768, 2304), (4100, 768, 768), (333, 768, 3072), (2048, 1024, 4096)])
+def test_dense_dgrad_hand_kernel(M, K, N):
+    """Dense data gradient on the hand-written MFMA kernel (ops/gemm.py DGRAD_TILES), plain and
+    accumulating into a fanned-out input's gradient, vs fp32 matmul; M tails included."""
+    from mdtf.ops import gemm as G
+    torch.manual_seed(M + N)
+    d = torch.randn(M, N).bfloat16()
+    w = (torch.randn(K, N) * 0.05).bfloat16()
+    ref = d.float() @ w.float().t()
+    dx = G._hand_dgrad(d.to(DEV), w.to(DEV))
+    assert dx is not None and dx.shape == (M, K)
+    assert _rel(dx, ref) < 1e-2
+    base = torch.randn(M, K).bfloat16()
+    out = base.to(DEV).clone()
+    G._hand_dgrad(d.to(DEV), w.to(DEV), out=out, accumulate=True)
+    assert _rel(out, ref + base.float()) < 1e-2
