@@ -7,8 +7,8 @@ pre-activation for backward) is the mdtf activation kernel.  Several weight
 matrices that share an input (BERT's query/key/value) run as one GEMM on the
 column-concatenated weights.
 
-Backward: ``dx = dpre @ W^T`` (bf16; the mdtf v2 dgrad kernel for the shapes of ``DGRAD_TILES``, else
-hipBLASLt; accumulated inside the GEMM into a fanned-out input's gradient sink), and the weight gradient is the mdtf weight-gradient
+Backward: ``dx = dpre @ W^T`` (bf16; hipBLASLt, or with ``MDTF_DENSE_DGRAD=mdtf`` the mdtf v2 dgrad kernel
+for the shapes of ``DGRAD_TILES``; accumulated inside the GEMM into a fanned-out input's gradient sink), and the weight gradient is the mdtf weight-gradient
 kernel (``csrc/conv_igemm.hip`` conv_wgrad_v2 run as a 1x1 convolution) writing
 *directly into the variable's fp32 gradient slot*.  The same kernel adds the bias
 gradient (the column sums of ``dpre``) from the B fragments it already holds, with an
@@ -65,7 +65,9 @@ def wgrad_into(out, x, d, dbias=None):
 # 768 x 3072 0.055 / 0.064, M 1280 768 x 768 0.019 / 0.026; K 3072 x N 768 stays on hipBLASLt (0.064 / 0.053)
 DGRAD_TILES = {(768, 2304): (128, 128, 2, 2), (768, 768): (128, 256, 2, 3), (768, 3072): (128, 128, 2, 2),
                (1024, 1024): (128, 256, 2, 3), (1024, 3072): (128, 128, 2, 2), (1024, 4096): (128, 128, 2, 2)}
-HAND_DGRAD = os.environ.get("MDTF_DENSE_DGRAD", "mdtf") != "hipblaslt"
+# In the captured BERT-base step the library GEMMs win end to end (A/B, 30 steps, alternating: hipBLASLt
+# 5625 / 5582 seq/s vs hand dgrad 5428 / 5473), so the hand-written path is opt-in: MDTF_DENSE_DGRAD=mdtf
+HAND_DGRAD = os.environ.get("MDTF_DENSE_DGRAD", "hipblaslt") == "mdtf"
 
 
 def _hand_dgrad(dpre, w, out=None, accumulate=False):

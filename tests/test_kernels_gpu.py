@@ -1130,10 +1130,11 @@ def test_stem_conv_forward(geo):
 
 
 @pytest.mark.parametrize("M,K,N", [(1000, 768, 2304), (4100, 768, 768), (333, 768, 3072), (2048, 1024, 4096)])
-def test_dense_dgrad_hand_kernel(M, K, N):
-    """Dense data gradient on the hand-written MFMA kernel (ops/gemm.py DGRAD_TILES), plain and
-    accumulating into a fanned-out input's gradient, vs fp32 matmul; M tails included."""
+def test_dense_dgrad_hand_kernel(M, K, N, monkeypatch):
+    """Dense data gradient on the hand-written MFMA kernel (ops/gemm.py DGRAD_TILES, MDTF_DENSE_DGRAD=mdtf),
+    plain and accumulating into a fanned-out input's gradient, vs fp32 matmul; M tails included."""
     from mdtf.ops import gemm as G
+    monkeypatch.setattr(G, "HAND_DGRAD", True)
     torch.manual_seed(M + N)
     d = torch.randn(M, N).bfloat16()
     w = (torch.randn(K, N) * 0.05).bfloat16()
