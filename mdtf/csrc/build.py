@@ -36,7 +36,8 @@ def _digest(paths, extra):
 
 
 def _headers():
-    return glob.glob(os.path.join(HERE, "include", "*.h"))
+    # shared headers and the kernel-template includes (conv_ws_kernel.inc is compiled by several .hip files)
+    return glob.glob(os.path.join(HERE, "include", "*.h")) + glob.glob(os.path.join(HERE, "*.inc"))
 
 
 def _compile_obj(src, flags, compiler):

@@ -270,7 +270,8 @@ def ws_ok(pass_, c, co, stride, kh, kw, dil=(1, 1)):
         red, ncol = co, c
     else:
         return False
-    return red % 32 == 0 and ncol % 64 == 0 and kh * kw <= 32 and 64 * kh * kw * red * 2 <= 160 * 1024
+    return (red % 32 == 0 and ncol % 64 == 0 and kh * kw <= 32 and kh * kw * red >= 64
+            and 64 * kh * kw * red * 2 <= 160 * 1024)
 
 
 N.register("mdtf_stem_pack4", [N.P, N.P] + [N.I] * 8 + [N.P])
@@ -313,7 +314,7 @@ def ws_depth_ok(k_total, d):
     """Load-ring depths the kernel instantiates for a reduction of ``k_total`` (csrc/conv_ws.hip
     dispatch_ws_d): K = 64 -> 2 or 4, K = 128 -> 4, longer K -> 3, 4 or 6 dividing K / 32."""
     ks = k_total // 32
-    if ks in (1, 2):
+    if ks == 2:
         return d in (2, 4)
     if ks == 3:
         return d == 3
