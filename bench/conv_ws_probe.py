@@ -62,7 +62,13 @@ def main():
                 continue
             ch = C.choose(pass_, x.shape, w.shape, (s, s), pads, (1, 1))
             sbuf = torch.zeros(2, 64, co if pass_ == "fwd" else c, device=dev)
-            if pass_ == "fwd":
+            if ch[0] == "ws":
+                if pass_ == "fwd":
+                    base = lambda: C.ws_fwd(x, wt, k, k, (oh, oh), (s, s), pads, (1, 1), ch[1],  # noqa: E731
+                                            (sbuf[0], sbuf[1]))
+                else:
+                    base = lambda: C.ws_dgrad(dy, w, x.shape, pads, (1, 1), ch[1])  # noqa: E731
+            elif pass_ == "fwd":
                 if ch[0] == "mdtf":
                     base = lambda: C.mdtf_fwd(x, w, (oh, oh), (s, s), pads, (1, 1), ch[1], ch[2],  # noqa: E731
                                               (sbuf[0], sbuf[1]), ch[4], ch[5])
