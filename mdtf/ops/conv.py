@@ -328,12 +328,12 @@ def _ws_code(tp, nw, cg, d=4):
     return tp + 10 * nw + 100 * cg + 1000 * d
 
 
-def ws_fwd(x, wt, kh, kw, out_hw, stride, pads, dil, tile, stats=None, grid_cap=0):
+def ws_fwd(x, wt, kh, kw, out_hw, stride, pads, dil, tile, stats=None, grid_cap=0, out=None):
     """Y = conv(X, W) on the weight-stationary kernel; ``wt`` = Wt[co][(kh,kw,ci)]
     (:func:`transpose_filter`).  ``tile`` = (tp, nw, cg[, d])."""
     n, h, wd, c = x.shape
     co = wt.shape[0]
-    y = torch.empty((n, out_hw[0], out_hw[1], co), dtype=x.dtype, device=x.device)
+    y = out if out is not None else torch.empty((n, out_hw[0], out_hw[1], co), dtype=x.dtype, device=x.device)
     s_sum, s_sq = stats if stats is not None else (None, None)
     slots = s_sum.shape[0] if s_sum is not None else 0
     N.check(N.fn("mdtf_conv_ws")(N.ptr(x), N.ptr(wt), N.ptr(y), n, h, wd, c, out_hw[0], out_hw[1], co, kh, kw,

@@ -1,11 +1,14 @@
-"""Non-fused Winograd F(2x2, 3x3) convolution (``csrc/winograd.hip`` + batched hipBLASLt GEMM).
+"""Non-fused Winograd F(2x2, 3x3) convolution (``csrc/winograd.hip`` transforms + hand-written MFMA GEMMs).
 
 The reference exposes Winograd only as an environment toggle for cuDNN
 (``TF_ENABLE_WINOGRAD_NONFUSED=1`` in ``distribute.py``).  Here
 the same switch (or ``MDTF_WINOGRAD=1`` / ``MDTF_CONV=winograd``) routes every
 eligible 3x3 stride-1 forward and data-gradient pass through this algorithm:
-input transform -> 16 batched GEMMs -> output transform, each transform one HIP
-kernel.  Weight gradients stay on the implicit-GEMM kernel.  The autotuner
+input transform -> 16 GEMMs -> output transform, each transform one HIP kernel.
+The 16 GEMMs [T tiles x C] x [C x K] run on the weight-stationary MFMA kernel
+(``csrc/conv_ws.hip`` as a 1x1 convolution over the T tiles; the transformed
+filters transposed once to [16][K][C]); shapes it does not take (C % 32,
+K % 64) use a batched hipBLASLt GEMM.  Weight gradients stay on the implicit-GEMM kernel.  The autotuner
 (``bench/conv_autotune.py``) measures it per shape next to the other backends;
 on MI355X the implicit GEMM usually wins because the transformed tensors cost
 more HBM traffic than the 2.25x MFMA saving (profiles/conv_autotune_*.md).
@@ -45,10 +48,30 @@ def _conv(x, w, out_hw, ph, pw, flip):
     u = torch.empty((16, c, k), dtype=x.dtype, device=x.device)
     N.check(N.fn("mdtf_wino_filter")(N.ptr(w), N.ptr(u), w.shape[2], w.shape[3], int(flip), N.stream_ptr()),
             "wino_filter")
-    m = torch.bmm(v, u)                       # [16, T, K]: hipBLASLt, fp32 accumulation
+    m = _gemm16(v, u)                         # [16, T, K], fp32 accumulation
     y = torch.empty((n, oh, ow, k), dtype=x.dtype, device=x.device)
     N.check(N.fn("mdtf_wino_output")(N.ptr(m), N.ptr(y), n, oh, ow, k, N.stream_ptr()), "wino_output")
     return y
+
+
+WS_TILE = (2, 8, 1, 4)
+
+
+def _gemm16(v, u):
+    """m[b] = v[b] @ u[b] for the 16 transform positions: hand-written kernel where it applies."""
+    from . import conv as C
+    from . import kernels
+    b, t, c = v.shape
+    k = u.shape[2]
+    if (N.use_native(v) and v.dtype == torch.bfloat16 and C.ws_ok("fwd", c, k, (1, 1), 1, 1)
+            and C.ws_depth_ok(c, WS_TILE[3])):
+        ut = kernels.transpose_brs(u, b, c, k)          # [16][K][C]: the kernel's A operand layout
+        m = torch.empty((b, t, k), dtype=v.dtype, device=v.device)
+        for i in range(b):
+            C.ws_fwd(v[i].view(1, 1, t, c), ut[i], 1, 1, (1, t), (1, 1), (0, 0, 0, 0), (1, 1), WS_TILE,
+                     out=m[i].view(1, 1, t, k))
+        return m
+    return torch.bmm(v, u)                  # hipBLASLt
 
 
 def winograd_fwd(x, w, out_hw, pads):
