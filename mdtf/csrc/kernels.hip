@@ -743,6 +743,58 @@ MDTF_EXPORT int mdtf_xent_bwd(const void* logits, int is_bf16, const long long* 
 }
 
 // elem_bytes: 2 (bf16/fp16) or 4 (fp32)
+// Many [R][S] -> [S][R] bf16 transposes in ONE launch (every conv filter -> its K-contiguous copy, once per
+// step): desc[i] = {src, dst, R | S << 32, first tile, tiles along S}; block b serves the descriptor whose
+// tile range holds b (linear scan over <= a few hundred scalar-loaded entries).
+struct TDesc {
+  const uint16_t* src;
+  uint16_t* dst;
+  long long rs;
+  int tile0, ts;
+};
+
+__global__ void __launch_bounds__(256) transpose16_multi(const TDesc* __restrict__ desc, int count) {
+  __shared__ uint16_t tile[64][66];
+  int i = 0;
+  while (i + 1 < count && desc[i + 1].tile0 <= (int)blockIdx.x) ++i;
+  const TDesc d = desc[i];
+  const int R = (int)(d.rs & 0xffffffff), S = (int)(d.rs >> 32);
+  const int local = blockIdx.x - d.tile0;
+  const int r0 = (local / d.ts) * 64, s0 = (local % d.ts) * 64;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = t + h * 256;
+    const int rr = idx >> 3, sc = (idx & 7) * 8;
+    if (r0 + rr < R && s0 + sc < S) {
+      uint4 v = *reinterpret_cast<const uint4*>(d.src + (long long)(r0 + rr) * S + s0 + sc);
+      const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) tile[sc + k][rr] = e[k];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = t + h * 256;
+    const int ss = idx >> 3, rc = (idx & 7) * 8;
+    if (s0 + ss < S && r0 + rc < R) {
+      uint4 v;
+      uint16_t* e = reinterpret_cast<uint16_t*>(&v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e[k] = tile[ss][rc + k];
+      *reinterpret_cast<uint4*>(d.dst + (long long)(s0 + ss) * R + r0 + rc) = v;
+    }
+  }
+}
+
+MDTF_EXPORT int mdtf_transpose_multi(const void* desc, int count, int total_tiles, hipStream_t st) {
+  if (count <= 0 || total_tiles <= 0) return 0;
+  hipLaunchKernelGGL(transpose16_multi, dim3(total_tiles), dim3(256), 0, st, (const TDesc*)desc, count);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
 MDTF_EXPORT int mdtf_transpose_brs(const void* in, void* out, int B, int R, int S, int elem_bytes, hipStream_t st) {
   dim3 grid(ceil_div(S, 64), ceil_div(R, 64), B);
   if (elem_bytes == 2 && R % 8 == 0 && S % 8 == 0)

@@ -106,8 +106,9 @@ def choose(pass_, x_shape, w_shape, stride, pads, dil):
     kh, kw, ci, co = w_shape
     forced = os.environ.get("MDTF_CONV", "auto")
     native_ok = c % 8 == 0 and co % 8 == 0
-    if pass_ == "fwd" and not native_ok and stem_ok(x_shape, w_shape, dil):
-        return ("stem",)
+    if pass_ in ("fwd", "wgrad") and not native_ok and stem_ok(x_shape, w_shape, dil):
+        if pass_ == "fwd" or (co == 64 and kh <= 8 and not N.deterministic()):
+            return ("stem",)
     if not native_ok or forced == "miopen":
         return ("miopen",)
     if pass_ in ("fwd", "dgrad") and winograd.enabled() and winograd.eligible(w_shape, stride, pads, dil, c, co):
@@ -198,9 +199,95 @@ def _geo(x, w, out_hw, stride, pads, dil):
 
 def transpose_filter(w):
     """HWIO [kh,kw,ci,co] -> Wt [co][(kh,kw,ci)] (the v2 forward kernel's K-contiguous B operand)."""
+    cached = _WT.get(w)
+    if cached is not None:
+        return cached
     from . import kernels
     kh, kw, ci, co = w.shape
     return kernels.transpose_brs(w.reshape(1, kh * kw * ci, co), 1, kh * kw * ci, co).view(co, kh * kw * ci)
+
+
+N.register("mdtf_transpose_multi", [N.P, N.I, N.I, N.P])
+
+
+class _FilterTransposes(object):
+    """All conv filters' K-contiguous copies, refreshed by ONE batched kernel per training step.
+
+    The bf16 filter shadows change only in the optimizer update, so a training step marks the cache stale
+    at its start (``step_begin``) and invalid again after the update (``step_end``).  The first filter a
+    step's forward asks for launches the batched transpose of every filter registered in earlier steps
+    (52 launches -> 1 for ResNet-50); a filter seen for the first time is transposed on its own and
+    registered.  Outside a step (eval, checkpoint restore) nothing is cached.
+    """
+
+    def __init__(self):
+        self.entries = {}          # (data_ptr, shape) -> (filter view, Wt buffer)
+        self.order = []
+        self.desc = None
+        self.tiles = 0
+        self.active = False        # inside a training step
+        self.fresh = False         # every registered copy is current for this step
+
+    def step_begin(self):
+        self.active = os.environ.get("MDTF_FILTER_CACHE", "1") != "0"
+        self.fresh = False
+
+    def step_end(self):
+        self.active = False
+        self.fresh = False
+
+    def _rebuild(self):
+        import struct
+        recs, tile = [], 0
+        for key in self.order:
+            w, wt = self.entries[key]
+            r = w.numel() // w.shape[-1]
+            sdim = w.shape[-1]
+            ts = -(-sdim // 64)
+            recs.append(struct.pack("<qqqii", w.data_ptr(), wt.data_ptr(), r | (sdim << 32), tile, ts))
+            tile += ts * -(-r // 64)
+        raw = torch.frombuffer(bytearray(b"".join(recs)), dtype=torch.uint8)
+        self.desc = raw.to(self.order and self.entries[self.order[0]][0].device)
+        self.tiles = tile
+
+    @staticmethod
+    def _is_shadow(w):
+        """Only filters living in a flat parameter space's bf16 shadow (stable storage, rewritten in place by
+        the optimizer) are cached; per-step temporaries are not."""
+        flat = getattr(V.get_store(), "flat", None)
+        if flat is None:
+            return False
+        sp = w.untyped_storage().data_ptr()
+        return any(g.shadow is not None and g.shadow.untyped_storage().data_ptr() == sp for g in flat.groups)
+
+    def get(self, w):
+        if not self.active or not w.is_cuda or w.dtype != torch.bfloat16 or not w.is_contiguous():
+            return None
+        key = (w.data_ptr(), tuple(w.shape))
+        ent = self.entries.get(key)
+        if ent is None:
+            if torch.cuda.is_current_stream_capturing() or not self._is_shadow(w):
+                return None                      # no new registrations inside a graph capture
+            from . import kernels
+            kh, kw, ci, co = w.shape
+            wt = torch.empty((co, kh * kw * ci), dtype=w.dtype, device=w.device)
+            self.entries[key] = (w, wt)
+            self.order.append(key)
+            self.desc = None
+            wt.copy_(kernels.transpose_brs(w.reshape(1, kh * kw * ci, co), 1, kh * kw * ci, co).view(co, -1))
+            return wt
+        if not self.fresh:
+            if self.desc is None:
+                if torch.cuda.is_current_stream_capturing():
+                    return None
+                self._rebuild()
+            N.check(N.fn("mdtf_transpose_multi")(N.ptr(self.desc), len(self.order), self.tiles, N.stream_ptr()),
+                    "transpose_multi")
+            self.fresh = True
+        return ent[1]
+
+
+_WT = _FilterTransposes()
 
 
 def _v2_code(bm, stages, ver):
@@ -276,6 +363,7 @@ def ws_ok(pass_, c, co, stride, kh, kw, dil=(1, 1)):
 
 N.register("mdtf_stem_pack4", [N.P, N.P] + [N.I] * 8 + [N.P])
 N.register("mdtf_conv_ws_stem", [N.P, N.P, N.P] + [N.I] * 10 + [N.P, N.P, N.I, N.P])
+N.register("mdtf_stem_wgrad", [N.P, N.P, N.P] + [N.I] * 12 + [N.P])
 STEM = os.environ.get("MDTF_STEM", "mdtf")          # mdtf: hand-written stem forward | miopen
 STEM_TILE = (4, 4, 1, 4)          # bench/stem_ws_probe.py: 0.329 ms vs MIOpen 0.487 (batch 256)
 
@@ -287,7 +375,18 @@ def stem_ok(x_shape, w_shape, dil):
             and os.environ.get("MDTF_CONV", "auto") != "miopen")
 
 
-def stem_fwd(x, w, out_hw, stride, pads, stats=None, tile=None):
+def stem_wgrad(x4, dy, w_shape, stride, out=None, blocks=0):
+    """Stem weight gradient from the forward's packed x4 (csrc/stem_wgrad.hip): fp32 HWIO, accumulated
+    into ``out`` (a zeroed buffer or the variable's gradient slot)."""
+    kh, kw, ci, co = w_shape
+    dw = out if out is not None else torch.zeros(w_shape, dtype=torch.float32, device=dy.device)
+    n, h4, w4, _ = x4.shape
+    N.check(N.fn("mdtf_stem_wgrad")(N.ptr(x4), N.ptr(dy), N.ptr(dw), n, h4, w4, dy.shape[1], dy.shape[2],
+                                    stride[0], stride[1], kh, kw, ci, int(blocks), N.stream_ptr()), "stem_wgrad")
+    return dw
+
+
+def stem_fwd(x, w, out_hw, stride, pads, stats=None, tile=None, keep_x4=None):
     """Stem forward: repack x into a zero-haloed 4-channel image (one kernel), then the weight-stationary
     GEMM with one 32-deep k-step per filter row (filter rows packed [co][row][kw*4 + c], zero-padded)."""
     n, h, wd, c = x.shape
@@ -307,6 +406,8 @@ def stem_fwd(x, w, out_hw, stride, pads, stats=None, tile=None):
     N.check(N.fn("mdtf_conv_ws_stem")(N.ptr(x4), N.ptr(wt), N.ptr(y), n, h4, w4, out_hw[0], out_hw[1], co, khp,
                                       stride[0], stride[1], _ws_code(*(tile or STEM_TILE)), N.ptr(s_sum), N.ptr(s_sq),
                                       slots, N.stream_ptr()), "conv_ws_stem")
+    if keep_x4 is not None:
+        keep_x4.append(x4)                    # the weight gradient reads the packed image again
     return y
 
 
@@ -487,7 +588,9 @@ class _Conv(torch.autograd.Function):
             if want_stats:
                 buf = _stats_buffer(w.shape[3], x.device, STAT_SLOTS)
                 stats = (buf[0], buf[1])
-            y = stem_fwd(x, w, out_hw, stride, pads, stats)
+            keep = []
+            y = stem_fwd(x, w, out_hw, stride, pads, stats, keep_x4=keep)
+            ctx.stem_x4 = keep[0]
         elif ch[0] == "ws":
             if want_stats:
                 buf = _stats_buffer(w.shape[3], x.device, STAT_SLOTS)
@@ -521,7 +624,9 @@ class _Conv(torch.autograd.Function):
         dx = dw = None
         cd = choose("dgrad", x.shape, w.shape, stride, pads, dil) if need_dx else None
         cw = choose("wgrad", x.shape, w.shape, stride, pads, dil) if need_dw else None
-        lib_dx = need_dx and cd[0] == "miopen"
+        if need_dw and cw[0] == "stem" and getattr(ctx, "stem_x4", None) is None:
+            cw = ("miopen",)                   # the forward did not leave the packed image
+        lib_dx = need_dx and cd[0] in ("miopen", "stem")
         lib_dw = need_dw and cw[0] == "miopen"
         sink = ctx.sink
         if lib_dx or lib_dw:
@@ -571,7 +676,16 @@ class _Conv(torch.autograd.Function):
         if xs is not None and dx is not None:
             xs.adopt_or_add(dx)                    # library / v1 dgrad: contribute the tensor
             dx = None
-        if need_dw and not lib_dw:
+        if need_dw and cw[0] == "stem":
+            if sink is not None:
+                stem_wgrad(ctx.stem_x4, dy, w.shape, stride, out=sink.grad)
+                dw = V.grad_marker(w)
+            else:
+                dw = stem_wgrad(ctx.stem_x4, dy, w.shape, stride)
+                if dw.dtype != ctx.w_dtype:
+                    dw = dw.to(ctx.w_dtype)
+            ctx.stem_x4 = None
+        elif need_dw and not lib_dw:
             if sink is not None:
                 # fp32 atomics of the wgrad kernel accumulate into the flat gradient buffer
                 if WGRAD_STREAM and x.is_cuda:

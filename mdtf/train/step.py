@@ -312,12 +312,17 @@ class TrainOp(Fetchable):
 
     def _run_step(self, ctx, step, dyn=None):
         """forward + backward of every tower program, reduction, fused update (one step)."""
+        from ..ops import conv as _conv
         red = self.reducer
         red.begin_step()
-        for prog in self.programs:
-            out = prog.forward(ctx, grad=True)
-            loss = out[self.loss_key]
-            loss.backward()
+        _conv._WT.step_begin()                 # conv filters' K-contiguous copies: one batched refresh per step
+        try:
+            for prog in self.programs:
+                out = prog.forward(ctx, grad=True)
+                loss = out[self.loss_key]
+                loss.backward()
+        finally:
+            _conv._WT.step_end()
         scale = red.end_backward(step) * self.grad_scale_extra
         lr = self.optimizer.learning_rate(step)
         with torch.no_grad():

@@ -1121,12 +1121,26 @@ def test_stem_conv_forward(geo):
     yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wt.float().permute(3, 2, 0, 1), stride=s,
                                     padding=p).permute(0, 2, 3, 1)
     sbuf = torch.zeros(2, 8, co, device=DEV)
-    y = C.stem_fwd(x.to(DEV), wt.to(DEV), (oh, ow), (s, s), (p, p, p, p), (sbuf[0], sbuf[1]))
+    keep = []
+    y = C.stem_fwd(x.to(DEV), wt.to(DEV), (oh, ow), (s, s), (p, p, p, p), (sbuf[0], sbuf[1]), keep_x4=keep)
     assert y.shape == yr.shape
     assert _rel(y, yr) < 1e-2
     yf = yr.reshape(-1, co)
     assert _rel(sbuf[0].sum(0), yf.sum(0)) < 5e-3
     assert _rel(sbuf[1].sum(0), (yf * yf).sum(0)) < 5e-3
+    if co != 64 or k > 8:
+        return
+    # weight gradient from the packed image (csrc/stem_wgrad.hip), accumulated into a non-zero slot
+    dy = torch.randn(n, oh, ow, co).bfloat16()
+    wr = wt.float().permute(3, 2, 0, 1).requires_grad_(True)
+    torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wr, stride=s, padding=p).backward(
+        dy.float().permute(0, 3, 1, 2))
+    ref = wr.grad.permute(2, 3, 1, 0)
+    base = torch.randn(k, k, c, co)
+    for blocks in (0, 3):
+        dw = base.clone().to(DEV)
+        C.stem_wgrad(keep[0], dy.to(DEV), wt.shape, (s, s), out=dw, blocks=blocks)
+        assert _rel(dw.cpu() - base, ref) < 1e-2, blocks
 
 
 @pytest.mark.parametrize("M,K,N", [(1000, 768, 2304), (4100, 768, 768), (333, 768, 3072), (2048, 1024, 4096)])
@@ -1146,3 +1160,48 @@ def test_dense_dgrad_hand_kernel(M, K, N, monkeypatch):
     out = base.to(DEV).clone()
     G._hand_dgrad(d.to(DEV), w.to(DEV), out=out, accumulate=True)
     assert _rel(out, ref + base.float()) < 1e-2
+
+
+def _tiny_steps(steps, monkeypatch, cache):
+    import mdtf
+    from mdtf.models import SoftmaxCrossEntropyLoss
+    from mdtf.runtime import Model, Net, Tower
+    from mdtf.train import step as S
+    from mdtf.train import variables as V
+    monkeypatch.setenv("MDTF_FILTER_CACHE", "1" if cache else "0")
+    V.reset_default_graph()
+    S.reset()
+    store = V.get_store()
+    store.device = torch.device(DEV)
+    store.compute_dtype = torch.bfloat16
+    store.generator.manual_seed(123)
+    torch.manual_seed(0)
+    x = torch.randn(32, 16, 16, 8)
+    y = torch.randint(0, 16, (32,))
+    xp = mdtf.placeholder(torch.float32, [None, 16, 16, 8])
+    yp = mdtf.placeholder(torch.int64, [None])
+    opt = mdtf.train.MomentumOptimizer(0.1, 0.9)
+    tg = []
+    M = type("TinyModel", (_Tiny, Model), {})
+    Tower(Net(M()), "tower_0/", tg, xp, yp, SoftmaxCrossEntropyLoss(), opt, batch_size=32).process()
+    op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
+    sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
+    for _ in range(steps):
+        sess.run(op, feed_dict={xp: x, yp: y})
+    return {v.name: v.master.detach().float().cpu().clone() for v in store.trainable_variables()}
+
+
+def test_filter_transpose_cache_matches_per_call(monkeypatch):
+    """Conv filters' K-contiguous copies refreshed by one batched kernel per step (ops/conv.py
+    _FilterTransposes) give bitwise the same training as per-call transposes (deterministic mode)."""
+    from mdtf.ops import conv as C
+    _native.set_deterministic(True)
+    try:
+        monkeypatch.setenv("MDTF_CONV", "mdtf2")
+        a = _tiny_steps(4, monkeypatch, True)
+        assert len(C._WT.order) >= 3                 # every v2-forward filter was registered
+        b = _tiny_steps(4, monkeypatch, False)
+    finally:
+        _native.set_deterministic(False)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
