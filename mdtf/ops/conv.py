@@ -363,7 +363,7 @@ def ws_ok(pass_, c, co, stride, kh, kw, dil=(1, 1)):
 
 N.register("mdtf_stem_pack4", [N.P, N.P] + [N.I] * 8 + [N.P])
 N.register("mdtf_conv_ws_stem", [N.P, N.P, N.P] + [N.I] * 10 + [N.P, N.P, N.I, N.P])
-N.register("mdtf_stem_wgrad", [N.P, N.P, N.P] + [N.I] * 12 + [N.P])
+N.register("mdtf_stem_wgrad", [N.P, N.P, N.P] + [N.I] * 11 + [N.P])
 STEM = os.environ.get("MDTF_STEM", "mdtf")          # mdtf: hand-written stem forward | miopen
 STEM_TILE = (4, 4, 1, 4)          # bench/stem_ws_probe.py: 0.329 ms vs MIOpen 0.487 (batch 256)
 
