@@ -172,8 +172,10 @@ def main():
                 cands = [(bm, bn, sp, 1) for bm, bn in ((128, 128), (64, 64), (128, 64), (64, 128))
                          for sp in (0, 256, 2048)]
                 if C.v2_ok("wgrad", c, co, (s, s), kh * kw):
-                    cands += [((bm, st), bn, sp, 2) for bm, bn, st in WG2_TILES for sp in (0, 256, 2048)]
-                    cands += [((bm, st), bn, sp, 3) for bm, bn, st in WG3_TILES for sp in (0, 128, 1024)]
+                    # splits: 0 = ~4 (4-wave) / ~2 (8-wave) blocks per CU; fewer splits = longer pixel runs
+                    # per block and fewer fp32 atomics per output element
+                    cands += [((bm, st), bn, sp, 2) for bm, bn, st in WG2_TILES for sp in (0, 16, 32, 64, 256, 2048)]
+                    cands += [((bm, st), bn, sp, 3) for bm, bn, st in WG3_TILES for sp in (0, 8, 16, 32, 64, 128, 1024)]
                 mk = lambda bm, bn, sp, v: (lambda: C.mdtf_wgrad(  # noqa
                     x, dy, wt.shape, (s, s), pads4, (1, 1), bm[0] if v >= 2 else bm, bn, sp, None, v,
                     bm[1] if v >= 2 else 2))

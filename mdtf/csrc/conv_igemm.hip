@@ -76,6 +76,7 @@ struct ConvArgs {
   // into DW by one reduction pass, instead of fp32 atomics into DW (null: atomics)
   float* slab;
   int slab_cap;          // splits the slab has room for
+  int wg_xcd;            // wgrad v2: XCD-aware block order (the row/col tiles of one pixel split share an L2)
 };
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p, bool ok) {
@@ -970,8 +971,11 @@ __global__ void __launch_bounds__(64 * NW, (wgrad_min_waves<BM, BN, STAGES, NW>(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int tiles_mn = a.mtiles * a.ntiles;
-  const int tile = blockIdx.x % tiles_mn;
-  const int split = blockIdx.x / tiles_mn;
+  // consecutive blocks run on different XCDs (round robin); with wg_xcd the tiles of one pixel split
+  // (which read the same DY rows / X pixels) are consecutive in the remapped order, i.e. on one XCD's L2
+  const int lb = a.wg_xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int tile = lb % tiles_mn;
+  const int split = lb / tiles_mn;
   const int mt = tile / a.ntiles, nt = tile % a.ntiles;
   const int r0 = mt * BM, n0 = nt * BN;
   const int R = a.KH * a.KW * a.Cin;
@@ -1358,6 +1362,12 @@ int dispatch_wgrad_v2(ConvArgs& a, int bm, int bn, int stages, int w8, int split
     const char* e = getenv("MDTF_WGRAD_PIPE");
     return !(e && e[0] == '0');
   }();
+  // MDTF_WGRAD_XCD=0: blocks in launch order instead of the XCD-grouped order (A/B switch)
+  static const int xcd = [] {
+    const char* e = getenv("MDTF_WGRAD_XCD");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  a.wg_xcd = xcd;
 #define WG2(BM_, BN_, S_, NW_) \
   if (bm == BM_ && bn == BN_ && stages == S_ && (NW_ == 8) == (w8 != 0)) \
     return pipe ? launch_wgrad_v2<BM_, BN_, S_, NW_, true>(a, splits, st) \

@@ -6,8 +6,11 @@ import csv
 import re
 import sys
 
-CATS = [("conv_fwd", r"conv_fd_v2<.*, 0, |conv_fd_kernel<.*, 0,|conv_ws_kernel<.*, 1>"),
-        ("conv_dgrad", r"conv_fd_v2<.*, [12], |conv_fd_kernel<.*, [12],|conv_ws_kernel<.*, [0234]>"), ("conv_wgrad", r"conv_wgrad"),
+WS = r"conv_ws_kernel<\d+, \d+, \d+, \d+, \d+, "     # ...<TP, NW, CG, D, KSC, EPI, DIRECT>
+CATS = [("conv_fwd", r"conv_fd_v2<.*, 0, |conv_fd_kernel<.*, 0,|" + WS + r"1,|stem_pack4"),
+        ("conv_dgrad", r"conv_fd_v2<.*, [12], |conv_fd_kernel<.*, [12],|" + WS + r"[234],"),
+        ("conv_ws_plain", WS + r"0,"), ("conv_wgrad", r"conv_wgrad|stem_wgrad"),
+        ("winograd", r"wino"),
         ("miopen", r"^(naive_conv|igemm|MIOpen|miopen|ck::|gridwise|sp3A|kernel_batched|SubTensor|_ZN2ck)"),
         ("bn_apply", r"bn_apply"), ("bn_dx", r"bn_dx"), ("bn_reduce", r"bn_reduce"), ("bn_finalize", r"bn_finalize"),
         ("optimizer", r"momentum|adam_kernel|sgd_kernel"), ("pool", r"pool"), ("transpose", r"transpose"),

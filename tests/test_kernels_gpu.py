@@ -342,9 +342,21 @@ def test_resnet50_step_loss_matches_cpu_fp32_reference(monkeypatch):
     monkeypatch.setenv("MDTF_KERNELS", "native")
     assert abs(l_cpu - l_gpu) / abs(l_cpu) < 1.5e-2, (l_cpu, l_gpu, l_stk)
     assert len(g_cpu) > 150
-    for k in g_cpu:
-        e, e_stock = _rel(g_gpu[k], g_cpu[k]), _rel(g_stk[k], g_cpu[k])
-        assert e < max(0.05, 1.25 * e_stock), (k, e, e_stock)
+    _check_grads({k: (_rel(g_gpu[k], g_cpu[k]), _rel(g_stk[k], g_cpu[k])) for k in g_cpu})
+
+
+def _check_grads(errs):
+    """errs: name -> (mdtf bf16 relative error, stock bf16 relative error) vs fp32.  Per tensor: within
+    5 %, or within 1.5x of stock (near-cancelling BN sums are noise-dominated for both, and atomics make
+    either run's rounding order vary); over the tensors where bf16 itself exceeds 5 %: the median
+    mdtf/stock ratio below 1.1."""
+    ratios = []
+    for k, (e, e_stock) in errs.items():
+        assert e < max(0.05, 1.5 * e_stock), (k, e, e_stock)
+        if e_stock > 0.05:
+            ratios.append(e / e_stock)
+    if ratios:
+        assert sorted(ratios)[len(ratios) // 2] < 1.1, sorted(ratios)
 
 
 def test_resnet_stage1_every_gradient_matches_cpu_fp32(monkeypatch):
@@ -352,9 +364,10 @@ def test_resnet_stage1_every_gradient_matches_cpu_fp32(monkeypatch):
     the full stage 1 (3 bottleneck units incl. the projection shortcut) and the first stage-2 unit
     (strided 3x3, strided projection), batch 16: GPU bf16 (mdtf kernels) vs the fp32 CPU engine, next
     to the same step on stock PyTorch bf16 ops (MDTF_KERNELS=torch: MIOpen / hipBLASLt) as the measure
-    of what bf16 itself costs.  Each mdtf gradient must be within 5 % of fp32, or no worse than 1.25x
+    of what bf16 itself costs.  Each mdtf gradient must be within 5 % of fp32, or no worse than 1.5x
     the stock bf16 error for tensors where bf16 alone exceeds that (BN parameters of layers followed by
-    another BN get gradients that nearly cancel over the batch)."""
+    another BN get gradients that nearly cancel over the batch), and the median mdtf/stock error ratio
+    over those tensors must stay below 1.1."""
     torch.manual_seed(5)
     x = torch.randn(16, 64, 64, 3)
     y = torch.randint(0, 16, (16,))
@@ -368,8 +381,7 @@ def test_resnet_stage1_every_gradient_matches_cpu_fp32(monkeypatch):
     worst = sorted(errs.items(), key=lambda kv: -kv[1][0])[:8]
     print("worst relative gradient errors (mdtf, stock bf16):", worst)
     assert len(errs) > 40
-    for k, (e, e_stock) in errs.items():
-        assert e < max(0.05, 1.25 * e_stock), (k, e, e_stock)
+    _check_grads(errs)
 
 
 class _Tiny(object):
