@@ -46,9 +46,10 @@ def main():
         best = None
         x4 = x.view(M, 1, 1, K)
         dy4 = dy.view(M, 1, 1, N)
-        for bm, bn, st, v in ((128, 128, 2, 2), (128, 128, 3, 2), (64, 128, 2, 2), (128, 64, 2, 2), (64, 64, 3, 2),
+        for bm, bn, st, v in ((128, 128, 2, 2), (128, 128, 3, 2), (128, 128, 4, 2), (128, 128, 5, 2), (64, 128, 2, 2),
+                              (64, 128, 4, 2), (64, 128, 6, 2), (128, 64, 2, 2), (64, 64, 3, 2),
                               (256, 256, 2, 3), (256, 128, 2, 3), (256, 128, 3, 3), (128, 256, 2, 3),
-                              (128, 256, 3, 3), (128, 128, 3, 3)):
+                              (128, 256, 3, 3), (128, 128, 3, 3), (128, 128, 4, 3), (128, 128, 5, 3)):
             for sp in (0, 4, 8, 16, 32, 64):
                 try:
                     t = timeit(lambda: C.mdtf_wgrad(x4, dy4, (1, 1, K, N), (1, 1), (0, 0, 0, 0), (1, 1), bm, bn, sp,

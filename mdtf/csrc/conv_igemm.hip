@@ -1117,8 +1117,10 @@ __global__ void __launch_bounds__(64 * NW, (wgrad_min_waves<BM, BN, STAGES, NW>(
         wait_vmcnt<PER_STAGE>();
       else if (n == 2)
         wait_vmcnt<2 * PER_STAGE>();
-      else
+      else if (n == 3 || 4 * PER_STAGE > 63)
         wait_vmcnt<3 * PER_STAGE>();
+      else
+        wait_vmcnt<(4 * PER_STAGE > 63 ? 3 : 4) * PER_STAGE>();
     };
     // interleave this half's fragment reads with the other half's MFMAs (both in one block)
     constexpr int NRD = 2 * (TM + TN), NMF = TM * TN, NIL = NRD < NMF ? NRD : NMF;
@@ -1376,6 +1378,8 @@ int dispatch_wgrad_v2(ConvArgs& a, int bm, int bn, int stages, int w8, int split
   WG2(64, 128, 3, 4) WG2(64, 64, 2, 4) WG2(64, 64, 3, 4) WG2(64, 64, 4, 4)
   WG2(256, 256, 2, 8) WG2(256, 128, 2, 8) WG2(256, 128, 3, 8) WG2(128, 256, 2, 8) WG2(128, 256, 3, 8)
   WG2(128, 128, 2, 8) WG2(128, 128, 3, 8) WG2(128, 128, 4, 8)
+  // deeper rings (more LDS-DMA in flight per block): 4-5 stages of 128 x 128, 4-6 of 64 x 128
+  WG2(128, 128, 5, 8) WG2(128, 128, 4, 4) WG2(128, 128, 5, 4) WG2(64, 128, 4, 4) WG2(64, 128, 6, 4)
 #undef WG2
   return MDTF_EUNSUPPORTED;
 }

@@ -14,7 +14,7 @@ i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $P --kernel-trace -d "$ROOT/gpurun_out/${TAG}_p$i" -o run --output-format csv \
-      -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --hip_graph 0 > "$ROOT/gpurun_out/${TAG}_p$i.log" 2>&1 \
+      -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --hip_graph 0 --bert 0 > "$ROOT/gpurun_out/${TAG}_p$i.log" 2>&1 \
       || { echo "pass $i failed rc=$?"; tail -20 "$ROOT/gpurun_out/${TAG}_p$i.log"; exit 1; }
   echo "pass $i ok"
 done
