@@ -50,7 +50,7 @@ def main():
                               (64, 128, 4, 2), (64, 128, 6, 2), (128, 64, 2, 2), (64, 64, 3, 2),
                               (256, 256, 2, 3), (256, 128, 2, 3), (256, 128, 3, 3), (128, 256, 2, 3),
                               (128, 256, 3, 3), (128, 128, 3, 3), (128, 128, 4, 3), (128, 128, 5, 3)):
-            for sp in (0, 4, 8, 16, 32, 64):
+            for sp in (0, 1, 2, 3, 4, 8, 16):
                 try:
                     t = timeit(lambda: C.mdtf_wgrad(x4, dy4, (1, 1, K, N), (1, 1), (0, 0, 0, 0), (1, 1), bm, bn, sp,
                                                     out=out, ver=v, stages=st))

@@ -170,7 +170,15 @@ __device__ __forceinline__ bool sum_partials(const float* __restrict__ p0, const
   const int c = blockIdx.x * kFinCh + lc;
   float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
   if (c < C) {
-    int i = grp;
+    // the usual case (gx <= 4 * kFinGroups: the conv epilogues' 64-128 slots): all of a thread's loads
+    // issued back to back before the first add, instead of one dependent L2 round trip per loop trip
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = grp + u * kFinGroups;
+      a[u] = r < gx ? p0[(long long)r * C + c] : 0.f;
+      b[u] = r < gx ? p1[(long long)r * C + c] : 0.f;
+    }
+    int i = grp + 4 * kFinGroups;
     for (; i + 3 * kFinGroups < gx; i += 4 * kFinGroups) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
