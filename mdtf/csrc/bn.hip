@@ -321,6 +321,55 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
+// Residual block whose shortcut is a projection conv + BN (no ReLU): y = relu(x*scale + shift + r*scale2 + shift2),
+// the shortcut BN applied on the fly from its conv output r, so its normalised tensor is never written / re-read.
+__global__ void __launch_bounds__(kThreads)
+    bn_apply_dual_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r, bf16_t* __restrict__ y,
+                         uint8_t* __restrict__ mask, long long n8, int C, const float* __restrict__ scale,
+                         const float* __restrict__ shift, const float* __restrict__ scale2,
+                         const float* __restrict__ shift2) {
+  const long long base = (long long)blockIdx.x * (kThreads * kVpt) + threadIdx.x;
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  uint4 xr[kVpt], rr[kVpt];
+#pragma unroll
+  for (int u = 0; u < kVpt; ++u) {
+    const long long i = base + u * kThreads;
+    xr[u] = i < n8 ? *reinterpret_cast<const uint4*>(x + i * 8) : z4;
+    rr[u] = i < n8 ? *reinterpret_cast<const uint4*>(r + i * 8) : z4;
+  }
+  const bool fixed = (kThreads * 8) % C == 0;
+  float sc[8], sh[8], sc2[8], sh2[8];
+  int c0 = static_cast<int>((base * 8) % C);
+  load_coef8(scale, c0, sc);
+  load_coef8(shift, c0, sh);
+  load_coef8(scale2, c0, sc2);
+  load_coef8(shift2, c0, sh2);
+#pragma unroll
+  for (int u = 0; u < kVpt; ++u) {
+    const long long i = base + u * kThreads;
+    if (i >= n8) break;
+    if (!fixed) {
+      c0 = static_cast<int>((i * 8) % C);
+      load_coef8(scale, c0, sc);
+      load_coef8(shift, c0, sh);
+      load_coef8(scale2, c0, sc2);
+      load_coef8(shift2, c0, sh2);
+    }
+    float v[8], rv[8];
+    unpack8(xr[u], v);
+    unpack8(rr[u], rv);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float o = fmaxf(v[k] * sc[k] + sh[k] + (rv[k] * sc2[k] + sh2[k]), 0.f);
+      bits |= (o > 0.f ? 1u : 0u) << k;
+      v[k] = o;
+    }
+    store_bf8(y + i * 8, v);
+    mask[i] = static_cast<uint8_t>(bits);
+  }
+}
+
 __global__ void __launch_bounds__(1024)
     bn_finalize_bwd(const float* __restrict__ p0, const float* __restrict__ p1, int gx, long long M, int C,
                     const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -484,6 +533,30 @@ MDTF_EXPORT int mdtf_bn_fwd_stats(const void* x, const void* res, void* y, uint8
                      C, gamma, beta, mmean, mvar, decay, eps, mean, invstd, scale, shift, 1);
   long long n8 = M * C / 8;
   launch_apply(x, res, y, mask, n8, C, scale, shift, relu, st);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// Training forward of relu(BN(x) + BN2(r)) when both convs emitted their statistics partials: both finalizes,
+// then one apply pass.  mean/invstd and mean2/invstd2 are saved for the two backward passes.
+MDTF_EXPORT int mdtf_bn_fwd_dual(const void* x, const void* r, void* y, uint8_t* mask, long long M, int C,
+                                 const float* gamma, const float* beta, float* mmean, float* mvar, const float* psum,
+                                 const float* psq, int P, float* mean, float* invstd, const float* gamma2,
+                                 const float* beta2, float* mmean2, float* mvar2, const float* psum2,
+                                 const float* psq2, int P2, float* mean2, float* invstd2, float decay, float eps,
+                                 float* ws, hipStream_t st) {
+  if (C % 8 || !mask) return MDTF_EINVAL;
+  float* scale = ws;
+  float* shift = ws + C;
+  float* scale2 = ws + 2 * C;
+  float* shift2 = ws + 3 * C;
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M,
+                     C, gamma, beta, mmean, mvar, decay, eps, mean, invstd, scale, shift, 1);
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum2, psq2, P2,
+                     M, C, gamma2, beta2, mmean2, mvar2, decay, eps, mean2, invstd2, scale2, shift2, 1);
+  const long long n8 = M * C / 8;
+  hipLaunchKernelGGL(bn_apply_dual_kernel, dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
+                     (const bf16_t*)r, (bf16_t*)y, mask, n8, C, scale, shift, scale2, shift2);
   MDTF_LAUNCH_CHECK();
   return 0;
 }

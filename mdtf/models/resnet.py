@@ -38,7 +38,8 @@ class ResNet(Model):
         kw = dict(training=training, bn_decay=self.bn_decay, bn_epsilon=self.bn_epsilon)
         with V.variable_scope(name):
             if stride != 1 or x.shape[-1] != 4 * filters:
-                shortcut = tools.conv_bn("shortcut", x, 4 * filters, 1, stride, relu=False, **kw)
+                # GPU training: its BN is applied inside conv3's residual BN pass (ops.bn.DeferredBN)
+                shortcut = tools.conv_bn("shortcut", x, 4 * filters, 1, stride, relu=False, defer=True, **kw)
             else:
                 shortcut = x
             y = tools.conv_bn("conv1", x, filters, 1, 1, relu=True, **kw)

@@ -1,4 +1,6 @@
 """Fused BatchNorm(+residual)(+ReLU) autograd op on the HIP kernels of ``csrc/bn.hip``."""
+import os
+
 import torch
 
 from . import _native as N
@@ -10,11 +12,15 @@ N.register("mdtf_bn_fwd_eval", [N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F
 N.register("mdtf_bn_bwd", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P, N.I, N.P])
 N.register("mdtf_bn_bwd_stats", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P, N.P, N.I,
                                  N.P, N.I, N.P])
+N.register("mdtf_bn_fwd_dual", [N.P, N.P, N.P, N.P, N.L, N.I] + [N.P] * 6 + [N.I, N.P, N.P] + [N.P] * 6 + [N.I, N.P, N.P]
+           + [N.F, N.F, N.P, N.P])
 N.register("mdtf_bn_fwd_stats", [N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P,
                                  N.I, N.P, N.P])
 
 
-FUSED_BWD = [0]      # backward passes that took their statistics from the dgrad epilogue (tests)
+FUSED_BWD = [0]
+# projection-shortcut BNs applied inside the residual BN's pass (MDTF_DEFER_SHORTCUT_BN=0: separate apply)
+DEFER_SHORTCUT = os.environ.get("MDTF_DEFER_SHORTCUT_BN", "1") != "0"      # backward passes that took their statistics from the dgrad epilogue (tests)
 
 
 def _check(x):
@@ -130,8 +136,110 @@ class _BNTrain(torch.autograd.Function):
         return (dx, rg, rb, dres, None, None, None, None, None, None)
 
 
+class DeferredBN(object):
+    """A training BatchNorm (no ReLU, no residual) whose apply is deferred into its consumer: the projection
+    shortcut of a ResNet block.  The residual BN that adds it applies both normalisations in one pass
+    (``csrc/bn.hip`` bn_apply_dual_kernel), so the shortcut's normalised tensor is never written or re-read."""
+
+    def __init__(self, x, gamma, beta, moving_mean, moving_var, decay, epsilon, stats):
+        self.x, self.gamma, self.beta = x, gamma, beta
+        self.moving_mean, self.moving_var = moving_mean, moving_var
+        self.decay, self.epsilon, self.stats = decay, epsilon, stats
+        self.shape = x.shape
+        self.dtype = x.dtype
+
+    def materialize(self):
+        return _BNTrain.apply(self.x, self.gamma, self.beta, None, self.moving_mean, self.moving_var, self.decay,
+                              self.epsilon, False, self.stats)
+
+
+class _BNTrainDual(torch.autograd.Function):
+    """relu(BN(x) + BN2(r)): the last BN of a projection-shortcut block with the shortcut's BN fused in."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, mm, mv, r, gamma2, beta2, mm2, mv2, decay, eps, stats, stats2):
+        from . import actsink
+        ctx.set_materialize_grads(False)
+        x = x.contiguous()
+        r = r.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        y = torch.empty_like(x)
+        mean, invstd = (torch.empty(C, dtype=torch.float32, device=x.device) for _ in range(2))
+        mean2, invstd2 = (torch.empty(C, dtype=torch.float32, device=x.device) for _ in range(2))
+        mask = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device)
+        g, b, g2, b2 = _f32(gamma), _f32(beta), _f32(gamma2), _f32(beta2)
+        ws = torch.empty(4 * C, dtype=torch.float32, device=x.device)
+        (ps, pq, P), (ps2, pq2, P2) = stats, stats2
+        N.check(N.fn("mdtf_bn_fwd_dual")(N.ptr(x), N.ptr(r), N.ptr(y), N.ptr(mask), M, C, N.ptr(g), N.ptr(b),
+                                         N.ptr(mm), N.ptr(mv), N.ptr(ps), N.ptr(pq), int(P), N.ptr(mean),
+                                         N.ptr(invstd), N.ptr(g2), N.ptr(b2), N.ptr(mm2), N.ptr(mv2), N.ptr(ps2),
+                                         N.ptr(pq2), int(P2), N.ptr(mean2), N.ptr(invstd2), float(decay), float(eps),
+                                         N.ptr(ws), N.stream_ptr()), "bn_fwd_dual")
+        from . import conv as _conv
+        _conv.stats_consumed(x.device)               # both finalizes re-zeroed their partials
+        ctx.save_for_backward(x, mask, g, mean, invstd, r, g2, mean2, invstd2)
+        ctx.sinks = tuple(V.grad_sink(t) for t in (gamma, beta, gamma2, beta2))
+        ctx.like = (gamma, beta, gamma2, beta2)
+        ctx.out_sink = actsink.attach(y)
+        if ctx.out_sink is not None:
+            ctx.out_sink.stat_req = (x, mask)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mask, g, mean, invstd, r, g2, mean2, invstd2 = ctx.saved_tensors
+        pstats = None
+        if ctx.out_sink is not None:
+            pstats = ctx.out_sink.take_stats()
+            if pstats is not None and dy is not None:
+                from . import conv as _conv
+                _conv.bwd_stats_release(pstats, False)
+                pstats = None
+            dy = ctx.out_sink.take(dy)
+            ctx.out_sink.stat_req = None
+        if dy is None:
+            return (None,) * 14
+        dy = dy.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        dx = torch.empty_like(x)
+        dz = torch.empty_like(x)                     # relu-masked gradient: the shortcut BN's output gradient
+        grads = [sk.grad if sk is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
+                 for sk in ctx.sinks]
+        if pstats is not None:
+            from . import conv as _conv
+            ws = torch.empty(3 * C, dtype=torch.float32, device=x.device)
+            N.check(N.fn("mdtf_bn_bwd_stats")(N.ptr(dy), N.ptr(x), N.ptr(mask), N.ptr(dx), N.ptr(dz), M, C, N.ptr(g),
+                                              N.ptr(mean), N.ptr(invstd), N.ptr(grads[0]), N.ptr(grads[1]), 1,
+                                              N.ptr(pstats[0]), N.ptr(pstats[1]), int(pstats.shape[1]), N.ptr(ws), 0,
+                                              N.stream_ptr()), "bn_bwd_stats")
+            _conv.bwd_stats_release(pstats, True)
+            FUSED_BWD[0] += 1
+        else:
+            ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
+            N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(x), N.ptr(mask), N.ptr(dx), N.ptr(dz), M, C, N.ptr(g),
+                                        N.ptr(mean), N.ptr(invstd), N.ptr(grads[0]), N.ptr(grads[1]), 1, N.ptr(ws), 0,
+                                        N.stream_ptr()), "bn_bwd")
+        dr = torch.empty_like(r)
+        ws2 = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
+        N.check(N.fn("mdtf_bn_bwd")(N.ptr(dz), N.ptr(r), None, N.ptr(dr), None, M, C, N.ptr(g2), N.ptr(mean2),
+                                    N.ptr(invstd2), N.ptr(grads[2]), N.ptr(grads[3]), 0, N.ptr(ws2), 0,
+                                    N.stream_ptr()), "bn_bwd")
+        out = []
+        for t, sk, gr in zip(ctx.like, ctx.sinks, grads):
+            out.append(V.grad_marker(t) if sk is not None else gr)
+        return (dx, out[0], out[1], None, None, dr, out[2], out[3], None, None, None, None, None, None)
+
+
 def batch_norm_nhwc(x, gamma, beta, moving_mean, moving_var, training, decay, epsilon, relu, residual, stats=None):
     _check(x)
+    if isinstance(residual, DeferredBN):
+        d = residual
+        if training and relu and stats is not None and d.stats is not None and d.x.shape == x.shape:
+            return _BNTrainDual.apply(x, gamma, beta, moving_mean, moving_var, d.x, d.gamma, d.beta, d.moving_mean,
+                                      d.moving_var, decay, epsilon, stats, d.stats)
+        residual = d.materialize()
     if residual is not None and residual.dtype != x.dtype:
         residual = residual.to(x.dtype)
     if training:

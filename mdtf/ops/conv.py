@@ -577,23 +577,27 @@ class _Conv(torch.autograd.Function):
         w = w.contiguous()
         ch = choose("fwd", x.shape, w.shape, stride, pads, dil)
         stats = None
+        # want_stats 2: a private zeroed partial buffer (statistics consumed later than the next conv, e.g. a
+        # deferred shortcut BN), else the persistent per-device one
+        sbuf = _stats_buffer if want_stats != 2 else (
+            lambda co, dev, slots=STAT_SLOTS: torch.zeros((2, slots, co), dtype=torch.float32, device=dev))
         if ch[0] == "mdtf":
             if want_stats:
                 co = w.shape[3]
                 slots = stat_slots(-(-x.shape[0] * out_hw[0] * out_hw[1] // ch[1]))
-                buf = _stats_buffer(co, x.device, slots)
+                buf = sbuf(co, x.device, slots)
                 stats = (buf[0], buf[1])
             y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2], stats, ch[4], ch[5])
         elif ch[0] == "stem":
             if want_stats:
-                buf = _stats_buffer(w.shape[3], x.device, STAT_SLOTS)
+                buf = sbuf(w.shape[3], x.device, STAT_SLOTS)
                 stats = (buf[0], buf[1])
             keep = []
             y = stem_fwd(x, w, out_hw, stride, pads, stats, keep_x4=keep)
             ctx.stem_x4 = keep[0]
         elif ch[0] == "ws":
             if want_stats:
-                buf = _stats_buffer(w.shape[3], x.device, STAT_SLOTS)
+                buf = sbuf(w.shape[3], x.device, STAT_SLOTS)
                 stats = (buf[0], buf[1])
             y = ws_fwd(x, transpose_filter(w), w.shape[0], w.shape[1], out_hw, stride, pads, dil, ch[1], stats)
         elif ch[0] == "winograd":
@@ -728,13 +732,15 @@ def conv2d_nhwc(x, w, stride, pads, dil, bias=None, act=None):
     return y
 
 
-def conv2d_stats_nhwc(x, w, stride, pads, dil):
-    """conv2d that also returns fused BN statistics partials ``(psum, psq, P)`` (or None)."""
+def conv2d_stats_nhwc(x, w, stride, pads, dil, private=False):
+    """conv2d that also returns fused BN statistics partials ``(psum, psq, P)`` (or None); ``private``: in a
+    buffer of their own (consumed after later convs have run) instead of the shared per-device one."""
     if x.dtype != torch.bfloat16:
         raise TypeError("mdtf conv kernels take bf16 activations, got %s" % x.dtype)
     if w.dtype != x.dtype:
         w = w.to(x.dtype)
-    y, psum, psq = _Conv.apply(x, w, tuple(stride), tuple(pads), tuple(dil), _out_hw(x, w, stride, pads, dil), True)
+    y, psum, psq = _Conv.apply(x, w, tuple(stride), tuple(pads), tuple(dil), _out_hw(x, w, stride, pads, dil),
+                               2 if private else True)
     if psum.numel() == 0:
         return y, None
     return y, (psum, psq, psum.shape[0])

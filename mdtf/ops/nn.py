@@ -232,11 +232,13 @@ def batch_norm(x, gamma, beta, moving_mean, moving_var, training=True, decay=0.9
 
 
 def conv_bn(x, w, gamma, beta, moving_mean, moving_var, strides=1, padding="SAME", training=True, decay=0.9,
-            epsilon=1e-5, relu=True, residual=None):
+            epsilon=1e-5, relu=True, residual=None, defer=False):
     """conv2d (no bias) -> batch_norm (+residual) (+ReLU).
 
     On the GPU the conv epilogue emits the per-channel Σy/Σy² partials, so the
     BN statistics pass over y disappears (BN runs finalize + apply only).
+    ``defer`` (no ReLU / residual; a projection shortcut): on the GPU return a :class:`bn.DeferredBN` that
+    the residual BN consuming it applies in its own pass; elsewhere the normalised tensor as usual.
     """
     n, h, wd, c = x.shape
     kh, kw, ci, co = w.shape
@@ -245,7 +247,10 @@ def conv_bn(x, w, gamma, beta, moving_mean, moving_var, strides=1, padding="SAME
     if _native.use_native(x) and training:
         from . import conv as conv_mod
         from . import bn
-        y, stats = conv_mod.conv2d_stats_nhwc(x, w, (sh, sw), (pt, pb, pl, pr), (1, 1))
+        defer = defer and not relu and residual is None and bn.DEFER_SHORTCUT
+        y, stats = conv_mod.conv2d_stats_nhwc(x, w, (sh, sw), (pt, pb, pl, pr), (1, 1), private=defer)
+        if defer and stats is not None:
+            return bn.DeferredBN(y, gamma, beta, moving_mean, moving_var, decay, epsilon, stats)
         return bn.batch_norm_nhwc(y, gamma, beta, moving_mean, moving_var, True, decay, epsilon, relu, residual,
                                   stats=stats)
     y = conv2d(x, w, strides, (pt, pb, pl, pr))
