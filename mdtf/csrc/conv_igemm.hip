@@ -57,6 +57,10 @@ struct ConvArgs {
   int stat_slots;      // fwd: BN-statistics partial rows (power of two: atomics spread; = mtiles: deterministic)
   int ld_dy, ld_dw;    // wgrad v2: row strides of DY and DW in elements (Cout for convolutions)
   int accumulate;      // fwd/dgrad v2: out += result (fan-out gradient accumulation) instead of out = result
+  // accumulate source (default: out itself): out = result + acc_src * [acc_mask bit] -- a ReLU-masked
+  // gradient another consumer left unmaterialised (1 mask bit per element, null: no mask)
+  const bf16_t* acc_src;
+  const uint8_t* acc_mask;
   // strided dgrad (MODE 2), one stride-parity class of DX pixels per launch: pixels
   // (h0 + SH i, w0 + SW j), i < Hc, j < Wc; their taps kh = kh0 + SH t (t < th), kw = kw0 + SW u (u < tw)
   // read DY at (q0h + i - t, q0w + j - u)
@@ -78,6 +82,16 @@ struct ConvArgs {
   int slab_cap;          // splits the slab has room for
   int wg_xcd;            // wgrad v2: XCD-aware block order (the row/col tiles of one pixel split share an L2)
 };
+
+// zero the bf16 elements of an 8-element vector whose mask bit (element k: bit k) is clear
+__device__ __forceinline__ uint4 mask_bf8(const uint4& v, uint32_t m8) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    o[k] = (w[k] & (((m8 >> (2 * k)) & 1u) ? 0x0000ffffu : 0u)) | (w[k] & (((m8 >> (2 * k + 1)) & 1u) ? 0xffff0000u : 0u));
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p, bool ok) {
   return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
@@ -729,7 +743,10 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
         pix = (nb * a.H + a.cls_h0 + a.SH * i) * a.W + a.cls_w0 + a.SW * j;
       }
       off[it] = pix * a.Ncol + n;
-      if (a.accumulate) old4[it] = *reinterpret_cast<const uint4*>(a.out + off[it]);
+      if (a.accumulate) {
+        old4[it] = *reinterpret_cast<const uint4*>((a.acc_src ? a.acc_src : a.out) + off[it]);
+        if (a.acc_mask) old4[it] = mask_bf8(old4[it], a.acc_mask[off[it] >> 3]);
+      }
       if (bstat) {
         x4[it] = *reinterpret_cast<const uint4*>(a.bx + off[it]);
         mb[it] = a.bmask ? a.bmask[off[it] >> 3] : 0xffu;
@@ -1490,8 +1507,10 @@ MDTF_EXPORT int mdtf_conv_fwd_v2(const void* x, const void* wt, void* y, float* 
 MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int OH,
                                    int OW, int Cout, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW,
                                    int bm, int bn, int accumulate, const void* bx, const void* bmask,
-                                   float* bsum, float* bsq, int bslots, hipStream_t st) {
+                                   float* bsum, float* bsq, int bslots, const void* acc_src, const void* acc_mask,
+                                   hipStream_t st) {
   if (Cout % 64 || Cin % 8) return MDTF_EINVAL;
+  if ((acc_src || acc_mask) && !accumulate) return MDTF_EINVAL;
   if ((long long)N * OH * OW * Cout * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
   if ((SH != 1 || SW != 1) && (DH != 1 || DW != 1)) return MDTF_EUNSUPPORTED;
   // <= 32 taps per K walk (per stride-parity class when strided)
@@ -1501,6 +1520,8 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
   a.wgt = (const bf16_t*)w;
   a.out = (bf16_t*)dx;
   a.accumulate = accumulate;
+  a.acc_src = (const bf16_t*)acc_src;       // null: out itself
+  a.acc_mask = (const uint8_t*)acc_mask;
   a.bx = (const bf16_t*)bx;
   a.bmask = (const uint8_t*)bmask;
   a.bsum = bsum;
@@ -1531,7 +1552,8 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
       c.M = (long long)N * c.cls_Hc * c.cls_Wc;
       c.K = c.cls_th * c.cls_tw * Cout;
       // no pixels / nothing to add (unless the BN statistics need every pixel)
-      if (c.M == 0 || (c.K == 0 && accumulate && !bsum)) continue;
+      // (with a separate accumulate source the class's pixels must still be written)
+      if (c.M == 0 || (c.K == 0 && accumulate && !bsum && !acc_src)) continue;
       const int cs = c.K > 64 && stages == 1 ? 2 : stages;
       const int rc = dispatch_fd_v2<2, false>(c, bm, bn, cs, st);
       if (rc) return rc;

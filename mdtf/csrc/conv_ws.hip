@@ -72,7 +72,8 @@ namespace {
 int conv_ws_impl(const void* src, const void* wgt, void* out, int N, int H, int W, int C, int cs, int OH, int OW,
                  int Ncol, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW, int wmode, int tile,
                  int grid_cap, float* ssum, float* ssq, int sslots, const void* bx, const void* bmask, float* bsum,
-                 float* bsq, int bslots, int accumulate, hipStream_t st) {
+                 float* bsq, int bslots, int accumulate, const void* acc_src, const void* acc_mask,
+                 hipStream_t st) {
   WsArgs a{};
   a.cs = cs;
   a.src = (const bf16_t*)src;
@@ -89,6 +90,9 @@ int conv_ws_impl(const void* src, const void* wgt, void* out, int N, int H, int 
   a.bx = (const bf16_t*)bx; a.bmask = (const uint8_t*)bmask; a.bsum = bsum; a.bsq = bsq;
   a.bslots = bslots > 0 ? bslots : 1;
   a.accumulate = accumulate;
+  if ((acc_src || acc_mask) && !accumulate) return MDTF_EINVAL;
+  a.acc_src = (const bf16_t*)acc_src;
+  a.acc_mask = (const uint8_t*)acc_mask;
   a.direct = (KH == 1 && KW == 1 && SH == 1 && SW == 1 && PH == 0 && PW == 0 && OH == H && OW == W && cs == C) ? 1 : 0;
   magic_div((unsigned)OW, a.mow, a.sow);
   magic_div((unsigned)OH, a.mohh, a.sohh);
@@ -112,9 +116,9 @@ MDTF_EXPORT int mdtf_conv_ws(const void* src, const void* wgt, void* out, int N,
                              int Ncol, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW, int wmode,
                              int tile, int grid_cap, float* ssum, float* ssq, int sslots, const void* bx,
                              const void* bmask, float* bsum, float* bsq, int bslots, int accumulate,
-                             hipStream_t st) {
+                             const void* acc_src, const void* acc_mask, hipStream_t st) {
   return conv_ws_impl(src, wgt, out, N, H, W, C, C, OH, OW, Ncol, KH, KW, SH, SW, PH, PW, DH, DW, wmode, tile,
-                      grid_cap, ssum, ssq, sslots, bx, bmask, bsum, bsq, bslots, accumulate, st);
+                      grid_cap, ssum, ssq, sslots, bx, bmask, bsum, bsq, bslots, accumulate, acc_src, acc_mask, st);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -162,5 +166,5 @@ MDTF_EXPORT int mdtf_conv_ws_stem(const void* x4, const void* wt, void* out, int
                                   hipStream_t st) {
   if ((OH - 1) * SH + KHp > H4 + 3 || (OW - 1) * SW + 8 > W4) return MDTF_EINVAL;   // rows / taps stay in x4
   return conv_ws_impl(x4, wt, out, N, H4, W4, 32, 4, OH, OW, Ncol, KHp, 1, SH, SW, 0, 0, 1, 1, 0, tile, 0, ssum,
-                      ssq, sslots, nullptr, nullptr, nullptr, nullptr, 0, 0, st);
+                      ssq, sslots, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, nullptr, st);
 }

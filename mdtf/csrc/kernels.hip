@@ -585,6 +585,32 @@ __global__ void lrn_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict_
   }
 }
 
+// out = g * [mask bit] (+ out): materialise a ReLU-masked gradient a fan-out sink held unmaterialised
+__global__ void __launch_bounds__(256) mask_mul_kernel(const uint4* __restrict__ g, const uint8_t* __restrict__ mask,
+                                                      uint4* __restrict__ out, long long n8, int accumulate) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const uint4 v = g[i];
+  const uint32_t m = mask[i];
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  float f[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f[2 * k] = ((m >> (2 * k)) & 1u) ? __uint_as_float(w[k] << 16) : 0.f;
+    f[2 * k + 1] = ((m >> (2 * k + 1)) & 1u) ? __uint_as_float(w[k] & 0xffff0000u) : 0.f;
+  }
+  if (accumulate) {
+    const uint4 o = out[i];
+    const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[2 * k] += __uint_as_float(ow[k] << 16);
+      f[2 * k + 1] += __uint_as_float(ow[k] & 0xffff0000u);
+    }
+  }
+  store_bf8(reinterpret_cast<bf16_t*>(out + i), f);
+}
+
 }  // namespace
 
 // ============================================================== exports
@@ -626,6 +652,17 @@ MDTF_EXPORT int mdtf_reduce_partials_strided(const float* ws, int B, int C, long
   int slices = B < kSlices * 4 ? static_cast<int>(ceil_div(B, 4)) : kSlices;
   if (slices < 1 || g_deterministic) slices = 1;
   hipLaunchKernelGGL(reduce_partials, dim3(ceil_div(C, 64), slices), dim3(kT), 0, st, ws, B, C, ld, out);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+MDTF_EXPORT int mdtf_mask_mul(const void* g, const void* mask, void* out, long long n, int accumulate,
+                              hipStream_t st) {
+  if (n % 8) return MDTF_EINVAL;
+  const long long n8 = n / 8;
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(mask_mul_kernel, dim3((unsigned)ceil_div(n8, 256LL)), dim3(256), 0, st, (const uint4*)g,
+                     (const uint8_t*)mask, (uint4*)out, n8, accumulate);
   MDTF_LAUNCH_CHECK();
   return 0;
 }

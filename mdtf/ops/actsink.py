@@ -13,8 +13,15 @@ sink-aware consumer writes its gradient straight into the sink buffer:
 The producer's backward (called with ``None`` once all consumers are done)
 takes the summed gradient from the sink. It also adds whatever ordinary autograd
 gradient arrived, so consumers that are not sink-aware stay correct.
+
+A ReLU'd residual BatchNorm's backward may leave its contribution *pending* instead of writing it:
+``(g, mask)`` meaning ``g * mask`` (the identity shortcut's gradient).  A conv dgrad that supports a
+masked accumulate source (:meth:`target_ex`) folds it into its own epilogue, so that tensor is never
+written and re-read; any other access materialises it first (``mdtf_mask_mul``).
 """
 import os
+
+import torch
 
 
 
@@ -23,7 +30,7 @@ class ActGradSink(object):
     producing BatchNorm needs for its backward statistics, ``(x, relu_mask)``.  The contributor that
     completes the sum (the ``consumers``-th) may emit the statistics in its epilogue into ``stats``
     (the v2 conv dgrad does)."""
-    __slots__ = ("buf", "count", "consumers", "stat_req", "stats")
+    __slots__ = ("buf", "count", "consumers", "stat_req", "stats", "pend")
 
     def __init__(self):
         self.buf = None
@@ -31,6 +38,35 @@ class ActGradSink(object):
         self.consumers = 0
         self.stat_req = None
         self.stats = None
+        self.pend = None
+
+    def defer_masked(self, g, mask):
+        """Contribute ``g * mask`` without materialising it (only as the first contribution)."""
+        assert self.buf is None and self.pend is None
+        self.pend = (g, mask)
+        self.count += 1
+
+    def _materialize(self):
+        if self.pend is None:
+            return
+        from . import _native as N
+        g, mask = self.pend
+        self.pend = None
+        acc = self.buf is not None
+        out = self.buf if acc else torch.empty_like(g)
+        N.check(N.fn("mdtf_mask_mul")(N.ptr(g), N.ptr(mask), N.ptr(out), g.numel(), int(acc), N.stream_ptr()),
+                "mask_mul")
+        self.buf = out
+
+    def target_ex(self):
+        """(buffer, accumulate, pending) for a kernel that can also fold a pending ``(g, mask)`` into its
+        epilogue: with ``pending`` not None, write ``result + g * mask`` into ``buffer`` (None: allocate)."""
+        if self.pend is not None and self.buf is None:
+            p, self.pend = self.pend, None
+            FOLDED[0] += 1
+            return None, False, p
+        self._materialize()
+        return self.buf, self.buf is not None, None
 
     def register(self):
         self.consumers += 1
@@ -42,6 +78,7 @@ class ActGradSink(object):
 
     def adopt_or_add(self, g):
         """Contribute a materialised gradient tensor."""
+        self._materialize()
         if self.buf is None:
             self.buf = g
         else:
@@ -51,6 +88,7 @@ class ActGradSink(object):
     def target(self):
         """(buffer, accumulate) for a kernel that writes its contribution in place; call
         :meth:`written` after launching it.  ``None`` buffer: allocate and write (accumulate False)."""
+        self._materialize()
         return self.buf, self.buf is not None
 
     def written(self, buf):
@@ -61,6 +99,7 @@ class ActGradSink(object):
         """Producer side: the total gradient (autograd's ``dy`` may be None)."""
         if self.count == 0:
             return dy
+        self._materialize()
         total = self.buf
         if dy is not None:
             total = total.add_(dy)
@@ -74,6 +113,9 @@ class ActGradSink(object):
 
 
 ENABLED = os.environ.get("MDTF_ACT_SINKS", "1") != "0"      # switch for A/B tests and benches
+FOLDED = [0]         # pending masked contributions folded into a dgrad epilogue (tests)
+# residual BN backward leaves the identity shortcut's gradient pending (MDTF_MASKED_RESIDUAL=0: written)
+MASKED_RESIDUAL = os.environ.get("MDTF_MASKED_RESIDUAL", "1") != "0"
 
 
 def attach(t):

@@ -102,12 +102,20 @@ class _BNTrain(torch.autograd.Function):
         dx = torch.empty_like(x)
         dres, accum = None, 0
         rs = ctx.res_sink if ctx.needs_input_grad[3] else None
+        pending = False
         if ctx.has_res:
-            if rs is not None:
-                dres, acc = rs.target()
-                accum = int(acc)
-            if dres is None:
-                dres = torch.empty_like(x)
+            from . import actsink
+            if (rs is not None and ctx.relu and actsink.MASKED_RESIDUAL and rs.buf is None and rs.pend is None
+                    and not rs.completing()):
+                # identity shortcut: its gradient dy * mask is left pending in the sink; the conv dgrad that
+                # completes the sum folds it into its epilogue (never written / re-read here)
+                pending = True
+            else:
+                if rs is not None:
+                    dres, acc = rs.target()
+                    accum = int(acc)
+                if dres is None:
+                    dres = torch.empty_like(x)
         sg, sb = ctx.sinks
         # dgamma/dbeta accumulate straight into the fp32 grad slots when available
         dgamma = sg.grad if sg is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
@@ -127,7 +135,9 @@ class _BNTrain(torch.autograd.Function):
                                         C, N.ptr(g),
                                         N.ptr(mean), N.ptr(invstd), N.ptr(dgamma), N.ptr(dbeta), int(ctx.relu),
                                         N.ptr(ws), accum, N.stream_ptr()), "bn_bwd")
-        if rs is not None and dres is not None:
+        if pending:
+            rs.defer_masked(dy, mask)
+        elif rs is not None and dres is not None:
             rs.written(dres)
             dres = None                                  # delivered through the sink
         gamma, beta = ctx.like

@@ -23,7 +23,7 @@ N.register("mdtf_conv_fwd", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P])
 N.register("mdtf_conv_dgrad", [N.P, N.P, N.P] + [N.I] * 17 + [N.P])
 N.register("mdtf_conv_wgrad", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 N.register("mdtf_conv_fwd_v2", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P])
-N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P, N.P, N.P, N.I, N.P])
+N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P, N.P, N.P, N.I, N.P, N.P, N.P])
 N.register("mdtf_conv_wgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.I, N.P])
 
 # split-K weight gradients: per-split partial slabs + one reduction pass (plain stores) instead of fp32
@@ -318,21 +318,27 @@ def mdtf_fwd(x, w, out_hw, stride, pads, dil, bm, bn, stats=None, ver=1, stages=
 
 
 def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn, ver=1, stages=2, out=None, accumulate=False,
-               bn_stats=None):
+               bn_stats=None, acc_src=None):
     """DX of a conv; v2 can write into ``out`` and accumulate (out += dgrad) in its epilogue.
 
     ``bn_stats = (x, relu_mask or None, psum, psq, slots)``: DX is the complete gradient of a BatchNorm
-    output; the epilogue also accumulates that BN's backward statistics into ``psum``/``psq``."""
+    output; the epilogue also accumulates that BN's backward statistics into ``psum``/``psq``.
+    ``acc_src = (g, relu_mask)``: accumulate ``g * mask`` instead of ``out``'s contents (a pending
+    masked contribution of an activation-gradient sink, ``actsink``)."""
     dx = out if out is not None else torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
     n, h, wd, c = x_shape
     kh, kw, ci, co = w.shape
     geo = [n, h, wd, c, dy.shape[1], dy.shape[2], co, kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1]]
     if ver in (2, 3):
         bx, bmask, bsum, bsq, bslots = bn_stats if bn_stats is not None else (None, None, None, None, 0)
+        ag, am = acc_src if acc_src is not None else (None, None)
         N.check(N.fn("mdtf_conv_dgrad_v2")(N.ptr(dy), N.ptr(w), N.ptr(dx), *geo, _v2_code(bm, stages, ver), bn,
-                                           int(bool(accumulate)), N.ptr(bx), N.ptr(bmask), N.ptr(bsum), N.ptr(bsq),
-                                           int(bslots), N.stream_ptr()), "conv_dgrad_v2")
+                                           int(bool(accumulate) or acc_src is not None), N.ptr(bx), N.ptr(bmask),
+                                           N.ptr(bsum), N.ptr(bsq), int(bslots), N.ptr(ag), N.ptr(am),
+                                           N.stream_ptr()), "conv_dgrad_v2")
         return dx
+    if acc_src is not None:
+        raise ValueError("a masked accumulate source needs the v2 kernel")
     if bn_stats is not None:
         raise ValueError("BN statistics in the dgrad epilogue need the v2 kernel")
     if accumulate:
@@ -342,7 +348,7 @@ def mdtf_dgrad(dy, w, x_shape, stride, pads, dil, bm, bn, ver=1, stages=2, out=N
 
 
 N.register("mdtf_conv_ws", [N.P, N.P, N.P] + [N.I] * 16 + [N.I, N.I] +
-           [N.P, N.P, N.I, N.P, N.P, N.P, N.P, N.I, N.I, N.P])
+           [N.P, N.P, N.I, N.P, N.P, N.P, N.P, N.I, N.I, N.P, N.P, N.P])
 
 
 def ws_ok(pass_, c, co, stride, kh, kw, dil=(1, 1)):
@@ -440,13 +446,14 @@ def ws_fwd(x, wt, kh, kw, out_hw, stride, pads, dil, tile, stats=None, grid_cap=
     N.check(N.fn("mdtf_conv_ws")(N.ptr(x), N.ptr(wt), N.ptr(y), n, h, wd, c, out_hw[0], out_hw[1], co, kh, kw,
                                  stride[0], stride[1], pads[0], pads[2], dil[0], dil[1], 0, _ws_code(*tile),
                                  int(grid_cap), N.ptr(s_sum), N.ptr(s_sq), slots, N.ptr(None), N.ptr(None),
-                                 N.ptr(None), N.ptr(None), 0, 0, N.stream_ptr()), "conv_ws_fwd")
+                                 N.ptr(None), N.ptr(None), 0, 0, N.ptr(None), N.ptr(None), N.stream_ptr()),
+            "conv_ws_fwd")
     return y
 
 
-def ws_dgrad(dy, w, x_shape, pads, dil, tile, out=None, accumulate=False, bn_stats=None, grid_cap=0):
+def ws_dgrad(dy, w, x_shape, pads, dil, tile, out=None, accumulate=False, bn_stats=None, grid_cap=0, acc_src=None):
     """DX of a stride-1 conv on the weight-stationary kernel (the filter used flipped, HWIO as is).
-    ``bn_stats = (x, relu_mask or None, psum, psq, slots)`` as in :func:`mdtf_dgrad`."""
+    ``bn_stats = (x, relu_mask or None, psum, psq, slots)`` and ``acc_src`` as in :func:`mdtf_dgrad`."""
     n, h, wd, ci = x_shape
     kh, kw, _, co = w.shape
     dx = out if out is not None else torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
@@ -456,7 +463,9 @@ def ws_dgrad(dy, w, x_shape, pads, dil, tile, out=None, accumulate=False, bn_sta
     N.check(N.fn("mdtf_conv_ws")(N.ptr(dy), N.ptr(w), N.ptr(dx), n, dy.shape[1], dy.shape[2], co, h, wd, ci, kh, kw,
                                  1, 1, ph, pw, dil[0], dil[1], 1, _ws_code(*tile), int(grid_cap), N.ptr(None),
                                  N.ptr(None), 0, N.ptr(bx), N.ptr(bmask), N.ptr(bsum), N.ptr(bsq), int(bslots),
-                                 int(bool(accumulate)), N.stream_ptr()), "conv_ws_dgrad")
+                                 int(bool(accumulate) or acc_src is not None),
+                                 N.ptr(acc_src[0] if acc_src is not None else None),
+                                 N.ptr(acc_src[1] if acc_src is not None else None), N.stream_ptr()), "conv_ws_dgrad")
     return dx
 
 
@@ -649,21 +658,22 @@ class _Conv(torch.autograd.Function):
         elif need_dx and cd[0] == "ws":
             tile = cd[1]
             if xs is not None:
-                buf, acc = xs.target()
+                buf, acc, pend = xs.target_ex()
                 bst = None
                 if xs.stat_req is not None and xs.completing() and BWD_STATS:
                     bx, bmask = xs.stat_req
                     sbuf = bwd_stats_acquire(x.device, x.shape[3], STAT_SLOTS)
                     bst = (bx, bmask, sbuf[0], sbuf[1], sbuf.shape[1])
                     tile = (2,) + tuple(tile[1:])      # the statistics epilogue's register budget
-                xs.written(ws_dgrad(dy, w, x.shape, pads, dil, tile, out=buf, accumulate=acc, bn_stats=bst))
+                xs.written(ws_dgrad(dy, w, x.shape, pads, dil, tile, out=buf, accumulate=acc, bn_stats=bst,
+                                    acc_src=pend))
                 if bst is not None:
                     xs.stats = sbuf
             else:
                 dx = ws_dgrad(dy, w, x.shape, pads, dil, tile)
         elif need_dx and not lib_dx:
             if xs is not None and cd[4] in (2, 3):
-                buf, acc = xs.target()
+                buf, acc, pend = xs.target_ex()
                 bst = None
                 if xs.stat_req is not None and xs.completing() and BWD_STATS and not N.deterministic():
                     # this dgrad completes the BN output's gradient: emit the BN backward statistics
@@ -671,7 +681,7 @@ class _Conv(torch.autograd.Function):
                     sbuf = bwd_stats_acquire(x.device, x.shape[3], stat_slots(-(-x.numel() // x.shape[3] // cd[1])))
                     bst = (bx, bmask, sbuf[0], sbuf[1], sbuf.shape[1])
                 xs.written(mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5], out=buf,
-                                      accumulate=acc, bn_stats=bst))
+                                      accumulate=acc, bn_stats=bst, acc_src=pend))
                 if bst is not None:
                     xs.stats = sbuf
                 dx = None

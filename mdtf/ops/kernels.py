@@ -7,6 +7,7 @@ from ..train import variables as V
 N.register("mdtf_bias_act_fwd", [N.P, N.P, N.P, N.P, N.L, N.I, N.I, N.P])
 N.register("mdtf_act_bwd", [N.P, N.P, N.P, N.P, N.L, N.I, N.P])
 N.register("mdtf_colsum", [N.P, N.L, N.I, N.P, N.P, N.P])
+N.register("mdtf_mask_mul", [N.P, N.P, N.P, N.L, N.I, N.P])
 N.register("mdtf_colsum_ws", [N.L, N.I], restype=N.L)
 N.register("mdtf_pool_fwd", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.P])
 N.register("mdtf_pool_bwd", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.P])

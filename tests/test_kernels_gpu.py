@@ -991,6 +991,33 @@ def test_bn_backward_stats_from_dgrad_epilogue(model, monkeypatch):
         assert _rel(gf[k], go[k]) < 1e-2, (k, _rel(gf[k], go[k]))
 
 
+@pytest.mark.parametrize("conv_backend", ["mdtf2", "ws"])
+def test_masked_residual_gradient_folded_into_dgrad(conv_backend, monkeypatch):
+    """The residual BN's identity-shortcut gradient dy*mask left pending in the sink and folded into the
+    completing conv dgrad's epilogue (v2 or weight-stationary kernel, masked accumulate source) ==
+    writing it out and accumulating (MDTF_MASKED_RESIDUAL=0); the folded path must actually run."""
+    from mdtf.ops import actsink
+    if conv_backend == "mdtf2":
+        monkeypatch.setenv("MDTF_CONV", "mdtf2")
+    global _Tiny
+    saved = _Tiny
+    _Tiny = _TinyRes
+    try:
+        torch.manual_seed(6)
+        x = torch.randn(16, 12, 12, 64)
+        y = torch.randint(0, 16, (16,))
+        n0 = actsink.FOLDED[0]
+        lf, gf = _tiny_step(DEV, torch.bfloat16, x, y)
+        assert actsink.FOLDED[0] > n0
+        monkeypatch.setattr(actsink, "MASKED_RESIDUAL", False)
+        lo, go = _tiny_step(DEV, torch.bfloat16, x, y)
+    finally:
+        _Tiny = saved
+    assert lf == lo
+    for k in go:
+        assert _rel(gf[k], go[k]) < 1e-2, (k, _rel(gf[k], go[k]))
+
+
 @pytest.mark.parametrize("conv_backend", ["mdtf2", "miopen"])
 def test_fanout_gradient_sinks(conv_backend, monkeypatch):
     """In-place fan-out gradient accumulation == autograd's add (same kernels otherwise), and both ~ fp32 CPU."""
