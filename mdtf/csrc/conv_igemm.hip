@@ -81,6 +81,14 @@ struct ConvArgs {
   float* slab;
   int slab_cap;          // splits the slab has room for
   int wg_xcd;            // wgrad v2: XCD-aware block order (the row/col tiles of one pixel split share an L2)
+  // dense forward (fd v2 MODE 3): Y[M][Ncol] = act(X[M][K] W + bias), W N-contiguous [K][ld_b] read as
+  // [64 k][64 col] half-images by transposed fragment reads (no transposed weight copy).  The columns are
+  // nseg segments of seg_cols, each its own matrix wseg[s] (q | k | v without a concatenated copy).
+  const bf16_t* wseg[4];
+  int seg_cols, ld_b;
+  const bf16_t* bias;    // bf16 [Ncol], added to the fp32 accumulators (null: none)
+  bf16_t* pre_out;       // act != 0: the bf16 pre-activation is also stored here (null: not kept)
+  int act;               // 0 none, 1 relu, 2 gelu (tanh form)
 };
 
 // zero the bf16 elements of an 8-element vector whose mask bit (element k: bit k) is clear
@@ -121,6 +129,33 @@ __device__ __forceinline__ bf16x8_t frag_ncontig(const bf16_t* tile, int ld, int
   v4s r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a2);
   v4s lo = odd ? r2 : r1;
   v4s hi = odd ? r1 : r2;
+  short8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, f);
+}
+
+// dense-layer activation epilogue: 1 relu, 2 gelu (tanh form, as kernels.hip's act_f).  0.5 (1 + tanh u) is
+// sigmoid(2u): one v_exp_f32 and one v_rcp_f32 per element instead of a libm tanhf in the GEMM's epilogue
+__device__ __forceinline__ float dense_act(float v, int act) {
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) {
+    const float u2 = 1.5957691216f * (v + 0.044715f * v * v * v);     // 2u
+    return v * __builtin_amdgcn_rcpf(1.f + __expf(-u2));
+  }
+  return v;
+}
+
+// chunk swizzle of the [64 k][64 col] half-images read by transposed fragment reads (see the v2 wgrad)
+__device__ __forceinline__ int trswz(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
+
+// fragment (16 cols x 32 k) of a [64 k][64 col] half-image: lane l -> col (l&15), k = 8*(l>>4) .. +7
+__device__ __forceinline__ bf16x8_t frag_tr(const char* img, int col0, int kbase, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int c = col0 + 4 * p;                       // first of this lane's 4 columns
+  const int k1 = kbase + 8 * g + q, k2 = k1 + 4;
+  const char* a1 = img + k1 * 128 + (((c >> 3) ^ trswz(k1)) << 4) + (c & 7) * 2;
+  const char* a2 = img + k2 * 128 + (((c >> 3) ^ trswz(k2)) << 4) + (c & 7) * 2;
+  v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a1);
+  v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a2);
   short8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8_t, f);
 }
@@ -543,11 +578,13 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   const long long m0 = (long long)mt * BM;
   const int n0 = nt * BN;
 
-  const int GH = MODE == 0 ? a.H : a.OH;
-  const int GW = MODE == 0 ? a.W : a.OW;
-  const int GC = MODE == 0 ? a.Cin : a.Cout;
-  const int RH = MODE == 0 ? a.OH : MODE == 1 ? a.H : a.cls_Hc;
-  const int RW = MODE == 0 ? a.OW : MODE == 1 ? a.W : a.cls_Wc;
+  // MODE 3 (dense forward) gathers A like a 1x1 forward convolution
+  constexpr int AM = MODE == 3 ? 0 : MODE;
+  const int GH = AM == 0 ? a.H : a.OH;
+  const int GW = AM == 0 ? a.W : a.OW;
+  const int GC = AM == 0 ? a.Cin : a.Cout;
+  const int RH = AM == 0 ? a.OH : AM == 1 ? a.H : a.cls_Hc;
+  const int RW = AM == 0 ? a.OW : AM == 1 ? a.W : a.cls_Wc;
   const int lrow = lane >> 3;
   const int TKW = MODE == 2 ? a.cls_tw : a.KW;      // taps per filter row of the K walk
   const int ntaps = MODE == 2 ? a.cls_th * a.cls_tw : a.KH * a.KW;   // <= 32 (host-checked)
@@ -556,7 +593,12 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   // buffer ranges: bounds-checked loads, out-of-range offsets read as zero (host checks < 2 GiB)
   const int bytes_a = (int)((long long)a.N * GH * GW * GC * 2);
   // (MODE 2 walks a subset of the filter taps: the range is the whole filter)
-  const int bytes_b = (int)((long long)(MODE == 2 ? a.KH * a.KW * a.Cout : a.K) * a.Ncol * 2);
+  const int bytes_b = MODE == 3 ? (int)((long long)a.K * a.ld_b * 2)
+                                : (int)((long long)(MODE == 2 ? a.KH * a.KW * a.Cout : a.K) * a.Ncol * 2);
+  // MODE 3: this block's column segment (seg_cols % BN == 0, host-checked)
+  const int seg = MODE == 3 ? n0 / a.seg_cols : 0;
+  const bf16_t* wbase = MODE == 3 ? a.wseg[seg] : a.wgt;
+  const int nl0 = MODE == 3 ? n0 - seg * a.seg_cols : n0;
 
   // per A row: element offset of tap (0,0) (may be "negative", wraps) + valid-tap bitmask
   unsigned a_off[RA], a_mask[RA];
@@ -570,16 +612,16 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
     const long long t = mm / RW;
     const int oh = static_cast<int>(t % RH);
     const int n = static_cast<int>(t / RH);
-    const int y0 = MODE == 0 ? oh * a.SH - a.PH : MODE == 1 ? oh + a.PH : a.cls_q0h + oh;
-    const int x0 = MODE == 0 ? ow * a.SW - a.PW : MODE == 1 ? ow + a.PW : a.cls_q0w + ow;
+    const int y0 = AM == 0 ? oh * a.SH - a.PH : AM == 1 ? oh + a.PH : a.cls_q0h + oh;
+    const int x0 = AM == 0 ? ow * a.SW - a.PW : AM == 1 ? ow + a.PW : a.cls_q0w + ow;
     const int ch = 8 * ((lane & 7) ^ ((row >> 1) & 7));
     a_off[i] = (unsigned)((((long long)n * GH + y0) * GW + x0) * GC + ch);
     unsigned mask = 0;
     if (ok) {
       for (int tt = 0; tt < ntaps; ++tt) {
         const int kh = tt / TKW, kw = tt - kh * TKW;
-        const int iy = MODE == 0 ? y0 + kh * DHe : y0 - kh * DHe;
-        const int ix = MODE == 0 ? x0 + kw * DWe : x0 - kw * DWe;
+        const int iy = AM == 0 ? y0 + kh * DHe : y0 - kh * DHe;
+        const int ix = AM == 0 ? x0 + kw * DWe : x0 - kw * DWe;
         if (iy >= 0 && iy < GH && ix >= 0 && ix < GW) mask |= 1u << tt;
       }
     }
@@ -589,6 +631,15 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   unsigned b_off[RB];
 #pragma unroll
   for (int i = 0; i < RB; ++i) {
+    if (MODE == 3) {
+      // 1 KiB block (wave + NW i) = rows 8 (blk & 7) .. +7 of half-image blk >> 3; each lane fetches the
+      // 16-B column chunk that the transposed reads expect at its LDS slot
+      const int blk = wave + NW * i;
+      const int krow = 8 * (blk & 7) + lrow;
+      const int col = nl0 + 64 * (blk >> 3) + 8 * ((lane & 7) ^ trswz(krow));
+      b_off[i] = (unsigned)(((long long)krow * a.ld_b + col) * 2);
+      continue;
+    }
     const int row = 8 * (wave + NW * i) + lrow;
     const int n = n0 + row;
     const int ch = 8 * ((lane & 7) ^ ((row >> 1) & 7));
@@ -599,7 +650,7 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   // scalar K-walk state: tap index, (kh, kw), channel offset c0 within the tap
   int s_t = 0, s_kh = 0, s_kw = 0, s_c0 = 0, s_k0 = 0;
   auto stage = [&](int buf) {
-    const int tap_e = (MODE == 0 ? (s_kh * DHe * GW + s_kw * DWe) : -(s_kh * DHe * GW + s_kw * DWe)) * GC + s_c0;
+    const int tap_e = (AM == 0 ? (s_kh * DHe * GW + s_kw * DWe) : -(s_kh * DHe * GW + s_kw * DWe)) * GC + s_c0;
     char* lds = smem_raw + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
@@ -609,10 +660,10 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
     }
     char* ldsb = lds + BM * ROWB;
     const int wtap = MODE == 2 ? (a.cls_kh0 + a.SH * s_kh) * a.KW + a.cls_kw0 + a.SW * s_kw : s_t;
-    const int sb = MODE == 0 ? s_k0 * 2 : (wtap * a.Cin * a.Cout + s_c0) * 2;
+    const int sb = MODE == 3 ? s_k0 * a.ld_b * 2 : MODE == 0 ? s_k0 * 2 : (wtap * a.Cin * a.Cout + s_c0) * 2;
 #pragma unroll
     for (int i = 0; i < RB; ++i)
-      dma16(a.wgt, bytes_b, ldsb + (wave + NW * i) * 1024, b_off[i], sb);
+      dma16(wbase, bytes_b, ldsb + (wave + NW * i) * 1024, b_off[i], sb);
     // advance the K walk by 64
     s_k0 += 64;
     s_c0 += 64;
@@ -666,6 +717,11 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
+        if (MODE == 3) {
+          const int col = wn * (TN * 16) + j * 16;
+          fb[h][j] = frag_tr(Bs + (col >> 6) * 8192, col & 63, 32 * h, lane);
+          continue;
+        }
         const int row = wn * (TN * 16) + j * 16 + fr;
         const int pc = (h * 4 + fq) ^ ((row >> 1) & 7);
         fb[h][j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(Bs + row * ROWB + pc * 16));
@@ -703,6 +759,13 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
     for (int j = 0; j < TN; ++j) {
       const int cl = wn * (TN * 16) + j * 16 + 4 * g;
       float4v v = acc[i][j];
+      if (MODE == 3 && a.bias) {                 // bias on the fp32 accumulators (one rounding)
+        const uint2 b4 = *reinterpret_cast<const uint2*>(a.bias + n0 + cl);
+        v[0] += __uint_as_float(b4.x << 16);
+        v[1] += __uint_as_float(b4.x & 0xffff0000u);
+        v[2] += __uint_as_float(b4.y << 16);
+        v[3] += __uint_as_float(b4.y & 0xffff0000u);
+      }
       uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
       // 8-B half swap on rows 8..15 of every 16: rows li and li+8 would otherwise share
@@ -711,7 +774,7 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
     }
   }
   __syncthreads();
-  const bool bstat = MODE != 0 && a.bsum != nullptr;
+  const bool bstat = (MODE == 1 || MODE == 2) && a.bsum != nullptr;
   float bs0[8], bs1[8];                        // this thread's BN-backward partials (fixed c8 per thread)
 #pragma unroll
   for (int k = 0; k < 8; ++k) bs0[k] = bs1[k] = 0.f;
@@ -761,7 +824,17 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
     uint4 v = *reinterpret_cast<const uint4*>(smem_raw + row * LDC + c8 * 16);
     if ((row >> 3) & 1) v = make_uint4(v.z, v.w, v.x, v.y);
     bf16_t* dst = a.out + off[it];
-    if (a.accumulate || bstat) {
+    if (MODE == 3 && a.act) {                    // activation epilogue on the rounded pre-activation
+      if (a.pre_out) *reinterpret_cast<uint4*>(a.pre_out + off[it]) = v;
+      float c[8];
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        c[2 * k] = dense_act(__uint_as_float(w4[k] << 16), a.act);
+        c[2 * k + 1] = dense_act(__uint_as_float(w4[k] & 0xffff0000u), a.act);
+      }
+      store_bf8(dst, c);
+    } else if (a.accumulate || bstat) {
       float c[8];
       const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -945,20 +1018,6 @@ int dispatch_fd_v2(ConvArgs& a, int bm, int bn, int stages, hipStream_t st) {
 // split-K partial tiles accumulate into DW with fp32 atomics (16 consecutive
 // co per 16-lane group).
 // ============================================================================
-__device__ __forceinline__ int trswz(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
-
-// fragment (16 cols x 32 k) of a [64 k][64 col] half-image: lane l -> col (l&15), k = 8*(l>>4) .. +7
-__device__ __forceinline__ bf16x8_t frag_tr(const char* img, int col0, int kbase, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int c = col0 + 4 * p;                       // first of this lane's 4 columns
-  const int k1 = kbase + 8 * g + q, k2 = k1 + 4;
-  const char* a1 = img + k1 * 128 + (((c >> 3) ^ trswz(k1)) << 4) + (c & 7) * 2;
-  const char* a2 = img + k2 * 128 + (((c >> 3) ^ trswz(k2)) << 4) + (c & 7) * 2;
-  v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a1);
-  v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a2);
-  short8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8_t, f);
-}
 
 // register budget: as many waves per SIMD as the LDS ring lets blocks be resident
 template <int BM, int BN, int STAGES, int NW>
@@ -1604,4 +1663,36 @@ MDTF_EXPORT int mdtf_gemm_wgrad(const void* x, const void* dy, float* dw, long l
   a.slab_cap = slab_cap;
   a.dbias = dbias;
   return dispatch_wgrad_v2(a, bm % 10000, bn, stages, bm / 10000, splits, st);
+}
+
+// Dense forward on the fd v2 kernel (MODE 3): Y[M][nseg * seg_cols] = act(X[M][K] [W_0 | .. | W_{nseg-1}] + bias),
+// each W_s bf16 [K][seg_cols] (row-major, no transposed copy), bias bf16 [nseg * seg_cols] or null; with act != 0
+// the pre-activation is also written to pre (null: not kept).  K % 64 == 0, seg_cols % bn == 0, nseg <= 4.
+// bm encodes [10000 if 8 waves] + stages * 1000 + tile rows.
+MDTF_EXPORT int mdtf_gemm_fwd(const void* x, const void* w0, const void* w1, const void* w2, const void* w3, int nseg,
+                              int seg_cols, const void* bias, void* y, void* pre, int act, long long M, int K, int bm,
+                              int bn, hipStream_t st) {
+  if (nseg < 1 || nseg > 4 || K % 64 || bn <= 0 || seg_cols % bn || seg_cols % 64 || M <= 0 || act < 0 || act > 2)
+    return MDTF_EINVAL;
+  if (M > 0x7fffffff || M * K * 2 > 0x7fffffffLL || (long long)K * seg_cols * 2 > 0x7fffffffLL)
+    return MDTF_EUNSUPPORTED;
+  ConvArgs a = make_args((int)M, 1, 1, K, 1, 1, nseg * seg_cols, 1, 1, 1, 1, 0, 0, 1, 1);
+  a.src = (const bf16_t*)x;
+  const void* ws[4] = {w0, w1, w2, w3};
+  for (int s = 0; s < 4; ++s) {
+    if (s < nseg && !ws[s]) return MDTF_EINVAL;
+    a.wseg[s] = (const bf16_t*)(s < nseg ? ws[s] : w0);
+  }
+  a.seg_cols = seg_cols;
+  a.ld_b = seg_cols;
+  a.bias = (const bf16_t*)bias;
+  a.pre_out = (bf16_t*)pre;
+  a.act = act;
+  a.out = (bf16_t*)y;
+  a.M = M;
+  a.Ncol = nseg * seg_cols;
+  a.K = K;
+  const int w8 = bm / 10000, stages = (bm % 10000) / 1000 ? (bm % 10000) / 1000 : 2;
+  bm = w8 * 10000 + bm % 1000;
+  return dispatch_fd_v2<3, false>(a, bm, bn, stages, st);
 }

@@ -34,6 +34,10 @@ def _f32(t):
     return None if t is None else t.detach().float().contiguous()
 
 
+# MDTF_BN_TRACE=1: record (input shape, has residual, how the backward statistics were obtained) per BN backward
+BWD_TRACE = [] if os.environ.get("MDTF_BN_TRACE") == "1" else None
+
+
 class _BNTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, mm, mv, decay, eps, relu, stats):
@@ -85,13 +89,18 @@ class _BNTrain(torch.autograd.Function):
     def backward(ctx, dy):
         x, mask, g, mean, invstd = ctx.saved_tensors
         pstats = None
+        why = "no_sink"
         if ctx.out_sink is not None:
             pstats = ctx.out_sink.take_stats()
+            why = "no_epilogue_stats" if pstats is None else "fused"
             if pstats is not None and dy is not None:
                 # part of dy came through plain autograd: the epilogue statistics are incomplete
                 from . import conv as _conv
                 _conv.bwd_stats_release(pstats, False)
                 pstats = None
+                why = "autograd_part"
+        if BWD_TRACE is not None:
+            BWD_TRACE.append((tuple(x.shape), ctx.has_res, why))
             dy = ctx.out_sink.take(dy)
             ctx.out_sink.stat_req = None
         if dy is None:
@@ -214,13 +223,14 @@ class _BNTrainDual(torch.autograd.Function):
         C = x.shape[-1]
         M = x.numel() // C
         dx = torch.empty_like(x)
-        dz = torch.empty_like(x)                     # relu-masked gradient: the shortcut BN's output gradient
+        # the shortcut BN's output gradient is dy * mask: its backward reads dy and the ReLU mask itself
+        # (no masked copy dz is written and re-read)
         grads = [sk.grad if sk is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
                  for sk in ctx.sinks]
         if pstats is not None:
             from . import conv as _conv
             ws = torch.empty(3 * C, dtype=torch.float32, device=x.device)
-            N.check(N.fn("mdtf_bn_bwd_stats")(N.ptr(dy), N.ptr(x), N.ptr(mask), N.ptr(dx), N.ptr(dz), M, C, N.ptr(g),
+            N.check(N.fn("mdtf_bn_bwd_stats")(N.ptr(dy), N.ptr(x), N.ptr(mask), N.ptr(dx), None, M, C, N.ptr(g),
                                               N.ptr(mean), N.ptr(invstd), N.ptr(grads[0]), N.ptr(grads[1]), 1,
                                               N.ptr(pstats[0]), N.ptr(pstats[1]), int(pstats.shape[1]), N.ptr(ws), 0,
                                               N.stream_ptr()), "bn_bwd_stats")
@@ -228,13 +238,13 @@ class _BNTrainDual(torch.autograd.Function):
             FUSED_BWD[0] += 1
         else:
             ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
-            N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(x), N.ptr(mask), N.ptr(dx), N.ptr(dz), M, C, N.ptr(g),
+            N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(x), N.ptr(mask), N.ptr(dx), None, M, C, N.ptr(g),
                                         N.ptr(mean), N.ptr(invstd), N.ptr(grads[0]), N.ptr(grads[1]), 1, N.ptr(ws), 0,
                                         N.stream_ptr()), "bn_bwd")
         dr = torch.empty_like(r)
         ws2 = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
-        N.check(N.fn("mdtf_bn_bwd")(N.ptr(dz), N.ptr(r), None, N.ptr(dr), None, M, C, N.ptr(g2), N.ptr(mean2),
-                                    N.ptr(invstd2), N.ptr(grads[2]), N.ptr(grads[3]), 0, N.ptr(ws2), 0,
+        N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(r), N.ptr(mask), N.ptr(dr), None, M, C, N.ptr(g2), N.ptr(mean2),
+                                    N.ptr(invstd2), N.ptr(grads[2]), N.ptr(grads[3]), 1, N.ptr(ws2), 0,
                                     N.stream_ptr()), "bn_bwd")
         out = []
         for t, sk, gr in zip(ctx.like, ctx.sinks, grads):

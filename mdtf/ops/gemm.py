@@ -1,11 +1,12 @@
 """Dense / matmul on the GPU: hand-written MFMA kernels where they win, hipBLASLt GEMMs elsewhere,
 fp32 weight-gradient sinks.
 
-Forward: ``y = act(x @ W + b)`` — the GEMM and the bias run as ONE hipBLASLt
-call (``addmm``'s bias epilogue); GELU/ReLU (which must keep the
-pre-activation for backward) is the mdtf activation kernel.  Several weight
-matrices that share an input (BERT's query/key/value) run as one GEMM on the
-column-concatenated weights.
+Forward: ``y = act(x @ W + b)`` in ONE hand-written MFMA launch (``hand_fwd``: the fd v2 kernel's MODE 3
+reads W in place through transposed LDS fragment reads, adds the bias to the fp32 accumulators and applies
+GELU/ReLU in the epilogue, also storing the pre-activation GELU's backward needs).  Several weight matrices
+that share an input (BERT's query/key/value) are column segments of the same launch, with no concatenated
+copy.  Shapes it does not take (and ``MDTF_DENSE_FWD=hipblaslt``) use ``addmm`` (hipBLASLt, bias epilogue)
+plus the mdtf activation kernel.
 
 Backward: ``dx = dpre @ W^T`` (bf16; hipBLASLt, or with ``MDTF_DENSE_DGRAD=mdtf`` the mdtf v2 dgrad kernel
 for the shapes of ``DGRAD_TILES``; accumulated inside the GEMM into a fanned-out input's gradient sink), and the weight gradient is the mdtf weight-gradient
@@ -31,6 +32,18 @@ _fp32_out_ok = None      # does this torch build accept addmm(out_dtype=float32,
 FUSED_BIAS_GRAD = os.environ.get("MDTF_FUSED_BIAS_GRAD", "1") != "0"
 
 N.register("mdtf_gemm_wgrad", [N.P, N.P, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.P, N.I, N.P, N.P])
+N.register("mdtf_gemm_fwd", [N.P, N.P, N.P, N.P, N.P, N.I, N.I, N.P, N.P, N.P, N.I, N.L, N.I, N.I, N.I, N.P])
+
+# forward y = act(x W + b) on the hand-written MFMA kernel (csrc/conv_igemm.hip fd v2 MODE 3: W read in place,
+# N-contiguous, by transposed LDS fragment reads; bias on the fp32 accumulators; GELU/ReLU and the saved
+# pre-activation in the epilogue; q|k|v as column segments of one launch, no concatenated weight copy).
+# MDTF_DENSE_FWD: "auto" (default) = the shapes of FWD_TILES, where the kernel beats hipBLASLt inside the
+# captured BERT-base step; "mdtf" = every shape it takes; "hipblaslt" = none (torch.addmm + activation kernel).
+FWD_MODE = os.environ.get("MDTF_DENSE_FWD", "auto")
+HAND_FWD = FWD_MODE != "hipblaslt"
+# (K, segment width, segments) -> (bm, bn, stages, ver) at M >= 2048 (bench/dense_fwd_probe.py on MI355X, ms
+# mdtf / hipBLASLt at M 8192: 768 x 768 0.030 / 0.040; M 1280: 0.022 / 0.027 on a 64 x 128 tile)
+FWD_TILES = {(768, 768, 1): (128, 128, 2, 2), (1024, 1024, 1): (128, 128, 2, 2)}
 
 
 def wgrad_into(out, x, d, dbias=None):
@@ -86,6 +99,46 @@ def _hand_dgrad(dpre, w, out=None, accumulate=False):
                         accumulate=accumulate).view(M, K)
 
 
+def _fwd_tile(M, K, nw, nseg):
+    """The tile for this shape, or None when "auto" keeps it on hipBLASLt."""
+    t = FWD_TILES.get((K, nw, nseg))
+    if t is None and FWD_MODE == "auto":
+        return None
+    if M < 2048:
+        return (64, 128, 3, 2) if nw % 128 == 0 else (64, 64, 2, 2)
+    if t is not None and nw % t[1] == 0:
+        return t
+    return (128, 128 if nw % 128 == 0 else 64, 2, 2)
+
+
+def hand_fwd(x, ws, b, act, tile=None):
+    """(y, pre) = (act(x [W_0|..] + b), pre-activation or None) on the MODE 3 kernel, or None if it does not
+    take the operands (then the caller uses hipBLASLt)."""
+    if not HAND_FWD or not x.is_cuda or x.dtype != torch.bfloat16 or not x.is_contiguous() or len(ws) > 4:
+        return None
+    M, K = x.shape
+    nw = ws[0].shape[1]
+    if K % 64 or nw % 64 or any(w.dtype != torch.bfloat16 or not w.is_contiguous() or tuple(w.shape) != (K, nw)
+                                for w in ws):
+        return None
+    ncol = nw * len(ws)
+    if b is not None and (b.dtype != torch.bfloat16 or not b.is_contiguous() or b.numel() != ncol):
+        return None
+    tile = tile or _fwd_tile(M, K, nw, len(ws))
+    if tile is None:
+        return None
+    bm, bn, st, ver = tile
+    y = torch.empty((M, ncol), dtype=x.dtype, device=x.device)
+    pre = torch.empty_like(y) if act == 2 else None
+    p = [N.ptr(w) for w in ws] + [None] * (4 - len(ws))
+    from . import conv as C
+    rc = N.fn("mdtf_gemm_fwd")(N.ptr(x), p[0], p[1], p[2], p[3], len(ws), nw, N.ptr(b), N.ptr(y), N.ptr(pre), act,
+                               M, K, C._v2_code(bm, st, ver), bn, N.stream_ptr())
+    if rc != 0:
+        return None
+    return y, pre
+
+
 def _accum_mm(out, a, b):
     """``out += a @ b`` with bf16 a/b and fp32 out."""
     global _fp32_out_ok
@@ -123,8 +176,9 @@ def _adjacent(ts):
     if t0 is None or any(t is None or t.dim() != 1 or t.dtype != t0.dtype or not t.is_contiguous() for t in ts):
         return None
     off = t0.data_ptr()
+    sp = t0.untyped_storage().data_ptr()
     for t in ts:
-        if t.data_ptr() != off:
+        if t.data_ptr() != off or t.untyped_storage().data_ptr() != sp:     # back to back in ONE storage
             return None
         off += t.numel() * t.element_size()
     return t0.as_strided((sum(t.numel() for t in ts),), (1,))
@@ -141,9 +195,6 @@ class _Dense(torch.autograd.Function):
     def forward(ctx, x, act, trans, nw, x_sink, x_shape, *wb):
         tunable.ensure(x.device)
         ws, bs = wb[:nw], wb[nw:]
-        w = ws[0] if nw == 1 else torch.cat(ws, 1)
-        if trans:
-            w = w.t()
         has_b = bs[0] is not None
         if has_b:
             b = bs[0] if nw == 1 else _adjacent(bs)
@@ -153,12 +204,21 @@ class _Dense(torch.autograd.Function):
         ctx.x_sink, ctx.x_shape = x_sink, x_shape
         if x_sink is not None:
             x_sink.register()
-        pre = torch.addmm(b, x, w) if has_b else torch.mm(x, w)
-        if act == 0:
-            y, saved = pre, None
+        hand = None if trans else hand_fwd(x, ws, b, act)
+        if hand is not None:
+            y, pre = hand
+            saved = pre if act == 2 else (y if act == 1 else None)
+            w = ws[0] if nw == 1 else None          # the data gradient reads the segments in place
         else:
-            y = _act_fwd(pre, act)
-            saved = pre if act == 2 else y
+            w = ws[0] if nw == 1 else torch.cat(ws, 1)
+            if trans:
+                w = w.t()
+            pre = torch.addmm(b, x, w) if has_b else torch.mm(x, w)
+            if act == 0:
+                y, saved = pre, None
+            else:
+                y = _act_fwd(pre, act)
+                saved = pre if act == 2 else y
         ctx.act, ctx.trans, ctx.nw, ctx.has_b = act, trans, nw, has_b
         ctx.widths = [t.shape[0] if trans else t.shape[1] for t in ws]
         ctx.wsinks = [V.grad_sink(t) for t in ws]
@@ -170,6 +230,8 @@ class _Dense(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, saved = ctx.saved_tensors
+        if w is None:                             # hand-written forward over q|k|v segments
+            w = torch.cat(ctx.like[:ctx.nw], 1)
         dy = dy.contiguous()
         dpre = dy if ctx.act == 0 else _act_bwd(dy, saved, ctx.act)
         dx = None

@@ -148,6 +148,7 @@ class StepGraph(object):
         self.eager_steps = 0
         self.replays = 0
         self.fallbacks = 0
+        self.disabled = False       # capture failed once: eager from then on
         self.dyn = None
         self._dyn_vals = None
         self._static_src = {}       # id(source) -> (source, tuple of static tensors)
@@ -197,13 +198,26 @@ class StepGraph(object):
         """Run one training step (eager, capture or replay); returns the gradient scale."""
         if not self._eligible():
             return self.op._run_step(ctx, step)
+        if self.disabled:
+            return self.op._run_step(ctx, step)
         if self.graph is None:
             if self.eager_steps < self.warmup:
                 self.eager_steps += 1
                 vals = self._resolve_inputs(ctx)
                 self._note_ptrs(vals)
                 return self.op._run_step(ctx, step)
-            return self._capture(ctx, step)
+            try:
+                return self._capture(ctx, step)
+            except RuntimeError as e:
+                # a capture the runtime rejects (e.g. a collective it cannot record) fails identically on every
+                # replica before anything was executed: stay eager for the rest of the run instead of aborting
+                from ..utils import log
+                log.warn("hipGraph capture failed (%s); running the step eagerly from now on"
+                         % (str(e).splitlines() or [""])[0][:200])
+                self.disabled = True
+                self.graph = None
+                torch.cuda.synchronize()
+                return self.op._run_step(ctx, step)
         vals = self._resolve_inputs(ctx)
         if not self._bind(vals):
             self.fallbacks += 1

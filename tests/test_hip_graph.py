@@ -131,6 +131,22 @@ def test_hip_graph_shape_change_falls_back():
 
 
 @pytest.mark.gpu
+def test_hip_graph_capture_failure_stays_eager(monkeypatch):
+    """A capture the runtime rejects does not abort training: that step and every later one run eagerly."""
+    _gpu()
+    from mdtf.train import graph as G
+
+    def boom(self, ctx, step):
+        raise RuntimeError("operation not permitted when stream is capturing")
+    monkeypatch.setattr(G.StepGraph, "_capture", boom)
+    torch.manual_seed(0)
+    batches = [(torch.randn(8, 16, 16, 8), torch.randint(0, 16, (8,))) for _ in range(5)]
+    l_g, _, op = _run_resnetish("cuda", torch.bfloat16, batches, hip_graph=True)
+    assert op.graph.disabled and op.graph.graph is None and op.graph.replays == 0
+    assert len(l_g) == 5 and all(v == v for v in l_g)
+
+
+@pytest.mark.gpu
 def test_hip_graph_bert_dropout_advances_per_replay():
     """BERT-tiny with dropout under graph replay: the device step counter advances every replay (fresh
     dropout masks), the loss keeps decreasing, and every replay is a real step."""
