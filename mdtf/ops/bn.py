@@ -36,6 +36,7 @@ def _f32(t):
 
 # MDTF_BN_TRACE=1: record (input shape, has residual, how the backward statistics were obtained) per BN backward
 BWD_TRACE = [] if os.environ.get("MDTF_BN_TRACE") == "1" else None
+DUAL_DZ = os.environ.get("MDTF_DUAL_DZ", "0") == "1"
 
 
 class _BNTrain(torch.autograd.Function):
@@ -99,10 +100,10 @@ class _BNTrain(torch.autograd.Function):
                 _conv.bwd_stats_release(pstats, False)
                 pstats = None
                 why = "autograd_part"
-        if BWD_TRACE is not None:
-            BWD_TRACE.append((tuple(x.shape), ctx.has_res, why))
             dy = ctx.out_sink.take(dy)
             ctx.out_sink.stat_req = None
+        if BWD_TRACE is not None:
+            BWD_TRACE.append((tuple(x.shape), ctx.has_res, why))
         if dy is None:
             return (None,) * 10
         dy = dy.contiguous()
@@ -224,13 +225,14 @@ class _BNTrainDual(torch.autograd.Function):
         M = x.numel() // C
         dx = torch.empty_like(x)
         # the shortcut BN's output gradient is dy * mask: its backward reads dy and the ReLU mask itself
-        # (no masked copy dz is written and re-read)
+        # (no masked copy dz is written and re-read); MDTF_DUAL_DZ=1: the written-copy path (A/B, tests)
+        dz = torch.empty_like(x) if DUAL_DZ else None
         grads = [sk.grad if sk is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
                  for sk in ctx.sinks]
         if pstats is not None:
             from . import conv as _conv
             ws = torch.empty(3 * C, dtype=torch.float32, device=x.device)
-            N.check(N.fn("mdtf_bn_bwd_stats")(N.ptr(dy), N.ptr(x), N.ptr(mask), N.ptr(dx), None, M, C, N.ptr(g),
+            N.check(N.fn("mdtf_bn_bwd_stats")(N.ptr(dy), N.ptr(x), N.ptr(mask), N.ptr(dx), N.ptr(dz), M, C, N.ptr(g),
                                               N.ptr(mean), N.ptr(invstd), N.ptr(grads[0]), N.ptr(grads[1]), 1,
                                               N.ptr(pstats[0]), N.ptr(pstats[1]), int(pstats.shape[1]), N.ptr(ws), 0,
                                               N.stream_ptr()), "bn_bwd_stats")
@@ -238,14 +240,15 @@ class _BNTrainDual(torch.autograd.Function):
             FUSED_BWD[0] += 1
         else:
             ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
-            N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(x), N.ptr(mask), N.ptr(dx), None, M, C, N.ptr(g),
+            N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(x), N.ptr(mask), N.ptr(dx), N.ptr(dz), M, C, N.ptr(g),
                                         N.ptr(mean), N.ptr(invstd), N.ptr(grads[0]), N.ptr(grads[1]), 1, N.ptr(ws), 0,
                                         N.stream_ptr()), "bn_bwd")
         dr = torch.empty_like(r)
         ws2 = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
-        N.check(N.fn("mdtf_bn_bwd")(N.ptr(dy), N.ptr(r), N.ptr(mask), N.ptr(dr), None, M, C, N.ptr(g2), N.ptr(mean2),
-                                    N.ptr(invstd2), N.ptr(grads[2]), N.ptr(grads[3]), 1, N.ptr(ws2), 0,
-                                    N.stream_ptr()), "bn_bwd")
+        N.check(N.fn("mdtf_bn_bwd")(N.ptr(dz if dz is not None else dy), N.ptr(r),
+                                    N.ptr(mask) if dz is None else None, N.ptr(dr), None, M, C, N.ptr(g2),
+                                    N.ptr(mean2), N.ptr(invstd2), N.ptr(grads[2]), N.ptr(grads[3]), int(dz is None),
+                                    N.ptr(ws2), 0, N.stream_ptr()), "bn_bwd")
         out = []
         for t, sk, gr in zip(ctx.like, ctx.sinks, grads):
             out.append(V.grad_marker(t) if sk is not None else gr)
