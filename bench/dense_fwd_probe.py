@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Dense forward on the hand-written MFMA kernel (ops/gemm.py hand_fwd: fd v2 MODE 3, W read in place,
 bias + activation epilogue, q|k|v segments) vs hipBLASLt (addmm with the bias epilogue, + the mdtf activation
-kernel for GELU) on the BERT-base shapes, every candidate tile; prints one JSON line per shape."""
+kernel for GELU) on the BERT-base shapes, every candidate tile, timed inside captured graphs; prints one JSON
+line per shape."""
 import json
 import os
 import statistics
@@ -20,17 +21,26 @@ TILES = [(128, 128, 2, 2), (128, 128, 3, 2), (128, 128, 4, 2), (128, 64, 3, 2), 
          (256, 128, 3, 3), (256, 256, 2, 3), (128, 256, 2, 3), (128, 256, 3, 3), (256, 64, 3, 3), (256, 64, 4, 3)]
 
 
-def timeit(fn, reps=30):
-    for _ in range(5):
+def timeit(fn, reps=20):
+    """Kernel time per call inside a captured graph (as in the training step: no host launch cost, which
+    inflates an eagerly timed hipBLASLt call by up to 50 %)."""
+    for _ in range(3):
         fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     ts = []
-    for _ in range(reps):
+    for _ in range(5):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        fn()
+        g.replay()
         b.record()
         b.synchronize()
-        ts.append(a.elapsed_time(b))
+        ts.append(a.elapsed_time(b) / reps)
     return statistics.median(ts)
 
 

@@ -39,11 +39,13 @@ N.register("mdtf_gemm_fwd", [N.P, N.P, N.P, N.P, N.P, N.I, N.I, N.P, N.P, N.P, N
 # pre-activation in the epilogue; q|k|v as column segments of one launch, no concatenated weight copy).
 # MDTF_DENSE_FWD: "auto" (default) = the shapes of FWD_TILES, where the kernel beats hipBLASLt inside the
 # captured BERT-base step; "mdtf" = every shape it takes; "hipblaslt" = none (torch.addmm + activation kernel).
+# Inside the captured BERT-base step (rocprofv3, batch 64 x 128, us per call mdtf / hipBLASLt): q|k|v 62 / 52,
+# FFN-in + GELU 78 / 50 + 23 (bias_act), FFN-out and attention-out ~62 / 41 and 20: so the table is empty and the
+# library keeps the forward until the kernel wins (bench/dense_fwd_probe.py times both inside graphs).
 FWD_MODE = os.environ.get("MDTF_DENSE_FWD", "auto")
 HAND_FWD = FWD_MODE != "hipblaslt"
-# (K, segment width, segments) -> (bm, bn, stages, ver) at M >= 2048 (bench/dense_fwd_probe.py on MI355X, ms
-# mdtf / hipBLASLt at M 8192: 768 x 768 0.030 / 0.040; M 1280: 0.022 / 0.027 on a 64 x 128 tile)
-FWD_TILES = {(768, 768, 1): (128, 128, 2, 2), (1024, 1024, 1): (128, 128, 2, 2)}
+# (K, segment width, segments) -> (bm, bn, stages, ver) at M >= 2048
+FWD_TILES = {}
 
 
 def wgrad_into(out, x, d, dbias=None):
