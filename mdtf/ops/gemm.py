@@ -48,6 +48,10 @@ HAND_FWD = FWD_MODE != "hipblaslt"
 FWD_TILES = {}
 
 
+# MDTF_DENSE_WGRAD=hipblaslt: the library's fp32-output GEMM (C += A^T B) and column sums instead (A/B)
+HAND_WGRAD = os.environ.get("MDTF_DENSE_WGRAD", "mdtf") != "hipblaslt"
+
+
 def wgrad_into(out, x, d, dbias=None):
     """``out[K][N] += x[M][K]^T d[M][N]`` in fp32 (``d`` may be a column slice).
 
@@ -59,7 +63,7 @@ def wgrad_into(out, x, d, dbias=None):
     """
     M, K = x.shape
     Nn = d.shape[1]
-    if (K % 64 == 0 and Nn % 64 == 0 and x.is_contiguous() and d.stride(1) == 1 and out.is_contiguous()
+    if (HAND_WGRAD and K % 64 == 0 and Nn % 64 == 0 and x.is_contiguous() and d.stride(1) == 1 and out.is_contiguous()
             and x.dtype == torch.bfloat16 and d.dtype == torch.bfloat16 and out.dtype == torch.float32):
         splits = 1 if N.deterministic() else (8 if K * Nn <= 768 * 768 else 0)
         bm, bn = (128, 128) if M < 4096 else (64, 128)
