@@ -94,7 +94,36 @@ def _stats(co, bm, M):
     return (buf[0], buf[1])
 
 
-def timeit(fn, reps, warm=3):
+GRAPH = [False]     # --graph: time the mdtf candidates inside captured graphs (kernel time only, as in the step)
+
+
+def gtime(fn, reps, warm=3):
+    """Kernel time per launch: ``reps`` launches captured into one graph, median of 5 replays."""
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(5):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) / reps)
+    del g
+    return statistics.median(ts)
+
+
+def timeit(fn, reps, warm=3, graph=False):
+    if graph:
+        return gtime(fn, reps, warm)
     for _ in range(warm):
         fn()
     ts = []
@@ -119,7 +148,10 @@ def main():
     p.add_argument("--passes", default="fwd,dgrad,wgrad")
     p.add_argument("--strides", default="", help="only shapes with these strides (e.g. 2)")
     p.add_argument("--merge", action="store_true", help="update the existing table at --out instead of replacing it")
+    p.add_argument("--graph", action="store_true",
+                   help="time the mdtf and Winograd candidates inside captured graphs (no host launch cost)")
     args = p.parse_args()
+    GRAPH[0] = args.graph
     dev = torch.device("cuda")
     shapes, all_convs = resnet_convs(args.depth, args.batch)
     counts = {s: all_convs.count(s) for s in shapes}
@@ -184,16 +216,19 @@ def main():
             t_lib = timeit(lib, args.reps)
             t_wino = None
             if pass_ in ("fwd", "dgrad") and Wg.eligible((kh, kw), (s, s), pads4, (1, 1), c, co):
-                if pass_ == "fwd":
-                    t_wino = timeit(lambda: Wg.winograd_fwd(x, wt, (oh, ow), pads4), args.reps)
-                else:
-                    t_wino = timeit(lambda: Wg.winograd_dgrad(dy, wt, x.shape, pads4), args.reps)
+                wfn = ((lambda: Wg.winograd_fwd(x, wt, (oh, ow), pads4)) if pass_ == "fwd"
+                       else (lambda: Wg.winograd_dgrad(dy, wt, x.shape, pads4)))
+                try:
+                    t_wino = timeit(wfn, args.reps, graph=GRAPH[0])
+                except RuntimeError:
+                    t_wino = timeit(wfn, args.reps)
             best = None
             if native_ok:
                 for bm, bn, sp, v in cands:
                     try:
-                        t = timeit(mk(bm, bn, sp, v), args.reps)
+                        t = timeit(mk(bm, bn, sp, v), args.reps, graph=GRAPH[0])
                     except RuntimeError:
+                        torch.cuda.synchronize()
                         continue
                     if best is None or t < best[0]:
                         best = (t, bm, bn, sp, v)

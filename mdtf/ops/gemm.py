@@ -52,6 +52,21 @@ FWD_TILES = {}
 HAND_WGRAD = os.environ.get("MDTF_DENSE_WGRAD", "mdtf") != "hipblaslt"
 
 
+# (K, N) at M >= 4096 -> (bm, bn, splits, slab reduction) of the 4-wave tiles (the ones that also sum the bias
+# gradient); bench/dense_wgrad_sweep.py, graph-timed at M 8192, ms new / old choice: 768 x 3072 0.077 / 0.085,
+# 3072 x 768 0.073 / 0.080; M < 4096 (768 x 768 at M 1280): 0.0127 / 0.0208
+DENSE_WGRAD_TILES = {(768, 3072): (64, 128, 2, False), (3072, 768): (64, 128, 4, True)}
+
+
+def _wgrad_tile(M, K, Nn):
+    if M < 4096:
+        return 64, 128, 2, False
+    t = DENSE_WGRAD_TILES.get((K, Nn))
+    if t is not None:
+        return t
+    return 64, 128, (8 if K * Nn <= 768 * 768 else 0), True
+
+
 def wgrad_into(out, x, d, dbias=None):
     """``out[K][N] += x[M][K]^T d[M][N]`` in fp32 (``d`` may be a column slice).
 
@@ -65,10 +80,11 @@ def wgrad_into(out, x, d, dbias=None):
     Nn = d.shape[1]
     if (HAND_WGRAD and K % 64 == 0 and Nn % 64 == 0 and x.is_contiguous() and d.stride(1) == 1 and out.is_contiguous()
             and x.dtype == torch.bfloat16 and d.dtype == torch.bfloat16 and out.dtype == torch.float32):
-        splits = 1 if N.deterministic() else (8 if K * Nn <= 768 * 768 else 0)
-        bm, bn = (128, 128) if M < 4096 else (64, 128)
+        bm, bn, splits, use_slab = _wgrad_tile(M, K, Nn)
+        if N.deterministic():
+            splits = 1
         from . import conv as C
-        slab, cap = C.wgrad_slab(M, K, Nn, bm, bn, 2, splits, x.device, dense=True)
+        slab, cap = C.wgrad_slab(M, K, Nn, bm, bn, 2, splits, x.device, dense=True) if use_slab else (None, 0)
         fuse = dbias is not None and FUSED_BIAS_GRAD and dbias.is_contiguous() and dbias.dtype == torch.float32
         rc = N.fn("mdtf_gemm_wgrad")(N.ptr(x), N.ptr(d), N.ptr(out), M, K, Nn, d.stride(0), out.stride(0), bm, bn, 2,
                                      splits, N.ptr(slab), cap, N.ptr(dbias) if fuse else None, N.stream_ptr())
