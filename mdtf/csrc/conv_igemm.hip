@@ -144,6 +144,17 @@ __device__ __forceinline__ float dense_act(float v, int act) {
   return v;
 }
 
+// its derivative at the pre-activation x: relu [x > 0]; gelu s + 2 x s (1 - s) u'(x), s = sigmoid(2u)
+// (= kernels.hip act_grad's tanh form: 0.5 (1 + t) = s, 1 - t^2 = 4 s (1 - s))
+__device__ __forceinline__ float dense_act_grad(float x, int act) {
+  if (act == 1) return x > 0.f ? 1.f : 0.f;
+  if (act == 2) {
+    const float s = __builtin_amdgcn_rcpf(1.f + __expf(-1.5957691216f * (x + 0.044715f * x * x * x)));
+    return s + 2.f * x * s * (1.f - s) * 0.7978845608f * (1.f + 0.134145f * x * x);
+  }
+  return 1.f;
+}
+
 // chunk swizzle of the [64 k][64 col] half-images read by transposed fragment reads (see the v2 wgrad)
 __device__ __forceinline__ int trswz(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
 
@@ -814,6 +825,7 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
         x4[it] = *reinterpret_cast<const uint4*>(a.bx + off[it]);
         mb[it] = a.bmask ? a.bmask[off[it] >> 3] : 0xffu;
       }
+      if (MODE == 1 && a.act) x4[it] = *reinterpret_cast<const uint4*>(a.pre_out + off[it]);   // (not with bstat)
     }
   }
 #pragma unroll
@@ -832,6 +844,16 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
       for (int k = 0; k < 4; ++k) {
         c[2 * k] = dense_act(__uint_as_float(w4[k] << 16), a.act);
         c[2 * k + 1] = dense_act(__uint_as_float(w4[k] & 0xffff0000u), a.act);
+      }
+      store_bf8(dst, c);
+    } else if (MODE == 1 && a.act) {             // the producer's activation backward: dx = (dy W^T) act'(pre)
+      float c[8];
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t p4[4] = {x4[it].x, x4[it].y, x4[it].z, x4[it].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        c[2 * k] = __uint_as_float(w4[k] << 16) * dense_act_grad(__uint_as_float(p4[k] << 16), a.act);
+        c[2 * k + 1] = __uint_as_float(w4[k] & 0xffff0000u) * dense_act_grad(__uint_as_float(p4[k] & 0xffff0000u), a.act);
       }
       store_bf8(dst, c);
     } else if (a.accumulate || bstat) {
@@ -1695,4 +1717,25 @@ MDTF_EXPORT int mdtf_gemm_fwd(const void* x, const void* w0, const void* w1, con
   const int w8 = bm / 10000, stages = (bm % 10000) / 1000 ? (bm % 10000) / 1000 : 2;
   bm = w8 * 10000 + bm % 1000;
   return dispatch_fd_v2<3, false>(a, bm, bn, stages, st);
+}
+
+// Dense data gradient with the producer's activation backward in the epilogue (fd v2 MODE 1 as a 1x1 "conv"):
+// dx[M][K] = (dy[M][N] W[K][N]^T) * act'(pre[M][K]); act 1 relu (pre = the forward output), 2 gelu.
+// N % 64 == 0, K % 8 == 0.  bm encodes [10000 if 8 waves] + stages * 1000 + tile rows.
+MDTF_EXPORT int mdtf_gemm_dgrad_act(const void* dy, const void* w, void* dx, const void* pre, int act, long long M,
+                                    int K, int N, int bm, int bn, hipStream_t st) {
+  if (N % 64 || K % 8 || M <= 0 || !pre || act < 1 || act > 2) return MDTF_EINVAL;
+  if (M > 0x7fffffff || M * N * 2 > 0x7fffffffLL || M * K * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
+  ConvArgs a = make_args((int)M, 1, 1, K, 1, 1, N, 1, 1, 1, 1, 0, 0, 1, 1);
+  a.src = (const bf16_t*)dy;
+  a.wgt = (const bf16_t*)w;
+  a.out = (bf16_t*)dx;
+  a.pre_out = (bf16_t*)pre;
+  a.act = act;
+  a.Ncol = K;
+  a.M = M;
+  a.K = N;
+  const int w8 = bm / 10000, stages = (bm % 10000) / 1000 ? (bm % 10000) / 1000 : 2;
+  bm = w8 * 10000 + bm % 1000;
+  return dispatch_fd_v2<1, false>(a, bm, bn, stages, st);
 }

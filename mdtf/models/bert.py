@@ -150,9 +150,15 @@ class Bert(Model):
                 a = _dense("dense", ctx, H)
                 x = _ln("LayerNorm", a, residual=x, dropout=self.dropout)
         with V.variable_scope("intermediate"):
-            i = _dense("dense", x, self.I, act="gelu")
+            with V.variable_scope("dense"):
+                w1 = V.get_variable("kernel", [H, self.I], initializer=_init())
+                b1 = V.get_variable("bias", [self.I], initializer=V.constant_initializer(0.0))
         with V.variable_scope("output"):
-            o = _dense("dense", i, H)
+            with V.variable_scope("dense"):
+                w2 = V.get_variable("kernel", [self.I, H], initializer=_init())
+                b2 = V.get_variable("bias", [H], initializer=V.constant_initializer(0.0))
+            # one feed-forward op: the GELU backward rides in the second layer's data-gradient epilogue
+            o = ops.ffn(x, w1, b1, w2, b2, act="gelu")
             x = _ln("LayerNorm", o, residual=x, dropout=self.dropout)
         return x
 

@@ -37,6 +37,18 @@ N.register("mdtf_gemm_fwd", [N.P, N.P, N.P, N.P, N.P, N.I, N.I, N.P, N.P, N.P, N
 # forward y = act(x W + b) on the hand-written MFMA kernel (csrc/conv_igemm.hip fd v2 MODE 3: W read in place,
 # N-contiguous, by transposed LDS fragment reads; bias on the fp32 accumulators; GELU/ReLU and the saved
 # pre-activation in the epilogue; q|k|v as column segments of one launch, no concatenated weight copy).
+N.register("mdtf_gemm_dgrad_act", [N.P, N.P, N.P, N.P, N.I, N.L, N.I, N.I, N.I, N.I, N.P])
+
+# ffn(): the second layer's data gradient multiplies by the first layer's activation derivative in its epilogue
+# (csrc/conv_igemm.hip mdtf_gemm_dgrad_act), so no separate activation-backward pass runs.  Graph-timed it wins
+# (0.071 vs 0.081 ms at BERT-base's 8192 x 3072 x 768), but inside the step the kernel runs at 0.0815 ms (the
+# epilogue's pre-activation reads come from HBM, not from the probe's warm MALL) vs hipBLASLt 0.042 + act
+# backward 0.030: BERT-base A/B 5646 / 5608 fused vs 5664 / 5638 seq/s.  Opt-in: MDTF_FFN_FUSE=1.
+FFN_FUSE = os.environ.get("MDTF_FFN_FUSE", "0") == "1"
+# (K, N) of the second layer's W [K][N] -> (bm, bn, stages, ver) of the fused data gradient (output K columns)
+# (bench/dgrad_act_probe.py, graph-timed at M 8192: 128 x 256 8-wave 0.071 ms vs hipBLASLt + act backward 0.081)
+DGRAD_ACT_TILES = {(3072, 768): (128, 256, 2, 3), (4096, 1024): (128, 256, 2, 3)}
+
 # MDTF_DENSE_FWD: "auto" (default) = the shapes of FWD_TILES, where the kernel beats hipBLASLt inside the
 # captured BERT-base step; "mdtf" = every shape it takes; "hipblaslt" = none (torch.addmm + activation kernel).
 # Inside the captured BERT-base step (rocprofv3, batch 64 x 128, us per call mdtf / hipBLASLt): q|k|v 62 / 52,
@@ -161,6 +173,32 @@ def hand_fwd(x, ws, b, act, tile=None):
     return y, pre
 
 
+def hand_dgrad_act(dpre, w, pre, act, tile=None):
+    """dx = (dpre @ w^T) * act'(pre) on the v2 dgrad kernel with the activation-backward epilogue, or None."""
+    if not (dpre.is_cuda and dpre.dtype == torch.bfloat16 and dpre.is_contiguous() and w.is_contiguous()
+            and pre.is_contiguous() and w.dtype == torch.bfloat16 and pre.dtype == torch.bfloat16):
+        return None
+    M, Nn = dpre.shape
+    K = w.shape[0]
+    if Nn % 64 or K % 8 or tuple(pre.shape) != (M, K) or act not in (1, 2):
+        return None
+    bm, bn, st, ver = tile or DGRAD_ACT_TILES.get((K, Nn)) or ((128, 128, 2, 2) if M >= 2048 else (64, 128, 3, 2))
+    dx = torch.empty((M, K), dtype=dpre.dtype, device=dpre.device)
+    from . import conv as C
+    rc = N.fn("mdtf_gemm_dgrad_act")(N.ptr(dpre), N.ptr(w), N.ptr(dx), N.ptr(pre), act, M, K, Nn,
+                                     C._v2_code(bm, st, ver), bn, N.stream_ptr())
+    return dx if rc == 0 else None
+
+
+class _ActLink(object):
+    """Between the two layers of ffn(): the first layer's saved pre-activation (GELU) or output (ReLU), and
+    whether the second layer's data gradient already applied the activation derivative."""
+    __slots__ = ("pre", "act", "fused")
+
+    def __init__(self):
+        self.pre, self.act, self.fused = None, 0, False
+
+
 def _accum_mm(out, a, b):
     """``out += a @ b`` with bf16 a/b and fp32 out."""
     global _fp32_out_ok
@@ -214,7 +252,7 @@ class _Dense(torch.autograd.Function):
     autograd adding two gradient tensors."""
 
     @staticmethod
-    def forward(ctx, x, act, trans, nw, x_sink, x_shape, *wb):
+    def forward(ctx, x, act, trans, nw, x_sink, x_shape, link_out, link_in, *wb):
         tunable.ensure(x.device)
         ws, bs = wb[:nw], wb[nw:]
         has_b = bs[0] is not None
@@ -242,6 +280,9 @@ class _Dense(torch.autograd.Function):
                 y = _act_fwd(pre, act)
                 saved = pre if act == 2 else y
         ctx.act, ctx.trans, ctx.nw, ctx.has_b = act, trans, nw, has_b
+        ctx.link_out, ctx.link_in = link_out, link_in
+        if link_out is not None:
+            link_out.pre, link_out.act, link_out.fused = saved, act, False
         ctx.widths = [t.shape[0] if trans else t.shape[1] for t in ws]
         ctx.wsinks = [V.grad_sink(t) for t in ws]
         ctx.bsinks = [V.grad_sink(t) if t is not None else None for t in bs]
@@ -255,16 +296,24 @@ class _Dense(torch.autograd.Function):
         if w is None:                             # hand-written forward over q|k|v segments
             w = torch.cat(ctx.like[:ctx.nw], 1)
         dy = dy.contiguous()
-        dpre = dy if ctx.act == 0 else _act_bwd(dy, saved, ctx.act)
+        lo = ctx.link_out
+        fused_in = lo is not None and lo.fused          # the consumer's dgrad applied act' already
+        dpre = dy if (ctx.act == 0 or fused_in) else _act_bwd(dy, saved, ctx.act)
+        if lo is not None:
+            lo.pre = None
         dx = None
         if ctx.needs_input_grad[0]:
             xs = ctx.x_sink
             hand = not ctx.trans
-            if xs is None:
+            li = ctx.link_in
+            if xs is None and li is not None and li.pre is not None and hand and ctx.nw == 1:
+                dx = hand_dgrad_act(dpre, w, li.pre, li.act)      # ffn(): dx already carries act'(pre)
+                li.fused = dx is not None
+            if dx is None and xs is None:
                 dx = _hand_dgrad(dpre, w) if hand else None
                 if dx is None:
                     dx = torch.mm(dpre, w.t())
-            else:
+            elif dx is None:
                 buf, acc = xs.target()
                 if acc:                        # second contribution: C += dpre @ w^T inside the GEMM
                     b2 = buf.view(-1, w.shape[0])
@@ -290,7 +339,7 @@ class _Dense(torch.autograd.Function):
                     if wgrad_into(sink.grad, x, d, bsink.grad if bsink is not None else None):
                         bias_done[j] = True
                 gws.append(V.grad_marker(ws[j]))
-            elif ctx.needs_input_grad[6 + j]:
+            elif ctx.needs_input_grad[8 + j]:
                 g = torch.mm(d.t(), x) if ctx.trans else torch.mm(x.t(), d)
                 gws.append(g.to(ws[j].dtype))
             else:
@@ -333,7 +382,7 @@ class _Dense(torch.autograd.Function):
                         gbs.append(part.to(bs[j].dtype))
         else:
             gbs = [None] * ctx.nw
-        return (dx, None, None, None, None, None) + tuple(gws) + tuple(gbs)
+        return (dx, None, None, None, None, None, None, None) + tuple(gws) + tuple(gbs)
 
 
 def matmul(a, b):
@@ -357,7 +406,7 @@ def dense_multi(x, ws, bs, act=None):
     shp = x.shape
     x2 = x.reshape(-1, shp[-1])
     ws = [w.to(x.dtype) if w.dtype != x.dtype else w for w in ws]
-    y = _Dense.apply(x2, _ACT[act], False, len(ws), actsink.sink_of(x), tuple(shp), *ws, *bs)
+    y = _Dense.apply(x2, _ACT[act], False, len(ws), actsink.sink_of(x), tuple(shp), None, None, *ws, *bs)
     return y.reshape(*shp[:-1], y.shape[-1])
 
 
@@ -366,5 +415,21 @@ def dense_transposed(x, w, b=None):
     _check(x, "dense")
     shp = x.shape
     w = w.to(x.dtype) if w.dtype != x.dtype else w
-    y = _Dense.apply(x.reshape(-1, shp[-1]), 0, True, 1, None, tuple(shp), w, b)
+    y = _Dense.apply(x.reshape(-1, shp[-1]), 0, True, 1, None, tuple(shp), None, None, w, b)
+    return y.reshape(*shp[:-1], y.shape[-1])
+
+
+def ffn(x, w1, b1, w2, b2, act="gelu"):
+    """``act(x @ w1 + b1) @ w2 + b2`` (a transformer feed-forward block).  The intermediate has exactly one
+    consumer, so the second layer's data gradient applies the activation derivative in its epilogue
+    (:func:`hand_dgrad_act`) and the first layer skips its activation-backward pass."""
+    _check(x, "ffn")
+    from . import actsink
+    shp = x.shape
+    x2 = x.reshape(-1, shp[-1])
+    w1 = w1.to(x.dtype) if w1.dtype != x.dtype else w1
+    w2 = w2.to(x.dtype) if w2.dtype != x.dtype else w2
+    link = _ActLink() if (FFN_FUSE and _ACT[act] != 0) else None
+    h = _Dense.apply(x2, _ACT[act], False, 1, actsink.sink_of(x), tuple(shp), link, None, w1, b1)
+    y = _Dense.apply(h, 0, False, 1, None, tuple(h.shape), None, link, w2, b2)
     return y.reshape(*shp[:-1], y.shape[-1])

@@ -311,6 +311,15 @@ def dense(x, w, b=None, act=None):
     return y
 
 
+def ffn(x, w1, b1, w2, b2, act="gelu"):
+    """``act(x @ w1 + b1) @ w2 + b2``: a feed-forward block (native: the activation backward is fused into the
+    second layer's data gradient)."""
+    if _native.use_native(x):
+        from . import gemm
+        return gemm.ffn(x, w1, b1, w2, b2, act)
+    return dense(dense(x, w1, b1, act), w2, b2)
+
+
 def dense_multi(x, ws, bs, act=None):
     """One GEMM for several ``[K, N_i]`` weights sharing input ``x``; outputs concatenated on the last axis."""
     if _native.use_native(x):

@@ -1274,6 +1274,50 @@ def test_dense_fwd_hand_kernel(M, K, nw, nseg, act, bias, tile, monkeypatch):
         assert pre is None
 
 
+@pytest.mark.parametrize("M,K,N,act,tile", [(8192, 3072, 768, 2, None), (1000, 3072, 768, 2, None),
+                                             (333, 1024, 256, 1, None), (4096, 3072, 768, 2, (128, 256, 2, 3)),
+                                             (4096, 768, 768, 2, (64, 128, 3, 2))])
+def test_dense_dgrad_act_epilogue(M, K, N, act, tile):
+    """Data gradient with the producer's activation backward in the epilogue: dx = (dy W^T) * act'(pre), vs
+    fp32 (GELU tanh form / ReLU); M tails, 4- and 8-wave tiles."""
+    from mdtf.ops import gemm as G
+    torch.manual_seed(M + K)
+    dy = torch.randn(M, N).bfloat16()
+    w = (torch.randn(K, N) * 0.05).bfloat16()
+    pre = (torch.randn(M, K) * 2).bfloat16()
+    p = pre.float().requires_grad_()
+    y = torch.nn.functional.gelu(p, approximate="tanh") if act == 2 else torch.relu(p)
+    y.backward((dy.float() @ w.float().t()))
+    dx = G.hand_dgrad_act(dy.to(DEV), w.to(DEV), pre.to(DEV), act, tile=tile)
+    assert dx is not None and dx.shape == (M, K)
+    assert _rel(dx, p.grad) < 1e-2
+
+
+def test_ffn_fused_act_backward_matches_unfused(monkeypatch):
+    """ffn(): GELU backward fused into the second layer's data gradient gives the same gradients as the
+    separate activation-backward pass."""
+    from mdtf.ops import gemm as G
+    torch.manual_seed(5)
+    x = torch.randn(2048, 768, device=DEV).bfloat16()
+    w1 = (torch.randn(768, 3072, device=DEV) * 0.03).bfloat16().requires_grad_()
+    b1 = (torch.randn(3072, device=DEV) * 0.1).bfloat16().requires_grad_()
+    w2 = (torch.randn(3072, 768, device=DEV) * 0.02).bfloat16().requires_grad_()
+    b2 = (torch.randn(768, device=DEV) * 0.1).bfloat16().requires_grad_()
+    res = []
+    fused = []
+    for fuse in (True, False):
+        monkeypatch.setattr(G, "FFN_FUSE", fuse)
+        xi = x.clone().requires_grad_()
+        y = G.ffn(xi, w1, b1, w2, b2)
+        fused.append(y.grad_fn is not None)
+        y.float().square().mean().backward()
+        res.append([y.detach(), xi.grad] + [t.grad for t in (w1, b1, w2, b2)])
+        for t in (w1, b1, w2, b2):
+            t.grad = None
+    for a, r in zip(res[0], res[1]):
+        assert _rel(a, r) < 1e-2
+
+
 def test_dense_layer_hand_fwd_matches_library(monkeypatch):
     """A dense layer (q|k|v segments + GELU FFN) forward and backward: the hand-written forward vs the
     hipBLASLt path give the same outputs and gradients."""
