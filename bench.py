@@ -104,7 +104,7 @@ def main():
     if distributed:
         server = Server.from_env()
         world, rank = dist.get_world_size(), dist.get_rank()
-        dev = torch.device("cuda", server.local_rank) if torch.cuda.is_available() else torch.device("cpu")
+        dev = server.device()
         pg = server.worker_group
     else:
         server, world, rank, pg = None, 1, 0, None

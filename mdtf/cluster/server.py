@@ -120,7 +120,9 @@ class Server(object):
         if not torch.cuda.is_available():
             return torch.device("cpu")
         if self._torchrun:
-            return torch.device("cuda", self.local_rank)
+            # (local ranks beyond the visible devices share them: the MDTF_DIST_BACKEND=gloo rehearsal of an
+            # N-rank job on fewer GPUs; a real launch has one device per local rank)
+            return torch.device("cuda", self.local_rank % max(torch.cuda.device_count(), 1))
         idx = self.layout.local_device_index(self.job_name, self.task_index, self.local_rank)
         return torch.device("cuda", idx % max(torch.cuda.device_count(), 1))
 
@@ -139,7 +141,10 @@ class Server(object):
         os.environ.setdefault("TORCH_FR_BUFFER_SIZE", "2000")
         timeout = datetime.timedelta(seconds=self.store_timeout_s)
         if self._torchrun:
-            backend = self.backend or ("nccl" if torch.cuda.is_available() else "gloo")
+            # MDTF_DIST_BACKEND=gloo: multi-rank rehearsal on a box with fewer GPUs than ranks (RCCL needs one
+            # device per rank); the step then cannot be graph-captured and runs eagerly (train/graph.py)
+            backend = self.backend or os.environ.get("MDTF_DIST_BACKEND") or (
+                "nccl" if torch.cuda.is_available() else "gloo")
             if backend == "nccl":
                 torch.cuda.set_device(self.local_rank)
             if not dist.is_initialized():

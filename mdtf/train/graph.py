@@ -191,6 +191,10 @@ class StepGraph(object):
     def _eligible(self):
         red = self.op.reducer
         dev = self.op.space.groups[0].device if self.op.space.groups else None
+        if red.world > 1:
+            import torch.distributed as dist
+            if dist.is_initialized() and dist.get_backend() != "nccl":
+                return False            # gloo collectives synchronise with the host: not capturable
         return dev is not None and dev.type == "cuda" and red.R == red.world
 
     # ------------------------------------------------------------------
