@@ -184,7 +184,9 @@ def main():
                        "comm_dtype": "bf16" if str(opt.comm_dtype or os.environ.get("MDTF_COMM_DTYPE", "fp32")).startswith("bf") else "fp32",
                        "optimizer": "momentum-sgd (fused)",
                        "kernels": os.environ.get("MDTF_KERNELS", "native"),
-                       "hip_graph": bool(args.hip_graph) and dev.type == "cuda"},
+                       # whether the step really replayed a captured graph (gloo rehearsals and a rejected
+                       # capture run eagerly)
+                       "hip_graph": bool(getattr(getattr(train_op, "graph", None), "replays", 0))},
             "loss_first": float(lv), "loss_last": final_loss,
         }
         if bert is not None:

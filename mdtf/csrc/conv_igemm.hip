@@ -589,8 +589,9 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   const long long m0 = (long long)mt * BM;
   const int n0 = nt * BN;
 
-  // MODE 3 (dense forward) gathers A like a 1x1 forward convolution
-  constexpr int AM = MODE == 3 ? 0 : MODE;
+  // MODE 3 (dense forward) gathers A like a 1x1 forward convolution; MODE 4 (dense data gradient with the
+  // producer's activation backward in the epilogue) like a stride-1 dgrad
+  constexpr int AM = MODE == 3 ? 0 : MODE == 4 ? 1 : MODE;
   const int GH = AM == 0 ? a.H : a.OH;
   const int GW = AM == 0 ? a.W : a.OW;
   const int GC = AM == 0 ? a.Cin : a.Cout;
@@ -693,6 +694,22 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  // MODE 4: this thread's pre-activation vectors of the copy-out, loaded before the first stage so their HBM
+  // latency hides under the main loop (the copy-out's row mapping: idx = tid + it * NT, 8 columns per idx)
+  constexpr int PITER = MODE == 4 ? BM * (BN / 8) / (64 * NW) : 1;
+  uint4 prepf[PITER];
+  if constexpr (MODE == 4) {
+#pragma unroll
+    for (int it = 0; it < PITER; ++it) {
+      const int idx = tid + it * 64 * NW;
+      const int row = idx / (BN / 8), c8 = idx - row * (BN / 8);
+      const long long m = m0 + row;
+      const int n = n0 + c8 * 8;
+      prepf[it] = (m < a.M && n < a.Ncol) ? *reinterpret_cast<const uint4*>(a.pre_out + m * a.Ncol + n)
+                                          : make_uint4(0, 0, 0, 0);
+    }
+  }
 
   const int KT = a.K / 64;
   // prologue: stages 0 .. STAGES-2 in flight
@@ -825,7 +842,6 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
         x4[it] = *reinterpret_cast<const uint4*>(a.bx + off[it]);
         mb[it] = a.bmask ? a.bmask[off[it] >> 3] : 0xffu;
       }
-      if (MODE == 1 && a.act) x4[it] = *reinterpret_cast<const uint4*>(a.pre_out + off[it]);   // (not with bstat)
     }
   }
 #pragma unroll
@@ -846,10 +862,11 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
         c[2 * k + 1] = dense_act(__uint_as_float(w4[k] & 0xffff0000u), a.act);
       }
       store_bf8(dst, c);
-    } else if (MODE == 1 && a.act) {             // the producer's activation backward: dx = (dy W^T) act'(pre)
+    } else if (MODE == 4) {                      // the producer's activation backward: dx = (dy W^T) act'(pre)
       float c[8];
       const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-      const uint32_t p4[4] = {x4[it].x, x4[it].y, x4[it].z, x4[it].w};
+      const uint4 pv = prepf[(g0 + it) % PITER];
+      const uint32_t p4[4] = {pv.x, pv.y, pv.z, pv.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         c[2 * k] = __uint_as_float(w4[k] << 16) * dense_act_grad(__uint_as_float(p4[k] << 16), a.act);
@@ -1737,5 +1754,5 @@ MDTF_EXPORT int mdtf_gemm_dgrad_act(const void* dy, const void* w, void* dx, con
   a.K = N;
   const int w8 = bm / 10000, stages = (bm % 10000) / 1000 ? (bm % 10000) / 1000 : 2;
   bm = w8 * 10000 + bm % 1000;
-  return dispatch_fd_v2<1, false>(a, bm, bn, stages, st);
+  return dispatch_fd_v2<4, false>(a, bm, bn, stages, st);
 }

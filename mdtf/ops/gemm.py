@@ -40,14 +40,14 @@ N.register("mdtf_gemm_fwd", [N.P, N.P, N.P, N.P, N.P, N.I, N.I, N.P, N.P, N.P, N
 N.register("mdtf_gemm_dgrad_act", [N.P, N.P, N.P, N.P, N.I, N.L, N.I, N.I, N.I, N.I, N.P])
 
 # ffn(): the second layer's data gradient multiplies by the first layer's activation derivative in its epilogue
-# (csrc/conv_igemm.hip mdtf_gemm_dgrad_act), so no separate activation-backward pass runs.  Graph-timed it wins
-# (0.071 vs 0.081 ms at BERT-base's 8192 x 3072 x 768), but inside the step the kernel runs at 0.0815 ms (the
-# epilogue's pre-activation reads come from HBM, not from the probe's warm MALL) vs hipBLASLt 0.042 + act
-# backward 0.030: BERT-base A/B 5646 / 5608 fused vs 5664 / 5638 seq/s.  Opt-in: MDTF_FFN_FUSE=1.
-FFN_FUSE = os.environ.get("MDTF_FFN_FUSE", "0") == "1"
+# (csrc/conv_igemm.hip mdtf_gemm_dgrad_act, fd v2 MODE 4: the epilogue's pre-activation vectors are loaded before
+# the main loop, so their HBM latency hides under it), and no separate activation-backward pass runs.  Graph-timed
+# 0.071 vs 0.076 ms (hipBLASLt + act backward) at BERT-base's 8192 x 3072 x 768; BERT-base A/B (30 steps,
+# alternating): fused 5668 / 5666 vs separate 5661 / 5648 seq/s.  MDTF_FFN_FUSE=0: the separate pass.
+FFN_FUSE = os.environ.get("MDTF_FFN_FUSE", "1") != "0"
 # (K, N) of the second layer's W [K][N] -> (bm, bn, stages, ver) of the fused data gradient (output K columns)
-# (bench/dgrad_act_probe.py, graph-timed at M 8192: 128 x 256 8-wave 0.071 ms vs hipBLASLt + act backward 0.081)
-DGRAD_ACT_TILES = {(3072, 768): (128, 256, 2, 3), (4096, 1024): (128, 256, 2, 3)}
+# (bench/dgrad_act_probe.py, graph-timed at M 8192: 128 x 256 8-wave, 3 stages)
+DGRAD_ACT_TILES = {(3072, 768): (128, 256, 3, 3)}
 
 # MDTF_DENSE_FWD: "auto" (default) = the shapes of FWD_TILES, where the kernel beats hipBLASLt inside the
 # captured BERT-base step; "mdtf" = every shape it takes; "hipblaslt" = none (torch.addmm + activation kernel).
