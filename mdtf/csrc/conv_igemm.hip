@@ -697,33 +697,17 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
 
   // MODE 4: this thread's pre-activation vectors of the copy-out, loaded before the first stage so their HBM
   // latency hides under the main loop (the copy-out's row mapping: idx = tid + it * NT, 8 columns per idx)
-  // STATS in a dgrad (MODE 1/2): the BN-backward-statistics epilogue with the BN input x and ReLU mask
-  // prefetched the same way (tiles with <= 8 copy-out rows per thread; the host launches it only with bsum)
-  constexpr int CITER = BM * (BN / 8) / (64 * NW);
-  constexpr bool PBX = STATS && (MODE == 1 || MODE == 2) && CITER <= 8;
-  constexpr int PITER = (MODE == 4 || PBX) ? CITER : 1;
+  constexpr int PITER = MODE == 4 ? BM * (BN / 8) / (64 * NW) : 1;
   uint4 prepf[PITER];
-  uint32_t pmb[PBX ? PITER : 1];
-  if constexpr (MODE == 4 || PBX) {
+  if constexpr (MODE == 4) {
 #pragma unroll
     for (int it = 0; it < PITER; ++it) {
       const int idx = tid + it * 64 * NW;
       const int row = idx / (BN / 8), c8 = idx - row * (BN / 8);
       const long long m = m0 + row;
       const int n = n0 + c8 * 8;
-      const bool ok = m < a.M && n < a.Ncol;
-      long long pix = ok ? m : 0;
-      if (MODE == 2) {          // class pixel (n, i, j) -> DX pixel (as in the copy-out)
-        const int j = static_cast<int>(pix % a.cls_Wc);
-        const long long t = pix / a.cls_Wc;
-        const int i = static_cast<int>(t % a.cls_Hc);
-        const long long nb = t / a.cls_Hc;
-        pix = (nb * a.H + a.cls_h0 + a.SH * i) * a.W + a.cls_w0 + a.SW * j;
-      }
-      const long long o = pix * a.Ncol + n;
-      const bf16_t* src = MODE == 4 ? a.pre_out : a.bx;
-      prepf[it] = ok ? *reinterpret_cast<const uint4*>(src + o) : make_uint4(0, 0, 0, 0);
-      if constexpr (PBX) pmb[it] = (ok && a.bmask) ? a.bmask[o >> 3] : 0xffu;
+      prepf[it] = (m < a.M && n < a.Ncol) ? *reinterpret_cast<const uint4*>(a.pre_out + m * a.Ncol + n)
+                                          : make_uint4(0, 0, 0, 0);
     }
   }
 
@@ -854,7 +838,7 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
         old4[it] = *reinterpret_cast<const uint4*>((a.acc_src ? a.acc_src : a.out) + off[it]);
         if (a.acc_mask) old4[it] = mask_bf8(old4[it], a.acc_mask[off[it] >> 3]);
       }
-      if (bstat && !PBX) {
+      if (bstat) {
         x4[it] = *reinterpret_cast<const uint4*>(a.bx + off[it]);
         mb[it] = a.bmask ? a.bmask[off[it] >> 3] : 0xffu;
       }
@@ -911,13 +895,11 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
         *reinterpret_cast<uint4*>(dst) = v;
       }
       if (bstat) {
-        const uint4 xv = PBX ? prepf[(g0 + it) % PITER] : x4[it];
-        const uint32_t mv = PBX ? pmb[(g0 + it) % PITER] : mb[it];
-        const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
+        const uint32_t xw[4] = {x4[it].x, x4[it].y, x4[it].z, x4[it].w};
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float xk = (k & 1) ? __uint_as_float(xw[k >> 1] & 0xffff0000u) : __uint_as_float(xw[k >> 1] << 16);
-          const float gk = ((mv >> k) & 1u) ? c[k] : 0.f;
+          const float gk = ((mb[it] >> k) & 1u) ? c[k] : 0.f;
           bs0[k] += gk;
           bs1[k] += gk * xk;
         }
@@ -954,7 +936,7 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
       }
     }
   }
-  if (STATS && (MODE == 0 || MODE == 3)) {
+  if (STATS) {
     float ssum[TN][4], ssq[TN][4];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -1619,12 +1601,6 @@ MDTF_EXPORT int mdtf_conv_fwd_v2(const void* x, const void* wt, void* y, float* 
   return rc;
 }
 
-// MDTF_DGRAD_PBX=0: the BN-statistics dgrad loads x / mask in the copy-out instead of before the main loop (A/B)
-static const bool PBX_ON = [] {
-  const char* e = getenv("MDTF_DGRAD_PBX");
-  return !(e && e[0] == '0');
-}();
-
 // v2 (Cout % 64 == 0): DX = dgrad(DY, W), W in HWIO
 MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int OH,
                                    int OW, int Cout, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW,
@@ -1655,8 +1631,7 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
   if (SH == 1 && SW == 1) {
     a.M = (long long)N * H * W;
     a.K = KH * KW * Cout;
-    return (bsum && PBX_ON) ? dispatch_fd_v2<1, true>(a, bm, bn, stages, st)
-                            : dispatch_fd_v2<1, false>(a, bm, bn, stages, st);
+    return dispatch_fd_v2<1, false>(a, bm, bn, stages, st);
   }
   // strided: one launch per stride-parity class (rh, rw) = ((h + PH) % SH, (w + PW) % SW)
   for (int rh = 0; rh < SH; ++rh)
@@ -1678,8 +1653,7 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
       // (with a separate accumulate source the class's pixels must still be written)
       if (c.M == 0 || (c.K == 0 && accumulate && !bsum && !acc_src)) continue;
       const int cs = c.K > 64 && stages == 1 ? 2 : stages;
-      const int rc = (bsum && PBX_ON) ? dispatch_fd_v2<2, true>(c, bm, bn, cs, st)
-                                      : dispatch_fd_v2<2, false>(c, bm, bn, cs, st);
+      const int rc = dispatch_fd_v2<2, false>(c, bm, bn, cs, st);
       if (rc) return rc;
     }
   return 0;
