@@ -136,6 +136,8 @@ class Server(object):
             self.job_name, self.task_index, "/%d" % self.local_rank if self.layout.gpu_num > 1 else ""))
         # surface RCCL errors / dead peers as exceptions instead of silent hangs
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        # RCCL prints the failing call before it aborts a process (silent otherwise)
+        os.environ.setdefault("NCCL_DEBUG", "WARN")
         # flight recorder on: hipGraph capture waits until the RCCL watchdog has retired every eager
         # work (train/graph.py _drain_comm_watchdog reads the recorder's active entries)
         os.environ.setdefault("TORCH_FR_BUFFER_SIZE", "2000")
