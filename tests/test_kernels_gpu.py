@@ -1304,16 +1304,23 @@ def test_ffn_fused_act_backward_matches_unfused(monkeypatch):
     w2 = (torch.randn(3072, 768, device=DEV) * 0.02).bfloat16().requires_grad_()
     b2 = (torch.randn(768, device=DEV) * 0.1).bfloat16().requires_grad_()
     res = []
-    fused = []
+    calls = []
+    real = G.hand_dgrad_act
+
+    def counted(*a, **k):
+        out = real(*a, **k)
+        calls.append(out is not None)
+        return out
+    monkeypatch.setattr(G, "hand_dgrad_act", counted)
     for fuse in (True, False):
         monkeypatch.setattr(G, "FFN_FUSE", fuse)
         xi = x.clone().requires_grad_()
         y = G.ffn(xi, w1, b1, w2, b2)
-        fused.append(y.grad_fn is not None)
         y.float().square().mean().backward()
         res.append([y.detach(), xi.grad] + [t.grad for t in (w1, b1, w2, b2)])
         for t in (w1, b1, w2, b2):
             t.grad = None
+    assert calls == [True], calls              # the fused epilogue ran once (fused pass only)
     for a, r in zip(res[0], res[1]):
         assert _rel(a, r) < 1e-2
 
