@@ -94,6 +94,7 @@ STOCK_SEQ128_PER_GPU = 3319.0
 
 def main():
     args = parse()
+    graph_op = None                  # the mdtf train op (its StepGraph says whether replays happened)
     from mdtf.utils.launch import ensure_ranks
     ensure_ranks(args.gpus, os.path.abspath(__file__))     # --gpus N: N ranks or a non-zero exit
     distributed = int(os.environ.get("WORLD_SIZE", "1")) > 1
@@ -156,6 +157,7 @@ def main():
                                                mode=args.mode, comm_dtype=args.comm_dtype,
                                                bucket_bytes=(args.bucket_mb << 20) if args.bucket_mb else None)
         op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
+        graph_op = op
         sess = mdtf.train.MonitoredTrainingSession(is_chief=rank == 0, log_step_count_steps=0, server=server)
 
         def run():
@@ -211,7 +213,9 @@ def main():
                           "baseline": "stock PyTorch-ROCm comparator, %.0f seq/s/GPU x %d" % (
                               STOCK_SEQ128_PER_GPU, world),
                           "impl": "stock-pytorch" if args.stock else "mdtf",
-                          "hip_graph": bool(args.hip_graph) and not args.stock and gpu,
+                          # a captured step really replayed (gloo rehearsals / a rejected capture run eagerly)
+                          "hip_graph": (not args.stock and gpu
+                                        and bool(getattr(getattr(graph_op, "graph", None), "replays", 0))),
                           "dtype": "bf16" if gpu else "fp32",
                           "data": "synthetic (random token ids, random-init weights)",
                           "config": {"model": "bert-%s" % args.size, "global_batch": world * args.batch,
