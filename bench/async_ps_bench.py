@@ -35,6 +35,7 @@ def parse(argv=None):
     p.add_argument("--steps", type=int, default=30, help="timed steps per worker")
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--cpu", action="store_true", help="plumbing run on the CPU (gloo)")
+    p.add_argument("--share_gpu", action="store_true", help="all tasks on GPU 0, gloo transport (1-GPU rehearsal)")
     p.add_argument("--timeout_s", type=float, default=1800)
     return p.parse_known_args(argv)
 
@@ -46,6 +47,10 @@ def parent(a):
     if a.cpu:
         env["CUDA_VISIBLE_DEVICES"] = ""
         env["HIP_VISIBLE_DEVICES"] = ""
+    elif a.share_gpu:
+        # every task on the one visible GPU, tensors exchanged over gloo (RCCL needs a device per rank): the
+        # 1-GPU rehearsal of the async data plane, not a throughput measurement of config 5
+        env["MDTF_DIST_BACKEND"] = "gloo"
     argv = [os.path.abspath(__file__), "--depth=%d" % a.depth, "--batch=%d" % a.batch, "--image=%d" % a.image,
             "--steps=%d" % a.steps, "--warmup=%d" % a.warmup, "--ps_mode=async"]
     t0 = time.time()
@@ -69,10 +74,11 @@ def parent(a):
     print(json.dumps({
         "metric": "images/sec ResNet-%d async parameter-server, %d ps + %d workers, one node" % (
             a.depth, a.num_ps, a.num_workers),
-        "value": round(value, 2), "unit": "images/sec", "n_gpus": 0 if a.cpu else a.num_ps + a.num_workers,
+        "value": round(value, 2), "unit": "images/sec", "n_gpus": 0 if a.cpu else (1 if a.share_gpu else a.num_ps + a.num_workers),
         "higher_is_better": True, "per_worker": [round(x, 2) for x in rates], "wall_s": round(wall, 1),
-        "ps": [{k: r[k] for k in ("ps", "updates", "mean_staleness", "max_staleness", "apply_s", "idle_s", "wall_s",
-                                  "store_wait_s", "wire")} for r in ps_stats],
+        "ps": [{k: r.get(k) for k in ("ps", "updates", "mean_staleness", "max_staleness", "apply_s", "idle_s", "wall_s",
+                                      "store_wait_s", "store_calls", "applies", "batched_max", "poll", "wire")}
+               for r in ps_stats],
         "dtype": "bf16" if not a.cpu else "fp32", "data": "synthetic", "config": {
             "model": "resnet%d_v1.5" % a.depth, "per_worker_batch": a.batch, "image": a.image,
             "parallelism": "async-ps %dps+%dw" % (a.num_ps, a.num_workers)}}), flush=True)

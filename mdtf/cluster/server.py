@@ -163,7 +163,9 @@ class Server(object):
         self.store = dist.TCPStore(host, port, is_master=self.is_coordinator, timeout=timeout,
                                    wait_for_workers=False)
         if self.rank is not None:
-            backend = self.backend or ("nccl" if torch.cuda.is_available() else "gloo")
+            # MDTF_DIST_BACKEND=gloo: several tasks sharing one GPU (the 1-GPU async-PS rehearsal)
+            backend = self.backend or os.environ.get("MDTF_DIST_BACKEND") or (
+                "nccl" if torch.cuda.is_available() else "gloo")
             dev = self.device()
             if dev.type == "cuda":
                 torch.cuda.set_device(dev)

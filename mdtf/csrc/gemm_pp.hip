@@ -1,0 +1,481 @@
+// Ping-pong MFMA GEMM core (gfx950 / CDNA4): the dense matmul of every FC / transformer layer.
+//
+// Replaces the cuBLAS GEMM the reference reaches through tf.matmul in FC_layer
+// (distribute_tools.py:204-206) and its autodiff backward (distribute_tower.py:27), SURVEY §2.5 K8.
+//
+//   C[M][N] (+)= Σ_k A(m, k) B(k, n)
+//     A stored [M][K] (reduction-contiguous) or, ATR, [K][M];  B stored [N][K] or, BTR, [K][N].
+//   dense forward   y  = x W       : A = x [M][K], B = W [K][N] (BTR)
+//   data gradient   dx = dy W^T    : A = dy [M][N], B = W [K][N] read as [n=K][k=N]   (no transposes)
+//   weight gradient dW = x^T dy    : A = x stored [m][k] (ATR), B = dy [m][n] (BTR), fp32 into the grad slot
+//
+// Structure (one 512-thread workgroup per CU, 8 waves = two groups of 4 that share the 4 SIMDs):
+//   * 16x16x32 bf16 MFMA (on random data it holds a ~12-15 % higher clock than 32x32x16 at equal cycles
+//     per FLOP, MI355X_MICROARCH.md 'DVFS give-back' item 7); each wave owns a RW x 64 output tile.
+//   * K-tiles of 64, split into four LDS units per tile -- A rows half 0/1, B columns half 0/1 -- each
+//     double-buffered (2 x (BM+BN) x 128 B: 128 KiB for 256 x 256).  Units are filled by LDS-DMA
+//     (buffer_load_dwordx4 ... lds, bounds-checked zero fill), one unit per phase, so loads stream
+//     continuously and never need a vmcnt(0) inside the loop.
+//   * Four quadrant phases per K-tile.  Each phase is {ds_read fragments, issue one unit's DMA} ->
+//     s_barrier -> {16..32 MFMAs} -> s_barrier.  Group 1 runs one barrier behind group 0, so on every
+//     SIMD one wave issues MFMAs while its partner reads LDS and issues loads (ping-pong): the matrix
+//     pipe never waits for a fragment read.  The DMA schedule below is derived from the barrier
+//     numbering so every read of a unit follows (a) each issuing wave's vmcnt and (b) a barrier, and
+//     every DMA into a slot follows the last read of the tile that used it (comments at `issue_unit`).
+//   * Reduction-contiguous tiles are [rows][64 k] images read by ds_read_b128 with a 16-B chunk XOR
+//     swizzle (conflict-free for the four 16-lane groups); k-major tiles are [64 k][cols] images read by
+//     ds_read_b64_tr_b16 (hardware transpose) with a 32-B block XOR swizzle (conflict-free per 32-lane
+//     half).  Both swizzles are applied to the DMA's per-lane SOURCE address, the LDS image stays linear.
+//   * Epilogue straight from the accumulators: the MFMA is issued as C^T = B^T A^T, so each lane holds 4
+//     consecutive output columns of one row (8 B bf16 / 16 B fp32 stores, 128-B rows per instruction),
+//     with bias, ReLU/GELU (+ saved pre-activation), bf16 accumulate, or fp32 accumulate / split-K atomics.
+//   * Tiles are XCD-remapped (bijective) so the column tiles of a row panel share an L2.
+#include "mdtf_common.h"
+
+using namespace mdtf;
+
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+constexpr unsigned kOOB = 0x80000000u;   // buffer offset past num_records: the DMA writes zeros
+
+struct GemmArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  long long lda, ldb;        // row strides (elements) of the stored layouts
+  int M, N, K;               // C is M x N; K = reduction (multiple of 64)
+  int tiles_m, tiles_n;
+  int kt_split;              // K-tiles per split (gridDim.y splits)
+  int bytes_a, bytes_b;      // buffer ranges for the bounds checks (< 2 GiB)
+  // bf16 output
+  bf16_t* C;
+  long long ldc;
+  const bf16_t* bias;        // [N] bf16, added on the fp32 accumulators (null: none)
+  bf16_t* pre;               // act != 0: the bf16 pre-activation is also stored here (null: not kept)
+  int act;                   // 0 none, 1 relu, 2 gelu (tanh form)
+  int accumulate;            // C = result + C
+  // fp32 output
+  float* Cf;
+  long long ldcf;
+  int atomic;                // 1: fp32 atomics (split-K); 0: Cf += result (one writer per element)
+};
+
+__device__ __forceinline__ float act_fwd(float v, int act) {
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) {   // x * sigmoid(2u), u = sqrt(2/pi) (x + 0.044715 x^3)  (== 0.5 x (1 + tanh u))
+    const float u2 = 1.5957691216f * (v + 0.044715f * v * v * v);
+    return v * __builtin_amdgcn_rcpf(1.f + __expf(-u2));
+  }
+  return v;
+}
+
+// LDS-DMA of 16 B per lane: LDS destination = m0 (wave-uniform) + 16 * lane, source = rsrc + voff + soff.
+// Issued from inline asm so the compiler neither sees an LDS write (no vmcnt(0) before our ds_reads) nor
+// counts it: the kernel's own wait_vmcnt<N> + s_barrier order every read after it.
+__device__ __forceinline__ void dma16(i32x4_t rsrc, unsigned lds_addr, unsigned voff, int soff) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc), "s"(soff), "{m0}"(m0)
+               : "memory");
+}
+
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// bijective XCD-aware remap of a 1-D block index (cdna_hip_programming.md §5 T1)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+// 32-B block swizzle of a [64 k][W cols] image (row pitch 2W bytes) for the transposed fragment reads:
+// the 8 rows one 32-lane half reads ({0-3, 8-11} + 16 h, and +4) land in 8 distinct 32-B bank slots
+template <int PITCH>
+__device__ __forceinline__ int trg(int row) {
+  if constexpr (PITCH >= 256) return (row & 3) | (((row >> 3) & 1) << 2);
+  else return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+}
+
+// One operand's four-unit pipeline geometry.  W = rows (or cols, TR) per unit image = tile / 2.
+template <int W, bool TR>
+struct Unit {
+  static constexpr int BYTES = W * 128;            // 64 k x W x 2 B
+  static constexpr int PER_WAVE = W / 64;          // DMA wave-instructions per wave per unit
+  static constexpr int PITCH = TR ? 2 * W : 128;   // image row pitch (bytes)
+};
+
+template <int BM, int BN, bool ATR, bool BTR, int EPI>
+__global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
+  constexpr int WCN = BN / 64;             // waves of a group along N (2 or 4)
+  constexpr int WRN = 4 / WCN;             // along M
+  constexpr int RW = BM / 2 / WRN;         // output rows per wave
+  constexpr int FM = RW / 16, FMH = FM / 2;   // row fragments per wave / per half
+  constexpr int WA = BM / 2, WB = BN / 2;
+  using UA = Unit<WA, ATR>;
+  using UB = Unit<WB, BTR>;
+  constexpr int SLOT = 2 * UA::BYTES + 2 * UB::BYTES;
+  static_assert(FMH >= 1 && WCN * WRN == 4, "tile");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = wave >> 2, w4 = wave & 3;
+  const int wc = w4 % WCN, wrr = w4 / WCN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kt0 = blockIdx.y * a.kt_split;
+  const int T = min(a.kt_split, a.K / 64 - kt0);
+
+  const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<unsigned long long>(
+      (__attribute__((address_space(3))) char*)smem));
+  const i32x4_t ra = buffer_rsrc(a.A, a.bytes_a);
+  const i32x4_t rb = buffer_rsrc(a.B, a.bytes_b);
+
+  // ---- per-lane DMA source offsets (bytes, at k-tile 0 of this split) for this wave's share of each unit
+  // unit u: 0,1 = A halves (rows/cols m0 + u*WA ..), 2,3 = B halves
+  auto src_off = [&](bool tr, int w, long long ld, int base, int limit, int ii) -> unsigned {
+    const int off = ii * 1024 + lane * 16;          // byte offset inside the unit image
+    if (!tr) {
+      const int row = off >> 7, pc = (off >> 4) & 7;
+      const int lc = pc ^ ((row >> 1) & 7);
+      const int r = base + row;
+      if (r >= limit) return kOOB;
+      return static_cast<unsigned>(((long long)r * ld + (long long)kt0 * 64 + lc * 8) * 2);
+    }
+    const int pitch = 2 * w;
+    const int row = off / pitch, cb = off - row * pitch;
+    const int pb = cb >> 5, half = (cb >> 4) & 1;
+    const int lb = pb ^ (pitch >= 256 ? trg<256>(row) : trg<128>(row));
+    const int col = base + lb * 16 + half * 8;
+    if (col >= limit) return kOOB;
+    return static_cast<unsigned>((((long long)kt0 * 64 + row) * ld + col) * 2);
+  };
+  unsigned offA[2][UA::PER_WAVE], offB[2][UB::PER_WAVE];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+#pragma unroll
+    for (int j = 0; j < UA::PER_WAVE; ++j)
+      offA[u][j] = src_off(ATR, WA, a.lda, m0 + u * WA, a.M, j * 8 + wave);
+#pragma unroll
+    for (int j = 0; j < UB::PER_WAVE; ++j)
+      offB[u][j] = src_off(BTR, WB, a.ldb, n0 + u * WB, a.N, j * 8 + wave);
+  }
+  // per K-tile advance of the source (wave-uniform soffset)
+  const int stepA = ATR ? (int)(64 * a.lda * 2) : 128;
+  const int stepB = BTR ? (int)(64 * a.ldb * 2) : 128;
+
+  // issue this wave's share of unit u (0,1 A; 2,3 B) of K-tile t into slot t & 1
+  auto issue_unit = [&](int u, int t) {
+    const unsigned slot = lds0 + (t & 1) * SLOT;
+    if (u < 2) {
+#pragma unroll
+      for (int j = 0; j < UA::PER_WAVE; ++j)
+        dma16(ra, slot + u * UA::BYTES + (j * 8 + wave) * 1024, offA[u][j], t * stepA);
+    } else {
+#pragma unroll
+      for (int j = 0; j < UB::PER_WAVE; ++j)
+        dma16(rb, slot + 2 * UA::BYTES + (u - 2) * UB::BYTES + (j * 8 + wave) * 1024, offB[u - 2][j], t * stepB);
+    }
+  };
+
+  // ---- fragment read addresses (bytes relative to a slot)
+  const int fr = lane & 15, fq = lane >> 4;
+  const int q4 = (lane >> 2) & 3, p4 = lane & 3;
+  // this wave's A unit (its group's rows) and B unit (its column strip)
+  const int ua = G;
+  const int ub = (wc * 64) / WB;
+  const int a_row0 = wrr * RW;                // inside the A unit image
+  const int b_col0 = wc * 64 - ub * WB;       // inside the B unit image
+  const unsigned baseA = ua * UA::BYTES;
+  const unsigned baseB = 2 * UA::BYTES + ub * UB::BYTES;
+
+  auto frag = [&](bool tr, int pitch, unsigned ubase, int r0, int s, const char* slotp) -> bf16x8_t {
+    if (!tr) {
+      const int row = r0 + fr;
+      const int ch = (4 * s + fq) ^ ((row >> 1) & 7);
+      const uint4 v = *reinterpret_cast<const uint4*>(slotp + ubase + row * 128 + ch * 16);
+      return __builtin_bit_cast(bf16x8_t, v);
+    }
+    const int row = 32 * s + 8 * fq + q4;
+    const int g = pitch >= 256 ? trg<256>(row) : trg<128>(row);
+    const int blk = (r0 >> 4) ^ g;
+    const char* p1 = slotp + ubase + row * pitch + blk * 32 + p4 * 8;
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p1);
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p1 + 4 * pitch));
+    const short8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, f);
+  };
+
+  float4v acc[FM][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  // ---- DMA schedule.  Barrier numbering: group 0 passes b(2P) / b(2P+1) around the MFMAs of phase P
+  // (P = 4t + q), group 1 b(2P+1) / b(2P+2).  Reads of K-tile t: group 0 in phases 4t..4t+2, group 1 one
+  // barrier later; the B units of tile t are last read before b(8t+4), A half 0 before b(8t+5), A half 1
+  // before b(8t+6).  Tile t+1 reuses tile t-1's slots and is first read after b(8t+7).  Hence:
+  //   group 0 issues in phase 4t+q:  q0 B1(t+1)  q1 A0(t+1)  q2 A1(t+1)  q3 B0(t+2)
+  //   group 1 issues in phase 4t+q:  q0 A0(t+1)  q1 A1(t+1)  q2 B0(t+2)  q3 B1(t+2)
+  // and each wave waits for everything but its B0(t+2) (vmcnt) before b(8t+7): group 0 after the MFMAs
+  // of phase 4t+3, group 1 before its first barrier of that phase.
+  constexpr int UBW = UB::PER_WAVE;
+  // prologue: tile 0 whole, plus the units of tile 1 the schedule expects issued before tile 0's phases
+#pragma unroll
+  for (int u = 0; u < 4; ++u) issue_unit(u, 0);
+  if (T > 1) {
+    issue_unit(2, 1);
+    if (G == 1) issue_unit(3, 1);
+  }
+  if (T > 1) {
+    if (G == 0) wait_vmcnt<UBW>();
+    else wait_vmcnt<2 * UBW>();
+  } else {
+    wait_vmcnt<0>();
+  }
+  barrier();
+  if (G == 1) barrier();
+
+  bf16x8_t fa[FMH][2], fb[4][2];
+  for (int t = 0; t < T; ++t) {
+    const char* slotp = smem + (t & 1) * SLOT;
+    const bool n1 = t + 1 < T, n2 = t + 2 < T;
+    // ---------------- phase q0: A top + B left; MFMA top x left
+#pragma unroll
+    for (int i = 0; i < FMH; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fa[i][s] = frag(ATR, UA::PITCH, baseA, a_row0 + 16 * i, s, slotp);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fb[j][s] = frag(BTR, UB::PITCH, baseB, b_col0 + 16 * j, s, slotp);
+    if (n1) issue_unit(G == 0 ? 3 : 0, t + 1);
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < FMH; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    // ---------------- phase q1: B right; MFMA top x right
+#pragma unroll
+    for (int j = 2; j < 4; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fb[j][s] = frag(BTR, UB::PITCH, baseB, b_col0 + 16 * j, s, slotp);
+    if (n1) issue_unit(G == 0 ? 0 : 1, t + 1);
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < FMH; ++i)
+#pragma unroll
+        for (int j = 2; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    // ---------------- phase q2: A bottom; MFMA bottom x right
+#pragma unroll
+    for (int i = 0; i < FMH; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fa[i][s] = frag(ATR, UA::PITCH, baseA, a_row0 + 16 * (FMH + i), s, slotp);
+    if (G == 0) {
+      if (n1) issue_unit(1, t + 1);
+    } else {
+      if (n2) issue_unit(2, t + 2);
+    }
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < FMH; ++i)
+#pragma unroll
+        for (int j = 2; j < 4; ++j)
+          acc[FMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[FMH + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    // ---------------- phase q3: no reads; MFMA bottom x left
+    if (G == 1) {
+      if (n2) wait_vmcnt<UBW>();
+      else wait_vmcnt<0>();
+      if (n2) issue_unit(3, t + 2);
+    } else {
+      if (n2) issue_unit(2, t + 2);
+    }
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < FMH; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[FMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[FMH + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (G == 0) {
+      if (n2) wait_vmcnt<UBW>();
+      else wait_vmcnt<0>();
+    }
+    barrier();
+  }
+  if (G == 0) barrier();
+
+  // ---- epilogue: lane holds C[row][col .. col+3] for each (i, j)
+  const int rbase = m0 + G * (BM / 2) + wrr * RW + fr;
+  const int cbase = n0 + wc * 64 + 4 * fq;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int row = rbase + 16 * i;
+    if (row >= a.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = cbase + 16 * j;
+      if (col >= a.N) continue;     // N % 4 == 0 (host-checked): whole 4-column groups
+      float4v v = acc[i][j];
+      if constexpr (EPI == 0) {
+        if (a.bias) {
+          const uint2 b4 = *reinterpret_cast<const uint2*>(a.bias + col);
+          v[0] += __uint_as_float(b4.x << 16);
+          v[1] += __uint_as_float(b4.x & 0xffff0000u);
+          v[2] += __uint_as_float(b4.y << 16);
+          v[3] += __uint_as_float(b4.y & 0xffff0000u);
+        }
+        bf16_t* dst = a.C + (long long)row * a.ldc + col;
+        if (a.accumulate) {
+          const uint2 o = *reinterpret_cast<const uint2*>(dst);
+          v[0] += __uint_as_float(o.x << 16);
+          v[1] += __uint_as_float(o.x & 0xffff0000u);
+          v[2] += __uint_as_float(o.y << 16);
+          v[3] += __uint_as_float(o.y & 0xffff0000u);
+        }
+        if (a.act) {
+          const uint2 pr = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+          if (a.pre) *reinterpret_cast<uint2*>(a.pre + (long long)row * a.ldc + col) = pr;
+          // the activation of the ROUNDED pre-activation (what the backward recomputes from)
+          v[0] = act_fwd(__uint_as_float(pr.x << 16), a.act);
+          v[1] = act_fwd(__uint_as_float(pr.x & 0xffff0000u), a.act);
+          v[2] = act_fwd(__uint_as_float(pr.y << 16), a.act);
+          v[3] = act_fwd(__uint_as_float(pr.y & 0xffff0000u), a.act);
+        }
+        *reinterpret_cast<uint2*>(dst) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+      } else {
+        float* dst = a.Cf + (long long)row * a.ldcf + col;
+        if (a.atomic) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) unsafeAtomicAdd(dst + e, v[e]);
+        } else {
+          float4 o = *reinterpret_cast<const float4*>(dst);
+          o.x += v[0];
+          o.y += v[1];
+          o.z += v[2];
+          o.w += v[3];
+          *reinterpret_cast<float4*>(dst) = o;
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, bool ATR, bool BTR, int EPI>
+int launch_pp(const GemmArgs& a0, int splits, hipStream_t st) {
+  GemmArgs a = a0;
+  a.tiles_m = (a.M + BM - 1) / BM;
+  a.tiles_n = (a.N + BN - 1) / BN;
+  const int KT = a.K / 64;
+  if (splits < 1) splits = 1;
+  if (splits > KT) splits = KT;
+  a.kt_split = (KT + splits - 1) / splits;
+  splits = (KT + a.kt_split - 1) / a.kt_split;
+  if (EPI == 1) a.atomic = splits > 1 ? 1 : a.atomic;
+  constexpr int lds = 2 * (BM + BN) * 128;
+  auto k = gemm_pp_kernel<BM, BN, ATR, BTR, EPI>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  dim3 grid(a.tiles_m * a.tiles_n, splits);
+  hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// tile code: 0 = 256x256, 1 = 256x128, 2 = 128x256, 3 = 128x128
+template <bool ATR, bool BTR, int EPI>
+int dispatch(int tile, const GemmArgs& a, int splits, hipStream_t st) {
+  switch (tile) {
+    case 0: return launch_pp<256, 256, ATR, BTR, EPI>(a, splits, st);
+    case 1: return launch_pp<256, 128, ATR, BTR, EPI>(a, splits, st);
+    case 2: return launch_pp<128, 256, ATR, BTR, EPI>(a, splits, st);
+    case 3: return launch_pp<128, 128, ATR, BTR, EPI>(a, splits, st);
+  }
+  return MDTF_EINVAL;
+}
+
+bool fits(long long rows, long long ld) { return rows * ld * 2 < (1ll << 31); }
+
+}  // namespace
+
+extern "C" int mdtf_get_deterministic();
+
+// layout code: 0 = fwd (A [M][K], B [K][N] -> BTR), 1 = dgrad (A [M][K], B [N][K]), 2 = wgrad (A [K][M], B [K][N])
+// C / Cf: exactly one non-null.  Returns 0, or MDTF_EUNSUPPORTED for shapes the kernel does not take.
+MDTF_EXPORT int mdtf_gemm_pp(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
+                             int layout, int tile, int splits, bf16_t* C, long long ldc, const bf16_t* bias,
+                             bf16_t* pre, int act, int accumulate, float* Cf, long long ldcf, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 4 || (lda % 8) || (ldb % 8)) return MDTF_EUNSUPPORTED;
+  if ((C == nullptr) == (Cf == nullptr)) return MDTF_EINVAL;
+  const bool atr = layout == 2, btr = layout == 0 || layout == 2;
+  // operand ranges (the buffer descriptors' 32-bit offsets)
+  if (!(atr ? fits(K, lda) : fits(M, lda)) || !(btr ? fits(K, ldb) : fits(N, ldb))) return MDTF_EUNSUPPORTED;
+  if (atr && M % 8) return MDTF_EUNSUPPORTED;     // k-major operands: whole 16-B column chunks
+  if (btr && N % 8) return MDTF_EUNSUPPORTED;
+  GemmArgs a{};
+  a.A = A;
+  a.B = B;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.bytes_a = (int)((atr ? (long long)K : (long long)M) * lda * 2);
+  a.bytes_b = (int)((btr ? (long long)K : (long long)N) * ldb * 2);
+  a.C = C;
+  a.ldc = ldc;
+  a.bias = bias;
+  a.pre = pre;
+  a.act = act;
+  a.accumulate = accumulate;
+  a.Cf = Cf;
+  a.ldcf = ldcf;
+  a.atomic = 0;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (C != nullptr) {
+    if (splits > 1) return MDTF_EUNSUPPORTED;
+    switch (layout) {
+      case 0: return dispatch<false, true, 0>(tile, a, 1, st);
+      case 1: return dispatch<false, false, 0>(tile, a, 1, st);
+      case 2: return dispatch<true, true, 0>(tile, a, 1, st);
+    }
+    return MDTF_EINVAL;
+  }
+  if (mdtf_get_deterministic()) splits = 1;
+  switch (layout) {
+    case 0: return dispatch<false, true, 1>(tile, a, splits, st);
+    case 1: return dispatch<false, false, 1>(tile, a, splits, st);
+    case 2: return dispatch<true, true, 1>(tile, a, splits, st);
+  }
+  return MDTF_EINVAL;
+}

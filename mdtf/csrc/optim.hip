@@ -125,7 +125,86 @@ __global__ void __launch_bounds__(kThreads) adam_kernel(long long n, float* __re
   }
 }
 
+
+// ---- several sequential updates in one pass (async PS: every gradient that arrived since the last apply).
+// Update i uses gradient g[i] (bf16 wire or fp32) and lr[i] / lr_t[i]; the result equals k launches of the
+// single-update kernel in order, but master / state / shadow are read and written once.
+constexpr int kMaxMulti = 8;
+struct MultiGrads {
+  const void* g[kMaxMulti];
+  float lr[kMaxMulti];
+  float lr_t[kMaxMulti];
+};
+
+__device__ __forceinline__ float4 load_g4(const void* g, long long i, bool bf) {
+  if (bf) {
+    const uint2 v = reinterpret_cast<const uint2*>(g)[i];
+    return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
+                       __uint_as_float(v.y & 0xffff0000u));
+  }
+  return reinterpret_cast<const float4*>(g)[i];
+}
+
+// kind 0 sgd, 1 momentum (flag = nesterov), 2 adam (flag = decoupled weight decay)
+__global__ void __launch_bounds__(kThreads) apply_multi_kernel(int kind, long long n, float* __restrict__ w,
+                                                              float* __restrict__ s1, float* __restrict__ s2,
+                                                              bf16_t* __restrict__ shadow, MultiGrads mg, int k,
+                                                              int gbf16, float mom, float b1, float b2, float eps,
+                                                              float gs, float wd, int flag) {
+  const long long n4 = n >> 2;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    float4 wv = reinterpret_cast<float4*>(w)[i];
+    float4 av = kind >= 1 ? reinterpret_cast<float4*>(s1)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 vv = kind == 2 ? reinterpret_cast<float4*>(s2)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float* wp = &wv.x;
+    float* ap = &av.x;
+    float* vp = &vv.x;
+    for (int u = 0; u < k; ++u) {
+      const float4 gv = load_g4(mg.g[u], i, gbf16 != 0);
+      const float* gp = &gv.x;
+      const float lr = mg.lr[u], lr_t = mg.lr_t[u];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (kind == 2) {
+          adam1(wp[e], gp[e], ap[e], vp[e], lr, lr_t, b1, b2, eps, gs, wd, flag);
+        } else {
+          const float g = gp[e] * gs + wd * wp[e];
+          if (kind == 1) {
+            ap[e] = mom * ap[e] + g;
+            wp[e] -= lr * (flag ? g + mom * ap[e] : ap[e]);
+          } else {
+            wp[e] -= lr * g;
+          }
+        }
+      }
+    }
+    if (kind >= 1) reinterpret_cast<float4*>(s1)[i] = av;
+    if (kind == 2) reinterpret_cast<float4*>(s2)[i] = vv;
+    reinterpret_cast<float4*>(w)[i] = wv;
+    if (shadow) store_shadow4(shadow, i * 4, wv);
+  }
+}
+
 }  // namespace
+
+// k <= 8 sequential updates of one flat group; grads: k device pointers (bf16 if gbf16 else fp32), lrs / lr_ts:
+// k host floats each
+MDTF_EXPORT int mdtf_fused_apply_multi(int kind, long long n, void* w, void* s1, void* s2, void* shadow,
+                                       const void* const* grads, const float* lrs, const float* lr_ts, int k, int gbf16,
+                                       float mom, float b1, float b2, float eps, float gs, float wd, int flag,
+                                       hipStream_t st) {
+  if (n % 4 || k < 1 || k > kMaxMulti || kind < 0 || kind > 2) return MDTF_EINVAL;
+  MultiGrads mg{};
+  for (int u = 0; u < k; ++u) {
+    mg.g[u] = grads[u];
+    mg.lr[u] = lrs[u];
+    mg.lr_t[u] = lr_ts[u];
+  }
+  hipLaunchKernelGGL(apply_multi_kernel, dim3(grid_for(n / 4)), dim3(kThreads), 0, st, kind, n, (float*)w, (float*)s1,
+                     (float*)s2, (bf16_t*)shadow, mg, k, gbf16, mom, b1, b2, eps, gs, wd, flag);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
 
 // n must be a multiple of 4 (flat groups are padded to 64 elements).
 MDTF_EXPORT int mdtf_fused_sgd(long long n, void* w, const void* g, void* shadow, float lr, float gs, float wd,

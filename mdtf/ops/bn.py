@@ -18,9 +18,9 @@ N.register("mdtf_bn_fwd_stats", [N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.
                                  N.I, N.P, N.P])
 
 
-FUSED_BWD = [0]
+FUSED_BWD = [0]      # backward passes that took their statistics from the dgrad epilogue (tests)
 # projection-shortcut BNs applied inside the residual BN's pass (MDTF_DEFER_SHORTCUT_BN=0: separate apply)
-DEFER_SHORTCUT = os.environ.get("MDTF_DEFER_SHORTCUT_BN", "1") != "0"      # backward passes that took their statistics from the dgrad epilogue (tests)
+DEFER_SHORTCUT = os.environ.get("MDTF_DEFER_SHORTCUT_BN", "1") != "0"
 
 
 def _check(x):

@@ -228,6 +228,15 @@ class _FilterTransposes(object):
         self.active = False        # inside a training step
         self.fresh = False         # every registered copy is current for this step
 
+    def clear(self):
+        """Forget every registered filter (a new model / flat space, a released step graph): dead filters
+        must neither stay referenced nor keep being transposed by the batched kernel."""
+        self.entries.clear()
+        del self.order[:]
+        self.desc = None
+        self.tiles = 0
+        self.fresh = False
+
     def step_begin(self):
         self.active = os.environ.get("MDTF_FILTER_CACHE", "1") != "0"
         self.fresh = False

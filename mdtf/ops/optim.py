@@ -120,3 +120,52 @@ def adam_(master, grad, m, v, shadow, lr, beta1, beta2, epsilon, step, grad_scal
     master.sub_(upd)
     if shadow is not None:
         shadow.copy_(master)
+
+
+_native.register("mdtf_fused_apply_multi", [_native.I, _native.L, _native.P, _native.P, _native.P, _native.P, _native.P,
+                                            _native.P, _native.P, _native.I, _native.I, _native.F, _native.F,
+                                            _native.F, _native.F, _native.F, _native.F, _native.I, _native.P])
+MAX_MULTI = 8
+_KIND = {"sgd": 0, "momentum": 1, "adam": 2}
+
+
+def apply_multi_(kind, master, grads, s1, s2, shadow, lrs, lr_ts, momentum=0.0, beta1=0.9, beta2=0.999,
+                 epsilon=1e-8, grad_scale=1.0, weight_decay=0.0, flag=False):
+    """``len(grads)`` (<= 8) SEQUENTIAL updates of one flat group in one pass: update i applies ``grads[i]``
+    (bf16 wire or fp32) with ``lrs[i]`` / ``lr_ts[i]``.  Equals that many single-update launches in order
+    (the async parameter server applies every gradient that arrived since its last apply this way).
+    ``flag``: nesterov (momentum) / decoupled weight decay (adam)."""
+    k = len(grads)
+    assert 1 <= k <= MAX_MULTI and len(lrs) == k and len(lr_ts) == k
+    if _native_ok(master) and all(g.dtype == grads[0].dtype for g in grads):
+        import ctypes
+        gp = (ctypes.c_void_p * k)(*[g.data_ptr() for g in grads])
+        fl = (ctypes.c_float * k)(*[float(x) for x in lrs])
+        ft = (ctypes.c_float * k)(*[float(x) for x in lr_ts])
+        _native.check(_native.fn("mdtf_fused_apply_multi")(
+            _KIND[kind], master.numel(), _native.ptr(master), _native.ptr(s1), _native.ptr(s2), _native.ptr(shadow),
+            ctypes.cast(gp, ctypes.c_void_p), ctypes.cast(fl, ctypes.c_void_p), ctypes.cast(ft, ctypes.c_void_p), k,
+            int(grads[0].dtype == torch.bfloat16), float(momentum), float(beta1), float(beta2), float(epsilon),
+            float(grad_scale), float(weight_decay), int(bool(flag)), _native.stream_ptr()), "fused_apply_multi")
+        return
+    for g, lr, lr_t in zip(grads, lrs, lr_ts):
+        g = g.float() * grad_scale
+        if kind == "adam":
+            if weight_decay and not flag:
+                g = g + weight_decay * master
+            s1.mul_(beta1).add_(g, alpha=1 - beta1)
+            s2.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+            upd = lr_t * s1 / (s2.sqrt() + epsilon)
+            if weight_decay and flag:
+                upd = upd + lr * weight_decay * master
+            master.sub_(upd)
+            continue
+        if weight_decay:
+            g = g + weight_decay * master
+        if kind == "momentum":
+            s1.mul_(momentum).add_(g)
+            master.sub_(lr * (g + momentum * s1) if flag else lr * s1)
+        else:
+            master.sub_(lr * g)
+    if shadow is not None:
+        shadow.copy_(master)

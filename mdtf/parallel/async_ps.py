@@ -38,6 +38,7 @@ MI355X design:
   tensor-bundle checkpoint (one data file per PS task — the TF layout).
 """
 import json
+import os
 import time
 
 import torch
@@ -85,6 +86,57 @@ def _varspec(variables):
 
 
 K_PULL, K_PUSH, K_DONE, K_MASTER = 0, 1, 2, 3
+
+
+class _Posted(object):
+    """A posted receive whose completion is polled without blocking, on both backends.  An RCCL work answers
+    ``is_completed()`` from its HIP event; a gloo receive completes only inside ``wait()`` (its
+    ``is_completed()`` stays False), so a helper thread waits on it and the poll reads a flag."""
+    __slots__ = ("work", "ev")
+
+    def __init__(self, work, threaded):
+        self.work = work
+        self.ev = None
+        if threaded:
+            import threading
+            self.ev = threading.Event()
+            threading.Thread(target=self._wait, daemon=True).start()
+
+    def _wait(self):
+        self.work.wait()
+        self.ev.set()
+
+    def done(self):
+        return self.ev.is_set() if self.ev is not None else self.work.is_completed()
+
+    def wait(self):
+        if self.ev is not None:
+            self.ev.wait()
+        else:
+            self.work.wait()
+
+
+class _TimedStore(object):
+    """Proxy of the cluster store that counts and times every call made through it."""
+
+    def __init__(self, store):
+        self._store = store
+        self.calls = 0
+        self.wait_s = 0.0
+
+    def __getattr__(self, name):
+        fn = getattr(self._store, name)
+        if not callable(fn):
+            return fn
+
+        def timed(*a, **k):
+            t = time.time()
+            try:
+                return fn(*a, **k)
+            finally:
+                self.calls += 1
+                self.wait_s += time.time() - t
+        return timed
 WIRE = torch.bfloat16            # gradient wire dtype (MDTF_ASYNC_WIRE=fp32 for full-precision pushes)
 
 
@@ -133,7 +185,10 @@ def run_parameter_server(op, server):
     hdr = {w: _hdr(cdev) for w in workers}
     gbuf = {}                             # worker -> per-group wire buffers (payloads of several workers in flight)
     vt = torch.zeros(1, dtype=torch.int64, device=cdev)
-    st = {"version": 0, "done": 0, "stale_sum": 0, "stale_max": 0, "updates": 0, "apply": 0.0, "idle": 0.0}
+    st = {"version": 0, "done": 0, "stale_sum": 0, "stale_max": 0, "updates": 0, "apply": 0.0, "idle": 0.0,
+          "applies": 0, "batched_max": 0}
+    timed_store = _TimedStore(store)
+    server.store = timed_store            # any store call made while serving is timed (the data plane makes none)
     t0 = time.time()
 
     def bufs(w):
@@ -148,19 +203,28 @@ def run_parameter_server(op, server):
         for g in groups:
             dist.send(g.shadow if g.shadow is not None else g.master, dst=w)
 
-    def apply(w, wver):
+    def apply_batch(batch):
+        """Every payload that completed since the last apply, as consecutive updates in ONE fused pass per group
+        (chunks of MAX_MULTI); then one reply per worker with the weights after the chunk."""
+        from ..ops.optim import MAX_MULTI
         ta = time.time()
-        lr = optimizer.learning_rate(st["version"])
-        with torch.no_grad():
-            for g, buf in zip(groups, gbuf[w]):
-                g.grad.copy_(buf)             # bf16 wire -> the fp32 gradient the optimizer reads
-                optimizer.update(UpdateTarget(g, g.master, g.grad, g.shadow, "full"), lr, 1.0, st["version"])
-        stale = st["version"] - wver
-        st["stale_sum"] += stale
-        st["stale_max"] = max(st["stale_max"], stale)
-        st["updates"] += 1
-        st["version"] += 1
-        reply(w)
+        for c0 in range(0, len(batch), MAX_MULTI):
+            chunk = batch[c0:c0 + MAX_MULTI]
+            steps = [st["version"] + i for i in range(len(chunk))]
+            with torch.no_grad():
+                for gi, g in enumerate(groups):
+                    optimizer.update_multi(UpdateTarget(g, g.master, g.grad, g.shadow, "full"),
+                                           [gbuf[w][gi] for w, _ in chunk], steps)
+            for w, wver in chunk:
+                stale = st["version"] - wver
+                st["stale_sum"] += stale
+                st["stale_max"] = max(st["stale_max"], stale)
+                st["updates"] += 1
+                st["version"] += 1
+            st["applies"] += 1
+            st["batched_max"] = max(st["batched_max"], len(chunk))
+            for w, _ in chunk:
+                reply(w)
         st["apply"] += time.time() - ta
 
     def serve(w, kind, wver):
@@ -175,60 +239,51 @@ def run_parameter_server(op, server):
             reply(w)
         return True
 
-    if dist.get_backend() == "nccl":
-        # RCCL: one posted header receive per worker, polled; a push's payload receives stay in flight
-        # while other workers' requests are served and earlier pushes are applied
-        req = {w: dist.irecv(hdr[w], src=w) for w in workers}
-        inflight = {}
-        while st["done"] < len(workers):
-            progressed = False
-            for w in workers:
-                r = req.get(w)
-                if r is None or not r.is_completed():
-                    continue
-                progressed = True
-                r.wait()
-                kind, wver = int(hdr[w][0].item()), int(hdr[w][1].item())
-                if kind == K_PUSH:
-                    inflight[w] = ([dist.irecv(b, src=w) for b in bufs(w)], wver)
-                    req[w] = None                 # re-posted once the update is applied
-                    continue
-                req[w] = dist.irecv(hdr[w], src=w) if serve(w, kind, wver) else None
-            for w in list(inflight):
-                reqs, wver = inflight[w]
-                if not all(x.is_completed() for x in reqs):
-                    continue
-                progressed = True
-                for x in reqs:
-                    x.wait()
-                del inflight[w]
-                apply(w, wver)
-                req[w] = dist.irecv(hdr[w], src=w)
-            if not progressed:
-                ti = time.time()
-                time.sleep(0.0002)
-                st["idle"] += time.time() - ti
-    else:
-        # gloo: requests are served in arrival order with any-source header receives
-        any_hdr = _hdr(cdev)
-        while st["done"] < len(workers):
-            ti = time.time()
-            w = dist.recv(any_hdr, src=None)
-            st["idle"] += time.time() - ti
-            kind, wver = int(any_hdr[0].item()), int(any_hdr[1].item())
+    # ONE service loop for RCCL and gloo: a posted header receive per worker, polled; a push's payload receives
+    # stay in flight while other workers are served; completed payloads are applied together
+    threaded = dist.get_backend() != "nccl"
+    req = {w: _Posted(dist.irecv(hdr[w], src=w), threaded) for w in workers}
+    inflight = {}
+    while st["done"] < len(workers):
+        progressed = False
+        for w in workers:
+            r = req.get(w)
+            if r is None or not r.done():
+                continue
+            progressed = True
+            r.wait()
+            kind, wver = hdr[w].tolist()      # one device->host read per header
             if kind == K_PUSH:
-                for b in bufs(w):
-                    dist.recv(b, src=w)
-                apply(w, wver)
-            else:
-                serve(w, kind, wver)
+                inflight[w] = ([_Posted(dist.irecv(b, src=w), threaded) for b in bufs(w)], wver)
+                req[w] = None                 # re-posted once the update is applied
+                continue
+            req[w] = _Posted(dist.irecv(hdr[w], src=w), threaded) if serve(w, kind, wver) else None
+        ready = [w for w, (rs, _) in inflight.items() if all(x.done() for x in rs)]
+        if ready:
+            progressed = True
+            batch = []
+            for w in ready:
+                rs, wver = inflight.pop(w)
+                for x in rs:
+                    x.wait()
+                batch.append((w, wver))
+            apply_batch(batch)
+            for w, _ in batch:
+                req[w] = _Posted(dist.irecv(hdr[w], src=w), threaded)
+        if not progressed:
+            ti = time.time()
+            os.sched_yield()
+            st["idle"] += time.time() - ti
+    server.store = store
     updates = st["updates"]
     stale_sum, stale_max = st["stale_sum"], st["stale_max"]
     t_apply, t_idle = st["apply"], st["idle"]
     dt = time.time() - t0
     stats = {"ps": ps, "updates": updates, "mean_staleness": stale_sum / max(updates, 1), "max_staleness": stale_max,
              "updates_per_sec": updates / max(dt, 1e-9), "apply_s": round(t_apply, 3), "idle_s": round(t_idle, 3),
-             "wall_s": round(dt, 3), "store_wait_s": 0.0, "wire": str(wire).replace("torch.", "")}
+             "wall_s": round(dt, 3), "store_wait_s": round(timed_store.wait_s, 6), "store_calls": timed_store.calls,
+             "applies": st["applies"], "batched_max": st["batched_max"], "wire": str(wire).replace("torch.", ""),
+             "poll": "threaded-gloo" if threaded else "rccl-is_completed"}
     store.set("%s/ps%d/stats" % (_PREFIX, ps), json.dumps(stats))
     out_dir = os.environ.get("MDTF_BENCH_OUT")
     if out_dir:
@@ -274,10 +329,11 @@ class AsyncWorker(object):
                                           device=dev) for g in self.space.groups}
         self.steps_done = 0
 
-    def _send_hdr(self, kind):
+    def _send_hdr(self, kind, version=None):
+        version = self.version if version is None else version
         for p, pr in enumerate(self.ps_ranks):
             self._h[p][0] = kind
-            self._h[p][1] = self.version[p]
+            self._h[p][1] = version[p]
             dist.send(self._h[p], dst=pr)
 
     def _post_reply(self, into_staging):
@@ -299,9 +355,10 @@ class AsyncWorker(object):
             for g in self.space.groups:
                 (g.shadow if g.shadow is not None else g.master).copy_(self._stage[id(g)])
 
-    def _push(self):
-        """Cast this step's gradients onto the wire buffers and send them (header first) to every PS."""
-        self._send_hdr(K_PUSH)
+    def _push(self, version):
+        """Cast this step's gradients onto the wire buffers and send them (header first) to every PS, labelled
+        with ``version``: the PS versions of the weights forward/backward ran on."""
+        self._send_hdr(K_PUSH, version)
         for g in self.space.groups:
             self._wire[id(g)].copy_(g.grad)
         reqs = []
@@ -356,6 +413,7 @@ class AsyncWorker(object):
             out["loss"].backward()
             from ..ops import conv as _conv
             _conv.join_side_streams()
+            used = list(self.version)         # the weights this gradient was computed on
             if pending is not None:
                 for r in pending[0]:
                     r.wait()
@@ -364,7 +422,7 @@ class AsyncWorker(object):
             if step >= self.total_step:
                 pending = None
                 break
-            pending = (self._push(), self._post_reply(True))
+            pending = (self._push(used), self._post_reply(True))
             self.steps_done += 1
             last = out["loss"]
             if self.steps_done % 10 == 0:

@@ -39,7 +39,8 @@ import time
 import torch
 
 _RNG = {}
-LAST_DRAIN = [None]     # how the last capture drained the RCCL watchdog: "recorder" | "fallback" (tests)
+LAST_DRAIN = [None]     # how the last capture drained the RCCL watchdog: "recorder" | "refused" (tests)
+LAST_DRAIN_POLLS = [0]  # recorder polls the last drain needed before every eager work had retired (tests)
 
 
 def env_enabled():
@@ -56,51 +57,74 @@ def rng_offset_tensor(device):
     return t
 
 
-def _active_comm_works():
-    """RCCL works the process groups' watchdog threads still hold (flight-recorder entries not yet
-    retired), or None when the recorder is unavailable or disabled."""
+_CAPTURED_IDS = set()   # flight-recorder ids of collectives recorded inside a capture (never retired)
+
+
+def _recorder_entries():
+    """Every flight-recorder entry of the process groups (retired ones included), or None when the
+    recorder is unavailable or disabled (``TORCH_FR_BUFFER_SIZE`` 0)."""
     try:
         import json
         from torch._C._distributed_c10d import _dump_nccl_trace_json
-        d = json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=True))
-        every = json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=False))
+        d = json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=False))
     except (ImportError, RuntimeError, ValueError, TypeError):
         return None
-    if not every.get("entries"):
-        return None                       # recorder disabled (buffer size 0) or nothing ever issued
-    return len(d.get("entries", []))
+    ents = d.get("entries")
+    if ents is None or (ents and "retired" not in ents[0]):
+        return None
+    return ents
+
+
+def _unretired(ents, watermark):
+    """Entries issued eagerly before the drain (record id <= watermark) the watchdog still holds."""
+    return [e for e in ents if e.get("record_id", -1) <= watermark and e.get("record_id") not in _CAPTURED_IDS
+            and not e.get("retired", False)]
 
 
 def _drain_comm_watchdog(timeout_s=60.0):
-    """Wait, on a state and not on a clock, until the RCCL watchdog has retired every eager work.
+    """Wait, on the flight recorder's ``retired`` state and not on a clock, until the RCCL watchdog has
+    dropped every eager work.  Returns the record-id watermark (None: not an RCCL job).
 
-    A ProcessGroupNCCL watchdog thread polls the completion event of each work issued OUTSIDE graph
-    capture until it retires it (works issued during capture are never handed to it).  A poll that
-    lands while this thread is capturing raced the capture and intermittently aborted the process
-    (the RCCL capture test).  So: drain the device and the warm-up works, then read the flight
-    recorder's active entries (``TORCH_FR_BUFFER_SIZE`` is set by :class:`mdtf.cluster.Server`) until
-    none are left — after that the watchdog has nothing to query during capture.  Without a
-    recorder the old bounded wait is the fallback."""
+    A ProcessGroupNCCL watchdog thread polls the end event of each work issued OUTSIDE capture until it
+    retires it; works issued during capture are never handed to it.  A watchdog event query that lands
+    while this thread captures raced the capture (the intermittent abort of the RCCL capture test).  The
+    dump's ``time_discovered_completed`` (what ``onlyActive`` filters on) is set by the dump itself, so
+    "no active entries" says nothing about the watchdog; ``retired`` is set only when the watchdog removed
+    the work from its list.  Entries recorded by an earlier capture never retire and are excluded.
+    Without a recorder there is no state to wait on: refuse to capture (the caller stays eager)."""
     try:
         import torch.distributed as dist
         if not (dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"):
-            return
+            return None
     except (RuntimeError, ValueError):
-        return
+        return None
     torch.cuda.synchronize()
-    n = _active_comm_works()
-    if n is None:
-        LAST_DRAIN[0] = "fallback"
-        time.sleep(0.5)
-        return
+    ents = _recorder_entries()
+    if ents is None:
+        LAST_DRAIN[0] = "refused"
+        raise RuntimeError("RCCL flight recorder unavailable (TORCH_FR_BUFFER_SIZE=0?): cannot prove the "
+                           "watchdog idle, refusing to capture collectives")
+    watermark = max([e.get("record_id", -1) for e in ents] or [-1])
     LAST_DRAIN[0] = "recorder"
     deadline = time.time() + timeout_s
-    while n:
+    polls = 0
+    while _unretired(ents, watermark):
         if time.time() > deadline:
-            raise RuntimeError("RCCL watchdog still holds %d completed works after %.0f s; refusing to capture"
-                               % (n, timeout_s))
-        time.sleep(0.005)
-        n = _active_comm_works()
+            raise RuntimeError("RCCL watchdog still holds %d works after %.0f s; refusing to capture"
+                               % (len(_unretired(ents, watermark)), timeout_s))
+        os.sched_yield()
+        polls += 1
+        ents = _recorder_entries() or []
+    LAST_DRAIN_POLLS[0] = polls
+    return watermark
+
+
+def _note_captured(watermark):
+    """Remember the ids the capture recorded: they never retire, later drains skip them."""
+    if watermark is None:
+        return
+    ents = _recorder_entries() or []
+    _CAPTURED_IDS.update(e["record_id"] for e in ents if e.get("record_id", -1) > watermark)
 
 
 def _leaves(x, out):
@@ -310,11 +334,12 @@ class StepGraph(object):
         cap_ctx = RunContext(feed_dict=fd, session=ctx.session)
         cap_ctx.cache.update(cache)
         torch.cuda.synchronize(dev)
-        _drain_comm_watchdog()
+        watermark = _drain_comm_watchdog()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             rng.add_(1)
             op._run_step(cap_ctx, step, dyn=self.dyn)
+        _note_captured(watermark)
         self.graph = g
         for p in op.programs:
             self._outputs[id(p)] = cap_ctx.cache[("prog", id(p))]

@@ -68,6 +68,13 @@ class Optimizer(object):
         """The per-step ``lr_t`` the kernel applies (Adam folds its bias correction in)."""
         return lr
 
+    def update_multi(self, target, grads, steps, grad_scale=1.0):
+        """Apply ``grads`` (<= 8, in order) to ``target`` as consecutive updates at global ``steps``, in ONE
+        fused pass (async parameter server).  Default: one ``update`` per gradient."""
+        for g, st in zip(grads, steps):
+            target.grad.copy_(g)
+            self.update(target, self.learning_rate(st), grad_scale, st)
+
     def _wd(self, target):
         return self.weight_decay if target.decay else 0.0
 
@@ -86,6 +93,11 @@ class GradientDescentOptimizer(Optimizer):
     def update(self, target, lr, grad_scale, step, dyn=None):
         K.sgd_(target.master, target.grad, target.shadow, lr, grad_scale, self._wd(target), dyn=dyn)
 
+    def update_multi(self, target, grads, steps, grad_scale=1.0):
+        lrs = [self.learning_rate(s) for s in steps]
+        K.apply_multi_("sgd", target.master, grads, None, None, target.shadow, lrs, lrs, grad_scale=grad_scale,
+                       weight_decay=self._wd(target))
+
 
 class MomentumOptimizer(Optimizer):
     def __init__(self, learning_rate, momentum=0.9, use_locking=False, name="Momentum", use_nesterov=False,
@@ -97,6 +109,12 @@ class MomentumOptimizer(Optimizer):
     def update(self, target, lr, grad_scale, step, dyn=None):
         K.momentum_(target.master, target.grad, target.state("momentum"), target.shadow, lr, self.momentum,
                     grad_scale, self._wd(target), self.use_nesterov, dyn=dyn)
+
+    def update_multi(self, target, grads, steps, grad_scale=1.0):
+        lrs = [self.learning_rate(s) for s in steps]
+        K.apply_multi_("momentum", target.master, grads, target.state("momentum"), None, target.shadow, lrs, lrs,
+                       momentum=self.momentum, grad_scale=grad_scale, weight_decay=self._wd(target),
+                       flag=self.use_nesterov)
 
     def slot_checkpoint_names(self):
         return [("momentum", "Momentum")]
@@ -117,6 +135,13 @@ class AdamOptimizer(Optimizer):
 
     def step_size(self, lr, step):
         return K.adam_lr_t(lr, self.beta1, self.beta2, step + 1, self.bias_correction)
+
+    def update_multi(self, target, grads, steps, grad_scale=1.0):
+        lrs = [self.learning_rate(s) for s in steps]
+        lrts = [self.step_size(lr, s) for lr, s in zip(lrs, steps)]
+        K.apply_multi_("adam", target.master, grads, target.state("m"), target.state("v"), target.shadow, lrs, lrts,
+                       beta1=self.beta1, beta2=self.beta2, epsilon=self.epsilon, grad_scale=grad_scale,
+                       weight_decay=self._wd(target), flag=self.decoupled)
 
     def slot_checkpoint_names(self):
         return [("m", "Adam"), ("v", "Adam_1")]
@@ -166,6 +191,9 @@ class SyncReplicasOptimizer(Optimizer):
 
     def update(self, target, lr, grad_scale, step, dyn=None):
         self._opt.update(target, lr, grad_scale, step, dyn=dyn)
+
+    def update_multi(self, target, grads, steps, grad_scale=1.0):
+        self._opt.update_multi(target, grads, steps, grad_scale)
 
     def step_size(self, lr, step):
         return self._opt.step_size(lr, step)

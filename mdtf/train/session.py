@@ -21,9 +21,17 @@ Recovery (TF's ``_RecoverableSession``): a ``run`` that raises ``mdtf.errors.Abo
 ``UnavailableError`` (or a transient store failure, ``mdtf.errors.as_recoverable``) re-creates the
 session in this process — captured step graphs released, the latest checkpoint restored (else the
 chief's broadcast state), hooks' ``after_create_session`` called again — and retries the step, up to
-``max_recoveries`` times.  With several replicas every one of them must see the error (a collective
-restore); a single replica's failure is handled one level up, by the job supervisor's restart
-(``mdtf.cluster.health.supervise``).
+``max_recoveries`` times.
+
+With several replicas the restore is a collective, so the replicas first AGREE, at a step boundary, that
+one of them failed (reference ``distribute_train.py:169-180``: TF re-creates every worker's session when
+a PS restart aborts them).  Every ``run`` does, on every replica and in the same place:
+``before_run`` hooks -> one host all-reduce(MAX) of a "recovery needed" bit over a gloo group of the
+replicas -> the step -> ``after_run`` hooks.  A recoverable error raised by a hook on ONE replica (the
+step's collectives have all been issued, or none of them) is held and its bit set at the next agreement;
+then every replica re-creates its session from the chief's latest checkpoint in process and they continue
+from the same global step.  An error raised inside the step itself (mid-collective) cannot be agreed on
+safely and is re-raised, for the job supervisor's restart (``mdtf.cluster.health.supervise``).
 """
 import os
 import time
@@ -148,6 +156,8 @@ class MonitoredSession(Session):
         self.server = server
         self._stop = False
         self.restored_from = None
+        self._agree_pg = None          # gloo group of the replicas for the recovery agreement (world > 1)
+        self._pending = None           # recoverable error a hook raised, held for the next agreement
         for h in self._hooks:
             h.begin()
         self._create()
@@ -179,6 +189,8 @@ class MonitoredSession(Session):
         from .saver import Saver, latest_checkpoint
         distributed = dist.is_available() and dist.is_initialized() and pg is not None
         multi = distributed and dist.get_world_size(pg) > 1
+        if multi and self._agree_pg is None and self.max_recoveries > 0:
+            self._agree_pg = self._agreement_group(pg)
         # the chief picks the checkpoint; EVERY replica restores it (each takes its own
         # optimizer-state shard in sharded mode), so no restored state is broadcast
         ckpt = None
@@ -222,6 +234,24 @@ class MonitoredSession(Session):
             op.reducer.load_shards_from_master()
 
     @staticmethod
+    def _agreement_group(pg):
+        """A gloo (host) group over the same replicas: the per-step agreement never touches the device
+        stream, so it neither syncs the host with the GPU nor enters a captured step graph."""
+        import torch.distributed as dist
+        if dist.get_backend(pg) == "gloo":
+            return pg
+        ranks = list(range(dist.get_world_size())) if pg is dist.group.WORLD else \
+            [dist.get_global_rank(pg, i) for i in range(dist.get_world_size(pg))]
+        return dist.new_group(ranks, backend="gloo", use_local_synchronization=True)
+
+    def _agree(self, bad):
+        """All-reduce(MAX) of this replica's "recovery needed" bit: True if any replica needs it."""
+        import torch.distributed as dist
+        t = torch.tensor([1 if bad else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._agree_pg)
+        return bool(t.item())
+
+    @staticmethod
     def _visible_everywhere(ckpt, pg):
         """All-reduce(MIN) of 'this replica sees <ckpt>.index' over the group."""
         import os
@@ -254,6 +284,8 @@ class MonitoredSession(Session):
     # -- running -----------------------------------------------------------
     def run(self, fetches, feed_dict=None, options=None, run_metadata=None):
         from .. import errors
+        if self._agree_pg is not None:
+            return self._run_agreed(fetches, feed_dict)
         while True:
             try:
                 return self._run_once(fetches, feed_dict)
@@ -266,6 +298,45 @@ class MonitoredSession(Session):
                     type(err).__name__, err, self.recoveries, self.max_recoveries))
                 self._recreate()
 
+    def _run_agreed(self, fetches, feed_dict):
+        """Multi-replica run: hooks, step-boundary agreement, step (see the module docstring)."""
+        from .. import errors
+        while True:
+            if self._stop:
+                raise RuntimeError("Run called even after should_stop requested.")
+            pre = None
+            try:
+                pre = self._before_run(fetches, feed_dict)
+            except Exception as e:  # noqa: BLE001 - classified below
+                err = errors.as_recoverable(e)
+                if err is None:
+                    raise
+                self._pending = self._pending or err
+            if self._agree(self._pending is not None):
+                err = self._pending or errors.AbortedError(message="a peer replica requested session recovery")
+                self._pending = None
+                if self.recoveries >= self.max_recoveries:
+                    raise err
+                self.recoveries += 1
+                logger.warn("replica recovery agreed (%s: %s); re-creating the session from the chief's checkpoint "
+                            "(recovery %d of %d)" % (type(err).__name__, err, self.recoveries, self.max_recoveries))
+                self._recreate()
+                continue                     # retry this run on the restored state
+            rc, extra, feed = pre
+            results = self.run_raw(self._all_fetches(fetches, extra), feed)
+            try:
+                self._after_run(rc, extra, results)
+            except Exception as e:  # noqa: BLE001 - classified below
+                err = errors.as_recoverable(e)
+                if err is None:
+                    raise
+                self._pending = err          # every replica finished this step's collectives: agree next run
+                logger.warn("%s after the step on this replica; recovery is agreed at the next step boundary"
+                            % type(err).__name__)
+            if rc.stop_requested:
+                self._stop = True
+            return results["__user__"]
+
     def _recreate(self):
         """Drop per-session device state and create again: restore the latest checkpoint, re-broadcast."""
         if torch.cuda.is_available():
@@ -276,9 +347,7 @@ class MonitoredSession(Session):
         for h in self._hooks:
             h.after_create_session(self, None)
 
-    def _run_once(self, fetches, feed_dict=None):
-        if self._stop:
-            raise RuntimeError("Run called even after should_stop requested.")
+    def _before_run(self, fetches, feed_dict):
         args = H.SessionRunArgs(fetches, feed_dict)
         rc = H.SessionRunContext(args, self)
         extra = {}
@@ -289,15 +358,28 @@ class MonitoredSession(Session):
                 extra[h] = req.fetches
                 if req.feed_dict:
                     feed.update(req.feed_dict)
+        return rc, extra, feed
+
+    @staticmethod
+    def _all_fetches(fetches, extra):
         all_fetches = {"__user__": fetches}
         for i, (h, f) in enumerate(extra.items()):
             all_fetches["__hook%d__" % i] = f
-        results = self.run_raw(all_fetches, feed)
-        for i, h in enumerate(self._hooks):
+        return all_fetches
+
+    def _after_run(self, rc, extra, results):
+        for h in self._hooks:
             key = None
             if h in extra:
                 key = "__hook%d__" % list(extra).index(h)
             h.after_run(rc, H.SessionRunValues(results.get(key) if key else None))
+
+    def _run_once(self, fetches, feed_dict=None):
+        if self._stop:
+            raise RuntimeError("Run called even after should_stop requested.")
+        rc, extra, feed = self._before_run(fetches, feed_dict)
+        results = self.run_raw(self._all_fetches(fetches, extra), feed)
+        self._after_run(rc, extra, results)
         if rc.stop_requested:
             self._stop = True
         return results["__user__"]

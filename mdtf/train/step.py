@@ -374,6 +374,8 @@ def train_ops():
 def release_graphs():
     for op in _TRAIN_OPS:
         op.release_graph()
+    from ..ops import conv as _conv
+    _conv._WT.clear()               # the filter-transpose cache holds the released space's shadows
 
 
 def reset():

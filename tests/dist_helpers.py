@@ -145,3 +145,41 @@ def hidden_ckpt_restore_worker(rank, world, port, out_dir):
         json.dump({"step": step, "weights": w, "adam_m": m, "restored": sess.restored_from}, f)
     sess.close()
     server.shutdown()
+
+
+def recovery_worker(rank, world, port, steps, out_dir, fault_step=None, fault_task="worker:1", mode="abort"):
+    """Sync replicas under MonitoredTrainingSession with a chief checkpoint every 2 steps; ``fault_task``
+    raises an in-process AbortedError after ``fault_step`` (one replica only): every replica must agree on
+    the recovery, restore the chief's checkpoint in process and finish at the same global step."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    import mdtf
+    from mdtf.cluster import Server
+    from mdtf.cluster.health import FaultInjectionHook
+    from mdtf.train import hooks as H
+    from mdtf.train import variables as V
+    server = Server.from_env(backend="gloo")
+    batch = 4
+    Lin, MSE, xs, ys, x_ph, y_ph, Tower, Net = _linear_setup(rank, world, batch)
+    base = mdtf.train.MomentumOptimizer(0.1, 0.9)
+    tg = []
+    Tower(Net(Lin()), "tower_0/", tg, x_ph, y_ph, MSE(), base, batch_size=batch).process()
+    opt = mdtf.train.SyncReplicasOptimizer(base, replicas_to_aggregate=world, total_num_replicas=world)
+    gs = mdtf.train.get_or_create_global_step()
+    op = opt.apply_gradients(Tower.average_gradients(tg), global_step=gs)
+    hooks = [H.StopAtStepHook(last_step=steps), opt.make_session_run_hook(rank == 0)]
+    if fault_step is not None:
+        hooks.append(FaultInjectionHook("worker", rank, step=fault_step, task=fault_task, mode=mode))
+    md = os.path.join(out_dir, "model")
+    lo, hi = rank * batch, (rank + 1) * batch
+    runs = 0
+    with mdtf.train.MonitoredTrainingSession(is_chief=rank == 0, checkpoint_dir=md, save_checkpoint_steps=2,
+                                             hooks=hooks, log_step_count_steps=0, server=server) as sess:
+        while not sess.should_stop():
+            sess.run(op, feed_dict={x_ph: xs[lo:hi], y_ph: ys[lo:hi]})
+            runs += 1
+        rec = sess.recoveries
+    w = {v.name: v.master.tolist() for v in V.get_store().trainable_variables()}
+    with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
+        json.dump({"step": gs.value(), "recoveries": rec, "runs": runs, "weights": w}, f)
+    server.shutdown()

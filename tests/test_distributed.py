@@ -243,3 +243,26 @@ def test_restore_when_checkpoint_visible_only_on_chief(tmp_path):
             assert torch.allclose(torch.tensor(vals), r.get_tensor(name).float().reshape(torch.tensor(vals).shape))
     assert res[0]["adam_m"] == res[1]["adam_m"]
     assert any(abs(x) > 0 for x in res[0]["adam_m"])
+
+
+def test_coordinated_recovery_one_replica_aborts(tmp_path):
+    """ONE of two sync replicas raises AbortedError after step 5 (reference distribute_train.py:169-180: the
+    recoverable MonitoredTrainingSession).  Both replicas agree on the recovery at the next step boundary,
+    re-create their sessions in process from the chief's step-4 checkpoint, and finish at the same global
+    step with the weights of an uninterrupted run."""
+    sys.path.insert(0, os.path.dirname(__file__))
+    import dist_helpers
+    res = {}
+    for tag, fault in (("ref", None), ("run", 5)):
+        d = tmp_path / tag
+        d.mkdir()
+        mp.start_processes(dist_helpers.recovery_worker, args=(2, free_port(), 8, str(d), fault),
+                           nprocs=2, join=True, start_method="spawn")
+        res[tag] = [json.load(open(str(d / ("rank%d.json" % r)))) for r in range(2)]
+    ref, run = res["ref"], res["run"]
+    assert [r["step"] for r in run] == [8, 8] and [r["recoveries"] for r in run] == [1, 1]
+    assert [r["recoveries"] for r in ref] == [0, 0]
+    assert run[0]["runs"] == run[1]["runs"] == ref[0]["runs"] + 1     # step 5 re-runs from the step-4 state
+    for k, w in ref[0]["weights"].items():
+        for r in run:
+            assert torch.allclose(torch.tensor(r["weights"][k]), torch.tensor(w), atol=1e-6), k

@@ -223,3 +223,37 @@ def test_hip_graph_captures_rccl_collectives(mode, monkeypatch):
         from mdtf.train import step as S
         S.release_graphs()                 # the captured RCCL collectives go before their communicator
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_drain_waits_for_watchdog_retirement(monkeypatch):
+    """Capture starts only after the RCCL watchdog RETIRED every eager work (flight-recorder ``retired``),
+    not merely after the device finished it: an eager all-reduce is still held by the watchdog right after
+    synchronize(), and the drain returns only once it is gone."""
+    _gpu()
+    import socket
+    import torch.distributed as dist
+    from mdtf.train import graph as G
+    monkeypatch.setenv("TORCH_FR_BUFFER_SIZE", "2000")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    try:
+        t = torch.ones(1 << 16, device="cuda")
+        for _ in range(3):
+            dist.all_reduce(t)
+        torch.cuda.synchronize()
+        ents = G._recorder_entries()
+        assert ents, "flight recorder must be on for the drain"
+        wm = max(e["record_id"] for e in ents)
+        held_before = len(G._unretired(ents, wm))
+        got = G._drain_comm_watchdog(timeout_s=30.0)
+        assert got == wm and G.LAST_DRAIN[0] == "recorder"
+        assert G._unretired(G._recorder_entries(), wm) == []
+        # the watchdog loop sleeps between polls, so right after synchronize() it normally still held the works
+        # and the drain had to poll; when it had already retired them the drain returns at once
+        assert held_before == 0 or G.LAST_DRAIN_POLLS[0] > 0
+    finally:
+        dist.destroy_process_group()
