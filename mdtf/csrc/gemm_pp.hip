@@ -61,6 +61,16 @@ struct GemmArgs {
   float* Cf;
   long long ldcf;
   int atomic;                // 1: fp32 atomics (split-K); 0: Cf += result (one writer per element)
+  // segmented operands (q|k|v as three matrices, no concatenated copy): nseg segments of seg_cols, segment s of
+  // B at bseg[s] (row stride ldb), split along the output columns (fwd) or the reduction (dgrad); bias, Cf and
+  // dbias are split the same way along the output columns.  nseg = 1: bseg[0] = B.
+  int nseg, seg_cols;
+  const bf16_t* bseg[4];
+  const bf16_t* biasseg[4];
+  float* cfseg[4];
+  float* dbseg[4];           // wgrad: the column sums of B (dy: the bias gradient) are added here (null: none)
+  const bf16_t* act_pre;     // dgrad: C = acc * act'(act_pre) (the producer's activation backward), null: none
+  int act_bwd;
 };
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
@@ -70,6 +80,20 @@ __device__ __forceinline__ float act_fwd(float v, int act) {
     return v * __builtin_amdgcn_rcpf(1.f + __expf(-u2));
   }
   return v;
+}
+
+// its derivative at the pre-activation x: relu [x > 0]; gelu s + 2 x s (1 - s) u'(x), s = sigmoid(2u)
+__device__ __forceinline__ float act_grad(float x, int act) {
+  if (act == 1) return x > 0.f ? 1.f : 0.f;
+  const float s = __builtin_amdgcn_rcpf(1.f + __expf(-1.5957691216f * (x + 0.044715f * x * x * x)));
+  return s + 2.f * x * s * (1.f - s) * 0.7978845608f * (1.f + 0.134145f * x * x);
+}
+
+__device__ __forceinline__ int seg_of(int col, int seg_cols, int nseg) {
+  int s = 0;
+#pragma unroll
+  for (int i = 1; i < 4; ++i) s += (i < nseg && col >= i * seg_cols) ? 1 : 0;
+  return s;
 }
 
 // LDS-DMA of 16 B per lane: LDS destination = m0 (wave-uniform) + 16 * lane, source = rsrc + voff + soff.
@@ -94,38 +118,47 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 // 32-B block swizzle of a [64 k][W cols] image (row pitch 2W bytes) for the transposed fragment reads:
-// the 8 rows one 32-lane half reads ({0-3, 8-11} + 16 h, and +4) land in 8 distinct 32-B bank slots
+// the 8 rows one 32-lane half reads ({0-3, 8-11} + 16 h, and +4) land in 8 distinct 32-B bank slots.
+// pitch 256: 8 blocks per bank row; 128: two rows per bank row; 192: rows advance 6 slots, so only rows
+// r and r+8 collide and one XOR bit separates them.
 template <int PITCH>
 __device__ __forceinline__ int trg(int row) {
-  if constexpr (PITCH >= 256) return (row & 3) | (((row >> 3) & 1) << 2);
+  if constexpr (PITCH % 256 == 0) return (row & 3) | (((row >> 3) & 1) << 2);
+  else if constexpr (PITCH == 192) return (row >> 3) & 1;
   else return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
 }
 
-// One operand's four-unit pipeline geometry.  W = rows (or cols, TR) per unit image = tile / 2.
+// One LDS unit image: W = rows (or, TR, columns) = half of the tile's side, 64 k deep.
 template <int W, bool TR>
 struct Unit {
   static constexpr int BYTES = W * 128;            // 64 k x W x 2 B
-  static constexpr int PER_WAVE = W / 64;          // DMA wave-instructions per wave per unit
+  static constexpr int NI = W / 8;                 // 1-KiB DMA wave-instructions that fill it
   static constexpr int PITCH = TR ? 2 * W : 128;   // image row pitch (bytes)
+  // instructions issued by a wave of group G (wave w issues w, w + 8, ...: equal within a group)
+  template <int G>
+  static constexpr int per_wave() { return (NI - 4 * G + 7) / 8; }
 };
 
+// Tile geometry.  Eight waves = group G (M half) x 4 column strips; each wave owns (BM/2) x (BN/4).
+//   BM = 256: four quadrant phases per 64-deep K-tile, 2 LDS stages, unit-level DMA schedule;
+//   BM = 128: two k-substep phases per K-tile, 3 LDS stages, whole-tile DMA one tile further ahead.
 template <int BM, int BN, bool ATR, bool BTR, int EPI>
 __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
-  constexpr int WCN = BN / 64;             // waves of a group along N (2 or 4)
-  constexpr int WRN = 4 / WCN;             // along M
-  constexpr int RW = BM / 2 / WRN;         // output rows per wave
-  constexpr int FM = RW / 16, FMH = FM / 2;   // row fragments per wave / per half
+  constexpr int RW = BM / 2, CW = BN / 4;
+  constexpr int FM = RW / 16, FN = CW / 16;
+  constexpr int FMH = FM / 2, FNL = (FN + 1) / 2;
   constexpr int WA = BM / 2, WB = BN / 2;
+  constexpr bool QUAD = BM == 256;
+  constexpr int STAGES = QUAD ? 2 : 3;
   using UA = Unit<WA, ATR>;
   using UB = Unit<WB, BTR>;
   constexpr int SLOT = 2 * UA::BYTES + 2 * UB::BYTES;
-  static_assert(FMH >= 1 && WCN * WRN == 4, "tile");
+  static_assert(FM >= 2 && FN >= 2 && CW % 16 == 0 && WA % 64 == 0 && WB % 8 == 0, "tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int G = wave >> 2, w4 = wave & 3;
-  const int wc = w4 % WCN, wrr = w4 / WCN;
+  const int G = wave >> 2, wc = wave & 3;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -135,64 +168,68 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
   const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<unsigned long long>(
       (__attribute__((address_space(3))) char*)smem));
   const i32x4_t ra = buffer_rsrc(a.A, a.bytes_a);
-  const i32x4_t rb = buffer_rsrc(a.B, a.bytes_b);
 
-  // ---- per-lane DMA source offsets (bytes, at k-tile 0 of this split) for this wave's share of each unit
-  // unit u: 0,1 = A halves (rows/cols m0 + u*WA ..), 2,3 = B halves
-  auto src_off = [&](bool tr, int w, long long ld, int base, int limit, int ii) -> unsigned {
+  // ---- per-lane DMA source offsets.  One VGPR per operand: instruction j of a wave and unit half u differ by a
+  // wave-uniform byte delta (soffset), because the swizzles depend only on row bits that those steps preserve.
+  // Rows past the operand (non-TR) fall past the buffer range by themselves and read zeros; columns past it
+  // (TR) are marked out of range, and the host only takes TR operands whose extent is a multiple of the tile.
+  auto src_off = [&](bool tr, int pitch, long long ld, int base, int limit, int ii) -> unsigned {
     const int off = ii * 1024 + lane * 16;          // byte offset inside the unit image
     if (!tr) {
       const int row = off >> 7, pc = (off >> 4) & 7;
       const int lc = pc ^ ((row >> 1) & 7);
-      const int r = base + row;
-      if (r >= limit) return kOOB;
-      return static_cast<unsigned>(((long long)r * ld + (long long)kt0 * 64 + lc * 8) * 2);
+      return static_cast<unsigned>(((long long)(base + row) * ld + (long long)kt0 * 64 + lc * 8) * 2);
     }
-    const int pitch = 2 * w;
     const int row = off / pitch, cb = off - row * pitch;
     const int pb = cb >> 5, half = (cb >> 4) & 1;
-    const int lb = pb ^ (pitch >= 256 ? trg<256>(row) : trg<128>(row));
-    const int col = base + lb * 16 + half * 8;
+    const int g = pitch % 256 == 0 ? trg<256>(row) : pitch == 192 ? trg<192>(row) : trg<128>(row);
+    const int col = base + (pb ^ g) * 16 + half * 8;
     if (col >= limit) return kOOB;
     return static_cast<unsigned>((((long long)kt0 * 64 + row) * ld + col) * 2);
   };
-  unsigned offA[2][UA::PER_WAVE], offB[2][UB::PER_WAVE];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-#pragma unroll
-    for (int j = 0; j < UA::PER_WAVE; ++j)
-      offA[u][j] = src_off(ATR, WA, a.lda, m0 + u * WA, a.M, j * 8 + wave);
-#pragma unroll
-    for (int j = 0; j < UB::PER_WAVE; ++j)
-      offB[u][j] = src_off(BTR, WB, a.ldb, n0 + u * WB, a.N, j * 8 + wave);
-  }
-  // per K-tile advance of the source (wave-uniform soffset)
-  const int stepA = ATR ? (int)(64 * a.lda * 2) : 128;
+  const unsigned vA = src_off(ATR, UA::PITCH, a.lda, m0, a.M, wave);
+  const unsigned vB = src_off(BTR, UB::PITCH, a.ldb, n0, a.N, wave);
+  // a 192-B-pitch transposed image: instruction j = 1 does not start on a row boundary -> its own offsets
+  constexpr bool B_J1 = BTR && UB::PITCH == 192;
+  const unsigned vB1 = B_J1 ? src_off(true, UB::PITCH, a.ldb, n0, a.N, 8 + wave) : 0u;
+  const int duA = ATR ? WA * 2 : (int)(WA * a.lda * 2);                   // unit half 1
+  const int djA = ATR ? (int)((8192 / UA::PITCH) * a.lda * 2) : (int)(64 * a.lda * 2);   // instruction j = 1
+  const int duB = BTR ? WB * 2 : (int)(WB * a.ldb * 2);
+  const int djB = BTR ? (B_J1 ? 0 : (int)((8192 / UB::PITCH) * a.ldb * 2)) : (int)(64 * a.ldb * 2);
+  const int stepA = ATR ? (int)(64 * a.lda * 2) : 128;     // per K-tile source advance
   const int stepB = BTR ? (int)(64 * a.ldb * 2) : 128;
 
-  // issue this wave's share of unit u (0,1 A; 2,3 B) of K-tile t into slot t & 1
+  // this wave's (group-uniform) share of unit u of K-tile t, into slot t % STAGES
   auto issue_unit = [&](int u, int t) {
-    const unsigned slot = lds0 + (t & 1) * SLOT;
+    const unsigned slot = lds0 + (t % STAGES) * SLOT;
     if (u < 2) {
+      const int cnt = G == 0 ? UA::template per_wave<0>() : UA::template per_wave<1>();
 #pragma unroll
-      for (int j = 0; j < UA::PER_WAVE; ++j)
-        dma16(ra, slot + u * UA::BYTES + (j * 8 + wave) * 1024, offA[u][j], t * stepA);
+      for (int j = 0; j < 2; ++j)
+        if (j < cnt) dma16(ra, slot + u * UA::BYTES + (j * 8 + wave) * 1024, vA, t * stepA + u * duA + j * djA);
     } else {
+      const int cnt = G == 0 ? UB::template per_wave<0>() : UB::template per_wave<1>();
+      // the segment this unit reads: by output column (transposed B) or by reduction index (dgrad)
+      const int seg = BTR ? (n0 + (u - 2) * WB) / a.seg_cols : ((kt0 + t) * 64) / a.seg_cols;
+      const i32x4_t rb = buffer_rsrc(a.bseg[seg], a.bytes_b);
+      const int sb = t * stepB + (u - 2) * duB - seg * a.seg_cols * 2;
 #pragma unroll
-      for (int j = 0; j < UB::PER_WAVE; ++j)
-        dma16(rb, slot + 2 * UA::BYTES + (u - 2) * UB::BYTES + (j * 8 + wave) * 1024, offB[u - 2][j], t * stepB);
+      for (int j = 0; j < 2; ++j)
+        if (j < cnt)
+          dma16(rb, slot + 2 * UA::BYTES + (u - 2) * UB::BYTES + (j * 8 + wave) * 1024, (B_J1 && j) ? vB1 : vB,
+                sb + j * djB);
     }
   };
+  // per-wave DMA instruction counts of the groups (compile time)
+  constexpr int CB0 = UB::template per_wave<0>(), CB1 = UB::template per_wave<1>();
+  constexpr int CT0 = 2 * UA::template per_wave<0>() + 2 * CB0, CT1 = 2 * UA::template per_wave<1>() + 2 * CB1;
 
-  // ---- fragment read addresses (bytes relative to a slot)
+  // ---- fragment reads (bytes relative to a slot)
   const int fr = lane & 15, fq = lane >> 4;
   const int q4 = (lane >> 2) & 3, p4 = lane & 3;
-  // this wave's A unit (its group's rows) and B unit (its column strip)
-  const int ua = G;
-  const int ub = (wc * 64) / WB;
-  const int a_row0 = wrr * RW;                // inside the A unit image
-  const int b_col0 = wc * 64 - ub * WB;       // inside the B unit image
-  const unsigned baseA = ua * UA::BYTES;
+  const int ub = wc >> 1;                       // the B unit holding this wave's column strip
+  const int b_col0 = (wc & 1) * CW;             // its first column inside that unit
+  const unsigned baseA = G * UA::BYTES;
   const unsigned baseB = 2 * UA::BYTES + ub * UB::BYTES;
 
   auto frag = [&](bool tr, int pitch, unsigned ubase, int r0, int s, const char* slotp) -> bf16x8_t {
@@ -203,7 +240,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
       return __builtin_bit_cast(bf16x8_t, v);
     }
     const int row = 32 * s + 8 * fq + q4;
-    const int g = pitch >= 256 ? trg<256>(row) : trg<128>(row);
+    const int g = pitch % 256 == 0 ? trg<256>(row) : pitch == 192 ? trg<192>(row) : trg<128>(row);
     const int blk = (r0 >> 4) ^ g;
     const char* p1 = slotp + ubase + row * pitch + blk * 32 + p4 * 8;
     const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p1);
@@ -211,148 +248,248 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
     const short8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8_t, f);
   };
+  auto fragA = [&](int i, int s, const char* slotp) { return frag(ATR, UA::PITCH, baseA, 16 * i, s, slotp); };
+  auto fragB = [&](int j, int s, const char* slotp) {
+    return frag(BTR, UB::PITCH, baseB, b_col0 + 16 * j, s, slotp);
+  };
 
-  float4v acc[FM][4];
+  float4v acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
-
-  // ---- DMA schedule.  Barrier numbering: group 0 passes b(2P) / b(2P+1) around the MFMAs of phase P
-  // (P = 4t + q), group 1 b(2P+1) / b(2P+2).  Reads of K-tile t: group 0 in phases 4t..4t+2, group 1 one
-  // barrier later; the B units of tile t are last read before b(8t+4), A half 0 before b(8t+5), A half 1
-  // before b(8t+6).  Tile t+1 reuses tile t-1's slots and is first read after b(8t+7).  Hence:
-  //   group 0 issues in phase 4t+q:  q0 B1(t+1)  q1 A0(t+1)  q2 A1(t+1)  q3 B0(t+2)
-  //   group 1 issues in phase 4t+q:  q0 A0(t+1)  q1 A1(t+1)  q2 B0(t+2)  q3 B1(t+2)
-  // and each wave waits for everything but its B0(t+2) (vmcnt) before b(8t+7): group 0 after the MFMAs
-  // of phase 4t+3, group 1 before its first barrier of that phase.
-  constexpr int UBW = UB::PER_WAVE;
-  // prologue: tile 0 whole, plus the units of tile 1 the schedule expects issued before tile 0's phases
+    for (int j = 0; j < FN; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+  // wgrad bias gradient: the column sums of B by an all-ones A fragment, in the waves of the first row tile's
+  // group 0 (each output column once per split)
+  const bool dsum = EPI == 1 && a.dbseg[0] != nullptr && tm == 0 && G == 0;
+  float4v accb[FN];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) issue_unit(u, 0);
-  if (T > 1) {
-    issue_unit(2, 1);
-    if (G == 1) issue_unit(3, 1);
-  }
-  if (T > 1) {
-    if (G == 0) wait_vmcnt<UBW>();
-    else wait_vmcnt<2 * UBW>();
+  for (int j = 0; j < FN; ++j) accb[j] = float4v{0.f, 0.f, 0.f, 0.f};
+  const short8 ones8 = {0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80};
+  const bf16x8_t ones = __builtin_bit_cast(bf16x8_t, ones8);
+
+  if constexpr (QUAD) {
+    // ---- DMA schedule (quadrant phases).  Barrier numbering: group 0 passes b(2P) / b(2P+1) around the MFMAs
+    // of phase P (P = 4t + q), group 1 b(2P+1) / b(2P+2).  Reads of K-tile t: group 0 in phases 4t..4t+2, group
+    // 1 one barrier later; the B units of tile t are last read before b(8t+4), A half 0 before b(8t+5), A half 1
+    // before b(8t+6).  Tile t+1 reuses tile t-1's slots and is first read after b(8t+7).  Hence:
+    //   group 0 issues in phase 4t+q:  q0 B1(t+1)  q1 A0(t+1)  q2 A1(t+1)  q3 B0(t+2)
+    //   group 1 issues in phase 4t+q:  q0 A0(t+1)  q1 A1(t+1)  q2 B0(t+2)  q3 B1(t+2)
+    // and each wave waits for everything but its B0(t+2) (vmcnt) before b(8t+7): group 0 after the MFMAs of
+    // phase 4t+3, group 1 before its first barrier of that phase.
+#pragma unroll
+    for (int u = 0; u < 4; ++u) issue_unit(u, 0);
+    if (T > 1) {
+      issue_unit(2, 1);
+      if (G == 1) issue_unit(3, 1);
+    }
+    if (T > 1) {
+      if (G == 0) wait_vmcnt<CB0>();
+      else wait_vmcnt<CB0 + CB1>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    barrier();
+    if (G == 1) barrier();
+
+    bf16x8_t fa[FMH][2], fb[FN][2];
+    for (int t = 0; t < T; ++t) {
+      const char* slotp = smem + (t & 1) * SLOT;
+      const bool n1 = t + 1 < T, n2 = t + 2 < T;
+      // ---------------- q0: A top + B left; MFMA top x left
+#pragma unroll
+      for (int i = 0; i < FMH; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) fa[i][s] = fragA(i, s, slotp);
+#pragma unroll
+      for (int j = 0; j < FNL; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) fb[j][s] = fragB(j, s, slotp);
+      if (n1) issue_unit(G == 0 ? 3 : 0, t + 1);
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < FMH; ++i)
+#pragma unroll
+          for (int j = 0; j < FNL; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[i][j], 0, 0, 0);
+      if (dsum) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = 0; j < FNL; ++j) accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], ones, accb[j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+      // ---------------- q1: B right; MFMA top x right
+#pragma unroll
+      for (int j = FNL; j < FN; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) fb[j][s] = fragB(j, s, slotp);
+      if (n1) issue_unit(G == 0 ? 0 : 1, t + 1);
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < FMH; ++i)
+#pragma unroll
+          for (int j = FNL; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[i][j], 0, 0, 0);
+      if (dsum) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = FNL; j < FN; ++j) accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], ones, accb[j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+      // ---------------- q2: A bottom; MFMA bottom x right
+#pragma unroll
+      for (int i = 0; i < FMH; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) fa[i][s] = fragA(FMH + i, s, slotp);
+      if (G == 0) {
+        if (n1) issue_unit(1, t + 1);
+      } else {
+        if (n2) issue_unit(2, t + 2);
+      }
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < FMH; ++i)
+#pragma unroll
+          for (int j = FNL; j < FN; ++j)
+            acc[FMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[FMH + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+      // ---------------- q3: no reads; MFMA bottom x left
+      if (G == 1) {
+        if (n2) wait_vmcnt<CB1>();
+        else wait_vmcnt<0>();
+        if (n2) issue_unit(3, t + 2);
+      } else {
+        if (n2) issue_unit(2, t + 2);
+      }
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < FMH; ++i)
+#pragma unroll
+          for (int j = 0; j < FNL; ++j)
+            acc[FMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[FMH + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (G == 0) {
+        if (n2) wait_vmcnt<CB0>();
+        else wait_vmcnt<0>();
+      }
+      barrier();
+    }
+    if (G == 0) barrier();
   } else {
-    wait_vmcnt<0>();
-  }
-  barrier();
-  if (G == 1) barrier();
+    // ---- DMA schedule (k-substep phases, 3 stages).  Phase P = 2t + s (s = k-substep); same barrier numbering.
+    // Tile t's reads end before b(4t+4); tile t+2 (slot of tile t-1, free after b(4t)) is issued whole by
+    // group 1 in phase 2t (after b(4t)) and by group 0 in phase 2t+1, and first read after b(4t+7).  Each wave
+    // waits for tile t+1 (everything but its tile-(t+2) instructions) before b(4t+3): group 1 before its first
+    // barrier of phase 2t+1, group 0 after that phase's MFMAs.
+#pragma unroll
+    for (int u = 0; u < 4; ++u) issue_unit(u, 0);
+    if (T > 1) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) issue_unit(u, 1);
+      if (G == 0) wait_vmcnt<CT0>();
+      else wait_vmcnt<CT1>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    barrier();
+    if (G == 1) barrier();
 
-  bf16x8_t fa[FMH][2], fb[4][2];
-  for (int t = 0; t < T; ++t) {
-    const char* slotp = smem + (t & 1) * SLOT;
-    const bool n1 = t + 1 < T, n2 = t + 2 < T;
-    // ---------------- phase q0: A top + B left; MFMA top x left
+    bf16x8_t fa[FM], fb[FN];
+    for (int t = 0; t < T; ++t) {
+      const char* slotp = smem + (t % 3) * SLOT;
+      const bool n2 = t + 2 < T;
 #pragma unroll
-    for (int i = 0; i < FMH; ++i)
+      for (int s = 0; s < 2; ++s) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) fa[i][s] = frag(ATR, UA::PITCH, baseA, a_row0 + 16 * i, s, slotp);
+        for (int i = 0; i < FM; ++i) fa[i] = fragA(i, s, slotp);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < FN; ++j) fb[j] = fragB(j, s, slotp);
+        if (s == 1 - G && n2) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) fb[j][s] = frag(BTR, UB::PITCH, baseB, b_col0 + 16 * j, s, slotp);
-    if (n1) issue_unit(G == 0 ? 3 : 0, t + 1);
-    barrier();
-    __builtin_amdgcn_s_setprio(1);
+          for (int u = 0; u < 4; ++u) issue_unit(u, t + 2);
+        }
+        if (s == 1 && G == 1) {
+          if (n2) wait_vmcnt<CT1>();
+          else wait_vmcnt<0>();
+        }
+        barrier();
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int i = 0; i < FMH; ++i)
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        if (dsum) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    barrier();
-    // ---------------- phase q1: B right; MFMA top x right
-#pragma unroll
-    for (int j = 2; j < 4; ++j)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) fb[j][s] = frag(BTR, UB::PITCH, baseB, b_col0 + 16 * j, s, slotp);
-    if (n1) issue_unit(G == 0 ? 0 : 1, t + 1);
-    barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < FMH; ++i)
-#pragma unroll
-        for (int j = 2; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    barrier();
-    // ---------------- phase q2: A bottom; MFMA bottom x right
-#pragma unroll
-    for (int i = 0; i < FMH; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) fa[i][s] = frag(ATR, UA::PITCH, baseA, a_row0 + 16 * (FMH + i), s, slotp);
-    if (G == 0) {
-      if (n1) issue_unit(1, t + 1);
-    } else {
-      if (n2) issue_unit(2, t + 2);
+          for (int j = 0; j < FN; ++j) accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], ones, accb[j], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        if (s == 1 && G == 0) {
+          if (n2) wait_vmcnt<CT0>();
+          else wait_vmcnt<0>();
+        }
+        barrier();
+      }
     }
-    barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < FMH; ++i)
-#pragma unroll
-        for (int j = 2; j < 4; ++j)
-          acc[FMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[FMH + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    barrier();
-    // ---------------- phase q3: no reads; MFMA bottom x left
-    if (G == 1) {
-      if (n2) wait_vmcnt<UBW>();
-      else wait_vmcnt<0>();
-      if (n2) issue_unit(3, t + 2);
-    } else {
-      if (n2) issue_unit(2, t + 2);
-    }
-    barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < FMH; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[FMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[FMH + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    if (G == 0) {
-      if (n2) wait_vmcnt<UBW>();
-      else wait_vmcnt<0>();
-    }
-    barrier();
+    if (G == 0) barrier();
   }
-  if (G == 0) barrier();
 
   // ---- epilogue: lane holds C[row][col .. col+3] for each (i, j)
-  const int rbase = m0 + G * (BM / 2) + wrr * RW + fr;
-  const int cbase = n0 + wc * 64 + 4 * fq;
+  const int rbase = m0 + G * (BM / 2) + fr;
+  const int cbase = n0 + wc * CW + 4 * fq;
+  if (dsum && fr == 0) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = cbase + 16 * j;
+      if (col >= a.N) continue;
+      const int sg = seg_of(col, a.seg_cols, a.nseg);
+      float* db = a.dbseg[sg] + (col - sg * a.seg_cols);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) unsafeAtomicAdd(db + e, accb[j][e]);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int row = rbase + 16 * i;
     if (row >= a.M) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < FN; ++j) {
       const int col = cbase + 16 * j;
       if (col >= a.N) continue;     // N % 4 == 0 (host-checked): whole 4-column groups
+      const int sg = seg_of(col, a.seg_cols, a.nseg);
       float4v v = acc[i][j];
       if constexpr (EPI == 0) {
-        if (a.bias) {
-          const uint2 b4 = *reinterpret_cast<const uint2*>(a.bias + col);
+        if (a.biasseg[0]) {
+          const uint2 b4 = *reinterpret_cast<const uint2*>(a.biasseg[sg] + (col - sg * a.seg_cols));
           v[0] += __uint_as_float(b4.x << 16);
           v[1] += __uint_as_float(b4.x & 0xffff0000u);
           v[2] += __uint_as_float(b4.y << 16);
           v[3] += __uint_as_float(b4.y & 0xffff0000u);
         }
         bf16_t* dst = a.C + (long long)row * a.ldc + col;
+        if (a.act_bwd) {           // the producer's activation backward on the data gradient
+          const uint2 pq = *reinterpret_cast<const uint2*>(a.act_pre + (long long)row * a.ldc + col);
+          v[0] *= act_grad(__uint_as_float(pq.x << 16), a.act_bwd);
+          v[1] *= act_grad(__uint_as_float(pq.x & 0xffff0000u), a.act_bwd);
+          v[2] *= act_grad(__uint_as_float(pq.y << 16), a.act_bwd);
+          v[3] *= act_grad(__uint_as_float(pq.y & 0xffff0000u), a.act_bwd);
+        }
         if (a.accumulate) {
           const uint2 o = *reinterpret_cast<const uint2*>(dst);
           v[0] += __uint_as_float(o.x << 16);
@@ -371,7 +508,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
         }
         *reinterpret_cast<uint2*>(dst) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
       } else {
-        float* dst = a.Cf + (long long)row * a.ldcf + col;
+        float* dst = a.cfseg[sg] + (long long)row * a.ldcf + (col - sg * a.seg_cols);
         if (a.atomic) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) unsafeAtomicAdd(dst + e, v[e]);
@@ -391,6 +528,8 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
 template <int BM, int BN, bool ATR, bool BTR, int EPI>
 int launch_pp(const GemmArgs& a0, int splits, hipStream_t st) {
   GemmArgs a = a0;
+  // a transposed (k-major) operand's tile must not straddle its edge (see src_off)
+  if ((ATR && a.M % BM) || (BTR && a.N % BN)) return MDTF_EUNSUPPORTED;
   a.tiles_m = (a.M + BM - 1) / BM;
   a.tiles_n = (a.N + BN - 1) / BN;
   const int KT = a.K / 64;
@@ -399,7 +538,7 @@ int launch_pp(const GemmArgs& a0, int splits, hipStream_t st) {
   a.kt_split = (KT + splits - 1) / splits;
   splits = (KT + a.kt_split - 1) / a.kt_split;
   if (EPI == 1) a.atomic = splits > 1 ? 1 : a.atomic;
-  constexpr int lds = 2 * (BM + BN) * 128;
+  constexpr int lds = (BM == 256 ? 2 : 3) * (BM + BN) * 128;
   auto k = gemm_pp_kernel<BM, BN, ATR, BTR, EPI>;
   static bool attr = false;
   if (!attr) {
@@ -412,7 +551,7 @@ int launch_pp(const GemmArgs& a0, int splits, hipStream_t st) {
   return 0;
 }
 
-// tile code: 0 = 256x256, 1 = 256x128, 2 = 128x256, 3 = 128x128
+// tile code: 0 = 256x256, 1 = 256x128, 2 = 128x256, 3 = 128x128, 4 = 256x192, 5 = 128x192
 template <bool ATR, bool BTR, int EPI>
 int dispatch(int tile, const GemmArgs& a, int splits, hipStream_t st) {
   switch (tile) {
@@ -420,6 +559,8 @@ int dispatch(int tile, const GemmArgs& a, int splits, hipStream_t st) {
     case 1: return launch_pp<256, 128, ATR, BTR, EPI>(a, splits, st);
     case 2: return launch_pp<128, 256, ATR, BTR, EPI>(a, splits, st);
     case 3: return launch_pp<128, 128, ATR, BTR, EPI>(a, splits, st);
+    case 4: return launch_pp<256, 192, ATR, BTR, EPI>(a, splits, st);
+    case 5: return launch_pp<128, 192, ATR, BTR, EPI>(a, splits, st);
   }
   return MDTF_EINVAL;
 }
@@ -431,38 +572,57 @@ bool fits(long long rows, long long ld) { return rows * ld * 2 < (1ll << 31); }
 extern "C" int mdtf_get_deterministic();
 
 // layout code: 0 = fwd (A [M][K], B [K][N] -> BTR), 1 = dgrad (A [M][K], B [N][K]), 2 = wgrad (A [K][M], B [K][N])
-// C / Cf: exactly one non-null.  Returns 0, or MDTF_EUNSUPPORTED for shapes the kernel does not take.
-MDTF_EXPORT int mdtf_gemm_pp(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
-                             int layout, int tile, int splits, bf16_t* C, long long ldc, const bf16_t* bias,
-                             bf16_t* pre, int act, int accumulate, float* Cf, long long ldcf, void* stream) {
+// C / Cf: exactly one non-null.  Segments (nseg 1..4, seg_cols): B = bseg[0..nseg) (fwd: along N, dgrad: along K),
+// bias / Cf / dbias along N = biasseg / cfseg / dbseg.  act: forward activation (+ pre store); act_bwd: dgrad
+// epilogue multiplies by act'(act_pre).  Returns 0, or MDTF_EUNSUPPORTED for shapes the kernel does not take.
+MDTF_EXPORT int mdtf_gemm_pp(const bf16_t* A, long long lda, const bf16_t* const* bseg, long long ldb, int M, int N,
+                             int K, int layout, int tile, int splits, int nseg, int seg_cols, bf16_t* C, long long ldc,
+                             const bf16_t* const* biasseg, bf16_t* pre, int act, int accumulate, const bf16_t* act_pre,
+                             int act_bwd, float* const* cfseg, long long ldcf, float* const* dbseg, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 4 || (lda % 8) || (ldb % 8)) return MDTF_EUNSUPPORTED;
-  if ((C == nullptr) == (Cf == nullptr)) return MDTF_EINVAL;
+  if (nseg < 1 || nseg > 4 || seg_cols <= 0) return MDTF_EINVAL;
+  const bool fp32out = cfseg != nullptr && cfseg[0] != nullptr;
+  if ((C == nullptr) == fp32out) return MDTF_EINVAL;
   const bool atr = layout == 2, btr = layout == 0 || layout == 2;
-  // operand ranges (the buffer descriptors' 32-bit offsets)
-  if (!(atr ? fits(K, lda) : fits(M, lda)) || !(btr ? fits(K, ldb) : fits(N, ldb))) return MDTF_EUNSUPPORTED;
+  // segment geometry: whole segments cover the segmented dimension
+  const int segdim = layout == 1 ? K : N;
+  if (nseg * seg_cols != segdim || (nseg > 1 && (seg_cols % 64))) return MDTF_EUNSUPPORTED;
+  // operand ranges (the buffer descriptors' 32-bit offsets): B per segment
+  const long long brows = btr ? K : N;
+  if (!(atr ? fits(K, lda) : fits(M, lda)) || !fits(brows, ldb)) return MDTF_EUNSUPPORTED;
   if (atr && M % 8) return MDTF_EUNSUPPORTED;     // k-major operands: whole 16-B column chunks
   if (btr && N % 8) return MDTF_EUNSUPPORTED;
   GemmArgs a{};
   a.A = A;
-  a.B = B;
+  a.B = bseg[0];
   a.lda = lda;
   a.ldb = ldb;
   a.M = M;
   a.N = N;
   a.K = K;
   a.bytes_a = (int)((atr ? (long long)K : (long long)M) * lda * 2);
-  a.bytes_b = (int)((btr ? (long long)K : (long long)N) * ldb * 2);
+  a.bytes_b = (int)(brows * ldb * 2);
+  a.nseg = nseg;
+  a.seg_cols = seg_cols;
+  for (int i = 0; i < 4; ++i) {
+    a.bseg[i] = i < nseg ? bseg[i] : bseg[0];
+    a.biasseg[i] = biasseg ? (i < nseg ? biasseg[i] : biasseg[0]) : nullptr;
+    a.cfseg[i] = fp32out ? (i < nseg ? cfseg[i] : cfseg[0]) : nullptr;
+    a.dbseg[i] = dbseg ? (i < nseg ? dbseg[i] : dbseg[0]) : nullptr;
+  }
   a.C = C;
   a.ldc = ldc;
-  a.bias = bias;
+  a.bias = a.biasseg[0];
   a.pre = pre;
   a.act = act;
   a.accumulate = accumulate;
-  a.Cf = Cf;
+  a.act_pre = act_pre;
+  a.act_bwd = act_pre ? act_bwd : 0;
+  a.Cf = a.cfseg[0];
   a.ldcf = ldcf;
   a.atomic = 0;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (C != nullptr) {
+  if (!fp32out) {
     if (splits > 1) return MDTF_EUNSUPPORTED;
     switch (layout) {
       case 0: return dispatch<false, true, 0>(tile, a, 1, st);

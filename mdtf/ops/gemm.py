@@ -23,8 +23,16 @@ import torch
 
 from . import _native as N
 from . import kernels
+from . import mm
 from . import tunable
 from ..train import variables as V
+
+# MDTF_DENSE: "pp" (default) = every dense GEMM the ping-pong MFMA core takes (csrc/gemm_pp.hip: forward with
+# bias/activation epilogue, data gradient with the producer's activation backward, weight gradient + bias
+# gradient straight into the fp32 slots; q|k|v as segments of one launch); "legacy" = the r2 mix of hipBLASLt
+# and the conv-kernel dense paths below (A/B comparisons).
+DENSE = os.environ.get("MDTF_DENSE", "pp")
+PP = DENSE == "pp"
 
 _ACT = {None: 0, "relu": 1, "gelu": 2}
 _fp32_out_ok = None      # does this torch build accept addmm(out_dtype=float32, out=...)?
@@ -256,14 +264,41 @@ class _Dense(torch.autograd.Function):
         tunable.ensure(x.device)
         ws, bs = wb[:nw], wb[nw:]
         has_b = bs[0] is not None
+        ctx.x_sink, ctx.x_shape = x_sink, x_shape
+        if x_sink is not None:
+            x_sink.register()
+        ctx.pp = False
+        if PP and x.is_cuda and x.dtype == torch.bfloat16 and x.stride(1) == 1 and N.use_native(x):
+            y = None
+            if not trans and all(w.is_contiguous() and w.dtype == torch.bfloat16 for w in ws):
+                pre = torch.empty((x.shape[0], ws[0].shape[1] * nw), dtype=x.dtype, device=x.device) if act == 2 \
+                    else None
+                bl = [t if t.dtype == x.dtype else t.to(x.dtype) for t in bs] if has_b else None
+                y = mm.fwd(x, list(ws), biases=bl, act=act, pre=pre)
+                if y is not None:
+                    saved = pre if act == 2 else (y if act == 1 else None)
+            elif trans and nw == 1 and act == 0 and ws[0].is_contiguous() and ws[0].dtype == torch.bfloat16:
+                y = mm.dgrad(x, ws[0])                   # x @ w^T with w [N, K]: the data-gradient layout
+                if y is not None and has_b:
+                    y.add_(bs[0].to(y.dtype))
+                saved = None
+            if y is not None:
+                ctx.pp = True
+                ctx.act, ctx.trans, ctx.nw, ctx.has_b = act, trans, nw, has_b
+                ctx.link_out, ctx.link_in = link_out, link_in
+                if link_out is not None:
+                    link_out.pre, link_out.act, link_out.fused = saved, act, False
+                ctx.widths = [t.shape[0] if trans else t.shape[1] for t in ws]
+                ctx.wsinks = [V.grad_sink(t) for t in ws]
+                ctx.bsinks = [V.grad_sink(t) if t is not None else None for t in bs]
+                ctx.like = wb
+                ctx.save_for_backward(x, saved)
+                return y
         if has_b:
             b = bs[0] if nw == 1 else _adjacent(bs)
             b = (b if b is not None else torch.cat(bs, 0)).to(x.dtype)
         else:
             b = None
-        ctx.x_sink, ctx.x_shape = x_sink, x_shape
-        if x_sink is not None:
-            x_sink.register()
         hand = None if trans else hand_fwd(x, ws, b, act)
         if hand is not None:
             y, pre = hand
@@ -292,6 +327,8 @@ class _Dense(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.pp:
+            return _Dense._backward_pp(ctx, dy)
         x, w, saved = ctx.saved_tensors
         if w is None:                             # hand-written forward over q|k|v segments
             w = torch.cat(ctx.like[:ctx.nw], 1)
@@ -383,6 +420,100 @@ class _Dense(torch.autograd.Function):
         else:
             gbs = [None] * ctx.nw
         return (dx, None, None, None, None, None, None, None) + tuple(gws) + tuple(gbs)
+
+
+def _backward_pp(ctx, dy):
+    """Backward of a dense layer on the ping-pong core: no weight concatenation, no bf16 weight gradient,
+    no separate bias column sums or activation-backward pass where the neighbouring GEMM can fold it in."""
+    x, saved = ctx.saved_tensors
+    ws, bs = list(ctx.like[:ctx.nw]), list(ctx.like[ctx.nw:])
+    dy = dy.contiguous()
+    lo = ctx.link_out
+    fused_in = lo is not None and lo.fused          # the consumer's data gradient applied act' already
+    dpre = dy if (ctx.act == 0 or fused_in) else _act_bwd(dy, saved, ctx.act)
+    if lo is not None:
+        lo.pre = None
+    dx = None
+    if ctx.needs_input_grad[0]:
+        xs, li = ctx.x_sink, ctx.link_in
+        if ctx.trans:                                   # y = x w^T (w [N, K]): dx = dy w
+            w = ws[0]
+            dx = mm.fwd(dpre, w) if dpre.shape[1] % 64 == 0 else None
+            if dx is None:
+                dx = torch.mm(dpre, w)
+            if xs is not None:
+                buf, acc = xs.target()
+                if acc:
+                    buf.view(-1, dx.shape[1]).add_(dx)
+                    xs.written(buf)
+                else:
+                    xs.written(dx.view(ctx.x_shape))
+                dx = None
+        elif xs is None:
+            ap = li.pre if (li is not None and li.pre is not None) else None
+            dx = mm.dgrad(dpre, ws, act_pre=ap, act_bwd=li.act if ap is not None else 0)
+            if dx is not None and ap is not None:
+                li.fused = True
+            if dx is None:
+                w = ws[0] if ctx.nw == 1 else torch.cat(ws, 1)
+                dx = torch.mm(dpre, w.t())
+        else:
+            buf, acc = xs.target()
+            K = ws[0].shape[0]
+            if acc:                                     # second contribution: C += dpre @ w^T inside the GEMM
+                b2 = buf.view(-1, K)
+                if mm.dgrad(dpre, ws, out=b2, accumulate=True) is None:
+                    torch.addmm(b2, dpre, torch.cat(ws, 1).t() if ctx.nw > 1 else ws[0].t(), out=b2)
+                xs.written(buf)
+            else:
+                d2 = mm.dgrad(dpre, ws)
+                if d2 is None:
+                    d2 = torch.mm(dpre, torch.cat(ws, 1).t() if ctx.nw > 1 else ws[0].t())
+                xs.written(d2.view(ctx.x_shape))
+    # weight (+ bias) gradients straight into the fp32 slots
+    wsinks, bsinks = ctx.wsinks, ctx.bsinks
+    gws, gbs = [None] * ctx.nw, [None] * ctx.nw
+    all_w = all(sk is not None for sk in wsinks)
+    all_b = ctx.has_b and all(sk is not None for sk in bsinks)
+    done = False
+    if all_w and (all_b or not ctx.has_b):
+        if ctx.trans:                                   # w [N, K]: g += dy^T x  (C rows = N)
+            done = ctx.nw == 1 and mm.wgrad_into([wsinks[0].grad], dpre, x, dbs=None)
+            if done and ctx.has_b:
+                kernels.colsum_into(dpre, bsinks[0].grad)
+        else:
+            done = mm.wgrad_into([sk.grad for sk in wsinks], x, dpre,
+                                 dbs=[sk.grad for sk in bsinks] if ctx.has_b else None)
+    if done:
+        gws = [V.grad_marker(w) for w in ws]
+        if ctx.has_b:
+            gbs = [V.grad_marker(b) for b in bs]
+    else:
+        col = 0
+        for j, n in enumerate(ctx.widths):
+            d = dpre[:, col:col + n] if ctx.nw > 1 else dpre
+            col += n
+            sink = wsinks[j]
+            if sink is not None:
+                if ctx.trans:
+                    _accum_mm(sink.grad, d.t(), x)
+                else:
+                    wgrad_into(sink.grad, x, d)
+                gws[j] = V.grad_marker(ws[j])
+            elif ctx.needs_input_grad[8 + j]:
+                g = torch.mm(d.t(), x) if ctx.trans else torch.mm(x.t(), d)
+                gws[j] = g.to(ws[j].dtype)
+            if ctx.has_b:
+                part = d.float().sum(0)
+                if bsinks[j] is not None:
+                    bsinks[j].grad.add_(part)
+                    gbs[j] = V.grad_marker(bs[j])
+                else:
+                    gbs[j] = part.to(bs[j].dtype)
+    return (dx, None, None, None, None, None, None, None) + tuple(gws) + tuple(gbs)
+
+
+_Dense._backward_pp = staticmethod(_backward_pp)
 
 
 def matmul(a, b):

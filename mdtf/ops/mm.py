@@ -1,99 +1,147 @@
 """The ping-pong MFMA GEMM core (``csrc/gemm_pp.hip``) as torch-facing calls.
 
-Three layouts cover every dense-layer product without a transposed copy of anything:
+Three layouts cover every dense-layer product without a transposed or concatenated copy of anything:
 
-* ``fwd``   ``y = act(x @ w + b)``             x [M, K], w [K, N]           (layout 0)
-* ``dgrad`` ``dx (+)= dy @ w^T``               dy [M, N], w [K, N]          (layout 1)
-* ``wgrad`` ``gw += x^T @ dy`` (fp32 slot)      x [M, K], dy [M, N] -> [K, N] (layout 2)
+* ``fwd``   ``y = act(x @ [w_0|..] + [b_0|..])``   x [M, K], w_s [K, Ns]        (layout 0)
+* ``dgrad`` ``dx (+)= dy @ [w_0|..]^T``             dy [M, sum Ns], w_s [K, Ns]  (layout 1)
+* ``wgrad`` ``g_s += x^T @ dy[:, seg s]`` (fp32)    x [M, K], dy [M, sum Ns]     (layout 2)
 
-Tile codes: 0 = 256x256, 1 = 256x128, 2 = 128x256, 3 = 128x128 (rows x cols of C).  ``pick_tile``
-chooses by the number of tiles the grid gets on the 256 CUs; ``TILES`` pins measured per-shape choices
-(``bench/gemm_pp_probe.py``).
+Several weight matrices that share an input (BERT's q|k|v) are *segments* of one launch: the kernel picks the
+segment per LDS unit (forward: output columns; data gradient: the reduction), so there is no ``torch.cat`` of
+the weights in either direction and the weight gradient lands directly in each variable's fp32 slot.
+
+Tile codes: 0 = 256x256, 1 = 256x128, 2 = 128x256, 3 = 128x128, 4 = 256x192, 5 = 128x192 (rows x cols of C).
+``pick_tile`` models the grid's wave quantisation on the 256 CUs and the per-tile efficiency of each shape;
+``TILES`` pins measured per-shape choices (``bench/gemm_pp_probe.py`` on an MI355X).
 """
+import ctypes
+
 import torch
 
 from . import _native as N
 
-N.register("mdtf_gemm_pp", [N.P, N.L, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.I, N.P, N.L, N.P, N.P, N.I, N.I, N.P,
-                            N.L, N.P])
+N.register("mdtf_gemm_pp", [N.P, N.L, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.I, N.P, N.L, N.P, N.P, N.I,
+                            N.I, N.P, N.I, N.P, N.L, N.P, N.P])
 
-_TILE_DIMS = {0: (256, 256), 1: (256, 128), 2: (128, 256), 3: (128, 128)}
+_TILE_DIMS = {0: (256, 256), 1: (256, 128), 2: (128, 256), 3: (128, 128), 4: (256, 192), 5: (128, 192)}
+# relative time per unit of tile work (LDS / L2 bytes per FLOP grow as the tile shrinks), from the probe
+_TILE_COST = {0: 1.0, 1: 1.14, 2: 1.10, 3: 1.35, 4: 1.05, 5: 1.16}
 CUS = 256
 
-# (layout, M, N, K) -> (tile, splits): measured choices (graph-timed on MI355X)
+# (layout, M, N, K) -> (tile, splits): measured choices (graph-timed on MI355X, bench/gemm_pp_probe.py)
 TILES = {}
 
+ACT = {None: 0, "relu": 1, "gelu": 2}
 
-def _waves(M, Nn, tile, splits=1):
+
+def _valid(layout, tile, M, Nn):
     bm, bn = _TILE_DIMS[tile]
-    t = -(-M // bm) * -(-Nn // bn) * splits
-    return t, t / (CUS * -(-t // CUS))      # tiles, fraction of the last round's CUs busy ... of all rounds
+    if layout == 2 and M % bm:          # transposed A must not straddle its edge
+        return False
+    if layout in (0, 2) and Nn % bn:    # transposed B
+        return False
+    return True
 
 
-def pick_tile(layout, M, Nn, K):
-    """(tile, splits) for C[M][Nn] with reduction K."""
+def pick_tile(layout, M, Nn, K, seg_cols=None):
+    """(tile, splits) for C[M][Nn] with reduction K (layout 2 may split K)."""
     t = TILES.get((layout, M, Nn, K))
     if t is not None:
         return t
     best = None
-    for tile in (0, 1, 2, 3):
+    for tile in _TILE_DIMS:
         bm, bn = _TILE_DIMS[tile]
+        if not _valid(layout, tile, M, Nn):
+            continue
+        if seg_cols and layout in (0, 2) and seg_cols % bn:
+            continue
         ntiles = -(-M // bm) * -(-Nn // bn)
-        splits_opts = (1,) if layout != 2 else (1, 2, 3, 4, 6, 8)
-        for sp in splits_opts:
-            if K // 64 < sp * 4 and sp > 1:
+        for sp in ((1,) if layout != 2 else (1, 2, 3, 4, 6, 8)):
+            if sp > 1 and K // 64 < sp * 8:
                 continue
             nt = ntiles * sp
             rounds = -(-nt // CUS)
-            # time ~ rounds x per-tile work; smaller tiles move more LDS/L2 bytes per FLOP (x1.0 .. x1.35)
-            per = (bm * bn) / float(256 * 256) * (K / sp) * {0: 1.0, 1: 1.12, 2: 1.12, 3: 1.35}[tile]
-            cost = rounds * per + (0.05 * K * (sp - 1) / sp if sp > 1 else 0.0)
+            per = (bm * bn) / 65536.0 * (K / 64.0 / sp + 3.0) * _TILE_COST[tile]    # +3: pipeline fill / epilogue
+            cost = rounds * per + (0.4 * (bm * bn) / 65536.0 * sp if sp > 1 else 0.0)  # split-K atomics
             if best is None or cost < best[0]:
                 best = (cost, tile, sp)
+    if best is None:
+        return None
     return best[1], best[2]
 
 
-def _call(A, lda, B, ldb, M, Nn, K, layout, tile, splits, C=None, ldc=0, bias=None, pre=None, act=0,
-          accumulate=0, Cf=None, ldcf=0):
-    return N.fn("mdtf_gemm_pp")(N.ptr(A), lda, N.ptr(B), ldb, M, Nn, K, layout, tile, splits, N.ptr(C), ldc,
-                                N.ptr(bias), N.ptr(pre), act, accumulate, N.ptr(Cf), ldcf, N.stream_ptr())
+def _arr(ts):
+    a = (ctypes.c_void_p * 4)()
+    for i, t in enumerate(ts):
+        a[i] = t if isinstance(t, int) else (t.data_ptr() if t is not None else 0)
+    return a
 
 
-def fwd(x, w, bias=None, act=0, pre=None, out=None, tile=None):
-    """act(x @ w + bias) in bf16 (x [M, K] row-major, w [K, N] with unit column stride)."""
+def _call(A, lda, bsegs, ldb, M, Nn, K, layout, tile, splits, seg_cols, C=None, ldc=0, biases=None, pre=None,
+          act=0, accumulate=0, act_pre=None, act_bwd=0, cfs=None, ldcf=0, dbs=None):
+    return N.fn("mdtf_gemm_pp")(
+        N.ptr(A), lda, ctypes.cast(_arr(bsegs), ctypes.c_void_p), ldb, M, Nn, K, layout, tile, splits, len(bsegs),
+        seg_cols, N.ptr(C), ldc, ctypes.cast(_arr(biases), ctypes.c_void_p) if biases else None, N.ptr(pre), act,
+        accumulate, N.ptr(act_pre), act_bwd, ctypes.cast(_arr(cfs), ctypes.c_void_p) if cfs else None, ldcf,
+        ctypes.cast(_arr(dbs), ctypes.c_void_p) if dbs else None, N.stream_ptr())
+
+
+def fwd(x, ws, biases=None, act=0, pre=None, out=None, tile=None):
+    """act(x @ [ws...] + [biases...]) in bf16.  x [M, K] (unit column stride); ws: one [K, N] or a list of
+    equal [K, Ns] segments (contiguous); biases: matching bf16 vectors or None; pre: the bf16 pre-activation
+    output (act != 0).  Returns None when the kernel does not take the shape."""
+    ws = ws if isinstance(ws, (list, tuple)) else [ws]
     M, K = x.shape
-    Nn = w.shape[1]
+    ns = ws[0].shape[1]
+    Nn = ns * len(ws)
+    t = (tile, 1) if tile is not None else pick_tile(0, M, Nn, K, ns if len(ws) > 1 else None)
+    if t is None:
+        return None
     y = out if out is not None else torch.empty((M, Nn), dtype=x.dtype, device=x.device)
-    t = (tile, 1) if tile is not None else pick_tile(0, M, Nn, K)
-    rc = _call(x, x.stride(0), w, w.stride(0), M, Nn, K, 0, t[0], 1, C=y, ldc=y.stride(0), bias=bias, pre=pre,
-               act=act)
+    rc = _call(x, x.stride(0), ws, ws[0].stride(0), M, Nn, K, 0, t[0], 1, ns, C=y, ldc=y.stride(0),
+               biases=biases if biases and biases[0] is not None else None, pre=pre, act=act)
+    if rc == -2:
+        return None
     N.check(rc, "gemm_pp fwd")
     return y
 
 
-def dgrad(dy, w, out=None, accumulate=False, tile=None):
-    """dy @ w^T (dy [M, N], w [K, N] row-major) -> [M, K] bf16; ``accumulate``: out += ..."""
+def dgrad(dy, ws, out=None, accumulate=False, act_pre=None, act_bwd=0, tile=None):
+    """dy @ [ws...]^T -> [M, K] bf16 (dy [M, sum Ns]; ws [K, Ns] segments).  ``accumulate``: out += ...;
+    ``act_pre``/``act_bwd``: multiply by the producer's activation derivative at ``act_pre`` [M, K]."""
+    ws = ws if isinstance(ws, (list, tuple)) else [ws]
     M, Nn = dy.shape
-    K = w.shape[0]
-    dx = out if out is not None else torch.empty((M, K), dtype=dy.dtype, device=dy.device)
+    K = ws[0].shape[0]
     t = (tile, 1) if tile is not None else pick_tile(1, M, K, Nn)
-    rc = _call(dy, dy.stride(0), w, w.stride(0), M, K, Nn, 1, t[0], 1, C=dx, ldc=dx.stride(0),
-               accumulate=int(accumulate))
+    if t is None:
+        return None
+    dx = out if out is not None else torch.empty((M, K), dtype=dy.dtype, device=dy.device)
+    rc = _call(dy, dy.stride(0), ws, ws[0].stride(0), M, K, Nn, 1, t[0], 1, ws[0].shape[1], C=dx, ldc=dx.stride(0),
+               accumulate=int(accumulate), act_pre=act_pre, act_bwd=act_bwd)
+    if rc == -2:
+        return None
     N.check(rc, "gemm_pp dgrad")
     return dx
 
 
-def wgrad_into(gw, x, dy, tile=None, splits=None):
-    """gw [K, N] fp32 += x^T @ dy (x [M, K], dy [M, N] bf16, unit column strides)."""
+def wgrad_into(gws, x, dy, dbs=None, tile=None, splits=None):
+    """gws[s] [K, Ns] fp32 += x^T @ dy[:, segment s] (x [M, K], dy [M, sum Ns] bf16, unit column strides);
+    ``dbs``: fp32 [Ns] slots that also receive the column sums of dy (the bias gradients).  False when the
+    kernel does not take the shape (the caller falls back)."""
+    gws = gws if isinstance(gws, (list, tuple)) else [gws]
     M, K = x.shape
     Nn = dy.shape[1]
+    ns = gws[0].shape[1]
     if tile is None:
-        tile, sp = pick_tile(2, K, Nn, M)
+        t = pick_tile(2, K, Nn, M, ns if len(gws) > 1 else None)
+        if t is None:
+            return False
+        tile, sp = t
         splits = splits or sp
-    rc = _call(x, x.stride(0), dy, dy.stride(0), K, Nn, M, 2, tile, splits or 1, Cf=gw, ldcf=gw.stride(0))
+    bsegs = [dy.data_ptr() + 2 * ns * i for i in range(len(gws))]     # dy's column segments, row stride = Nn
+    rc = _call(x, x.stride(0), bsegs, dy.stride(0), K, Nn, M, 2, tile, splits or 1, ns, cfs=gws,
+               ldcf=gws[0].stride(0), dbs=dbs)
+    if rc == -2:
+        return False
     N.check(rc, "gemm_pp wgrad")
-    return gw
-
-
-def supported(layout, M, Nn, K):
-    return K % 64 == 0 and Nn % 8 == 0 and M % 8 == 0
+    return True
