@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--hip_graph", type=int, default=1,
                    help="1: capture the whole training step in a hipGraph after 2 eager steps (mdtf.train.graph)")
     p.add_argument("--image_size", type=int, default=224, help="image side (CPU tests of the launch path use 32-64)")
+    p.add_argument("--ref_rate", type=float, default=None,
+                   help="per-GPU images/sec of the N=1 run of this config, for scaling_efficiency (default: the rate the "
+                        "last N=1 run of the same config cached in .bench_n1_rate.json)")
     p.add_argument("--bert", type=int, default=-1,
                    help="also measure BERT-base (bench/bert_bench.py, a child process run before the ResNet job) and "
                         "attach it under extra.bert_base; -1: on for the default 1-GPU run")
@@ -189,6 +192,25 @@ def main():
                        "hip_graph": bool(getattr(getattr(train_op, "graph", None), "replays", 0))},
             "loss_first": float(lv), "loss_last": final_loss,
         }
+        # scaling efficiency = rate(N) / (N x rate(1)) against this config's N=1 rate (--ref_rate, or the rate
+        # the last N=1 run cached next to this file)
+        key = "resnet%d/b%d/i%d/%s/%s" % (args.depth, args.batch, args.image_size, args.mode,
+                                          rec["config"]["comm_dtype"])
+        cache = os.path.join(os.path.dirname(os.path.abspath(__file__)), ".bench_n1_rate.json")
+        try:
+            cached = json.load(open(cache)) if os.path.exists(cache) else {}
+        except ValueError:
+            cached = {}
+        if world == 1:
+            cached[key] = ips
+            try:
+                with open(cache, "w") as f:
+                    json.dump(cached, f)
+            except OSError:
+                pass
+        ref = args.ref_rate or cached.get(key)
+        rec["scaling_efficiency"] = round(ips / (world * ref), 4) if ref else None
+        rec["scaling_ref_rate_per_gpu"] = round(ref, 2) if ref else None
         if bert is not None:
             rec["extra"] = {"bert_base": bert}
         print(json.dumps(rec), flush=True)

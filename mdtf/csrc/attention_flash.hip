@@ -1,4 +1,5 @@
-// Fused multi-head attention for any sequence length (S % 64 == 0) and head dim 64 / 128 (gfx950, bf16 MFMA).
+// Fused multi-head attention for any sequence length S % 64 == 0 (192, 384, 512, ...) and head dim 64 / 128
+// (gfx950, bf16 MFMA).
 //
 // BASELINE config 4 (BERT-base; phase-2 pre-training runs seq 512) -- csrc/attention.hip keeps the
 // whole-sequence-in-LDS kernels for S = 128, D = 64; these kernels tile the other dimension and
@@ -149,7 +150,8 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_flash(const bf16_t* __restrict
   for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
     for (int ds = 0; ds < D / 32; ++ds) {
-      const int q = q0 + 32 * wave + 16 * qt + li;
+      // the last block of an S % 128 == 64 sequence has 64 queries: waves past S load a valid row and store nothing
+      const int q = min(q0 + 32 * wave + 16 * qt + li, S - 1);
       qf[qt][ds] = gfrag(qkv + rowb + (long long)q * ld + h * D + 32 * ds + 8 * g);
     }
   const uint32_t thr = p_drop > 0.f ? (uint32_t)fminf(p_drop * 4294967296.f, 4294967295.f) : 0u;
@@ -234,6 +236,7 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_flash(const bf16_t* __restrict
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + 32 * wave + 16 * qt + li;
+    if (q >= S) continue;
     const float inv = 1.f / l[qt];
     if (g == 0) lse_out[(long long)bh * S + q] = m[qt] + __logf(l[qt]);
     bf16_t* o = out + ((long long)b * S + q) * H + h * D;
@@ -487,18 +490,18 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dq(const bf16_t* __restrict__ 
 }
 
 bool shape_ok(int B, int S, int nh, int dh) {
-  if (S % 128 || S < 128 || (dh != 64 && dh != 128)) return false;
+  if (S % 64 || S < 64 || (dh != 64 && dh != 128)) return false;
   return (long long)B * S * 3 * nh * dh * 2 <= 0x7fffffffLL && (long long)B * nh * S * S < 0xffffffffLL;
 }
 
 }  // namespace
 
-// ctx[B*S, H] = attention(qkv[B*S, 3H]) for S % 128 == 0, head dim 64 / 128; lse [B*nh, S] (fp32)
+// ctx[B*S, H] = attention(qkv[B*S, 3H]) for S % 64 == 0, head dim 64 / 128; lse [B*nh, S] (fp32)
 MDTF_EXPORT int mdtf_attn_fwd_flash(const void* qkv, const float* mask, void* out, float* lse, int B, int seq, int nh,
                                     int dh, float scale, float p_drop, unsigned seed, const long long* seed_off,
                                     hipStream_t st) {
   if (!shape_ok(B, seq, nh, dh)) return MDTF_EUNSUPPORTED;
-  const dim3 grid(B * nh, seq / 128);
+  const dim3 grid(B * nh, (seq + 127) / 128);
   if (dh == 64)
     hipLaunchKernelGGL(attn_fwd_flash<64>, grid, dim3(NT), 0, st, (const bf16_t*)qkv, mask, (bf16_t*)out, lse, B, seq,
                        nh, scale, p_drop, (uint32_t)seed, seed_off);

@@ -211,8 +211,10 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
       const int cnt = G == 0 ? UB::template per_wave<0>() : UB::template per_wave<1>();
       // the segment this unit reads: by output column (transposed B) or by reduction index (dgrad)
       const int seg = BTR ? (n0 + (u - 2) * WB) / a.seg_cols : ((kt0 + t) * 64) / a.seg_cols;
-      const i32x4_t rb = buffer_rsrc(a.bseg[seg], a.bytes_b);
-      const int sb = t * stepB + (u - 2) * duB - seg * a.seg_cols * 2;
+      // segment rebasing folded into the descriptor (a negative soffset would break the range check): the
+      // column / reduction index counts from the first segment's origin
+      const i32x4_t rb = buffer_rsrc(a.bseg[seg] - seg * a.seg_cols, a.bytes_b + seg * a.seg_cols * 2);
+      const int sb = t * stepB + (u - 2) * duB;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         if (j < cnt)
@@ -582,7 +584,7 @@ MDTF_EXPORT int mdtf_gemm_pp(const bf16_t* A, long long lda, const bf16_t* const
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 4 || (lda % 8) || (ldb % 8)) return MDTF_EUNSUPPORTED;
   if (nseg < 1 || nseg > 4 || seg_cols <= 0) return MDTF_EINVAL;
   const bool fp32out = cfseg != nullptr && cfseg[0] != nullptr;
-  if ((C == nullptr) == fp32out) return MDTF_EINVAL;
+  if ((C != nullptr) == fp32out) return MDTF_EINVAL;     // exactly one output
   const bool atr = layout == 2, btr = layout == 0 || layout == 2;
   // segment geometry: whole segments cover the segmented dimension
   const int segdim = layout == 1 ? K : N;

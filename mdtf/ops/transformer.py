@@ -234,8 +234,8 @@ FLASH_ALWAYS = os.environ.get("MDTF_ATTN_FLASH", "0") == "1"
 
 
 def flash_ok(seq, dh):
-    """Shapes of the tiled kernels: any S % 128 == 0, head dim 64 or 128."""
-    return seq % 128 == 0 and seq >= 128 and dh in (64, 128)
+    """Shapes of the tiled kernels: any S % 64 == 0 (192, 384, 512, ...), head dim 64 or 128."""
+    return seq % 64 == 0 and seq >= 64 and dh in (64, 128)
 
 
 class _FusedAttention(torch.autograd.Function):
@@ -283,7 +283,7 @@ def fused_attention(qkv, batch, seq, heads, mask=None, dropout=0.0):
     contiguous inside each) to the context [B*S, H].
 
     GPU, S = 128, head dim 64: one fused HIP kernel per direction (``csrc/attention.hip``);
-    any other S % 128 == 0 with head dim 64 / 128 (BERT phase-2 seq 512, BERT-large heads):
+    any other S % 64 == 0 with head dim 64 / 128 (SQuAD seq 384, phase-2 seq 512, BERT-large heads):
     the tiled online-softmax kernels (``csrc/attention_flash.hip``); otherwise the unfused
     matmul/softmax path.
     ``mask``: additive [B, S] key mask (0 keep, -10000 drop) or None.

@@ -29,7 +29,7 @@ def _round_up(x, m):
 
 class Bucket(object):
     __slots__ = ("group", "index", "start", "end", "variables", "pending", "work", "launched",
-                 "shard_offset", "shard_len")
+                 "shard_offset", "shard_len", "updated", "gather")
 
     def __init__(self, group, index, start, end, variables):
         self.group = group
@@ -40,6 +40,8 @@ class Bucket(object):
         self.pending = 0
         self.work = None
         self.launched = False
+        self.updated = False       # sharded overlap: shard updated + gather issued during backward
+        self.gather = None
         self.shard_offset = 0
         self.shard_len = 0
 

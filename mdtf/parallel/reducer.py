@@ -65,6 +65,18 @@ class UpdateTarget(object):
         return self.group.state_buffer("%s/%s" % (self.key, name), self.numel)
 
 
+class _SliceTarget(UpdateTarget):
+    """One bucket's slice of a group's shard buffers (sharded mode's per-bucket update during backward)."""
+    __slots__ = ("off", "total")
+
+    def __init__(self, group, master, grad, shadow, key, off, total):
+        super(_SliceTarget, self).__init__(group, master, grad, shadow, key)
+        self.off, self.total = off, total
+
+    def state(self, name):
+        return self.group.state_buffer("%s/%s" % (self.key, name), self.total)[self.off:self.off + self.numel]
+
+
 def resolve_comm_dtype(comm_dtype=None):
     """``comm_dtype`` argument, else ``MDTF_COMM_DTYPE`` (fp32 | bf16); -> torch dtype."""
     name = comm_dtype if comm_dtype is not None else os.environ.get("MDTF_COMM_DTYPE", "fp32")
@@ -76,6 +88,14 @@ def resolve_comm_dtype(comm_dtype=None):
     if name in ("bf16", "bfloat16"):
         return torch.bfloat16
     raise ValueError("comm_dtype must be fp32 or bf16, got %r" % (comm_dtype,))
+
+
+class _NullCtx(object):
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 class GradReducer(object):
@@ -101,6 +121,10 @@ class GradReducer(object):
         self.contributed = True
         self.num_contributors = self.world
         self._shards = {}
+        # sharded + overlap: each bucket's shard is updated and all-gathered as soon as its reduce-scatter
+        # lands, on a side stream, while backward continues (set per step by the TrainOp: set_update_fn)
+        self.eager_update = None
+        self._upd_stream = None
         if mode not in ("allreduce", "sharded"):
             raise ValueError("mode must be 'allreduce' or 'sharded'")
         if mode == "sharded":
@@ -145,12 +169,46 @@ class GradReducer(object):
             b.pending = len(b.variables)
             b.work = None
             b.launched = False
+            b.updated = False
+            b.gather = None
 
     def _on_grad_ready(self, var):
         b = var.bucket
         b.pending -= 1
         if b.pending == 0:
             self._launch(b)
+
+    def set_update_fn(self, fn):
+        """``fn(target)`` runs the fused optimizer on one update target.  In sharded mode with overlapped
+        reductions the reducer then updates and all-gathers every bucket during backward (the gather of the
+        refreshed weights no longer waits for the whole backward, and never for the host)."""
+        self.eager_update = fn if (self.mode == "sharded" and self.overlap and self.collective
+                                   and self.R == self.world) else None
+
+    def _update_bucket(self, b):
+        g = b.group
+        sh = self._shards[id(g)]
+        cuda = torch.device(g.device).type == "cuda"
+        us = None
+        if cuda:
+            if self._upd_stream is None:
+                self._upd_stream = torch.cuda.Stream(g.device)
+            us = self._upd_stream
+            us.wait_stream(torch.cuda.current_stream(g.device))
+        ctx = torch.cuda.stream(us) if cuda else _NullCtx()
+        with ctx, torch.no_grad():
+            b.work.wait()                       # the update stream waits for this bucket's reduce-scatter
+            b.work = None
+            if self.comm_dtype != torch.float32:
+                self._widen(b)
+            o, n = b.shard_offset, b.shard_len
+            total = sh["master"].numel()
+            self.eager_update(_SliceTarget(g, sh["master"][o:o + n], sh["grad"][o:o + n],
+                                           sh["out"][o:o + n] if g.shadow is not None else None, "shard", o, total))
+            src = (sh["out"] if g.shadow is not None else sh["master"])[o:o + n]
+            dst = (g.shadow if g.shadow is not None else g.master)[b.start:b.end]
+            b.gather = dist.all_gather_into_tensor(dst, src, group=self.pg, async_op=True)
+        b.updated = True
 
     def _launch(self, b):
         if b.launched:
@@ -168,12 +226,13 @@ class GradReducer(object):
                 b.work = dist.all_reduce(wire, group=self.pg, async_op=True)
             else:
                 b.work = dist.reduce_scatter_tensor(wshard, wire, group=self.pg, async_op=True)
-            return
-        if self.mode == "allreduce":
+        elif self.mode == "allreduce":
             b.work = dist.all_reduce(g.grad[b.start:b.end], group=self.pg, async_op=True)
         else:
             out = self._shards[id(g)]["grad"][b.shard_offset:b.shard_offset + b.shard_len]
             b.work = dist.reduce_scatter_tensor(out, g.grad[b.start:b.end], group=self.pg, async_op=True)
+        if self.eager_update is not None:
+            self._update_bucket(b)
 
     def _wire_buffers(self, b):
         """Persistent (graph-capture safe) bf16 wire buffers of one bucket."""
@@ -236,6 +295,8 @@ class GradReducer(object):
         return torch.cat([full[b.start:b.end] for b in g.buckets])
 
     def update_targets(self):
+        if self.eager_update is not None and all(getattr(b, "updated", False) for b in self.space.buckets):
+            return []                           # every bucket was updated during backward
         out = []
         for g in self.space.groups:
             if self.mode == "allreduce":
@@ -249,6 +310,16 @@ class GradReducer(object):
     def after_update(self):
         """Sharded mode: all-gather refreshed compute weights to every rank."""
         if self.mode != "sharded":
+            return
+        if self.eager_update is not None and all(getattr(b, "updated", False) for b in self.space.buckets):
+            # the gathers were issued during backward: the compute stream (and a capture) joins them here,
+            # a stream dependency, not a host wait
+            for b in self.space.buckets:
+                if b.gather is not None:
+                    b.gather.wait()
+                    b.gather = None
+            if self._upd_stream is not None:
+                torch.cuda.current_stream(self.space.device).wait_stream(self._upd_stream)
             return
         works = []
         for g in self.space.groups:

@@ -315,6 +315,13 @@ class TrainOp(Fetchable):
         from ..ops import conv as _conv
         red = self.reducer
         red.begin_step()
+        lr = self.optimizer.learning_rate(step)
+        if red.R == red.world:
+            # sharded mode: buckets are updated + all-gathered during backward with the (known) 1/N scale
+            pre_scale = (1.0 / red.world) * self.grad_scale_extra
+            red.set_update_fn(lambda t: self.optimizer.update(t, lr, pre_scale, self.step_count, dyn=dyn))
+        else:
+            red.set_update_fn(None)
         _conv._WT.step_begin()                 # conv filters' K-contiguous copies: one batched refresh per step
         try:
             for prog in self.programs:
@@ -324,7 +331,6 @@ class TrainOp(Fetchable):
         finally:
             _conv._WT.step_end()
         scale = red.end_backward(step) * self.grad_scale_extra
-        lr = self.optimizer.learning_rate(step)
         with torch.no_grad():
             for target in red.update_targets():
                 self.optimizer.update(target, lr, scale, self.step_count, dyn=dyn)

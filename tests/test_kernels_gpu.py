@@ -700,10 +700,12 @@ def _attn_keep_mask(seed, B, nh, S, p):
 
 @pytest.mark.parametrize("p_drop", [0.0, 0.1])
 @pytest.mark.parametrize("B,S,nh,dh,flash", [(3, 128, 4, 64, False), (3, 128, 4, 64, True), (2, 384, 3, 64, True),
-                                              (1, 512, 2, 64, True), (2, 256, 2, 128, True), (1, 512, 2, 128, True)])
+                                              (1, 512, 2, 64, True), (2, 256, 2, 128, True), (1, 512, 2, 128, True),
+                                              (2, 192, 3, 64, True), (1, 320, 2, 128, True), (2, 64, 2, 64, True)])
 def test_fused_attention_fwd_bwd(p_drop, B, S, nh, dh, flash, monkeypatch):
     """Fused attention (S = 128 whole-sequence kernels, or the tiled online-softmax kernels for any
-    S % 128 == 0 and head dim 64 / 128) forward and backward vs fp32 with the same dropout bits."""
+    S % 64 == 0 -- 192 / 320 end on a half query block -- and head dim 64 / 128) forward and backward vs fp32
+    with the same dropout bits."""
     from mdtf.ops import transformer as T
     monkeypatch.setattr(T, "FLASH_ALWAYS", flash)
     torch.manual_seed(21 + S + dh)
