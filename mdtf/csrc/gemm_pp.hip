@@ -41,6 +41,7 @@ typedef short v4s __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 constexpr unsigned kOOB = 0x80000000u;   // buffer offset past num_records: the DMA writes zeros
+constexpr int kCUs = 256;                 // MI355X compute units: one 512-thread GEMM block each
 
 struct GemmArgs {
   const bf16_t* A;
@@ -71,6 +72,7 @@ struct GemmArgs {
   float* dbseg[4];           // wgrad: the column sums of B (dy: the bias gradient) are added here (null: none)
   const bf16_t* act_pre;     // dgrad: C = acc * act'(act_pre) (the producer's activation backward), null: none
   int act_bwd;
+  int persistent;            // 1: grid = min(tiles, CUs) blocks loop over the tiles
 };
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
@@ -159,9 +161,19 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G = wave >> 2, wc = wave & 3;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  // persistent over output tiles (a.persistent: grid = min(tiles, CUs)); the next tile's first loads are issued
+  // before this tile's epilogue, so the pipeline fill overlaps the stores
+  const int ntiles = a.tiles_m * a.tiles_n;
+  int it = blockIdx.x;
+  int tm = 0, tn = 0, m0 = 0, n0 = 0;
+  auto set_tile = [&](int i) {
+    const int tile = xcd_remap(i, ntiles);
+    tm = tile / a.tiles_n;
+    tn = tile - tm * a.tiles_n;
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+  set_tile(it);
   const int kt0 = blockIdx.y * a.kt_split;
   const int T = min(a.kt_split, a.K / 64 - kt0);
 
@@ -187,11 +199,15 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
     if (col >= limit) return kOOB;
     return static_cast<unsigned>((((long long)kt0 * 64 + row) * ld + col) * 2);
   };
-  const unsigned vA = src_off(ATR, UA::PITCH, a.lda, m0, a.M, wave);
-  const unsigned vB = src_off(BTR, UB::PITCH, a.ldb, n0, a.N, wave);
   // a 192-B-pitch transposed image: instruction j = 1 does not start on a row boundary -> its own offsets
   constexpr bool B_J1 = BTR && UB::PITCH == 192;
-  const unsigned vB1 = B_J1 ? src_off(true, UB::PITCH, a.ldb, n0, a.N, 8 + wave) : 0u;
+  unsigned vA = 0, vB = 0, vB1 = 0;
+  auto set_offsets = [&]() {
+    vA = src_off(ATR, UA::PITCH, a.lda, m0, a.M, wave);
+    vB = src_off(BTR, UB::PITCH, a.ldb, n0, a.N, wave);
+    vB1 = B_J1 ? src_off(true, UB::PITCH, a.ldb, n0, a.N, 8 + wave) : 0u;
+  };
+  set_offsets();
   const int duA = ATR ? WA * 2 : (int)(WA * a.lda * 2);                   // unit half 1
   const int djA = ATR ? (int)((8192 / UA::PITCH) * a.lda * 2) : (int)(64 * a.lda * 2);   // instruction j = 1
   const int duB = BTR ? WB * 2 : (int)(WB * a.ldb * 2);
@@ -262,13 +278,48 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
     for (int j = 0; j < FN; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
   // wgrad bias gradient: the column sums of B by an all-ones A fragment, in the waves of the first row tile's
   // group 0 (each output column once per split)
-  const bool dsum = EPI == 1 && a.dbseg[0] != nullptr && tm == 0 && G == 0;
+  bool dsum = false;
   float4v accb[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) accb[j] = float4v{0.f, 0.f, 0.f, 0.f};
   const short8 ones8 = {0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80};
   const bf16x8_t ones = __builtin_bit_cast(bf16x8_t, ones8);
 
+  // the first loads of a tile: the whole K-tile 0, plus the K-tile-1 units the schedule expects in flight
+  auto prologue_issue = [&]() {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) issue_unit(u, 0);
+    if (T > 1) {
+      if constexpr (QUAD) {
+        issue_unit(2, 1);
+        if (G == 1) issue_unit(3, 1);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) issue_unit(u, 1);
+      }
+    }
+  };
+  prologue_issue();
+  bool first = true;
+  while (true) {
+    if (first && T > 1) {
+      if constexpr (QUAD) {
+        if (G == 0) wait_vmcnt<CB0>();
+        else wait_vmcnt<CB0 + CB1>();
+      } else {
+        if (G == 0) wait_vmcnt<CT0>();
+        else wait_vmcnt<CT1>();
+      }
+    } else {
+      wait_vmcnt<0>();       // (a later tile: the previous epilogue's stores were issued after these loads)
+    }
+    barrier();
+    if (G == 1) barrier();
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+    dsum = EPI == 1 && a.dbseg[0] != nullptr && tm == 0 && G == 0;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) accb[j] = float4v{0.f, 0.f, 0.f, 0.f};
   if constexpr (QUAD) {
     // ---- DMA schedule (quadrant phases).  Barrier numbering: group 0 passes b(2P) / b(2P+1) around the MFMAs
     // of phase P (P = 4t + q), group 1 b(2P+1) / b(2P+2).  Reads of K-tile t: group 0 in phases 4t..4t+2, group
@@ -278,21 +329,6 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
     //   group 1 issues in phase 4t+q:  q0 A0(t+1)  q1 A1(t+1)  q2 B0(t+2)  q3 B1(t+2)
     // and each wave waits for everything but its B0(t+2) (vmcnt) before b(8t+7): group 0 after the MFMAs of
     // phase 4t+3, group 1 before its first barrier of that phase.
-#pragma unroll
-    for (int u = 0; u < 4; ++u) issue_unit(u, 0);
-    if (T > 1) {
-      issue_unit(2, 1);
-      if (G == 1) issue_unit(3, 1);
-    }
-    if (T > 1) {
-      if (G == 0) wait_vmcnt<CB0>();
-      else wait_vmcnt<CB0 + CB1>();
-    } else {
-      wait_vmcnt<0>();
-    }
-    barrier();
-    if (G == 1) barrier();
-
     bf16x8_t fa[FMH][2], fb[FN][2];
     for (int t = 0; t < T; ++t) {
       const char* slotp = smem + (t & 1) * SLOT;
@@ -399,19 +435,6 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
     // group 1 in phase 2t (after b(4t)) and by group 0 in phase 2t+1, and first read after b(4t+7).  Each wave
     // waits for tile t+1 (everything but its tile-(t+2) instructions) before b(4t+3): group 1 before its first
     // barrier of phase 2t+1, group 0 after that phase's MFMAs.
-#pragma unroll
-    for (int u = 0; u < 4; ++u) issue_unit(u, 0);
-    if (T > 1) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) issue_unit(u, 1);
-      if (G == 0) wait_vmcnt<CT0>();
-      else wait_vmcnt<CT1>();
-    } else {
-      wait_vmcnt<0>();
-    }
-    barrier();
-    if (G == 1) barrier();
-
     bf16x8_t fa[FM], fb[FN];
     for (int t = 0; t < T; ++t) {
       const char* slotp = smem + (t % 3) * SLOT;
@@ -452,10 +475,32 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
     if (G == 0) barrier();
   }
 
+  // ---- next tile's first loads (every LDS read of this tile is done: all waves passed the last barrier)
+  const int em0 = m0, en0 = n0;
+  const bool edsum = dsum;
+  const int nxt = it + gridDim.x;
+  const bool more = a.persistent && nxt < ntiles;
+  // the compiler's own waits for epilogue loads would also wait for the (invisible) next-tile DMA: the bias is
+  // loaded first; epilogues that read C or the pre-activation per element issue the next loads after them
+  uint2 bpre[FN];
+  if (EPI == 0 && a.biasseg[0]) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = min(en0 + wc * CW + 4 * fq + 16 * j, a.N - 4);
+      const int sg = seg_of(col, a.seg_cols, a.nseg);
+      bpre[j] = *reinterpret_cast<const uint2*>(a.biasseg[sg] + (col - sg * a.seg_cols));
+    }
+  }
+  const bool early = !(a.act_bwd || a.accumulate || (EPI == 1 && !a.atomic));
+  if (more && early) {
+    set_tile(nxt);
+    set_offsets();
+    prologue_issue();
+  }
   // ---- epilogue: lane holds C[row][col .. col+3] for each (i, j)
-  const int rbase = m0 + G * (BM / 2) + fr;
-  const int cbase = n0 + wc * CW + 4 * fq;
-  if (dsum && fr == 0) {
+  const int rbase = em0 + G * (BM / 2) + fr;
+  const int cbase = en0 + wc * CW + 4 * fq;
+  if (edsum && fr == 0) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int col = cbase + 16 * j;
@@ -478,7 +523,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
       float4v v = acc[i][j];
       if constexpr (EPI == 0) {
         if (a.biasseg[0]) {
-          const uint2 b4 = *reinterpret_cast<const uint2*>(a.biasseg[sg] + (col - sg * a.seg_cols));
+          const uint2 b4 = bpre[j];
           v[0] += __uint_as_float(b4.x << 16);
           v[1] += __uint_as_float(b4.x & 0xffff0000u);
           v[2] += __uint_as_float(b4.y << 16);
@@ -525,6 +570,15 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
       }
     }
   }
+  if (!more) break;
+  if (!early) {
+    set_tile(nxt);
+    set_offsets();
+    prologue_issue();
+  }
+  it = nxt;
+  first = false;
+  }
 }
 
 template <int BM, int BN, bool ATR, bool BTR, int EPI>
@@ -547,7 +601,9 @@ int launch_pp(const GemmArgs& a0, int splits, hipStream_t st) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  dim3 grid(a.tiles_m * a.tiles_n, splits);
+  const int ntiles = a.tiles_m * a.tiles_n;
+  a.persistent = (splits == 1 && ntiles > kCUs) ? 1 : 0;
+  dim3 grid(a.persistent ? kCUs : ntiles, splits);
   hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a);
   MDTF_LAUNCH_CHECK();
   return 0;
