@@ -1395,3 +1395,78 @@ def test_filter_transpose_cache_matches_per_call(monkeypatch):
         _native.set_deterministic(False)
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
+
+# ---------------------------------------------------------------------------- ping-pong GEMM core (csrc/gemm_pp.hip)
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("M,N,K", [(1000, 768, 320), (264, 1536, 704), (4096, 768, 768), (768, 2304, 1024)])
+def test_gemm_core_three_layouts_vs_fp32(tile, M, N, K):
+    """Forward (bias + GELU + saved pre-activation), data gradient (plain and accumulate) and fp32 weight
+    gradient (1 and 2 K-splits) of every tile on odd row counts and K in {320, 704, 768, 1024}, vs fp32."""
+    from mdtf.ops import mm
+    torch.manual_seed(tile * 7 + M)
+    rnd = lambda *s: (torch.rand(*s, device=DEV) * 2 - 1).bfloat16()
+    x, w, b = rnd(M, K), rnd(K, N), rnd(N)
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    y = mm.fwd(x, w, biases=[b], act=2, pre=pre, tile=tile)
+    if y is not None:
+        ref = x.float() @ w.float() + b.float()
+        assert _rel(pre, ref) < 1e-2
+        assert _rel(y, torch.nn.functional.gelu(pre.float(), approximate="tanh")) < 1e-2
+    dy, w2 = rnd(M, K), rnd(N, K)
+    dx = mm.dgrad(dy, w2, tile=tile)
+    assert dx is not None and _rel(dx, dy.float() @ w2.float().t()) < 1e-2
+    acc0 = rnd(M, N)
+    dxa = mm.dgrad(dy, w2, out=acc0.clone(), accumulate=True, tile=tile)
+    assert _rel(dxa, dy.float() @ w2.float().t() + acc0.float()) < 1e-2
+    xt, dyt = rnd(K, M), rnd(K, N)
+    for sp in (1, 2):
+        gw = torch.randn(M, N, device=DEV)
+        ref = gw + xt.float().t() @ dyt.float()
+        if mm.wgrad_into(gw, xt, dyt, tile=tile, splits=sp):
+            assert _rel(gw, ref) < 1e-4
+
+
+def test_gemm_core_segments_and_fused_epilogues():
+    """q|k|v-style weight segments in one launch (no concatenation): forward with bias + ReLU, data gradient with
+    the activation backward, weight gradients into separate fp32 slots with the fused bias-gradient sums."""
+    from mdtf.ops import mm
+    torch.manual_seed(3)
+    rnd = lambda *s: (torch.rand(*s, device=DEV) * 2 - 1).bfloat16()
+    M, K, ns = 2048, 768, 768
+    x = rnd(M, K)
+    ws, bs = [rnd(K, ns) for _ in range(3)], [rnd(ns) for _ in range(3)]
+    W, B = torch.cat(ws, 1).float(), torch.cat(bs).float()
+    pre = torch.empty(M, 3 * ns, dtype=torch.bfloat16, device=DEV)
+    y = mm.fwd(x, ws, biases=bs, act=1, pre=pre)
+    assert _rel(pre, x.float() @ W + B) < 1e-2 and _rel(y, torch.relu(pre.float())) < 1e-2
+    dy = rnd(M, 3 * ns)
+    dx = mm.dgrad(dy, ws, act_pre=x, act_bwd=2)
+    xf = x.float()
+    s = torch.sigmoid(1.5957691216 * (xf + 0.044715 * xf ** 3))
+    gelu_grad = s + 2 * xf * s * (1 - s) * 0.7978845608 * (1 + 0.134145 * xf ** 2)
+    assert _rel(dx, (dy.float() @ W.t()) * gelu_grad) < 2e-2
+    gws = [torch.zeros(K, ns, device=DEV) for _ in range(3)]
+    dbs = [torch.zeros(ns, device=DEV) for _ in range(3)]
+    assert mm.wgrad_into(gws, x, dy, dbs=dbs)
+    assert _rel(torch.cat(gws, 1), x.float().t() @ dy.float()) < 1e-4
+    assert _rel(torch.cat(dbs), dy.float().sum(0)) < 1e-4
+
+
+def test_fused_apply_multi_matches_sequential():
+    """The async parameter server's batched apply: k sequential Adam / momentum updates in one kernel pass."""
+    from mdtf.ops import optim
+    torch.manual_seed(5)
+    for kind in ("momentum", "adam"):
+        n = 4096
+        w0 = torch.randn(n, device=DEV)
+        grads = [torch.randn(n, device=DEV).bfloat16() for _ in range(4)]
+        lrs, lrts = [0.1, 0.08, 0.06, 0.04], [0.01, 0.009, 0.008, 0.007]
+        kw = dict(momentum=0.9, beta1=0.9, beta2=0.999, epsilon=1e-8, weight_decay=1e-4)
+        a, s1, s2 = w0.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+        shadow = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        optim.apply_multi_(kind, a, grads, s1, s2, shadow, lrs, lrts, **kw)
+        b, t1, t2 = w0.cpu(), torch.zeros(n), torch.zeros(n)
+        optim.apply_multi_(kind, b, [g.cpu() for g in grads], t1, t2, None, lrs, lrts, **kw)
+        assert torch.allclose(a.cpu(), b, atol=1e-5), kind
+        assert torch.equal(shadow.cpu(), a.cpu().bfloat16())
