@@ -34,13 +34,18 @@ in ``tests/test_distributed.py``).
 
 Backup workers (``replicas_to_aggregate`` R < N): gradients of the first R
 replicas to finish backward are aggregated, the rest contribute zeros (TF
-drops them as stale); arrival order comes from an atomic counter in the
-cluster store, taken once the replica's backward has completed on its device.
-Overlap is disabled in that mode because the mask is only known after backward.
-Unlike TF's accumulators, stragglers are NOT skipped in time: every replica
-still joins every collective (its contribution zeroed), so a slow replica
-delays the step; backup workers here reproduce the gradient math (exactly R
-contributions per step), not the latency hiding.
+drops them as stale).  On GPUs the arrival order is decided ON THE DEVICE: each
+replica stamps the device clock when its backward has finished (a kernel on the
+compute stream), the stamps are all-gathered and every replica ranks itself
+(``csrc/backup.hip``; clock origins calibrated once against the host clock).
+The 0/1 mask scales the flat gradients before the bucket all-reduces, with no
+host synchronize and no store round trip, so the step stays hipGraph-capturable.
+On the CPU the order is an atomic counter in the cluster store.  Overlap is
+disabled in this mode because the mask is only known after backward.  Unlike
+TF's accumulators, stragglers are NOT skipped in time: every replica still joins
+every collective (its contribution zeroed), so a slow replica delays the step;
+backup workers here reproduce the gradient math (exactly R contributions per
+step), not the latency hiding.
 """
 import os
 
@@ -125,6 +130,10 @@ class GradReducer(object):
         # lands, on a side stream, while backward continues (set per step by the TrainOp: set_update_fn)
         self.eager_update = None
         self._upd_stream = None
+        # backup workers decided on the device (GPU replicas): see the module docstring
+        self.backup_device = (self.world > 1 and self.R < self.world and space.device is not None
+                              and torch.device(space.device).type == "cuda")
+        self._bk = None
         if mode not in ("allreduce", "sharded"):
             raise ValueError("mode must be 'allreduce' or 'sharded'")
         if mode == "sharded":
@@ -255,11 +264,52 @@ class GradReducer(object):
         else:
             self._shards[id(g)]["grad"][b.shard_offset:b.shard_offset + b.shard_len].copy_(wshard)
 
+    def _backup_buffers(self):
+        """Stamp / offset / mask buffers, and the one-time calibration of every replica's device clock origin
+        against the (shared) host clock: offset = device_ns - host_ns, all-gathered."""
+        if self._bk is not None:
+            return self._bk
+        import time
+        from ..ops import _native as N
+        N.register("mdtf_stamp_realtime", [N.P, N.P])
+        N.register("mdtf_backup_mask", [N.P, N.P, N.I, N.I, N.I, N.P, N.P])
+        dev = torch.device(self.space.device)
+        stamp = torch.zeros(1, dtype=torch.int64, device=dev)
+        best = None
+        for _ in range(5):                  # the tightest of a few host brackets around one device stamp
+            torch.cuda.synchronize(dev)
+            t0 = time.time_ns()
+            N.check(N.fn("mdtf_stamp_realtime")(N.ptr(stamp), N.stream_ptr()), "stamp_realtime")
+            torch.cuda.synchronize(dev)
+            t1 = time.time_ns()
+            if best is None or t1 - t0 < best[0]:
+                best = (t1 - t0, int(stamp.item()) * 10 - (t0 + t1) // 2)
+        off = torch.tensor([best[1]], dtype=torch.int64, device=dev)
+        offsets = torch.zeros(self.world, dtype=torch.int64, device=dev)
+        dist.all_gather(list(offsets.view(self.world, 1).unbind(0)), off, group=self.pg)
+        self._bk = {"stamp": stamp, "stamps": torch.zeros(self.world, dtype=torch.int64, device=dev),
+                    "offsets": offsets, "mask": torch.ones(1, dtype=torch.float32, device=dev)}
+        return self._bk
+
+    def _backup_mask_device(self):
+        from ..ops import _native as N
+        bk = self._backup_buffers()
+        N.check(N.fn("mdtf_stamp_realtime")(N.ptr(bk["stamp"]), N.stream_ptr()), "stamp_realtime")
+        dist.all_gather(list(bk["stamps"].view(self.world, 1).unbind(0)), bk["stamp"], group=self.pg)
+        N.check(N.fn("mdtf_backup_mask")(N.ptr(bk["stamps"]), N.ptr(bk["offsets"]), self.world, self.rank, self.R,
+                                         N.ptr(bk["mask"]), N.stream_ptr()), "backup_mask")
+        for g in self.space.groups:
+            g.grad.mul_(bk["mask"])         # a backup replica contributes zeros (TF drops its push as stale)
+        return bk["mask"]
+
     def end_backward(self, step=0):
         """Finish all reductions; returns the gradient scale (1/contributors)."""
         from ..ops import conv as _conv
         _conv.join_side_streams()          # every weight gradient is in the flat buffer
-        if self.world > 1 and self.R < self.world:
+        if self.backup_device:
+            self.contributed = self._backup_mask_device()      # device 0/1 (read only when someone asks)
+            self.num_contributors = self.R
+        elif self.world > 1 and self.R < self.world:
             # the ticket is taken after this replica's backward has COMPLETED on the device (not
             # merely been enqueued), so "first R" means first R to finish computing
             if self.space.device is not None and torch.device(self.space.device).type == "cuda":

@@ -25,8 +25,9 @@ Protocol (:class:`StepGraph`, driven by :class:`mdtf.train.step.TrainOp`):
    ``dyn`` if a value changed, ``graph.replay()``.
 
 A step falls back to eager execution when it cannot be replayed exactly: a
-changed input shape, backup workers (``replicas_to_aggregate < N`` needs a
-host-side arrival counter), or a non-CUDA device.  Dropout kernels read a
+changed input shape or a non-CUDA device.  Backup workers
+(``replicas_to_aggregate < N``) are captured too: their contributor mask is
+decided on the device (``mdtf.parallel.reducer``, ``csrc/backup.hip``).  Dropout kernels read a
 device step counter (:func:`rng_offset_tensor`) so replayed masks differ step
 to step.
 
@@ -219,7 +220,8 @@ class StepGraph(object):
             import torch.distributed as dist
             if dist.is_initialized() and dist.get_backend() != "nccl":
                 return False            # gloo collectives synchronise with the host: not capturable
-        return dev is not None and dev.type == "cuda" and red.R == red.world
+        # backup workers qualify when the contributor mask is decided on the device (reducer.backup_device)
+        return dev is not None and dev.type == "cuda" and (red.R == red.world or red.backup_device)
 
     # ------------------------------------------------------------------
     def run(self, ctx, step):
@@ -324,7 +326,7 @@ class StepGraph(object):
                 feed[k] = s
         # the scale is fixed for a replayable step (all replicas contribute)
         red = op.reducer
-        self._gs = (1.0 / red.world) * op.grad_scale_extra
+        self._gs = (1.0 / red.R) * op.grad_scale_extra       # R contributors (= N without backup workers)
         self.dyn = torch.zeros(3, dtype=torch.float32, device=dev)
         self._dyn_vals = None
         self._set_dyn(step)

@@ -358,7 +358,9 @@ class TrainOp(Fetchable):
             self.graph.run(ctx, step)
         else:
             self._run_step(ctx, step)
-        self.last_contributed = self.reducer.contributed
+        c = self.reducer.contributed
+        # (a device 0/1 mask for GPU backup workers: converted lazily by whoever reads it)
+        self.last_contributed = c
         self.step_count += 1
         if self.global_step is not None:
             self.global_step.increment()

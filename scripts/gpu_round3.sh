@@ -13,7 +13,7 @@ timeout -k 10 240 python -u bench/gemm_pp_probe.py --check > gpurun_out/gemm_che
   || { echo "check failed"; grep -v '"ok": true' gpurun_out/gemm_check_$TAG.jsonl | cut -c1-250 | head; tail -5 gpurun_out/gemm_check_$TAG.err; exit 1; }
 grep -c '"ok": true' gpurun_out/gemm_check_$TAG.jsonl
 step tests
-timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "dense or ffn or bert or gemm or attention or apply_multi" \
+timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "dense or ffn or bert or gemm or attention or apply_multi or backup" \
     --timeout 150 --timeout-method thread > gpurun_out/pytest_dense_$TAG.log 2>&1 \
   || { echo "pytest failed"; tail -40 gpurun_out/pytest_dense_$TAG.log; exit 1; }
 tail -1 gpurun_out/pytest_dense_$TAG.log

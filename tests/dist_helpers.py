@@ -183,3 +183,37 @@ def recovery_worker(rank, world, port, steps, out_dir, fault_step=None, fault_ta
     with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
         json.dump({"step": gs.value(), "recoveries": rec, "runs": runs, "weights": w}, f)
     server.shutdown()
+
+
+def backup_gpu_worker(rank, world, port, steps, out_dir, replicas):
+    """Backup workers on GPU tensors (ranks share the one GPU over gloo): the contributor mask is decided on the
+    device from all-gathered clock stamps."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), MDTF_DIST_BACKEND="gloo")
+    import mdtf
+    from mdtf.cluster import Server
+    from mdtf.train import variables as V
+    server = Server.from_env(backend="gloo")
+    torch.cuda.set_device(0)
+    store = V.get_store()
+    store.device = torch.device("cuda", 0)
+    batch = 4
+    Lin, MSE, xs, ys, x_ph, y_ph, Tower, Net = _linear_setup(rank, world, batch)
+    base = mdtf.train.MomentumOptimizer(0.1, 0.9)
+    tg = []
+    Tower(Net(Lin()), "tower_0/", tg, x_ph, y_ph, MSE(), base, batch_size=batch).process()
+    opt = mdtf.train.SyncReplicasOptimizer(base, replicas_to_aggregate=replicas, total_num_replicas=world)
+    gs = mdtf.train.get_or_create_global_step()
+    op = opt.apply_gradients(Tower.average_gradients(tg), global_step=gs)
+    sess = mdtf.train.MonitoredTrainingSession(is_chief=rank == 0, log_step_count_steps=0, server=server,
+                                               max_recoveries=0)
+    lo, hi = rank * batch, (rank + 1) * batch
+    contributed = 0
+    for _ in range(steps):
+        sess.run(op, feed_dict={x_ph: xs[lo:hi].cuda(), y_ph: ys[lo:hi].cuda()})
+        contributed += int(op.last_contributed)
+    sess.close()
+    w = {v.name: v.master.tolist() for v in V.get_store().trainable_variables()}
+    with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
+        json.dump({"weights": w, "contributed": contributed, "device_mask": bool(op.reducer.backup_device)}, f)
+    server.shutdown()

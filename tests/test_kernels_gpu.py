@@ -1470,3 +1470,22 @@ def test_fused_apply_multi_matches_sequential():
         optim.apply_multi_(kind, b, [g.cpu() for g in grads], t1, t2, None, lrs, lrts, **kw)
         assert torch.allclose(a.cpu(), b, atol=1e-5), kind
         assert torch.equal(shadow.cpu(), a.cpu().bfloat16())
+
+
+def test_backup_workers_device_mask_two_ranks(tmp_path):
+    """replicas_to_aggregate = 1 of 2 GPU replicas (sharing the GPU over gloo): the first finisher is chosen on the
+    device from clock stamps (no store ticket, no host sync); exactly one contribution per step, equal weights."""
+    import json
+    import os
+    import sys
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.dirname(__file__))
+    import dist_helpers
+    from mdtf.cluster.launcher import free_port
+    mp.start_processes(dist_helpers.backup_gpu_worker, args=(2, free_port(), 5, str(tmp_path), 1), nprocs=2,
+                       join=True, start_method="spawn")
+    res = [json.load(open(str(tmp_path / ("rank%d.json" % r)))) for r in range(2)]
+    assert all(r["device_mask"] for r in res)
+    assert sum(r["contributed"] for r in res) == 5
+    for k in res[0]["weights"]:
+        assert torch.allclose(torch.tensor(res[0]["weights"][k]), torch.tensor(res[1]["weights"][k]), atol=1e-6)
