@@ -191,8 +191,12 @@ class GradReducer(object):
         """``fn(target)`` runs the fused optimizer on one update target.  In sharded mode with overlapped
         reductions the reducer then updates and all-gathers every bucket during backward (the gather of the
         refreshed weights no longer waits for the whole backward, and never for the host)."""
+        # (not while a hipGraph captures the step: ending that capture with the side-stream updates and the
+        # in-backward gathers segfaulted in hipStreamEndCapture on ROCm 7.0 -- a captured sharded step gathers
+        # after the update as before)
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         self.eager_update = fn if (self.mode == "sharded" and self.overlap and self.collective
-                                   and self.R == self.world) else None
+                                   and self.R == self.world and not capturing) else None
 
     def _update_bucket(self, b):
         g = b.group

@@ -28,6 +28,9 @@ for mode in pp legacy; do
       || { echo "bert $mode failed"; tail -20 gpurun_out/bert_${mode}_$TAG.err; exit 1; }
   echo "$mode $(tail -1 gpurun_out/bert_${mode}_$TAG.json | cut -c1-160)"
 done
+MDTF_ATTN_FLASH=1 timeout -k 10 300 python bench/bert_bench.py --steps 20 --warmup 5 > gpurun_out/bert_flash_$TAG.json 2> gpurun_out/bert_flash_$TAG.err \
+    || { echo "bert flash failed"; tail -20 gpurun_out/bert_flash_$TAG.err; exit 1; }
+echo "pp+flash128 $(tail -1 gpurun_out/bert_flash_$TAG.json | cut -c1-160)"
 step bench
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --bert 0 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
   || { echo "bench failed"; tail -30 gpurun_out/bench_$TAG.err; exit 1; }

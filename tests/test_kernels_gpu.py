@@ -1295,10 +1295,12 @@ def test_dense_dgrad_act_epilogue(M, K, N, act, tile):
     assert _rel(dx, p.grad) < 1e-2
 
 
-def test_ffn_fused_act_backward_matches_unfused(monkeypatch):
+@pytest.mark.parametrize("engine", ["pp", "legacy"])
+def test_ffn_fused_act_backward_matches_unfused(engine, monkeypatch):
     """ffn(): GELU backward fused into the second layer's data gradient gives the same gradients as the
-    separate activation-backward pass."""
+    separate activation-backward pass (the GEMM core's act-backward epilogue, or the r2 conv-kernel MODE 4)."""
     from mdtf.ops import gemm as G
+    monkeypatch.setattr(G, "PP", engine == "pp")
     torch.manual_seed(5)
     x = torch.randn(2048, 768, device=DEV).bfloat16()
     w1 = (torch.randn(768, 3072, device=DEV) * 0.03).bfloat16().requires_grad_()
@@ -1307,13 +1309,23 @@ def test_ffn_fused_act_backward_matches_unfused(monkeypatch):
     b2 = (torch.randn(768, device=DEV) * 0.1).bfloat16().requires_grad_()
     res = []
     calls = []
-    real = G.hand_dgrad_act
+    if engine == "pp":
+        real = G.mm.dgrad
 
-    def counted(*a, **k):
-        out = real(*a, **k)
-        calls.append(out is not None)
-        return out
-    monkeypatch.setattr(G, "hand_dgrad_act", counted)
+        def counted(*a, **k):
+            out = real(*a, **k)
+            if k.get("act_pre") is not None:
+                calls.append(out is not None)
+            return out
+        monkeypatch.setattr(G.mm, "dgrad", counted)
+    else:
+        real = G.hand_dgrad_act
+
+        def counted(*a, **k):
+            out = real(*a, **k)
+            calls.append(out is not None)
+            return out
+        monkeypatch.setattr(G, "hand_dgrad_act", counted)
     for fuse in (True, False):
         monkeypatch.setattr(G, "FFN_FUSE", fuse)
         xi = x.clone().requires_grad_()
@@ -1328,8 +1340,9 @@ def test_ffn_fused_act_backward_matches_unfused(monkeypatch):
 
 
 def test_dense_layer_hand_fwd_matches_library(monkeypatch):
-    """A dense layer (q|k|v segments + GELU FFN) forward and backward: the hand-written forward vs the
-    hipBLASLt path give the same outputs and gradients."""
+    """A dense layer (q|k|v segments + GELU FFN) forward and backward: the hand-written GEMM core (segments,
+    bias + GELU epilogue, its data and weight gradients) vs the hipBLASLt path give the same outputs and
+    gradients."""
     from mdtf.ops import gemm as G
     torch.manual_seed(3)
     x = torch.randn(512, 768, device=DEV).bfloat16()
@@ -1339,8 +1352,9 @@ def test_dense_layer_hand_fwd_matches_library(monkeypatch):
     b2 = (torch.randn(3072, device=DEV) * 0.1).bfloat16().requires_grad_()
     res = []
     for hand in (True, False):
-        monkeypatch.setattr(G, "HAND_FWD", hand)
-        monkeypatch.setattr(G, "FWD_MODE", "mdtf" if hand else "hipblaslt")
+        monkeypatch.setattr(G, "PP", hand)
+        monkeypatch.setattr(G, "HAND_FWD", False)
+        monkeypatch.setattr(G, "FWD_MODE", "hipblaslt")
         xi = x.clone().requires_grad_()
         h = G.dense_multi(xi, ws, bs)
         y = G.dense(h, w2, b2, act="gelu")
