@@ -33,6 +33,18 @@ from ..train import variables as V
 # and the conv-kernel dense paths below (A/B comparisons).
 DENSE = os.environ.get("MDTF_DENSE", "pp")
 PP = DENSE == "pp"
+# Per-product engine inside "pp" (measured on MI355X, profiles/gemm_core_r3.md): the core takes the products where
+# it wins end to end -- a forward with a fused activation or several weight segments (no bias_act pass, no
+# q|k|v concatenation), and a data gradient that fuses the producer's activation backward or reads segments;
+# the plain products stay on hipBLASLt and the weight gradients on the conv-kernel wgrad (which beats both on
+# BERT's K = 8192 reductions).  MDTF_PP_{FWD,DGRAD,WGRAD} = all | fused | none (FWD also: act = only the forwards
+# with a fused activation; the layer's other products then run on the legacy path).  In-step BERT-base kernel
+# totals (profiles/bert_engine_ab_r3.md): the core's q|k|v forward (128x192 tiles) and segment dgrad lose to
+# hipBLASLt + cat, the GELU-consumer dgrad loses to the conv-kernel fused act dgrad; FFN-in + GELU is a tie
+# that saves the bias_act pass.
+PP_FWD = os.environ.get("MDTF_PP_FWD", "act")
+PP_DGRAD = os.environ.get("MDTF_PP_DGRAD", "fused")
+PP_WGRAD = os.environ.get("MDTF_PP_WGRAD", "none")
 
 _ACT = {None: 0, "relu": 1, "gelu": 2}
 _fp32_out_ok = None      # does this torch build accept addmm(out_dtype=float32, out=...)?
@@ -268,17 +280,30 @@ class _Dense(torch.autograd.Function):
         if x_sink is not None:
             x_sink.register()
         ctx.pp = False
-        if PP and x.is_cuda and x.dtype == torch.bfloat16 and x.stride(1) == 1 and N.use_native(x):
+        core = PP_FWD == "all" or (PP_FWD == "fused" and (act != 0 or nw > 1)) or (PP_FWD == "act" and act != 0)
+        if PP and (core or PP_FWD != "act") and x.is_cuda and x.dtype == torch.bfloat16 and x.stride(1) == 1 \
+                and N.use_native(x):
             y = None
             if not trans and all(w.is_contiguous() and w.dtype == torch.bfloat16 for w in ws):
-                pre = torch.empty((x.shape[0], ws[0].shape[1] * nw), dtype=x.dtype, device=x.device) if act == 2 \
-                    else None
-                bl = [t if t.dtype == x.dtype else t.to(x.dtype) for t in bs] if has_b else None
-                y = mm.fwd(x, list(ws), biases=bl, act=act, pre=pre)
-                if y is not None:
-                    saved = pre if act == 2 else (y if act == 1 else None)
+                if core:
+                    pre = torch.empty((x.shape[0], ws[0].shape[1] * nw), dtype=x.dtype, device=x.device) \
+                        if act == 2 else None
+                    bl = [t if t.dtype == x.dtype else t.to(x.dtype) for t in bs] if has_b else None
+                    y = mm.fwd(x, list(ws), biases=bl, act=act, pre=pre)
+                    if y is not None:
+                        saved = pre if act == 2 else (y if act == 1 else None)
+                if y is None:                            # hipBLASLt (bias epilogue) + the activation kernel
+                    w = ws[0] if nw == 1 else torch.cat(ws, 1)
+                    if has_b:
+                        b = bs[0] if nw == 1 else _adjacent(bs)
+                        b = (b if b is not None else torch.cat(bs, 0)).to(x.dtype)
+                        pre = torch.addmm(b, x, w)
+                    else:
+                        pre = torch.mm(x, w)
+                    y = pre if act == 0 else _act_fwd(pre, act)
+                    saved = None if act == 0 else (pre if act == 2 else y)
             elif trans and nw == 1 and act == 0 and ws[0].is_contiguous() and ws[0].dtype == torch.bfloat16:
-                y = mm.dgrad(x, ws[0])                   # x @ w^T with w [N, K]: the data-gradient layout
+                y = mm.dgrad(x, ws[0]) if PP_FWD == "all" else None     # x @ w^T, w [N, K]: the dgrad layout
                 if y is not None and has_b:
                     y.add_(bs[0].to(y.dtype))
                 saved = None
@@ -451,7 +476,8 @@ def _backward_pp(ctx, dy):
                 dx = None
         elif xs is None:
             ap = li.pre if (li is not None and li.pre is not None) else None
-            dx = mm.dgrad(dpre, ws, act_pre=ap, act_bwd=li.act if ap is not None else 0)
+            core = PP_DGRAD == "all" or (PP_DGRAD == "fused" and (ap is not None or ctx.nw > 1))
+            dx = mm.dgrad(dpre, ws, act_pre=ap, act_bwd=li.act if ap is not None else 0) if core else None
             if dx is not None and ap is not None:
                 li.fused = True
             if dx is None:
@@ -460,13 +486,14 @@ def _backward_pp(ctx, dy):
         else:
             buf, acc = xs.target()
             K = ws[0].shape[0]
+            core = PP_DGRAD == "all" or (PP_DGRAD == "fused" and ctx.nw > 1)
             if acc:                                     # second contribution: C += dpre @ w^T inside the GEMM
                 b2 = buf.view(-1, K)
-                if mm.dgrad(dpre, ws, out=b2, accumulate=True) is None:
+                if not core or mm.dgrad(dpre, ws, out=b2, accumulate=True) is None:
                     torch.addmm(b2, dpre, torch.cat(ws, 1).t() if ctx.nw > 1 else ws[0].t(), out=b2)
                 xs.written(buf)
             else:
-                d2 = mm.dgrad(dpre, ws)
+                d2 = mm.dgrad(dpre, ws) if core else None
                 if d2 is None:
                     d2 = torch.mm(dpre, torch.cat(ws, 1).t() if ctx.nw > 1 else ws[0].t())
                 xs.written(d2.view(ctx.x_shape))
@@ -476,7 +503,7 @@ def _backward_pp(ctx, dy):
     all_w = all(sk is not None for sk in wsinks)
     all_b = ctx.has_b and all(sk is not None for sk in bsinks)
     done = False
-    if all_w and (all_b or not ctx.has_b):
+    if all_w and (all_b or not ctx.has_b) and PP_WGRAD == "all":
         if ctx.trans:                                   # w [N, K]: g += dy^T x  (C rows = N)
             done = ctx.nw == 1 and mm.wgrad_into([wsinks[0].grad], dpre, x, dbs=None)
             if done and ctx.has_b:
@@ -494,22 +521,24 @@ def _backward_pp(ctx, dy):
             d = dpre[:, col:col + n] if ctx.nw > 1 else dpre
             col += n
             sink = wsinks[j]
+            bias_done = False
             if sink is not None:
                 if ctx.trans:
                     _accum_mm(sink.grad, d.t(), x)
-                else:
-                    wgrad_into(sink.grad, x, d)
+                else:                                   # conv-kernel wgrad, bias gradient fused in
+                    bsk = bsinks[j] if ctx.has_b else None
+                    bias_done = wgrad_into(sink.grad, x, d, bsk.grad if bsk is not None else None)
                 gws[j] = V.grad_marker(ws[j])
             elif ctx.needs_input_grad[8 + j]:
                 g = torch.mm(d.t(), x) if ctx.trans else torch.mm(x.t(), d)
                 gws[j] = g.to(ws[j].dtype)
-            if ctx.has_b:
-                part = d.float().sum(0)
-                if bsinks[j] is not None:
-                    bsinks[j].grad.add_(part)
-                    gbs[j] = V.grad_marker(bs[j])
-                else:
-                    gbs[j] = part.to(bs[j].dtype)
+            if ctx.has_b and bias_done:
+                gbs[j] = V.grad_marker(bs[j])
+            elif ctx.has_b and bsinks[j] is not None:
+                kernels.colsum_into(d, bsinks[j].grad) if d.is_contiguous() else bsinks[j].grad.add_(d.float().sum(0))
+                gbs[j] = V.grad_marker(bs[j])
+            elif ctx.has_b:
+                gbs[j] = d.float().sum(0).to(bs[j].dtype)
     return (dx, None, None, None, None, None, None, None) + tuple(gws) + tuple(gbs)
 
 

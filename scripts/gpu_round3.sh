@@ -37,7 +37,7 @@ timeout -k 10 400 python bench.py --steps 20 --warmup 5 --bert 0 > gpurun_out/be
 tail -1 gpurun_out/bench_$TAG.json | cut -c1-300
 [ "$STEPS" = "noasync" ] && exit 0
 step async
-timeout -k 10 500 python bench/async_ps_bench.py --share_gpu --num_ps 1 --num_workers 2 --depth 152 --batch 64 \
-    --steps 10 --warmup 3 --timeout_s 450 > gpurun_out/async_ps_$TAG.json 2> gpurun_out/async_ps_$TAG.err \
+timeout -k 10 500 python bench/async_ps_bench.py --share_gpu --num_ps 1 --num_workers 2 --depth 152 --batch 32 --image 160 \
+    --steps 6 --warmup 2 --timeout_s 450 > gpurun_out/async_ps_$TAG.json 2> gpurun_out/async_ps_$TAG.err \
   || { echo "async failed"; tail -30 gpurun_out/async_ps_$TAG.err; exit 1; }
 tail -1 gpurun_out/async_ps_$TAG.json | cut -c1-600

@@ -1301,6 +1301,7 @@ def test_ffn_fused_act_backward_matches_unfused(engine, monkeypatch):
     separate activation-backward pass (the GEMM core's act-backward epilogue, or the r2 conv-kernel MODE 4)."""
     from mdtf.ops import gemm as G
     monkeypatch.setattr(G, "PP", engine == "pp")
+    monkeypatch.setattr(G, "PP_FWD", "fused")      # the core takes both FFN layers (default "act": only the first)
     torch.manual_seed(5)
     x = torch.randn(2048, 768, device=DEV).bfloat16()
     w1 = (torch.randn(768, 3072, device=DEV) * 0.03).bfloat16().requires_grad_()
@@ -1353,6 +1354,8 @@ def test_dense_layer_hand_fwd_matches_library(monkeypatch):
     res = []
     for hand in (True, False):
         monkeypatch.setattr(G, "PP", hand)
+        for k in ("PP_FWD", "PP_DGRAD", "PP_WGRAD"):     # every product of both layers on the core
+            monkeypatch.setattr(G, k, "all")
         monkeypatch.setattr(G, "HAND_FWD", False)
         monkeypatch.setattr(G, "FWD_MODE", "hipblaslt")
         xi = x.clone().requires_grad_()
