@@ -637,3 +637,346 @@ void launch_dx(const void* dy, const void* x, const void* mask, void* dx, void* 
                        (const bf16_t*)x, nullptr, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3, 0);
 }
 }  // namespace
+
+// ------------------------------------------------------------------------------------------------------------
+// Stem: BatchNorm + ReLU + max pool fused (ResNet's conv1 -> bn -> relu -> 3x3/2 max pool).  The normalised
+// stem activation (the largest tensor of the network: N x 112 x 112 x 64) is never written or re-read:
+//   forward   finalize (the conv epilogue's partials) -> one pass over the conv output x that normalises,
+//             rectifies and pools each window on the fly (pooled y + the argmax byte per element);
+//   backward  one pass that gathers the pooled gradient back to each input element (argmax match), masks it
+//             with the ReLU derivative recomputed from x, and reduces the BN statistics Σ g·m, Σ g·m·x ->
+//             finalize -> one pass that gathers again and writes the BN input gradient.
+// Replaces the reference's tf.nn.max_pool after the stem's BN/ReLU (distribute_tools.py:160-165 pooling,
+// :168-180 normalisation) with a fused MI355X pass; the unfused path is bn_apply + maxpool_fwd (kernels.hip).
+namespace {
+
+struct PoolG {
+  int N, H, W, C, OH, OW, KH, KW, SH, SW, PT, PL;
+};
+
+__device__ __forceinline__ void pool_grad8(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                           const PoolG& g, int n, int h, int w, int c8, float (&acc)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  int oh0 = h + g.PT - g.KH + g.SH;
+  oh0 = oh0 < 0 ? 0 : oh0 / g.SH;
+  int oh1 = (h + g.PT) / g.SH;
+  int ow0 = w + g.PL - g.KW + g.SW;
+  ow0 = ow0 < 0 ? 0 : ow0 / g.SW;
+  int ow1 = (w + g.PL) / g.SW;
+  if (oh1 >= g.OH) oh1 = g.OH - 1;
+  if (ow1 >= g.OW) ow1 = g.OW - 1;
+  for (int oh = oh0; oh <= oh1; ++oh) {
+    const int kh = h - (oh * g.SH - g.PT);
+    if (kh < 0 || kh >= g.KH) continue;
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int kw = w - (ow * g.SW - g.PL);
+      if (kw < 0 || kw >= g.KW) continue;
+      const long long o = ((long long)(n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8;
+      const uint2 packed = *reinterpret_cast<const uint2*>(arg + o);
+      const uint32_t me = static_cast<uint32_t>(kh * g.KW + kw);
+      float gv[8];
+      load_bf8(dy + o, gv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t id = ((k < 4 ? packed.x : packed.y) >> (8 * (k & 3))) & 0xffu;
+        if (id == me) acc[k] += gv[k];
+      }
+    }
+  }
+}
+
+// one pooled 8-channel vector per thread
+__global__ void __launch_bounds__(kThreads)
+    bn_relu_maxpool_fwd(const bf16_t* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
+                        bf16_t* __restrict__ y, uint8_t* __restrict__ arg, PoolG g, int total) {
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= total) return;
+  const int cv = g.C / 8;
+  const int c8 = i % cv;
+  int p = i / cv;
+  const int ow = p % g.OW;
+  p /= g.OW;
+  const int oh = p % g.OH;
+  const int n = p / g.OH;
+  float sc[8], sh[8], best[8];
+  uint8_t bi[8];
+  load_coef8(scale, c8 * 8, sc);
+  load_coef8(shift, c8 * 8, sh);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    best[k] = -INFINITY;
+    bi[k] = 0;
+  }
+  for (int kh = 0; kh < g.KH; ++kh) {
+    const int h = oh * g.SH - g.PT + kh;
+    if (h < 0 || h >= g.H) continue;
+    for (int kw = 0; kw < g.KW; ++kw) {
+      const int w = ow * g.SW - g.PL + kw;
+      if (w < 0 || w >= g.W) continue;
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + ((long long)(n * g.H + h) * g.W + w) * g.C + c8 * 8), v);
+      const uint8_t idx = static_cast<uint8_t>(kh * g.KW + kw);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float o = fmaxf(v[k] * sc[k] + sh[k], 0.f);
+        if (o > best[k]) {
+          best[k] = o;
+          bi[k] = idx;
+        }
+      }
+    }
+  }
+  store_bf8(y + (long long)i * 8, best);
+  uint2 packed;
+  packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+  packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+  *reinterpret_cast<uint2*>(arg + (long long)i * 8) = packed;
+}
+
+// Σ g·m and Σ g·m·x over the stem's input pixels (bn_reduce_kernel's block geometry: tpr channel vectors per
+// row, rg row groups, one contiguous row range per block) -> partials [gx][C]
+__global__ void __launch_bounds__(kThreads)
+    maxpool_bn_bwd_reduce(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ x,
+                          const float* __restrict__ scale, const float* __restrict__ shift, PoolG g, int tpr, int rg,
+                          float* __restrict__ p0, float* __restrict__ p1) {
+  extern __shared__ float smem[];
+  const int t = threadIdx.x;
+  const int lane_c = t % tpr;
+  const int rgi = t / tpr;
+  const int c8 = blockIdx.y * tpr + lane_c;
+  const long long M = (long long)g.N * g.H * g.W;
+  float s0[8], s1[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s0[k] = s1[k] = 0.f;
+  if (c8 * 8 < g.C) {
+    float sc[8], sh[8];
+    load_coef8(scale, c8 * 8, sc);
+    load_coef8(shift, c8 * 8, sh);
+    const long long span = ceil_div(ceil_div(M, (long long)gridDim.x), (long long)rg) * rg;
+    const long long rbeg = (long long)blockIdx.x * span;
+    const long long rend = rbeg + span < M ? rbeg + span : M;
+    for (long long r = rbeg + rgi; r < rend; r += rg) {
+      const int w = static_cast<int>(r % g.W);
+      const long long q = r / g.W;
+      const int h = static_cast<int>(q % g.H);
+      const int n = static_cast<int>(q / g.H);
+      float xv[8], gv[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + r * g.C + c8 * 8), xv);
+      pool_grad8(dy, arg, g, n, h, w, c8, gv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gm = (xv[k] * sc[k] + sh[k] > 0.f) ? gv[k] : 0.f;
+        s0[k] += gm;
+        s1[k] += gm * xv[k];
+      }
+    }
+  }
+  const int W = tpr * 8;
+  float* L0 = smem;
+  float* L1 = smem + rg * W;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    L0[rgi * W + lane_c * 8 + k] = s0[k];
+    L1[rgi * W + lane_c * 8 + k] = s1[k];
+  }
+  __syncthreads();
+  for (int step = rg / 2; step > 0; step >>= 1) {
+    for (int e = t; e < step * W; e += kThreads) {
+      const int gi = e / W, k = e % W;
+      L0[gi * W + k] += L0[(gi + step) * W + k];
+      L1[gi * W + k] += L1[(gi + step) * W + k];
+    }
+    __syncthreads();
+  }
+  for (int k = t; k < W; k += kThreads) {
+    const int c = blockIdx.y * W + k;
+    if (c < g.C) {
+      p0[(long long)blockIdx.x * g.C + c] = L0[k];
+      p1[(long long)blockIdx.x * g.C + c] = L1[k];
+    }
+  }
+}
+
+// dx = k1·(g·m) + k2·x + k3, one input 8-channel vector per thread
+__global__ void __launch_bounds__(kThreads)
+    maxpool_bn_dx(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ x,
+                  const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ k1,
+                  const float* __restrict__ k2, const float* __restrict__ k3, bf16_t* __restrict__ dx, PoolG g,
+                  int total) {
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= total) return;
+  const int cv = g.C / 8;
+  const int c8 = i % cv;
+  int p = i / cv;
+  const int w = p % g.W;
+  p /= g.W;
+  const int h = p % g.H;
+  const int n = p / g.H;
+  float xv[8], gv[8], sc[8], sh[8], A[8], B[8], E[8];
+  unpack8(*reinterpret_cast<const uint4*>(x + (long long)i * 8), xv);
+  load_coef8(scale, c8 * 8, sc);
+  load_coef8(shift, c8 * 8, sh);
+  load_coef8(k1, c8 * 8, A);
+  load_coef8(k2, c8 * 8, B);
+  load_coef8(k3, c8 * 8, E);
+  pool_grad8(dy, arg, g, n, h, w, c8, gv);
+  float o[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float gm = (xv[k] * sc[k] + sh[k] > 0.f) ? gv[k] : 0.f;
+    o[k] = A[k] * gm + B[k] * xv[k] + E[k];
+  }
+  store_bf8(dx + (long long)i * 8, o);
+}
+
+bool pool_geo_ok(const PoolG& g) {
+  return g.C % 8 == 0 && g.KH * g.KW <= 255 && (long long)g.N * g.H * g.W * g.C < (1LL << 31) &&
+         g.OH > 0 && g.OW > 0;
+}
+
+}  // namespace
+
+// Training forward of maxpool(relu(BN(x))) when the producing conv emitted Σx / Σx² partials ([P][C]):
+// finalize (scale/shift -> ss[0:2C], kept by the caller for the backward) + the fused pooling pass.
+MDTF_EXPORT int mdtf_bn_relu_maxpool_fwd(const void* x, void* y, uint8_t* arg, int N, int H, int W, int C, int OH,
+                                         int OW, int KH, int KW, int SH, int SW, int PT, int PL, const float* gamma,
+                                         const float* beta, float* mmean, float* mvar, float decay, float eps,
+                                         float* mean, float* invstd, const float* psum, const float* psq, int P,
+                                         float* ss, hipStream_t st) {
+  PoolG g{N, H, W, C, OH, OW, KH, KW, SH, SW, PT, PL};
+  if (!pool_geo_ok(g)) return MDTF_EUNSUPPORTED;
+  const long long M = (long long)N * H * W;
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M,
+                     C, gamma, beta, mmean, mvar, decay, eps, mean, invstd, ss, ss + C, 1);
+  const int total = N * OH * OW * (C / 8);
+  hipLaunchKernelGGL(bn_relu_maxpool_fwd, dim3(ceil_div(total, kThreads)), dim3(kThreads), 0, st, (const bf16_t*)x,
+                     ss, ss + C, (bf16_t*)y, arg, g, total);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// Backward of mdtf_bn_relu_maxpool_fwd: dy = gradient of the pooled output, ss = the forward's scale/shift,
+// ws = mdtf_bn_workspace_floats(N*H*W, C) floats.  dgamma/dbeta accumulate.
+MDTF_EXPORT int mdtf_maxpool_bn_bwd(const void* dy, const uint8_t* arg, const void* x, void* dx, int N, int H, int W,
+                                    int C, int OH, int OW, int KH, int KW, int SH, int SW, int PT, int PL,
+                                    const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                                    float* dbeta, const float* ss, float* ws, hipStream_t st) {
+  PoolG g{N, H, W, C, OH, OW, KH, KW, SH, SW, PT, PL};
+  if (!pool_geo_ok(g)) return MDTF_EUNSUPPORTED;
+  const long long M = (long long)N * H * W;
+  Geo ge = make_geo(M, C);
+  float* p0 = ws;
+  float* p1 = ws + (long long)ge.gx * C;
+  float* k1 = p1 + (long long)ge.gx * C;
+  float* k2 = k1 + C;
+  float* k3 = k2 + C;
+  const size_t lds = 2 * sizeof(float) * ge.rg * ge.tpr * 8;
+  hipLaunchKernelGGL(maxpool_bn_bwd_reduce, dim3(ge.gx, ge.gy), dim3(kThreads), lds, st, (const bf16_t*)dy, arg,
+                     (const bf16_t*)x, ss, ss + C, g, ge.tpr, ge.rg, p0, p1);
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, p0, p1, ge.gx, M,
+                     C, gamma, mean, invstd, dgamma, dbeta, k1, k2, k3, 0);
+  const int total = (int)(M * (C / 8));
+  hipLaunchKernelGGL(maxpool_bn_dx, dim3(ceil_div(total, kThreads)), dim3(kThreads), 0, st, (const bf16_t*)dy, arg,
+                     (const bf16_t*)x, ss, ss + C, k1, k2, k3, (bf16_t*)dx, g, total);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Backward of relu(BN(x) + BN2(r)) (a projection-shortcut block's last BN with the shortcut BN fused in): both
+// BNs see the same dz = dy·mask.  Statistics: the main BN's from the dgrad epilogue partials (P > 0) or its own
+// reduction; the shortcut's from one reduction over (dy, mask, r).  Then ONE pass reads dy, mask, x, r and
+// writes both input gradients (the unfused path reads dy and the mask twice).
+namespace {
+__global__ void __launch_bounds__(kThreads)
+    bn_dx_dual_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
+                      const uint8_t* __restrict__ mk, bf16_t* __restrict__ dx, bf16_t* __restrict__ dr, long long n8,
+                      int C, const float* __restrict__ k, const float* __restrict__ k2) {
+  const long long base = (long long)blockIdx.x * (kThreads * kVpt) + threadIdx.x;
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  uint4 gr[kVpt], xr[kVpt], rr[kVpt];
+  uint32_t m8[kVpt];
+#pragma unroll
+  for (int u = 0; u < kVpt; ++u) {
+    const long long i = base + u * kThreads;
+    const bool ok = i < n8;
+    gr[u] = ok ? *reinterpret_cast<const uint4*>(dy + i * 8) : z4;
+    xr[u] = ok ? *reinterpret_cast<const uint4*>(x + i * 8) : z4;
+    rr[u] = ok ? *reinterpret_cast<const uint4*>(r + i * 8) : z4;
+    m8[u] = ok ? mk[i] : 0u;
+  }
+  const bool fixed = (kThreads * 8) % C == 0;
+  float A[8], B[8], E[8], A2[8], B2[8], E2[8];
+  int c0 = static_cast<int>((base * 8) % C);
+  load_coef8(k, c0, A);
+  load_coef8(k + C, c0, B);
+  load_coef8(k + 2 * C, c0, E);
+  load_coef8(k2, c0, A2);
+  load_coef8(k2 + C, c0, B2);
+  load_coef8(k2 + 2 * C, c0, E2);
+#pragma unroll
+  for (int u = 0; u < kVpt; ++u) {
+    const long long i = base + u * kThreads;
+    if (i >= n8) break;
+    if (!fixed) {
+      c0 = static_cast<int>((i * 8) % C);
+      load_coef8(k, c0, A);
+      load_coef8(k + C, c0, B);
+      load_coef8(k + 2 * C, c0, E);
+      load_coef8(k2, c0, A2);
+      load_coef8(k2 + C, c0, B2);
+      load_coef8(k2 + 2 * C, c0, E2);
+    }
+    float g[8], xv[8], rv[8], o[8], o2[8];
+    unpack8(gr[u], g);
+    unpack8(xr[u], xv);
+    unpack8(rr[u], rv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gm = ((m8[u] >> e) & 1u) ? g[e] : 0.f;
+      o[e] = A[e] * gm + B[e] * xv[e] + E[e];
+      o2[e] = A2[e] * gm + B2[e] * rv[e] + E2[e];
+    }
+    store_bf8(dx + i * 8, o);
+    store_bf8(dr + i * 8, o2);
+  }
+}
+}  // namespace
+
+// ws: 2 * mdtf_bn_workspace_floats(M, C) floats.  P == 0: the main BN's statistics are reduced here too.
+MDTF_EXPORT int mdtf_bn_bwd_dual(const void* dy, const void* x, const void* r, const uint8_t* mask, void* dx, void* dr,
+                                 long long M, int C, const float* gamma, const float* mean, const float* invstd,
+                                 float* dgamma, float* dbeta, float* psum, float* psq, int P, const float* gamma2,
+                                 const float* mean2, const float* invstd2, float* dgamma2, float* dbeta2, float* ws,
+                                 hipStream_t st) {
+  if (C % 8 || !mask) return MDTF_EINVAL;
+  Geo g = make_geo(M, C);
+  const long long half = 2LL * g.gx * C + 4LL * C;
+  float* q0 = ws;                         // shortcut partials
+  float* q1 = q0 + (long long)g.gx * C;
+  float* kk2 = q1 + (long long)g.gx * C;  // shortcut k1..k3
+  float* w2 = ws + half;                  // main: own partials (P == 0) + k1..k3
+  float* p0 = w2;
+  float* p1 = p0 + (long long)g.gx * C;
+  float* kk = p1 + (long long)g.gx * C;
+  const size_t lds = 2 * sizeof(float) * g.rg * g.tpr * 8;
+  if (P <= 0) {
+    hipLaunchKernelGGL((bn_reduce_kernel<true, true>), dim3(g.gx, g.gy), dim3(kThreads), lds, st, (const bf16_t*)dy,
+                       (const bf16_t*)x, mask, M, C, g.tpr, g.rg, p0, p1);
+    hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, p0, p1, g.gx, M,
+                       C, gamma, mean, invstd, dgamma, dbeta, kk, kk + C, kk + 2 * C, 0);
+  } else {
+    hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M,
+                       C, gamma, mean, invstd, dgamma, dbeta, kk, kk + C, kk + 2 * C, 1);
+  }
+  hipLaunchKernelGGL((bn_reduce_kernel<true, true>), dim3(g.gx, g.gy), dim3(kThreads), lds, st, (const bf16_t*)dy,
+                     (const bf16_t*)r, mask, M, C, g.tpr, g.rg, q0, q1);
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, q0, q1, g.gx, M, C,
+                     gamma2, mean2, invstd2, dgamma2, dbeta2, kk2, kk2 + C, kk2 + 2 * C, 0);
+  const long long n8 = M * C / 8;
+  hipLaunchKernelGGL(bn_dx_dual_kernel, dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
+                     (const bf16_t*)x, (const bf16_t*)r, mask, (bf16_t*)dx, (bf16_t*)dr, n8, C, kk, kk2);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}

@@ -174,11 +174,12 @@ def bias(bias_shape):
 
 
 def conv_bn(layer_name, x, out_channels, kernel_size=3, stride=1, relu=True, residual=None, training=True,
-            bn_decay=0.9, bn_epsilon=1e-5, zero_gamma=False, padding=None, defer=False):
+            bn_decay=0.9, bn_epsilon=1e-5, zero_gamma=False, padding=None, defer=False, pool=None):
     """conv (no bias) → BN (→ +residual) (→ ReLU), ResNet v1.5 building unit.
 
     Stride>1 convs use TF-official "fixed padding" (symmetric ``(k-1)//2``).  ``defer``: the BN may be
     returned unapplied (``ops.bn.DeferredBN``) for the residual BN that adds it to apply (GPU training).
+    ``pool = (ksize, stride, padding)``: a max pool after the ReLU (fused with the BN on the GPU).
     """
     cin = x.shape[-1]
     k = kernel_size
@@ -194,7 +195,7 @@ def conv_bn(layer_name, x, out_channels, kernel_size=3, stride=1, relu=True, res
         mv = V.get_variable('BatchNorm/moving_variance', [c], initializer=V.constant_initializer(1.0),
                             trainable=False)
         return ops.conv_bn(x, w, gamma, beta, mm, mv, stride, padding, training, bn_decay, bn_epsilon, relu, residual,
-                           defer=defer)
+                           defer=defer, pool=pool)
 
 
 def dense(layer_name, x, out_features, act=None, initializer=None):

@@ -56,9 +56,9 @@ class ResNet(Model):
         if store.compute_dtype is not None and x.dtype != store.compute_dtype:
             x = x.to(store.compute_dtype)
         with V.variable_scope(self.name):
+            # stem conv -> BN -> ReLU -> 3x3/2 max pool (BN + ReLU + pool one pass on the GPU)
             x = tools.conv_bn("conv1", x, self.width, 7, 2, relu=True, training=training,
-                              bn_decay=self.bn_decay, bn_epsilon=self.bn_epsilon)
-            x = ops.max_pool(x, 3, 2, "SAME")
+                              bn_decay=self.bn_decay, bn_epsilon=self.bn_epsilon, pool=(3, 2, "SAME"))
             for s, n in enumerate(self.blocks):
                 filters = self.width * (2 ** s)
                 for u in range(n):

@@ -16,6 +16,10 @@ N.register("mdtf_bn_fwd_dual", [N.P, N.P, N.P, N.P, N.L, N.I] + [N.P] * 6 + [N.I
            + [N.F, N.F, N.P, N.P])
 N.register("mdtf_bn_fwd_stats", [N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.I, N.P, N.P, N.P, N.P,
                                  N.I, N.P, N.P])
+N.register("mdtf_bn_relu_maxpool_fwd", [N.P, N.P, N.P] + [N.I] * 12 + [N.P] * 4 + [N.F, N.F] + [N.P] * 4 + [N.I]
+           + [N.P, N.P])
+N.register("mdtf_maxpool_bn_bwd", [N.P] * 4 + [N.I] * 12 + [N.P] * 8 + [N.P])
+N.register("mdtf_bn_bwd_dual", [N.P] * 6 + [N.L, N.I] + [N.P] * 7 + [N.I] + [N.P] * 6 + [N.P])
 
 
 FUSED_BWD = [0]      # backward passes that took their statistics from the dgrad epilogue (tests)
@@ -37,6 +41,9 @@ def _f32(t):
 # MDTF_BN_TRACE=1: record (input shape, has residual, how the backward statistics were obtained) per BN backward
 BWD_TRACE = [] if os.environ.get("MDTF_BN_TRACE") == "1" else None
 DUAL_DZ = os.environ.get("MDTF_DUAL_DZ", "0") == "1"
+# the dual BN's two input gradients in one pass (csrc/bn.hip mdtf_bn_bwd_dual); 0: two bn_dx passes (A/B)
+DUAL_FUSED = os.environ.get("MDTF_DUAL_BWD_FUSED", "1") != "0"
+DUAL_BWD = [0]       # one-pass dual backward launches (tests)
 
 
 class _BNTrain(torch.autograd.Function):
@@ -224,6 +231,24 @@ class _BNTrainDual(torch.autograd.Function):
         C = x.shape[-1]
         M = x.numel() // C
         dx = torch.empty_like(x)
+        if DUAL_FUSED and not DUAL_DZ:
+            grads = [sk.grad if sk is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
+                     for sk in ctx.sinks]
+            dr = torch.empty_like(r)
+            ws = torch.empty(2 * int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
+            ps, pq, P = (pstats[0], pstats[1], int(pstats.shape[1])) if pstats is not None else (None, None, 0)
+            N.check(N.fn("mdtf_bn_bwd_dual")(N.ptr(dy), N.ptr(x), N.ptr(r), N.ptr(mask), N.ptr(dx), N.ptr(dr), M, C,
+                                             N.ptr(g), N.ptr(mean), N.ptr(invstd), N.ptr(grads[0]), N.ptr(grads[1]),
+                                             N.ptr(ps), N.ptr(pq), P, N.ptr(g2), N.ptr(mean2), N.ptr(invstd2),
+                                             N.ptr(grads[2]), N.ptr(grads[3]), N.ptr(ws), N.stream_ptr()),
+                    "bn_bwd_dual")
+            DUAL_BWD[0] += 1
+            if pstats is not None:
+                from . import conv as _conv
+                _conv.bwd_stats_release(pstats, True)
+                FUSED_BWD[0] += 1
+            out = [V.grad_marker(t) if sk is not None else gr for t, sk, gr in zip(ctx.like, ctx.sinks, grads)]
+            return (dx, out[0], out[1], None, None, dr, out[2], out[3], None, None, None, None, None, None)
         # the shortcut BN's output gradient is dy * mask: its backward reads dy and the ReLU mask itself
         # (no masked copy dz is written and re-read); MDTF_DUAL_DZ=1: the written-copy path (A/B, tests)
         dz = torch.empty_like(x) if DUAL_DZ else None
@@ -253,6 +278,72 @@ class _BNTrainDual(torch.autograd.Function):
         for t, sk, gr in zip(ctx.like, ctx.sinks, grads):
             out.append(V.grad_marker(t) if sk is not None else gr)
         return (dx, out[0], out[1], None, None, dr, out[2], out[3], None, None, None, None, None, None)
+
+
+# MDTF_FUSED_STEM=0: the stem's BN apply and max pool as separate passes (A/B, tests)
+FUSED_STEM = os.environ.get("MDTF_FUSED_STEM", "1") != "0"
+
+
+class _BNReluMaxPool(torch.autograd.Function):
+    """maxpool(relu(BN(x))) with the BN statistics from the conv epilogue (``csrc/bn.hip``
+    mdtf_bn_relu_maxpool_fwd / mdtf_maxpool_bn_bwd): the normalised activation is never materialised; the
+    backward recomputes the ReLU mask from x and the saved scale/shift."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, mm, mv, decay, eps, stats, geo):
+        from . import actsink
+        ctx.set_materialize_grads(False)
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        oh, ow, kh, kw, sh, sw, pt, pl = geo
+        y = torch.empty((n, oh, ow, c), dtype=x.dtype, device=x.device)
+        arg = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=x.device)
+        mean, invstd = (torch.empty(c, dtype=torch.float32, device=x.device) for _ in range(2))
+        ss = torch.empty(2 * c, dtype=torch.float32, device=x.device)
+        psum, psq, P = stats
+        g, b = _f32(gamma), _f32(beta)
+        N.check(N.fn("mdtf_bn_relu_maxpool_fwd")(N.ptr(x), N.ptr(y), N.ptr(arg), n, h, w, c, oh, ow, kh, kw, sh, sw,
+                                                 pt, pl, N.ptr(g), N.ptr(b), N.ptr(mm), N.ptr(mv), float(decay),
+                                                 float(eps), N.ptr(mean), N.ptr(invstd), N.ptr(psum), N.ptr(psq),
+                                                 int(P), N.ptr(ss), N.stream_ptr()), "bn_relu_maxpool_fwd")
+        from . import conv as _conv
+        _conv.stats_consumed(x.device)
+        ctx.save_for_backward(x, arg, g, mean, invstd, ss)
+        ctx.geo = geo
+        ctx.sinks = (V.grad_sink(gamma) if gamma is not None else None,
+                     V.grad_sink(beta) if beta is not None else None)
+        ctx.like = (gamma, beta)
+        ctx.out_sink = actsink.attach(y)         # the pooled output feeds conv1 and the projection shortcut
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        if ctx.out_sink is not None:
+            dy = ctx.out_sink.take(dy)
+        if dy is None:
+            return (None,) * 9
+        x, arg, g, mean, invstd, ss = ctx.saved_tensors
+        dy = dy.contiguous()
+        n, h, w, c = x.shape
+        oh, ow, kh, kw, sh, sw, pt, pl = ctx.geo
+        dx = torch.empty_like(x)
+        sg, sb = ctx.sinks
+        dgamma = sg.grad if sg is not None else torch.zeros(c, dtype=torch.float32, device=x.device)
+        dbeta = sb.grad if sb is not None else torch.zeros(c, dtype=torch.float32, device=x.device)
+        ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(n * h * w, c)), dtype=torch.float32, device=x.device)
+        N.check(N.fn("mdtf_maxpool_bn_bwd")(N.ptr(dy), N.ptr(arg), N.ptr(x), N.ptr(dx), n, h, w, c, oh, ow, kh, kw,
+                                            sh, sw, pt, pl, N.ptr(g), N.ptr(mean), N.ptr(invstd), N.ptr(dgamma),
+                                            N.ptr(dbeta), N.ptr(ss), N.ptr(ws), N.stream_ptr()), "maxpool_bn_bwd")
+        gamma, beta = ctx.like
+        rg = (V.grad_marker(gamma) if sg is not None else dgamma) if gamma is not None else None
+        rb = (V.grad_marker(beta) if sb is not None else dbeta) if beta is not None else None
+        return (dx, rg, rb, None, None, None, None, None, None)
+
+
+def bn_relu_maxpool_nhwc(x, gamma, beta, moving_mean, moving_var, decay, epsilon, stats, geo):
+    """Training ``max_pool(relu(BN(x)))``; ``geo = (oh, ow, kh, kw, sh, sw, pad_top, pad_left)``."""
+    _check(x)
+    return _BNReluMaxPool.apply(x, gamma, beta, moving_mean, moving_var, decay, epsilon, stats, geo)
 
 
 def batch_norm_nhwc(x, gamma, beta, moving_mean, moving_var, training, decay, epsilon, relu, residual, stats=None):

@@ -232,13 +232,15 @@ def batch_norm(x, gamma, beta, moving_mean, moving_var, training=True, decay=0.9
 
 
 def conv_bn(x, w, gamma, beta, moving_mean, moving_var, strides=1, padding="SAME", training=True, decay=0.9,
-            epsilon=1e-5, relu=True, residual=None, defer=False):
+            epsilon=1e-5, relu=True, residual=None, defer=False, pool=None):
     """conv2d (no bias) -> batch_norm (+residual) (+ReLU).
 
     On the GPU the conv epilogue emits the per-channel Σy/Σy² partials, so the
     BN statistics pass over y disappears (BN runs finalize + apply only).
     ``defer`` (no ReLU / residual; a projection shortcut): on the GPU return a :class:`bn.DeferredBN` that
     the residual BN consuming it applies in its own pass; elsewhere the normalised tensor as usual.
+    ``pool = (ksize, stride, padding)``: a max pool follows (the ResNet stem); on the GPU BN + ReLU + pool run
+    as one pass (``bn.bn_relu_maxpool_nhwc``).
     """
     n, h, wd, c = x.shape
     kh, kw, ci, co = w.shape
@@ -251,10 +253,17 @@ def conv_bn(x, w, gamma, beta, moving_mean, moving_var, strides=1, padding="SAME
         y, stats = conv_mod.conv2d_stats_nhwc(x, w, (sh, sw), (pt, pb, pl, pr), (1, 1), private=defer)
         if defer and stats is not None:
             return bn.DeferredBN(y, gamma, beta, moving_mean, moving_var, decay, epsilon, stats)
-        return bn.batch_norm_nhwc(y, gamma, beta, moving_mean, moving_var, True, decay, epsilon, relu, residual,
-                                  stats=stats)
+        if pool is not None and relu and residual is None and stats is not None and bn.FUSED_STEM:
+            (pkh, pkw), (psh, psw) = _pool_args(pool[0], pool[1])
+            poh, pow_, ppt, _, ppl, _ = conv_geometry(oh, ow, pkh, pkw, (psh, psw), pool[2])
+            return bn.bn_relu_maxpool_nhwc(y, gamma, beta, moving_mean, moving_var, decay, epsilon, stats,
+                                           (poh, pow_, pkh, pkw, psh, psw, ppt, ppl))
+        y = bn.batch_norm_nhwc(y, gamma, beta, moving_mean, moving_var, True, decay, epsilon, relu, residual,
+                               stats=stats)
+        return y if pool is None else max_pool(y, pool[0], pool[1], pool[2])
     y = conv2d(x, w, strides, (pt, pb, pl, pr))
-    return batch_norm(y, gamma, beta, moving_mean, moving_var, training, decay, epsilon, relu, residual)
+    y = batch_norm(y, gamma, beta, moving_mean, moving_var, training, decay, epsilon, relu, residual)
+    return y if pool is None else max_pool(y, pool[0], pool[1], pool[2])
 
 
 def local_response_normalization(x, depth_radius=5, bias=1.0, alpha=1.0, beta=0.5, name=None):

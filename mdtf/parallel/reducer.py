@@ -219,7 +219,10 @@ class GradReducer(object):
             self.eager_update(_SliceTarget(g, sh["master"][o:o + n], sh["grad"][o:o + n],
                                            sh["out"][o:o + n] if g.shadow is not None else None, "shard", o, total))
             src = (sh["out"] if g.shadow is not None else sh["master"])[o:o + n]
-            dst = (g.shadow if g.shadow is not None else g.master)[b.start:b.end]
+            # .data: an alias with its own version counter -- the flat weight buffer's views are still saved by
+            # backward nodes that have not run yet (the values they read are unchanged: this bucket's layers'
+            # backward is complete), so the gather must not trip autograd's in-place check
+            dst = (g.shadow if g.shadow is not None else g.master).data[b.start:b.end]
             b.gather = dist.all_gather_into_tensor(dst, src, group=self.pg, async_op=True)
         b.updated = True
 

@@ -519,6 +519,39 @@ def test_conv_bn_fused_stats(shape, k, s, co, relu, res, monkeypatch):
         assert _rel(outs[DEV]["dr"], outs["cpu"]["dr"]) < 5e-2
 
 
+@pytest.mark.parametrize("fused", [True, False])
+def test_stem_conv_bn_relu_maxpool_vs_fp32(fused, monkeypatch):
+    """ResNet stem conv 7x7/2 -> BN -> ReLU -> max pool 3x3/2 SAME: the fused BN+ReLU+pool kernels
+    (csrc/bn.hip mdtf_bn_relu_maxpool_fwd / mdtf_maxpool_bn_bwd) and the unfused passes vs the fp32 CPU
+    reference (pooled output, input / filter / gamma / beta gradients, moving statistics)."""
+    from mdtf.ops import bn as B
+    monkeypatch.setattr(B, "FUSED_STEM", fused)
+    calls = []
+    real = B.bn_relu_maxpool_nhwc
+    monkeypatch.setattr(B, "bn_relu_maxpool_nhwc", lambda *a, **k: calls.append(1) or real(*a, **k))
+    torch.manual_seed(12)
+    x = torch.randn(4, 38, 38, 3)
+    w = torch.randn(7, 7, 3, 64) * (1.0 / 147 ** 0.5)
+    g = torch.rand(64) + 0.5
+    b = torch.randn(64) * 0.2
+    outs = {}
+    for dev, dt in ((DEV, torch.bfloat16), ("cpu", torch.float32)):
+        xx = x.to(dev).to(dt).requires_grad_(True)
+        ww = w.to(dev).to(dt).requires_grad_(True)
+        gg = g.to(dev).requires_grad_(True)
+        bb = b.to(dev).requires_grad_(True)
+        mm = torch.zeros(64, device=dev)
+        mv = torch.ones(64, device=dev)
+        y = ops.conv_bn(xx, ww, gg, bb, mm, mv, 2, (3, 3), True, 0.9, 1e-5, True, None, pool=(3, 2, "SAME"))
+        assert tuple(y.shape) == (4, 10, 10, 64)
+        dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(3)).to(dev).to(dt)
+        y.backward(dy)
+        outs[dev] = dict(y=y.detach(), dw=ww.grad, dg=gg.grad, db=bb.grad, mm=mm, mv=mv)
+    assert calls == ([1] if fused else [])
+    for key in ("y", "dw", "dg", "db", "mm", "mv"):
+        assert _rel(outs[DEV][key], outs["cpu"][key]) < 5e-2, key
+
+
 @pytest.mark.parametrize("H,res", [(768, True), (1024, False), (64, True)])
 def test_layernorm_kernel(H, res):
     from mdtf.ops import transformer as T
@@ -985,6 +1018,31 @@ def test_bn_backward_stats_from_dgrad_epilogue(model, monkeypatch):
         lf, gf = _tiny_step(DEV, torch.bfloat16, x, y)
         assert B.FUSED_BWD[0] - n0 >= 2
         monkeypatch.setattr(C, "BWD_STATS", False)
+        lo, go = _tiny_step(DEV, torch.bfloat16, x, y)
+    finally:
+        _Tiny = saved
+    assert lf == lo
+    for k in go:
+        assert _rel(gf[k], go[k]) < 1e-2, (k, _rel(gf[k], go[k]))
+
+
+@pytest.mark.parametrize("model", ["res", "strided"])
+def test_dual_bn_backward_one_pass_matches_two(model, monkeypatch):
+    """relu(BN(x) + BN2(r)) backward: both input gradients in one pass (mdtf_bn_bwd_dual, with the main BN's
+    statistics from the dgrad epilogue) == the two bn_dx passes; the one-pass kernel must actually run."""
+    from mdtf.ops import bn as B
+    global _Tiny
+    saved = _Tiny
+    _Tiny = _TinyRes if model == "res" else _TinyStrided
+    try:
+        torch.manual_seed(6)
+        x = torch.randn(16, 12, 12, 64)
+        y = torch.randint(0, 16, (16,))
+        monkeypatch.setattr(B, "DUAL_FUSED", True)
+        n0 = B.DUAL_BWD[0]
+        lf, gf = _tiny_step(DEV, torch.bfloat16, x, y)
+        assert B.DUAL_BWD[0] - n0 >= 1
+        monkeypatch.setattr(B, "DUAL_FUSED", False)
         lo, go = _tiny_step(DEV, torch.bfloat16, x, y)
     finally:
         _Tiny = saved
