@@ -171,7 +171,8 @@ def main():
     sync()
     if args.trace_ops and rank == 0:
         from torch.profiler import ProfilerActivity, profile
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
+                     with_stack=True) as prof:
             run()
             torch.cuda.synchronize()
         os.makedirs(args.trace_ops, exist_ok=True)
@@ -179,6 +180,9 @@ def main():
             f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=80,
                                                                        max_name_column_width=40,
                                                                        max_shapes_column_width=80))
+        with open(os.path.join(args.trace_ops, "ops_by_stack.txt"), "w") as f:
+            f.write(prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=60,
+                                                                 max_name_column_width=40))
         with open(os.path.join(args.trace_ops, "ops_parents.txt"), "w") as f:
             for e in prof.events():
                 if e.name in ("aten::add_", "aten::add", "aten::fill_", "aten::copy_", "aten::cat"):

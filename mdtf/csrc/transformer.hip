@@ -469,6 +469,109 @@ MDTF_EXPORT int mdtf_softmax_bwd(const void* dy, const void* y, void* dx, long l
   return 0;
 }
 
+// BERT input embedding in one pass each way: out[t] = word[ids[t]] + pos[t % S] + type[types[t]] (fp32 sum, one
+// rounding).  Backward (thread = one (position, 8-column vector), looping over 8 batch rows, dy read once): word rows
+// by fp32 atomics, the position row and the <= 4 token-type rows summed in registers, then one atomic each.  Replaces three gathers + two adds forward and three scatter passes back.
+namespace {
+constexpr int kTypeRows = 4;
+constexpr int kEmbBatch = 8;    // batch rows per backward block (grid.y = B / 8): the position partials add by atomics
+__global__ void bert_embed_fwd_kernel(const bf16_t* __restrict__ word, const bf16_t* __restrict__ pos,
+                                      const bf16_t* __restrict__ typ, const long long* __restrict__ ids,
+                                      const long long* __restrict__ types, bf16_t* __restrict__ out, long long n, int S,
+                                      int H, long long vocab, int ntypes) {
+  const int nvec = H / 8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n * nvec;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long t = i / nvec;
+    const int c = static_cast<int>(i % nvec);
+    const long long id = ids[t], ty = types[t];
+    const int s = static_cast<int>(t % S);
+    float a[8], b[8], o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = 0.f;
+    if (id >= 0 && id < vocab) load_bf8(word + id * H + c * 8, o);
+    load_bf8(pos + (long long)s * H + c * 8, a);
+    if (ty >= 0 && ty < ntypes) {
+      load_bf8(typ + ty * H + c * 8, b);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b[k] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] += a[k] + b[k];
+    store_bf8(out + t * H + c * 8, o);
+  }
+}
+
+__global__ void bert_embed_bwd_kernel(const bf16_t* __restrict__ dy, const long long* __restrict__ ids,
+                                      const long long* __restrict__ types, float* __restrict__ dword,
+                                      float* __restrict__ dpos, float* __restrict__ dtyp, int B, int S, int H,
+                                      long long vocab, int ntypes) {
+  const int nvec = H / 8;
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)S * nvec) return;
+  const int s = static_cast<int>(i / nvec), c = static_cast<int>(i % nvec);
+  float ps[8], ts[kTypeRows][8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    ps[k] = 0.f;
+#pragma unroll
+    for (int r = 0; r < kTypeRows; ++r) ts[r][k] = 0.f;
+  }
+  const int b0 = blockIdx.y * kEmbBatch, b1 = b0 + kEmbBatch < B ? b0 + kEmbBatch : B;
+  for (int b = b0; b < b1; ++b) {
+    const long long t = (long long)b * S + s;
+    float g[8];
+    load_bf8(dy + t * H + c * 8, g);
+    const long long id = ids[t], ty = types[t];
+    if (dword && id >= 0 && id < vocab) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) atomicAdd(dword + id * H + c * 8 + k, g[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ps[k] += g[k];
+#pragma unroll
+    for (int r = 0; r < kTypeRows; ++r)
+      if (r == ty) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ts[r][k] += g[k];
+      }
+  }
+  if (dpos) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) atomicAdd(dpos + (long long)s * H + c * 8 + k, ps[k]);
+  }
+  if (dtyp) {
+    for (int r = 0; r < ntypes && r < kTypeRows; ++r)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) atomicAdd(dtyp + (long long)r * H + c * 8 + k, ts[r][k]);
+  }
+}
+}  // namespace
+
+MDTF_EXPORT int mdtf_bert_embed_fwd(const void* word, const void* pos, const void* typ, const long long* ids,
+                                    const long long* types, void* out, long long n, int S, int H, long long vocab,
+                                    int npos, int ntypes, hipStream_t st) {
+  if (H % 8 || S > npos || ntypes > kTypeRows || n % S) return MDTF_EUNSUPPORTED;
+  hipLaunchKernelGGL(bert_embed_fwd_kernel, dim3(gcap(n * H / 8)), dim3(kT), 0, st, (const bf16_t*)word,
+                     (const bf16_t*)pos, (const bf16_t*)typ, ids, types, (bf16_t*)out, n, S, H, vocab, ntypes);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// dword/dpos/dtyp: fp32 [V][H] / [npos][H] / [ntypes][H] accumulated (zeroed buffers or gradient slots)
+MDTF_EXPORT int mdtf_bert_embed_bwd(const void* dy, const long long* ids, const long long* types, float* dword,
+                                    float* dpos, float* dtyp, int B, int S, int H, long long vocab, int ntypes,
+                                    hipStream_t st) {
+  if (H % 8 || ntypes > kTypeRows) return MDTF_EUNSUPPORTED;
+  const long long threads = (long long)S * (H / 8);
+  hipLaunchKernelGGL(bert_embed_bwd_kernel, dim3((unsigned)ceil_div(threads, kT), (unsigned)ceil_div(B, kEmbBatch)),
+                     dim3(kT), 0, st,
+                     (const bf16_t*)dy, ids, types, dword, dpos, dtyp, B, S, H, vocab, ntypes);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
 MDTF_EXPORT int mdtf_embed_fwd(const void* table, const long long* ids, void* out, long long n, int H,
                                long long vocab, hipStream_t st) {
   if (H % 8) return MDTF_EINVAL;

@@ -99,9 +99,7 @@ class Bert(Model):
                 word = V.get_variable("word_embeddings", [self.vocab, H], initializer=_init())
                 pos = V.get_variable("position_embeddings", [self.max_position, H], initializer=_init())
                 typ = V.get_variable("token_type_embeddings", [self.type_vocab, H], initializer=_init())
-                pos_ids = torch.arange(S_, device=ids.device).unsqueeze(0).expand(B, S_)
-                e = T.embedding_lookup(word, ids)
-                e = e + T.embedding_lookup(pos, pos_ids) + T.embedding_lookup(typ, types)
+                e = T.bert_embeddings(word, pos, typ, ids, types)      # one fused kernel each way on the GPU
                 x = _ln("LayerNorm", e)
                 x = _dropout(x, self.dropout)
             # additive attention mask over keys: 0 keep, -10000 masked

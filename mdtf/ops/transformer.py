@@ -212,6 +212,56 @@ def embedding_lookup(table, ids):
     return F.embedding(ids.long(), table)
 
 
+N.register("mdtf_bert_embed_fwd", [N.P] * 6 + [N.L, N.I, N.I, N.L, N.I, N.I, N.P])
+N.register("mdtf_bert_embed_bwd", [N.P] * 6 + [N.I, N.I, N.I, N.L, N.I, N.P])
+
+
+class _BertEmbed(torch.autograd.Function):
+    """word[ids] + position[s] + token_type[types] in one kernel each way (``csrc/transformer.hip``)."""
+
+    @staticmethod
+    def forward(ctx, word, pos, typ, ids, types):
+        B, S_ = ids.shape
+        H = word.shape[1]
+        ids = ids.to(torch.int64).contiguous()
+        types = types.to(torch.int64).contiguous()
+        out = torch.empty((B, S_, H), dtype=word.dtype, device=word.device)
+        rc = N.fn("mdtf_bert_embed_fwd")(N.ptr(word), N.ptr(pos), N.ptr(typ), N.ptr(ids), N.ptr(types), N.ptr(out),
+                                         B * S_, S_, H, word.shape[0], pos.shape[0], typ.shape[0], N.stream_ptr())
+        N.check(rc, "bert_embed_fwd")
+        ctx.save_for_backward(ids, types)
+        ctx.like = (word, pos, typ)
+        ctx.sinks = tuple(V.grad_sink(t) for t in (word, pos, typ))
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        ids, types = ctx.saved_tensors
+        B, S_ = ids.shape
+        word, pos, typ = ctx.like
+        H = word.shape[1]
+        dy = dy.contiguous()
+        bufs = [sk.grad if sk is not None else torch.zeros(t.shape, dtype=torch.float32, device=dy.device)
+                for sk, t in zip(ctx.sinks, ctx.like)]
+        N.check(N.fn("mdtf_bert_embed_bwd")(N.ptr(dy), N.ptr(ids), N.ptr(types), N.ptr(bufs[0]), N.ptr(bufs[1]),
+                                            N.ptr(bufs[2]), B, S_, H, word.shape[0], typ.shape[0], N.stream_ptr()),
+                "bert_embed_bwd")
+        out = [V.grad_marker(t) if sk is not None else b.to(t.dtype) for t, sk, b in zip(ctx.like, ctx.sinks, bufs)]
+        return out[0], out[1], out[2], None, None
+
+
+def bert_embeddings(word, pos, typ, ids, types):
+    """BERT input embedding ``word[ids] + pos[0..S) + typ[types]`` for ``ids``/``types`` [B, S]: one fused kernel
+    each way on the GPU (not in deterministic mode: the backward scatters with atomics); else three lookups."""
+    B, S_ = ids.shape
+    if (N.use_native(word) and not N.deterministic() and word.dtype == torch.bfloat16 and pos.dtype == word.dtype
+            and typ.dtype == word.dtype and word.shape[1] % 8 == 0 and S_ <= pos.shape[0] and typ.shape[0] <= 4):
+        return _BertEmbed.apply(word, pos, typ, ids, types)
+    pos_ids = torch.arange(S_, device=ids.device).unsqueeze(0).expand(B, S_)
+    e = embedding_lookup(word, ids)
+    return e + embedding_lookup(pos, pos_ids) + embedding_lookup(typ, types)
+
+
 def attention(q, k, v, mask=None, dropout=0.0):
     """Multi-head attention core: q, k, v [B, heads, S, d] -> [B, heads, S, d].
 

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 TAG=${1:-r3b}
 timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -v -m gpu --timeout 120 --timeout-method thread \
-    -k "stem or dual_bn or bn_backward_stats or conv_bn or masked_residual or tiny or resnet" > gpurun_out/pytest_$TAG.log 2>&1 \
+    -k "stem or dual_bn or bn_backward_stats or conv_bn or masked_residual or tiny or resnet or bert_embeddings" > gpurun_out/pytest_$TAG.log 2>&1 \
   || { echo "pytest failed"; tail -40 gpurun_out/pytest_$TAG.log; exit 1; }
 tail -1 gpurun_out/pytest_$TAG.log
 for i in 1 2; do

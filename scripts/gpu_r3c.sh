@@ -1,0 +1,16 @@
+#!/bin/bash
+# BERT torch-op attribution (profiler with Python stacks, eager) and the 1-GPU async-PS rehearsal.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+TAG=${1:-r3c}
+timeout -k 10 300 python bench/bert_bench.py --steps 3 --warmup 3 --hip_graph 0 --trace_ops gpurun_out/bert_ops_$TAG \
+    > gpurun_out/bert_ops_$TAG.json 2> gpurun_out/bert_ops_$TAG.err \
+  || { echo "bert trace failed"; tail -20 gpurun_out/bert_ops_$TAG.err; exit 1; }
+echo "bert trace ok"
+if [ "${ASYNC:-1}" = 1 ]; then
+timeout -k 10 500 python bench/async_ps_bench.py --share_gpu --num_ps 1 --num_workers 2 --depth 152 --batch 32 --image 160 \
+    --steps 6 --warmup 2 --timeout_s 450 > gpurun_out/async_ps_$TAG.json 2> gpurun_out/async_ps_$TAG.err \
+  || { echo "async failed"; tail -30 gpurun_out/async_ps_$TAG.err; exit 1; }
+tail -1 gpurun_out/async_ps_$TAG.json | cut -c1-900
+fi

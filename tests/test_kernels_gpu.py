@@ -519,6 +519,26 @@ def test_conv_bn_fused_stats(shape, k, s, co, relu, res, monkeypatch):
         assert _rel(outs[DEV]["dr"], outs["cpu"]["dr"]) < 5e-2
 
 
+def test_bert_embeddings_fused_vs_fp32():
+    """word[ids] + pos[s] + type[types] (one kernel each way, csrc/transformer.hip) vs fp32 lookups on the CPU:
+    output and the three table gradients (word rows by atomics, position rows summed over the batch)."""
+    from mdtf.ops import transformer as T
+    torch.manual_seed(21)
+    B, S_, H, Vv = 12, 24, 64, 50
+    word, pos, typ = torch.randn(Vv, H), torch.randn(40, H), torch.randn(2, H)
+    ids = torch.randint(0, Vv, (B, S_))
+    types = torch.randint(0, 2, (B, S_))
+    dy = torch.randn(B, S_, H)
+    outs = {}
+    for dev, dt in ((DEV, torch.bfloat16), ("cpu", torch.float32)):
+        ts = [t.to(dev).to(dt).requires_grad_(True) for t in (word, pos, typ)]
+        y = T.bert_embeddings(ts[0], ts[1], ts[2], ids.to(dev), types.to(dev))
+        y.backward(dy.to(dev).to(dt))
+        outs[dev] = [y.detach()] + [t.grad for t in ts]
+    for a, r in zip(outs[DEV], outs["cpu"]):
+        assert _rel(a, r) < 2e-2
+
+
 @pytest.mark.parametrize("fused", [True, False])
 def test_stem_conv_bn_relu_maxpool_vs_fp32(fused, monkeypatch):
     """ResNet stem conv 7x7/2 -> BN -> ReLU -> max pool 3x3/2 SAME: the fused BN+ReLU+pool kernels
