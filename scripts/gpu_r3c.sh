@@ -14,3 +14,6 @@ timeout -k 10 500 python bench/async_ps_bench.py --share_gpu --num_ps 1 --num_wo
   || { echo "async failed"; tail -30 gpurun_out/async_ps_$TAG.err; exit 1; }
 tail -1 gpurun_out/async_ps_$TAG.json | cut -c1-900
 fi
+timeout -k 10 200 python bench/conv_ws_probe.py --isolate --shapes 5,8 --tiles "4,8,1,3;2,8,1,3;4,8,2,3;2,8,2,3" \
+    > gpurun_out/ws_iso_$TAG.txt 2>&1 || { echo "ws probe failed"; tail -20 gpurun_out/ws_iso_$TAG.txt; exit 1; }
+cat gpurun_out/ws_iso_$TAG.txt | tail -30

@@ -789,6 +789,33 @@ def test_fused_attention_fwd_bwd(p_drop, B, S, nh, dh, flash, monkeypatch):
         assert _rel(g[:, sl], gr[:, sl]) < 3e-2, part
 
 
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+def test_attention_bwd_v2_matches_v1(p_drop):
+    """S = 128 attention backward: the register-resident v2 kernel (two workgroups per CU, S and dP recomputed
+    per phase) gives the same dQ/dK/dV as the v1 kernel with [q][k] LDS images, with and without dropout."""
+    from mdtf.ops import _native as NN
+    from mdtf.ops import transformer as T
+    torch.manual_seed(33)
+    B, S_, nh, dh = 5, 128, 12, 64
+    H = nh * dh
+    qkv = (torch.randn(B * S_, 3 * H, device=DEV) * 0.5).bfloat16()
+    mask = ((torch.rand(B, S_, device=DEV) < 0.2).float() * -10000.0)
+    dout = torch.randn(B * S_, H, device=DEV).bfloat16()
+    grads = []
+    prev = NN.fn("mdtf_set_attn_bwd")(2)
+    try:
+        for v in (2, 1):
+            NN.fn("mdtf_set_attn_bwd")(v)
+            x = qkv.clone().requires_grad_(True)
+            T._FusedAttention.apply(x, mask, B, S_, nh, p_drop, 777).backward(dout)
+            grads.append(x.grad.float())
+    finally:
+        NN.fn("mdtf_set_attn_bwd")(prev)
+    for part in range(3):
+        sl = slice(part * H, (part + 1) * H)
+        assert _rel(grads[0][:, sl], grads[1][:, sl]) < 1e-2, part
+
+
 def test_bert_fused_vs_unfused_attention_path(monkeypatch):
     """BERT step: fused-attention kernel path == unfused matmul/softmax path (same weights, no dropout)."""
     from mdtf.models import SyntheticBertLoader
