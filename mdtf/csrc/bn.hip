@@ -133,13 +133,18 @@ __global__ void __launch_bounds__(kThreads)
   const int W = tpr * 8;
   float* L0 = smem;
   float* L1 = smem + rg * W;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    L0[rgi * W + lane_c * 8 + i] = s0[i];
-    L1[rgi * W + lane_c * 8 + i] = s1[i];
+  // each thread's 8 partials as two 16-B stores: the 8 lanes of a store group cover 256 contiguous bytes (all 64
+  // banks once); eight scalar stores at an 8-float stride put 32 lanes on 4 banks
+  {
+    float4* d0 = reinterpret_cast<float4*>(L0 + rgi * W + lane_c * 8);
+    float4* d1 = reinterpret_cast<float4*>(L1 + rgi * W + lane_c * 8);
+    d0[0] = make_float4(s0[0], s0[1], s0[2], s0[3]);
+    d0[1] = make_float4(s0[4], s0[5], s0[6], s0[7]);
+    d1[0] = make_float4(s1[0], s1[1], s1[2], s1[3]);
+    d1[1] = make_float4(s1[4], s1[5], s1[6], s1[7]);
   }
   __syncthreads();
-  // tree over row groups
+  // tree over row groups (consecutive threads on consecutive floats)
   for (int step = rg / 2; step > 0; step >>= 1) {
     for (int e = t; e < step * W; e += kThreads) {
       int g = e / W, k = e % W;
@@ -775,10 +780,13 @@ __global__ void __launch_bounds__(kThreads)
   const int W = tpr * 8;
   float* L0 = smem;
   float* L1 = smem + rg * W;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    L0[rgi * W + lane_c * 8 + k] = s0[k];
-    L1[rgi * W + lane_c * 8 + k] = s1[k];
+  {
+    float4* d0 = reinterpret_cast<float4*>(L0 + rgi * W + lane_c * 8);
+    float4* d1 = reinterpret_cast<float4*>(L1 + rgi * W + lane_c * 8);
+    d0[0] = make_float4(s0[0], s0[1], s0[2], s0[3]);
+    d0[1] = make_float4(s0[4], s0[5], s0[6], s0[7]);
+    d1[0] = make_float4(s1[0], s1[1], s1[2], s1[3]);
+    d1[1] = make_float4(s1[4], s1[5], s1[6], s1[7]);
   }
   __syncthreads();
   for (int step = rg / 2; step > 0; step >>= 1) {
