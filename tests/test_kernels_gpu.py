@@ -1521,10 +1521,12 @@ def test_filter_transpose_cache_matches_per_call(monkeypatch):
 
 # ---------------------------------------------------------------------------- ping-pong GEMM core (csrc/gemm_pp.hip)
 @pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
-@pytest.mark.parametrize("M,N,K", [(1000, 768, 320), (264, 1536, 704), (4096, 768, 768), (768, 2304, 1024)])
+@pytest.mark.parametrize("M,N,K", [(1000, 768, 320), (264, 1536, 704), (4096, 768, 768), (768, 2304, 1024),
+                                   (1001, 768, 3072), (257, 512, 4096)])
 def test_gemm_core_three_layouts_vs_fp32(tile, M, N, K):
     """Forward (bias + GELU + saved pre-activation), data gradient (plain and accumulate) and fp32 weight
-    gradient (1 and 2 K-splits) of every tile on odd row counts and K in {320, 704, 768, 1024}, vs fp32."""
+    gradient (1 and 2 K-splits) of every tile on odd row counts (1001, 257) and K in {320, 704, 768, 1024, 3072,
+    4096}, vs fp32."""
     from mdtf.ops import mm
     torch.manual_seed(tile * 7 + M)
     rnd = lambda *s: (torch.rand(*s, device=DEV) * 2 - 1).bfloat16()
