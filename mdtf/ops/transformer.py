@@ -251,11 +251,15 @@ class _BertEmbed(torch.autograd.Function):
         return out[0], out[1], out[2], None, None
 
 
+# MDTF_BERT_EMBED=1: the one-kernel embedding (bert_embeddings)
+BERT_EMBED_FUSED = os.environ.get("MDTF_BERT_EMBED", "0") == "1"
+
+
 def bert_embeddings(word, pos, typ, ids, types):
     """BERT input embedding ``word[ids] + pos[0..S) + typ[types]`` for ``ids``/``types`` [B, S]: one fused kernel
     each way on the GPU (not in deterministic mode: the backward scatters with atomics); else three lookups."""
     B, S_ = ids.shape
-    if (N.use_native(word) and not N.deterministic() and word.dtype == torch.bfloat16 and pos.dtype == word.dtype
+    if (BERT_EMBED_FUSED and N.use_native(word) and not N.deterministic() and word.dtype == torch.bfloat16 and pos.dtype == word.dtype
             and typ.dtype == word.dtype and word.shape[1] % 8 == 0 and S_ <= pos.shape[0] and typ.shape[0] <= 4):
         return _BertEmbed.apply(word, pos, typ, ids, types)
     pos_ids = torch.arange(S_, device=ids.device).unsqueeze(0).expand(B, S_)
