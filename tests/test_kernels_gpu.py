@@ -540,23 +540,25 @@ def test_bert_embeddings_fused_vs_fp32(monkeypatch):
         assert _rel(a, r) < 2e-2
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_stem_conv_bn_relu_maxpool_vs_fp32(fused, monkeypatch):
+def test_stem_conv_bn_relu_maxpool_fused_vs_unfused(monkeypatch):
     """ResNet stem conv 7x7/2 -> BN -> ReLU -> max pool 3x3/2 SAME: the fused BN+ReLU+pool kernels
-    (csrc/bn.hip mdtf_bn_relu_maxpool_fwd / mdtf_maxpool_bn_bwd) and the unfused passes vs the fp32 CPU
-    reference (pooled output, input / filter / gamma / beta gradients, moving statistics)."""
+    (csrc/bn.hip mdtf_bn_relu_maxpool_fwd / mdtf_maxpool_bn_bwd) vs the unfused GPU passes on the same bf16
+    inputs (pooled output, filter / gamma / beta gradients, moving statistics), and the unfused path vs the fp32
+    CPU reference (looser: bf16 vs fp32 conv outputs flip some near-tie max-pool winners)."""
     from mdtf.ops import bn as B
-    monkeypatch.setattr(B, "FUSED_STEM", fused)
     calls = []
     real = B.bn_relu_maxpool_nhwc
     monkeypatch.setattr(B, "bn_relu_maxpool_nhwc", lambda *a, **k: calls.append(1) or real(*a, **k))
     torch.manual_seed(12)
-    x = torch.randn(4, 38, 38, 3)
+    x = torch.randn(8, 38, 38, 3)
     w = torch.randn(7, 7, 3, 64) * (1.0 / 147 ** 0.5)
     g = torch.rand(64) + 0.5
     b = torch.randn(64) * 0.2
+    dy0 = torch.randn(8, 10, 10, 64, generator=torch.Generator().manual_seed(3))
     outs = {}
-    for dev, dt in ((DEV, torch.bfloat16), ("cpu", torch.float32)):
+    for name, dev, dt, fused in (("fused", DEV, torch.bfloat16, True), ("unfused", DEV, torch.bfloat16, False),
+                                 ("cpu", "cpu", torch.float32, False)):
+        monkeypatch.setattr(B, "FUSED_STEM", fused)
         xx = x.to(dev).to(dt).requires_grad_(True)
         ww = w.to(dev).to(dt).requires_grad_(True)
         gg = g.to(dev).requires_grad_(True)
@@ -564,13 +566,13 @@ def test_stem_conv_bn_relu_maxpool_vs_fp32(fused, monkeypatch):
         mm = torch.zeros(64, device=dev)
         mv = torch.ones(64, device=dev)
         y = ops.conv_bn(xx, ww, gg, bb, mm, mv, 2, (3, 3), True, 0.9, 1e-5, True, None, pool=(3, 2, "SAME"))
-        assert tuple(y.shape) == (4, 10, 10, 64)
-        dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(3)).to(dev).to(dt)
-        y.backward(dy)
-        outs[dev] = dict(y=y.detach(), dw=ww.grad, dg=gg.grad, db=bb.grad, mm=mm, mv=mv)
-    assert calls == ([1] if fused else [])
+        assert tuple(y.shape) == (8, 10, 10, 64)
+        y.backward(dy0.to(dev).to(dt))
+        outs[name] = dict(y=y.detach(), dw=ww.grad, dg=gg.grad, db=bb.grad, mm=mm, mv=mv)
+    assert calls == [1]
     for key in ("y", "dw", "dg", "db", "mm", "mv"):
-        assert _rel(outs[DEV][key], outs["cpu"][key]) < 5e-2, key
+        assert _rel(outs["fused"][key], outs["unfused"][key]) < 2e-2, key
+        assert _rel(outs["unfused"][key], outs["cpu"][key]) < 8e-2, key
 
 
 @pytest.mark.parametrize("H,res", [(768, True), (1024, False), (64, True)])
