@@ -1079,6 +1079,30 @@ def test_bn_backward_stats_from_dgrad_epilogue(model, monkeypatch):
         assert _rel(gf[k], go[k]) < 1e-2, (k, _rel(gf[k], go[k]))
 
 
+class _TinyDual(object):
+    """A projection-shortcut block as ResNet builds it: the shortcut BN deferred into the residual BN
+    (relu(BN(x) + BN2(r)), ops.bn.DeferredBN); ``stride`` 2 makes both the shortcut and the 3x3 strided."""
+    stride = 1
+
+    def inference(self, x):
+        from mdtf.layers import tools
+        from mdtf.train import variables as V
+        store = V.get_store()
+        if store.compute_dtype is not None:
+            x = x.to(store.compute_dtype)
+        s = tools.conv_bn("c1", x, 64, 3, 1, relu=True)
+        sc = tools.conv_bn("sc", s, 128, 1, self.stride, relu=False, defer=True)
+        z = tools.conv_bn("c2", s, 64, 1, 1, relu=True)
+        z = tools.conv_bn("c3", z, 64, 3, self.stride, relu=True)
+        x = tools.conv_bn("c4", z, 128, 1, 1, relu=True, residual=sc)
+        x = ops.global_avg_pool(x)
+        return tools.dense("logits", x, 16)
+
+
+class _TinyDualStrided(_TinyDual):
+    stride = 2
+
+
 @pytest.mark.parametrize("model", ["res", "strided"])
 def test_dual_bn_backward_one_pass_matches_two(model, monkeypatch):
     """relu(BN(x) + BN2(r)) backward: both input gradients in one pass (mdtf_bn_bwd_dual, with the main BN's
@@ -1086,7 +1110,7 @@ def test_dual_bn_backward_one_pass_matches_two(model, monkeypatch):
     from mdtf.ops import bn as B
     global _Tiny
     saved = _Tiny
-    _Tiny = _TinyRes if model == "res" else _TinyStrided
+    _Tiny = _TinyDual if model == "res" else _TinyDualStrided
     try:
         torch.manual_seed(6)
         x = torch.randn(16, 12, 12, 64)
