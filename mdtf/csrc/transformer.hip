@@ -203,15 +203,17 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
       if (row + j * W < r1) do_row(row + j * W, gr[j], sr[j]);
   }
   // combine the 4 waves through LDS; block partials -> ws[block][2][H] (plain stores)
-  __shared__ float L[2][kT / 64][64 * 8];   // one 512-column slab per pass over NV
+  __shared__ __attribute__((aligned(16))) float L[2][kT / 64][64 * 8];   // one 512-column slab per pass over NV
   float* wg = ws + (long long)blockIdx.x * 2 * H;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      L[0][wave][lane * 8 + k] = dg[i][k];
-      L[1][wave][lane * 8 + k] = db[i][k];
-    }
+    // 16-B stores: 8 consecutive lanes cover all 64 banks (scalar stores at an 8-float stride hit 4 of them)
+    float4* l0 = reinterpret_cast<float4*>(&L[0][wave][lane * 8]);
+    float4* l1 = reinterpret_cast<float4*>(&L[1][wave][lane * 8]);
+    l0[0] = make_float4(dg[i][0], dg[i][1], dg[i][2], dg[i][3]);
+    l0[1] = make_float4(dg[i][4], dg[i][5], dg[i][6], dg[i][7]);
+    l1[0] = make_float4(db[i][0], db[i][1], db[i][2], db[i][3]);
+    l1[1] = make_float4(db[i][4], db[i][5], db[i][6], db[i][7]);
     __syncthreads();
     for (int j = threadIdx.x; j < 2 * 512; j += kT) {
       const int which = j >> 9, cc = j & 511;       // 0: dgamma, 1: dbeta
