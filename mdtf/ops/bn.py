@@ -41,8 +41,9 @@ def _f32(t):
 # MDTF_BN_TRACE=1: record (input shape, has residual, how the backward statistics were obtained) per BN backward
 BWD_TRACE = [] if os.environ.get("MDTF_BN_TRACE") == "1" else None
 DUAL_DZ = os.environ.get("MDTF_DUAL_DZ", "0") == "1"
-# MDTF_DUAL_BWD_FUSED=1: the dual BN's two input gradients in one pass (csrc/bn.hip mdtf_bn_bwd_dual)
-DUAL_FUSED = os.environ.get("MDTF_DUAL_BWD_FUSED", "0") == "1"
+# the dual BN's two input gradients in one pass (csrc/bn.hip mdtf_bn_bwd_dual); MDTF_DUAL_BWD_FUSED=0: two bn_dx
+# passes.  ResNet-50 A/B with the fused stem: 11102 / 11121 vs 10949 / 10983 img/s (profiles/resnet_fusions_r3.md)
+DUAL_FUSED = os.environ.get("MDTF_DUAL_BWD_FUSED", "1") != "0"
 DUAL_BWD = [0]       # one-pass dual backward launches (tests)
 
 
@@ -280,8 +281,8 @@ class _BNTrainDual(torch.autograd.Function):
         return (dx, out[0], out[1], None, None, dr, out[2], out[3], None, None, None, None, None, None)
 
 
-# MDTF_FUSED_STEM=1: the stem's BN + ReLU + max pool as one pass (bn_relu_maxpool_nhwc)
-FUSED_STEM = os.environ.get("MDTF_FUSED_STEM", "0") == "1"
+# the stem's BN + ReLU + max pool as one pass (bn_relu_maxpool_nhwc); MDTF_FUSED_STEM=0: BN apply + max pool
+FUSED_STEM = os.environ.get("MDTF_FUSED_STEM", "1") != "0"
 
 
 class _BNReluMaxPool(torch.autograd.Function):
