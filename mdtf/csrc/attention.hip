@@ -705,11 +705,11 @@ MDTF_EXPORT int mdtf_attn_bwd(const void* qkv, const float* mask, const void* ou
                               const long long* seed_off, hipStream_t st) {
   if (seq != S || dh != D) return MDTF_EUNSUPPORTED;
   if ((long long)B * S * 3 * nh * D * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
-  // MDTF_ATTN_BWD=v2: the register-resident kernel; v1 (default): the r1 kernel with [q][k] images
-  // (MDTF_ATTN_BWD_WAVES=4: its 4-wave form) -- A/B switches
+  // v2 (default; in the BERT-base step 39 vs 45 us per call, profiles/attention_bwd_v2_r3.md); MDTF_ATTN_BWD=v1:
+  // the r1 kernel with [q][k] images (MDTF_ATTN_BWD_WAVES=4: its 4-wave form) -- A/B switches
   if (g_attn_bwd < 0) {
     const char* e = getenv("MDTF_ATTN_BWD");
-    g_attn_bwd = (e && e[0] == 'v' && e[1] == '2') ? 2 : 1;
+    g_attn_bwd = (e && e[0] == 'v' && e[1] == '1') ? 1 : 2;
   }
   const bool v1 = g_attn_bwd == 1;
   static const bool w4 = [] {

@@ -472,8 +472,9 @@ MDTF_EXPORT int mdtf_softmax_bwd(const void* dy, const void* y, void* dx, long l
 }
 
 // BERT input embedding in one pass each way: out[t] = word[ids[t]] + pos[t % S] + type[types[t]] (fp32 sum, one
-// rounding).  Backward (thread = one (position, 8-column vector), looping over 8 batch rows, dy read once): word rows
-// by fp32 atomics, the position row and the <= 4 token-type rows summed in registers, then one atomic each.  Replaces three gathers + two adds forward and three scatter passes back.
+// rounding).  Backward: word rows by per-element fp32 atomics over the whole grid (embed_bwd_kernel); position and
+// <= 4 token-type rows by one thread per (position, 8-column vector) summing 8 batch rows in registers, then one
+// atomic each.  Replaces three gathers + two adds forward and three scatter passes back.
 namespace {
 constexpr int kTypeRows = 4;
 constexpr int kEmbBatch = 8;    // batch rows per backward block (grid.y = B / 8): the position partials add by atomics
@@ -505,10 +506,9 @@ __global__ void bert_embed_fwd_kernel(const bf16_t* __restrict__ word, const bf1
   }
 }
 
-__global__ void bert_embed_bwd_kernel(const bf16_t* __restrict__ dy, const long long* __restrict__ ids,
-                                      const long long* __restrict__ types, float* __restrict__ dword,
+__global__ void bert_embed_bwd_kernel(const bf16_t* __restrict__ dy, const long long* __restrict__ types,
                                       float* __restrict__ dpos, float* __restrict__ dtyp, int B, int S, int H,
-                                      long long vocab, int ntypes) {
+                                      int ntypes) {
   const int nvec = H / 8;
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (i >= (long long)S * nvec) return;
@@ -525,11 +525,7 @@ __global__ void bert_embed_bwd_kernel(const bf16_t* __restrict__ dy, const long 
     const long long t = (long long)b * S + s;
     float g[8];
     load_bf8(dy + t * H + c * 8, g);
-    const long long id = ids[t], ty = types[t];
-    if (dword && id >= 0 && id < vocab) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) atomicAdd(dword + id * H + c * 8 + k, g[k]);
-    }
+    const long long ty = types[t];
 #pragma unroll
     for (int k = 0; k < 8; ++k) ps[k] += g[k];
 #pragma unroll
@@ -566,10 +562,15 @@ MDTF_EXPORT int mdtf_bert_embed_bwd(const void* dy, const long long* ids, const 
                                     float* dpos, float* dtyp, int B, int S, int H, long long vocab, int ntypes,
                                     hipStream_t st) {
   if (H % 8 || ntypes > kTypeRows) return MDTF_EUNSUPPORTED;
+  // word rows: one thread per element (fp32 atomics spread over the whole grid); position / type rows: one thread
+  // per (position, 8-column vector) summing 8 batch rows in registers
+  const long long n = (long long)B * S;
+  if (dword)
+    hipLaunchKernelGGL(embed_bwd_kernel, dim3(gcap(n * H)), dim3(kT), 0, st, (const bf16_t*)dy, ids, dword, n, H,
+                       vocab);
   const long long threads = (long long)S * (H / 8);
   hipLaunchKernelGGL(bert_embed_bwd_kernel, dim3((unsigned)ceil_div(threads, kT), (unsigned)ceil_div(B, kEmbBatch)),
-                     dim3(kT), 0, st,
-                     (const bf16_t*)dy, ids, types, dword, dpos, dtyp, B, S, H, vocab, ntypes);
+                     dim3(kT), 0, st, (const bf16_t*)dy, types, dpos, dtyp, B, S, H, ntypes);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
