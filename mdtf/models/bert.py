@@ -121,7 +121,12 @@ class Bert(Model):
                     h = _dense("dense", h, H, act="gelu")
                     h = _ln("LayerNorm", h)
                 out_bias = V.get_variable("output_bias", [self.vocab], initializer=V.constant_initializer(0.0))
-                mlm = ops.dense_transposed(h, word, out_bias)                # tied decoder
+                # tied decoder on its own read of the embedding variable: both consumers then accumulate straight
+                # into the fp32 gradient slot (one shared read made autograd add their two zero-stride markers into
+                # a materialised [vocab, H] tensor and add that into the slot: two extra passes per step)
+                wvar = getattr(word, "_mdtf_var", None)
+                word_dec = wvar.read(store.compute_dtype) if wvar is not None else word
+                mlm = ops.dense_transposed(h, word_dec, out_bias)
             with V.variable_scope("seq_relationship"):
                 w = V.get_variable("output_weights", [2, H], initializer=_init())
                 b = V.get_variable("output_bias", [2], initializer=V.constant_initializer(0.0))
