@@ -13,6 +13,7 @@ Per kernel (aggregated over its dispatches in the profiled steps):
 """
 import collections
 import csv
+import os
 import re
 import sys
 
@@ -41,7 +42,11 @@ def main(prefix, top):
     aggs = []
     for i in (1, 2, 3):
         agg = collections.defaultdict(lambda: collections.defaultdict(float))
-        for d in load("%s_p%d/run_counter_collection.csv" % (prefix, i)):
+        path = "%s_p%d/run_counter_collection.csv" % (prefix, i)
+        if i > 1 and not os.path.exists(path):      # SQ-only runs: one pass
+            aggs.append(agg)
+            continue
+        for d in load(path):
             a = agg[short(d["name"])]
             a["calls"] += 1
             a["dur"] += d["dur"]
