@@ -1,0 +1,142 @@
+"""Correctness + graph-timed speed of the weight-gradient kernel (mdtf/csrc/gemm_wg.hip) against fp32 torch,
+hipBLASLt (fp32-output addmm) and the r2 conv-kernel weight gradient (ops.gemm.wgrad_into), on random data.
+
+  python bench/gemm_wg_probe.py --check     # numerics: tiles x stages x splits, segments, bias sums
+  python bench/gemm_wg_probe.py             # BERT-base / large weight-gradient shapes, every config
+Prints one JSON line per case.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from mdtf.ops import gemm, mm  # noqa: E402
+
+CONFIGS = [(128, 2), (128, 3), (128, 4), (256, 2), (256, 3)]
+
+
+def rnd(*shape):
+    return (torch.rand(*shape, device="cuda") * 2 - 1).to(torch.bfloat16)
+
+
+def rel_err(a, b):
+    return float((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6))
+
+
+def check():
+    ok = True
+    torch.manual_seed(0)
+    for (T, Kin, Nn, nseg) in [(512, 256, 384, 1), (1024, 768, 2304, 3), (8192, 768, 768, 1), (704, 512, 256, 2),
+                               (64, 128, 128, 1)]:
+        x, dy = rnd(T, Kin), rnd(T, Nn)
+        ns = Nn // nseg
+        ref = [x.float().t() @ dy[:, s * ns:(s + 1) * ns].float() for s in range(nseg)]
+        refb = [dy[:, s * ns:(s + 1) * ns].float().sum(0) for s in range(nseg)]
+        for (bm, st) in CONFIGS:
+            if Kin % bm:
+                continue
+            for sp in (1, 2, 3, 5):
+                g0 = [torch.randn(Kin, ns, device="cuda") for _ in range(nseg)]
+                b0 = [torch.randn(ns, device="cuda") for _ in range(nseg)]
+                gs = [g.clone() for g in g0]
+                bs = [b.clone() for b in b0]
+                done = mm.wg_into(gs, x, dy, dbs=bs, bm=bm, stages=st, splits=sp)
+                e = max(rel_err(gs[s] - g0[s], ref[s]) for s in range(nseg))
+                eb = max(rel_err(bs[s] - b0[s], refb[s]) for s in range(nseg))
+                # determinism across repeats (slab order fixed) -- same inputs, same bits
+                gs2 = [g.clone() for g in g0]
+                mm.wg_into(gs2, x, dy, bm=bm, stages=st, splits=sp)
+                same = all(torch.equal(gs[s], gs2[s]) for s in range(nseg))
+                good = bool(done) and e < 2e-3 and eb < 2e-3 and same
+                ok &= good
+                print(json.dumps({"check": [T, Kin, Nn, nseg], "bm": bm, "stages": st, "splits": sp,
+                                  "err": round(e, 7), "bias_err": round(eb, 7), "deterministic": same,
+                                  "ok": good}), flush=True)
+    # a column-slice dy (q|k|v gradient read in place) with the row stride of the full tensor
+    x, big = rnd(2048, 768), rnd(2048, 2304)
+    d = big[:, 768:1536]
+    g = torch.zeros(768, 768, device="cuda")
+    mm.wg_into([g], x, d)
+    e = rel_err(g, x.float().t() @ d.float())
+    ok &= e < 2e-3
+    print(json.dumps({"check": "slice", "err": round(e, 7), "ok": e < 2e-3}), flush=True)
+    return ok
+
+
+def gtime(fn, reps=20, rounds=5):
+    fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / reps)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+SHAPES = [("qkv", 8192, 768, 2304, 3), ("attn_out", 8192, 768, 768, 1), ("ffn_in", 8192, 768, 3072, 1),
+          ("ffn_out", 8192, 3072, 768, 1), ("large_qkv", 8192, 1024, 3072, 3), ("large_ffn_in", 8192, 1024, 4096, 1),
+          ("large_ffn_out", 8192, 4096, 1024, 1)]
+
+
+def bench(shapes):
+    for (name, T, Kin, Nn, nseg) in shapes:
+        flops = 2.0 * T * Kin * Nn
+        x, dy = rnd(T, Kin), rnd(T, Nn)
+        ns = Nn // nseg
+        gs = [torch.zeros(Kin, ns, device="cuda") for _ in range(nseg)]
+        bs = [torch.zeros(ns, device="cuda") for _ in range(nseg)]
+        res = {"shape": name, "T": T, "K": Kin, "N": Nn}
+        gw = torch.zeros(Kin, Nn, device="cuda")
+        res["hipblaslt"] = gtime(lambda: torch.addmm(gw, x.t(), dy, out_dtype=torch.float32, out=gw))
+
+        def legacy():
+            for s in range(nseg):
+                gemm.wgrad_into(gs[s], x, dy[:, s * ns:(s + 1) * ns], bs[s])
+        res["r2_kernel"] = gtime(legacy)
+        for (bm, st) in CONFIGS:
+            if Kin % bm:
+                continue
+            for sp in (1, 2, 3, 4, 6, 8, 12):
+                if (T // 64) < sp * 4:
+                    continue
+                res["wg_%d_%d_s%d" % (bm, st, sp)] = gtime(
+                    lambda: mm.wg_into(gs, x, dy, dbs=bs, bm=bm, stages=st, splits=sp))
+        pick = mm.wg_pick(Kin, Nn, T)
+        res["pick"] = "wg_%d_%d_s%d" % pick
+        best = min((v, k) for k, v in res.items() if isinstance(v, float) and k.startswith("wg_"))
+        out = {k: (round(v * 1000, 2) if isinstance(v, float) else v) for k, v in res.items()}   # us
+        out["best"] = best[1]
+        out["best_tf"] = round(flops / best[0] / 1e9, 1)
+        out["pick_tf"] = round(flops / res[res["pick"]] / 1e9, 1) if res["pick"] in res else None
+        out["lib_tf"] = round(flops / res["hipblaslt"] / 1e9, 1)
+        out["r2_tf"] = round(flops / res["r2_kernel"] / 1e9, 1)
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--check", action="store_true")
+    ap.add_argument("--shapes", default="")
+    args = ap.parse_args()
+    if args.check:
+        sys.exit(0 if check() else 1)
+    bench([s for s in SHAPES if not args.shapes or s[0] in args.shapes.split(",")])

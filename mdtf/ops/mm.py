@@ -145,3 +145,68 @@ def wgrad_into(gws, x, dy, dbs=None, tile=None, splits=None):
         return False
     N.check(rc, "gemm_pp wgrad")
     return True
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Weight-gradient kernel (csrc/gemm_wg.hip): C_s (fp32) += x^T dy[:, seg s], both operands k-major, split-K
+# partials reduced by the last arriving workgroup of each tile (no fp32 atomics on C, deterministic order).
+N.register("mdtf_gemm_wg", [N.P, N.L, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.P, N.L, N.P, N.I, N.I, N.I, N.P, N.P,
+                            N.P])
+N.register("mdtf_gemm_wg_slab_floats", [N.I, N.I, N.I, N.I], N.L)
+
+# (M, N, K) -> (bm, stages, splits): measured on an MI355X (bench/gemm_wg_probe.py); else wg_pick's model
+WG_TILES = {}
+_TICKETS = {}
+
+
+def _tickets(device, n):
+    t = _TICKETS.get(device)
+    if t is None or t.numel() < n:
+        t = torch.zeros(max(n, 4096), dtype=torch.int32, device=device)
+        _TICKETS[device] = t
+    return t
+
+
+def wg_pick(M, Nn, K):
+    """(bm, stages, splits) for C[M][Nn] += over K tokens: fill the 256 CUs (two 128-row workgroups or one
+    256-row workgroup per CU) with at least ~16 K-tiles per split."""
+    t = WG_TILES.get((M, Nn, K))
+    if t is not None:
+        return t
+    kt = K // 64
+    if M % 256 == 0:
+        tiles = (M // 256) * (Nn // 128)
+        sp = max(1, min(kt // 16, CUS // tiles))
+        if tiles * sp >= CUS // 2:
+            return 256, 3, sp
+    tiles = (M // 128) * (Nn // 128)
+    sp = max(1, min(kt // 16, (2 * CUS) // tiles))
+    return 128, 2, sp
+
+
+def wg_into(gws, x, dy, dbs=None, bm=None, stages=None, splits=None):
+    """gws[s] [K, Ns] fp32 += x^T @ dy[:, segment s] on the weight-gradient kernel.  x [T, K], dy [T, sum Ns]
+    bf16 with unit column stride (dy may be a column slice); dbs: fp32 [Ns] slots that also receive the column
+    sums of dy (the bias gradients).  Returns False when the kernel does not take the shape."""
+    gws = gws if isinstance(gws, (list, tuple)) else [gws]
+    T, Kin = x.shape
+    Nn = dy.shape[1]
+    ns = gws[0].shape[1]
+    if (x.stride(1) != 1 or dy.stride(1) != 1 or Nn % 128 or Kin % 128 or T % 64 or ns * len(gws) != Nn
+            or any(not g.is_contiguous() for g in gws)):
+        return False
+    pb, ps, psp = wg_pick(Kin, Nn, T)
+    bm, stages, splits = bm or pb, stages or ps, splits or psp
+    if N.deterministic():
+        dbs = None
+    slab_n = N.fn("mdtf_gemm_wg_slab_floats")(Kin, Nn, bm, splits)
+    slab = torch.empty(max(slab_n, 1), dtype=torch.float32, device=x.device) if slab_n > 0 else None
+    cnt = _tickets(x.device, (Kin // bm) * (Nn // 128)) if slab_n > 0 else None
+    rc = N.fn("mdtf_gemm_wg")(N.ptr(x), x.stride(0), N.ptr(dy), dy.stride(0), Kin, Nn, T, len(gws), ns,
+                              ctypes.cast(_arr(gws), ctypes.c_void_p), gws[0].stride(0),
+                              ctypes.cast(_arr(dbs), ctypes.c_void_p) if dbs else None, bm, stages, splits,
+                              N.ptr(slab), N.ptr(cnt), N.stream_ptr())
+    if rc == -2:
+        return False
+    N.check(min(rc, 0), "gemm_wg")
+    return True

@@ -1,12 +1,17 @@
 #!/bin/bash
+# Weight-gradient kernel: numerics, then the graph-timed sweep over the BERT shapes.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
 TAG=${1:-wg}
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread \
-    -k "wgrad or gemm" > gpurun_out/pytest_$TAG.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_$TAG.log; exit 1; }
-tail -1 gpurun_out/pytest_$TAG.log
-timeout -k 10 300 python bench/gemm_micro.py > gpurun_out/gemm_$TAG.md 2>&1 || { echo "gemm micro failed"; tail -20 gpurun_out/gemm_$TAG.md; exit 1; }
-cat gpurun_out/gemm_$TAG.md
-timeout -k 10 600 python -u bench/conv_autotune.py --passes wgrad --out gpurun_out/conv_table_$TAG.json \
-    --report gpurun_out/conv_autotune_$TAG.md > gpurun_out/tune_$TAG.log 2>&1 || { echo "autotune failed"; tail -30 gpurun_out/tune_$TAG.log; exit 1; }
-tail -1 gpurun_out/tune_$TAG.log
+timeout -k 10 180 python -u bench/gemm_wg_probe.py --check > gpurun_out/wg_check_$TAG.jsonl 2> gpurun_out/wg_check_$TAG.err \
+  || { echo "check failed"; grep -v '"ok": true' gpurun_out/wg_check_$TAG.jsonl | head -20; tail -5 gpurun_out/wg_check_$TAG.err; exit 1; }
+echo "check ok: $(grep -c '"ok": true' gpurun_out/wg_check_$TAG.jsonl)"
+timeout -k 10 300 python -u bench/gemm_wg_probe.py ${SHAPES:+--shapes $SHAPES} > gpurun_out/wg_probe_$TAG.jsonl 2> gpurun_out/wg_probe_$TAG.err \
+  || { echo "probe failed"; tail -5 gpurun_out/wg_probe_$TAG.err; exit 1; }
+python - <<'PY' gpurun_out/wg_probe_$TAG.jsonl
+import json, sys
+for l in open(sys.argv[1]):
+    d = json.loads(l)
+    print(d["shape"], "best", d["best"], d["best_tf"], "pick", d["pick"], d["pick_tf"], "lib", d["lib_tf"], "r2", d["r2_tf"])
+PY
