@@ -36,15 +36,47 @@ PP = DENSE == "pp"
 # Per-product engine inside "pp" (measured on MI355X, profiles/gemm_core_r3.md): the core takes the products where
 # it wins end to end -- a forward with a fused activation or several weight segments (no bias_act pass, no
 # q|k|v concatenation), and a data gradient that fuses the producer's activation backward or reads segments;
-# the plain products stay on hipBLASLt and the weight gradients on the conv-kernel wgrad (which beats both on
-# BERT's K = 8192 reductions).  MDTF_PP_{FWD,DGRAD,WGRAD} = all | fused | none (FWD also: act = only the forwards
+# the plain products stay on hipBLASLt.  Weight gradients (MDTF_PP_WGRAD=wg, default): the split-K weight-gradient
+# kernel (csrc/gemm_wg.hip, q|k|v in one launch) where _wg_ok says it wins, else the conv-kernel wgrad; "none" =
+# the conv-kernel wgrad everywhere.  MDTF_PP_{FWD,DGRAD,WGRAD} = all | fused | none (FWD also: act = only the forwards
 # with a fused activation; the layer's other products then run on the legacy path).  In-step BERT-base kernel
 # totals (profiles/bert_engine_ab_r3.md): the core's q|k|v forward (128x192 tiles) and segment dgrad lose to
 # hipBLASLt + cat, the GELU-consumer dgrad loses to the conv-kernel fused act dgrad; FFN-in + GELU is a tie
 # that saves the bias_act pass.
 PP_FWD = os.environ.get("MDTF_PP_FWD", "act")
 PP_DGRAD = os.environ.get("MDTF_PP_DGRAD", "fused")
-PP_WGRAD = os.environ.get("MDTF_PP_WGRAD", "none")
+PP_WGRAD = os.environ.get("MDTF_PP_WGRAD", "wg")
+
+
+def _wg_backward(ctx, x, dpre):
+    """Weight (+ bias) gradients of a dense layer on the weight-gradient kernel: every segment (q|k|v) in one
+    launch straight into the fp32 slots, bias column sums fused (not in deterministic mode: the per-split sums
+    are atomics; a column-sum pass then).  False (nothing done) where the kernel does not apply."""
+    if PP_WGRAD != "wg" or ctx.trans or any(sk is None for sk in ctx.wsinks):
+        return False
+    if ctx.has_b and any(sk is None for sk in ctx.bsinks):
+        return False
+    if not (x.dim() == 2 and x.dtype == torch.bfloat16 and dpre.dtype == torch.bfloat16 and _wg_ok(x, dpre)):
+        return False
+    fuse_b = ctx.has_b and not N.deterministic()
+    if not mm.wg_into([sk.grad for sk in ctx.wsinks], x, dpre, dbs=[sk.grad for sk in ctx.bsinks] if fuse_b else None):
+        return False
+    if ctx.has_b and not fuse_b:
+        col = 0
+        for j, n in enumerate(ctx.widths):
+            kernels.colsum_into(dpre[:, col:col + n].contiguous(), ctx.bsinks[j].grad)
+            col += n
+    return True
+
+
+def _wg_ok(x, d):
+    """Shapes the weight-gradient kernel (csrc/gemm_wg.hip) takes and wins on (profiles/gemm_wg_probe_r3a.jsonl):
+    K x N weights of 128-multiples over >= 4096 tokens except the square 768 x 768 (the split conv-kernel
+    weight gradient is 10 % faster there)."""
+    T, K = x.shape
+    Nn = d.shape[1]
+    return T >= 4096 and K % 128 == 0 and Nn % 128 == 0 and K * Nn > 768 * 768 and T % 64 == 0
+
 
 _ACT = {None: 0, "relu": 1, "gelu": 2}
 _fp32_out_ok = None      # does this torch build accept addmm(out_dtype=float32, out=...)?
@@ -386,6 +418,9 @@ class _Dense(torch.autograd.Function):
                     d2 = _hand_dgrad(dpre, w) if hand else None
                     xs.written((d2 if d2 is not None else torch.mm(dpre, w.t())).view(ctx.x_shape))
         ws, bs = ctx.like[:ctx.nw], ctx.like[ctx.nw:]
+        if _wg_backward(ctx, x, dpre):
+            return ((dx, None, None, None, None, None, None, None) + tuple(V.grad_marker(w) for w in ws)
+                    + tuple(V.grad_marker(b) for b in bs if ctx.has_b) + ((None,) * ctx.nw if not ctx.has_b else ()))
         gws, gbs = [], []
         bias_done = [False] * ctx.nw
         col = 0
@@ -503,7 +538,9 @@ def _backward_pp(ctx, dy):
     all_w = all(sk is not None for sk in wsinks)
     all_b = ctx.has_b and all(sk is not None for sk in bsinks)
     done = False
-    if all_w and (all_b or not ctx.has_b) and PP_WGRAD == "all":
+    if _wg_backward(ctx, x, dpre):
+        done = True
+    elif all_w and (all_b or not ctx.has_b) and PP_WGRAD == "all":
         if ctx.trans:                                   # w [N, K]: g += dy^T x  (C rows = N)
             done = ctx.nw == 1 and mm.wgrad_into([wsinks[0].grad], dpre, x, dbs=None)
             if done and ctx.has_b:

@@ -154,8 +154,10 @@ N.register("mdtf_gemm_wg", [N.P, N.L, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.P, N.
                             N.P])
 N.register("mdtf_gemm_wg_slab_floats", [N.I, N.I, N.I, N.I], N.L)
 
-# (M, N, K) -> (bm, stages, splits): measured on an MI355X (bench/gemm_wg_probe.py); else wg_pick's model
-WG_TILES = {}
+# (M, N, K) -> (bm, stages, splits): graph-timed on an MI355X (bench/gemm_wg_probe.py, profiles/gemm_wg_probe_r3a.jsonl)
+WG_TILES = {(768, 2304, 8192): (256, 2, 4), (768, 3072, 8192): (256, 2, 3), (3072, 768, 8192): (256, 2, 3),
+            (768, 768, 8192): (128, 2, 6), (1024, 3072, 8192): (256, 2, 2), (1024, 4096, 8192): (256, 2, 2),
+            (4096, 1024, 8192): (256, 2, 2)}
 _TICKETS = {}
 
 
@@ -168,20 +170,16 @@ def _tickets(device, n):
 
 
 def wg_pick(M, Nn, K):
-    """(bm, stages, splits) for C[M][Nn] += over K tokens: fill the 256 CUs (two 128-row workgroups or one
-    256-row workgroup per CU) with at least ~16 K-tiles per split."""
+    """(bm, stages, splits) for C[M][Nn] += over K tokens.  Measured: one 256-row workgroup per CU with a
+    2-stage ring beats the 128-row pairs; split until the tiles x splits grid just fills the 256 CUs (a second
+    round of workgroups costs more than it saves), keeping >= 16 K-tiles per split."""
     t = WG_TILES.get((M, Nn, K))
     if t is not None:
         return t
     kt = K // 64
-    if M % 256 == 0:
-        tiles = (M // 256) * (Nn // 128)
-        sp = max(1, min(kt // 16, CUS // tiles))
-        if tiles * sp >= CUS // 2:
-            return 256, 3, sp
-    tiles = (M // 128) * (Nn // 128)
-    sp = max(1, min(kt // 16, (2 * CUS) // tiles))
-    return 128, 2, sp
+    bm = 256 if M % 256 == 0 else 128
+    tiles = (M // bm) * (Nn // 128)
+    return bm, 2, max(1, min(kt // 16, CUS // tiles))
 
 
 def wg_into(gws, x, dy, dbs=None, bm=None, stages=None, splits=None):
