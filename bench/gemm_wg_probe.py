@@ -16,7 +16,7 @@ import torch  # noqa: E402
 
 from mdtf.ops import gemm, mm  # noqa: E402
 
-CONFIGS = [(128, 2), (128, 3), (128, 4), (256, 2), (256, 3)]
+CONFIGS = [(128, 2), (128, 3), (128, 4), (128, -3), (128, -4), (256, 2), (256, 3), (256, -3)]
 
 
 def rnd(*shape):

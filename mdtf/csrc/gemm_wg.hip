@@ -38,6 +38,7 @@ struct WgArgs {
   long long lda, ldb;        // row (k) strides of the stored operands, elements
   int M, N, K;               // C is M x N, K a multiple of 64
   int tiles_m, tiles_n, splits, kt_split;
+  int gm, gn;                // L2 groups: the workgroups one XCD runs cover a gm x gn block of tiles
   int bytes_a, bytes_b;      // buffer ranges (< 2 GiB)
   int nseg, seg_cols;        // C / bias-gradient column segments (each tile inside one segment)
   float* cf[4];
@@ -68,7 +69,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // of a transposed read touches ({0-3} + 8 fq and +4) land in 8 distinct 32-B bank slots.
 __device__ __forceinline__ int trg(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 
-template <int BM, int STAGES>
+template <int BM, int STAGES, bool PIPE>
 __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
   constexpr int BN = 128;
   constexpr int NT = 2 * BM, NW = NT / 64;          // waves: (BM / 64) rows x 2 columns of 64x64 blocks
@@ -87,7 +88,19 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
   const int ntiles = a.tiles_m * a.tiles_n;
   const int lid = xcd_remap(blockIdx.x, ntiles * a.splits);
   const int split = lid / ntiles, tile = lid - split * ntiles;
-  const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+  // tile order inside a split: gm x gn blocks (row-major over the block grid, edge blocks partial), so the
+  // contiguous range of logical ids one XCD gets shares few operand panels in its L2
+  int tm, tn;
+  {
+    const int gi = tile / (a.gm * a.tiles_n);
+    const int r2 = tile - gi * a.gm * a.tiles_n;
+    const int hm = min(a.gm, a.tiles_m - gi * a.gm);
+    const int gj = r2 / (hm * a.gn);
+    const int r3 = r2 - gj * hm * a.gn;
+    const int wn = min(a.gn, a.tiles_n - gj * a.gn);
+    tm = gi * a.gm + r3 / wn;
+    tn = gj * a.gn + r3 - (r3 / wn) * wn;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
   const int kt0 = split * a.kt_split;
   const int T = min(a.kt_split, a.K / 64 - kt0);
@@ -142,32 +155,66 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
   const short8 ones8 = {0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80};
   const bf16x8_t ones = __builtin_bit_cast(bf16x8_t, ones8);
 
+  auto load_frags = [&](const char* slotp, int s, bf16x8_t (&fa)[4], bf16x8_t (&fb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = frag(slotp, PA, wr * 64 + 16 * i, s);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = frag(slotp + BYTES_A, PB, wc * 64 + 16 * j, s);
+  };
+  auto mfmas = [&](const bf16x8_t (&fa)[4], const bf16x8_t (&fb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    if (dsum) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], ones, accb[j], 0, 0, 0);
+    }
+  };
+
 #pragma unroll
   for (int p = 0; p < STAGES - 1; ++p)
     if (p < T) issue(p);
-  for (int t = 0; t < T; ++t) {
-    // tile t landed: the tiles issued after it (up to STAGES - 2) may stay in flight
-    if (t + STAGES - 2 < T) wait_vmcnt<(STAGES - 2) * PER_TILE>();
+  if constexpr (!PIPE) {
+    for (int t = 0; t < T; ++t) {
+      // tile t landed: the tiles issued after it (up to STAGES - 2) may stay in flight
+      if (t + STAGES - 2 < T) wait_vmcnt<(STAGES - 2) * PER_TILE>();
+      else wait_vmcnt<0>();
+      barrier();
+      // every wave has finished reading tile t - 1: its slot takes tile t + STAGES - 1
+      if (t + STAGES - 1 < T) issue(t + STAGES - 1);
+      const char* slotp = smem + (t % STAGES) * SLOT;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8_t fa[4], fb[4];
+        load_frags(slotp, s, fa, fb);
+        mfmas(fa, fb);
+      }
+    }
+  } else {
+    // mid-tile barrier: the fragment reads of the next step always overlap MFMAs of the current one.
+    //   iteration t:  read s1(t) | MFMA s0(t) | wait tile t+1, barrier, DMA tile t+S-1 into tile t-1's slot,
+    //                 read s0(t+1) | MFMA s1(t)
+    // Every read of tile t-1 retired before iteration t (its MFMAs ran in iteration t-1), so the DMA after the
+    // barrier cannot overwrite live data; tile t+1 is read only after every wave's vmcnt wait + the barrier.
+    static_assert(STAGES >= 3, "PIPE needs the tile after next in flight");
+    if (STAGES - 2 < T) wait_vmcnt<(STAGES - 2) * PER_TILE>();
     else wait_vmcnt<0>();
     barrier();
-    // every wave has finished reading tile t - 1: its slot takes tile t + STAGES - 1
-    if (t + STAGES - 1 < T) issue(t + STAGES - 1);
-    const char* slotp = smem + (t % STAGES) * SLOT;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8_t fa[4], fb[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = frag(slotp, PA, wr * 64 + 16 * i, s);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = frag(slotp + BYTES_A, PB, wc * 64 + 16 * j, s);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-      if (dsum) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], ones, accb[j], 0, 0, 0);
+    bf16x8_t a0[4], b0[4], a1[4], b1[4];
+    load_frags(smem, 0, a0, b0);
+    for (int t = 0; t < T; ++t) {
+      const char* slotp = smem + (t % STAGES) * SLOT;
+      load_frags(slotp, 1, a1, b1);
+      mfmas(a0, b0);
+      if (t + 1 < T) {
+        if (t + STAGES - 2 < T) wait_vmcnt<(STAGES - 3) * PER_TILE>();
+        else wait_vmcnt<0>();
+        barrier();
+        if (t + STAGES - 1 < T) issue(t + STAGES - 1);
+        load_frags(smem + ((t + 1) % STAGES) * SLOT, 0, a0, b0);
       }
+      mfmas(a1, b1);
     }
   }
 
@@ -255,10 +302,10 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
   }
 }
 
-template <int BM, int STAGES>
+template <int BM, int STAGES, bool PIPE>
 int launch_wg(const WgArgs& a, hipStream_t st) {
   constexpr int lds = STAGES * (BM + 128) * 128;
-  auto k = gemm_wg_kernel<BM, STAGES>;
+  auto k = gemm_wg_kernel<BM, STAGES, PIPE>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -280,7 +327,7 @@ MDTF_EXPORT long long mdtf_gemm_wg_slab_floats(int M, int N, int bm, int splits)
 }
 
 // C_s[M][seg_cols] (fp32, ldc) += A^T B over the segment's columns; A [K][lda], B [K][ldb] bf16 (k-major), M % bm,
-// N % 128, K % 64 and seg_cols % 128 == 0.  bm: 128 or 256; stages 2..4; splits: K-split count (clamped so every
+// N % 128, K % 64 and seg_cols % 128 == 0.  bm: 128 or 256; stages 2..4 (negative: the pipelined loop); splits: K-split count (clamped so every
 // split has at least one 64-deep tile).  dbias (per segment, may be null): += column sums of B.  slab / cnt:
 // workspace of mdtf_gemm_wg_slab_floats() floats and tiles zeroed ints (splits > 1).  Returns the splits used
 // (> 0) or a negative MDTF status.
@@ -318,15 +365,39 @@ MDTF_EXPORT int mdtf_gemm_wg(const bf16_t* A, long long lda, const bf16_t* B, lo
   a.ldc = ldc;
   a.slab = slab;
   a.cnt = cnt;
+  // L2 block per XCD: ~ceil(grid / 8) tiles of one split as the gm x gn block with the fewest operand columns
+  // (gm * bm + gn * 128) -- a speed choice only, any gm / gn is correct
+  {
+    const int tiles = a.tiles_m * a.tiles_n;
+    const int per_xcd = (tiles * a.splits + 7) / 8;
+    const int want = per_xcd < tiles ? per_xcd : tiles;
+    int best = 1 << 30;
+    a.gm = a.tiles_m;
+    a.gn = a.tiles_n;
+    for (int g = 1; g <= a.tiles_m; ++g) {
+      const int h = (want + g - 1) / g;
+      if (h > a.tiles_n) continue;
+      const int cost = g * bm + h * 128;
+      if (cost < best) {
+        best = cost;
+        a.gm = g;
+        a.gn = h;
+      }
+    }
+  }
   hipStream_t st = static_cast<hipStream_t>(stream);
   int rc = MDTF_EINVAL;
+  // stages < 0: the mid-tile-barrier pipelined loop with |stages| LDS stages
   if (bm == 128) {
-    if (stages == 2) rc = launch_wg<128, 2>(a, st);
-    else if (stages == 3) rc = launch_wg<128, 3>(a, st);
-    else if (stages == 4) rc = launch_wg<128, 4>(a, st);
+    if (stages == 2) rc = launch_wg<128, 2, false>(a, st);
+    else if (stages == 3) rc = launch_wg<128, 3, false>(a, st);
+    else if (stages == 4) rc = launch_wg<128, 4, false>(a, st);
+    else if (stages == -3) rc = launch_wg<128, 3, true>(a, st);
+    else if (stages == -4) rc = launch_wg<128, 4, true>(a, st);
   } else {
-    if (stages == 2) rc = launch_wg<256, 2>(a, st);
-    else if (stages == 3) rc = launch_wg<256, 3>(a, st);
+    if (stages == 2) rc = launch_wg<256, 2, false>(a, st);
+    else if (stages == 3) rc = launch_wg<256, 3, false>(a, st);
+    else if (stages == -3) rc = launch_wg<256, 3, true>(a, st);
   }
   return rc == 0 ? a.splits : rc;
 }

@@ -154,8 +154,9 @@ N.register("mdtf_gemm_wg", [N.P, N.L, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.P, N.
                             N.P])
 N.register("mdtf_gemm_wg_slab_floats", [N.I, N.I, N.I, N.I], N.L)
 
-# (M, N, K) -> (bm, stages, splits): graph-timed on an MI355X (bench/gemm_wg_probe.py, profiles/gemm_wg_probe_r3a.jsonl)
-WG_TILES = {(768, 2304, 8192): (256, 2, 4), (768, 3072, 8192): (256, 2, 3), (3072, 768, 8192): (256, 2, 3),
+# (M, N, K) -> (bm, stages, splits): graph-timed on an MI355X (bench/gemm_wg_probe.py, profiles/gemm_wg_probe_r3b.jsonl;
+# the 3/4-stage rings and the mid-tile-barrier loop (stages < 0) measured slower than the 2-stage ring on every shape)
+WG_TILES = {(768, 2304, 8192): (256, 2, 4), (768, 3072, 8192): (256, 2, 3), (3072, 768, 8192): (128, 2, 3),
             (768, 768, 8192): (128, 2, 6), (1024, 3072, 8192): (256, 2, 2), (1024, 4096, 8192): (256, 2, 2),
             (4096, 1024, 8192): (256, 2, 2)}
 _TICKETS = {}

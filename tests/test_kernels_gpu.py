@@ -1607,6 +1607,76 @@ def test_gemm_core_segments_and_fused_epilogues():
     assert _rel(torch.cat(dbs), dy.float().sum(0)) < 1e-4
 
 
+# ------------------------------------------------------------------ weight-gradient kernel (csrc/gemm_wg.hip)
+@pytest.mark.parametrize("bm,stages", [(128, 2), (128, 3), (128, -3), (128, -4), (256, 2), (256, 3), (256, -3)])
+@pytest.mark.parametrize("T,K,N,nseg", [(8192, 768, 2304, 3), (4096, 3072, 768, 1), (704, 256, 384, 1),
+                                        (64, 256, 128, 1)])
+@pytest.mark.parametrize("splits", [1, 3, 7])
+def test_gemm_wg_vs_fp32(bm, stages, T, K, N, nseg, splits):
+    """C_s (fp32) += x^T dy[:, seg s] with the fused bias column sums, every ring depth / loop variant and split
+    count (slabs summed by the last arriving workgroup), vs fp32; repeated launches are bitwise equal."""
+    from mdtf.ops import mm
+    if K % bm:
+        pytest.skip("tile does not divide K")
+    torch.manual_seed(T + K + splits)
+    rnd = lambda *s: (torch.rand(*s, device=DEV) * 2 - 1).bfloat16()
+    x, dy = rnd(T, K), rnd(T, N)
+    ns = N // nseg
+    g0 = [torch.randn(K, ns, device=DEV) for _ in range(nseg)]
+    b0 = [torch.randn(ns, device=DEV) for _ in range(nseg)]
+    gs, bs = [g.clone() for g in g0], [b.clone() for b in b0]
+    assert mm.wg_into(gs, x, dy, dbs=bs, bm=bm, stages=stages, splits=splits)
+    for s in range(nseg):
+        d = dy[:, s * ns:(s + 1) * ns].float()
+        assert _rel(gs[s] - g0[s], x.float().t() @ d) < 1e-4
+        assert _rel(bs[s] - b0[s], d.sum(0)) < 1e-4
+    gs2 = [g.clone() for g in g0]
+    assert mm.wg_into(gs2, x, dy, bm=bm, stages=stages, splits=splits)
+    assert all(torch.equal(gs[s], gs2[s]) for s in range(nseg))
+
+
+def test_gemm_wg_column_slice_and_dense_backward_route():
+    """dy read in place as a column slice of a wider tensor, and the BERT dense layers' backward taking the
+    weight-gradient kernel (q|k|v segments, FFN) with gradients equal to fp32 autograd."""
+    from mdtf.ops import gemm, mm
+    torch.manual_seed(11)
+    rnd = lambda *s: (torch.rand(*s, device=DEV) * 2 - 1).bfloat16()
+    x, big = rnd(4096, 768), rnd(4096, 2304)
+    d = big[:, 768:1536]
+    g = torch.zeros(768, 768, device=DEV)
+    assert mm.wg_into([g], x, d)
+    assert _rel(g, x.float().t() @ d.float()) < 1e-4
+    assert gemm.PP_WGRAD == "wg"
+    calls = []
+    orig = mm.wg_into
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+    mm.wg_into = spy
+
+    class _Slot(object):            # a Variable's fp32 gradient slot, as V.grad_sink sees it
+        def __init__(self, shape):
+            self.grad = torch.zeros(shape, device=DEV)
+    try:
+        xin = rnd(4096, 768).requires_grad_(True)
+        ws = [(torch.randn(768, 768, device=DEV) * 0.05).bfloat16().requires_grad_(True) for _ in range(3)]
+        bs = [(torch.randn(768, device=DEV) * 0.05).bfloat16().requires_grad_(True) for _ in range(3)]
+        for t in ws + bs:
+            t._mdtf_var = _Slot(t.shape)
+        y = ops.dense_multi(xin, ws, bs)
+        gy = rnd(*y.shape)
+        y.backward(gy)
+    finally:
+        mm.wg_into = orig
+    assert calls, "the dense backward did not take the weight-gradient kernel"
+    xf = xin.detach().float()
+    for j in range(3):
+        d = gy[:, j * 768:(j + 1) * 768].float()
+        assert _rel(ws[j]._mdtf_var.grad, xf.t() @ d) < 1e-4
+        assert _rel(bs[j]._mdtf_var.grad, d.sum(0)) < 1e-4
+
+
 def test_fused_apply_multi_matches_sequential():
     """The async parameter server's batched apply: k sequential Adam / momentum updates in one kernel pass."""
     from mdtf.ops import optim
