@@ -48,6 +48,29 @@ PP_DGRAD = os.environ.get("MDTF_PP_DGRAD", "fused")
 PP_WGRAD = os.environ.get("MDTF_PP_WGRAD", "wg")
 
 
+# MDTF_DENSE_WGRAD_STREAM=1: a dense layer's weight (+ bias) gradients run on the side stream beside the data-gradient
+# chain (ops.conv's side stream, joined by the reducer before a bucket is reduced and at the end of backward), so
+# the GEMM tails of the two chains overlap; only when every output of the section lands in a gradient slot.
+DENSE_WGRAD_STREAM = os.environ.get("MDTF_DENSE_WGRAD_STREAM", "0") == "1"
+
+
+def _wgrad_section(ctx, x, dpre):
+    """Context for a dense backward's weight-gradient section: the side stream when enabled and safe."""
+    import contextlib
+    sinks = list(ctx.wsinks) + (list(ctx.bsinks) if ctx.has_b else [])
+    # every output must be a slot, and this must be each slot's last contribution of the step (uses == 1): an
+    # earlier main-stream writer is ordered by the wait below, a later one would race the side stream
+    if not (DENSE_WGRAD_STREAM and x.is_cuda and all(sk is not None and getattr(sk, "uses", 1) == 1 for sk in sinks)):
+        return contextlib.nullcontext()
+    from . import conv as _conv
+    side = _conv._side_stream(x.device)
+    side.wait_stream(torch.cuda.current_stream(x.device))
+    x.record_stream(side)
+    dpre.record_stream(side)
+    _conv._PENDING.add(x.device)
+    return torch.cuda.stream(side)
+
+
 def _wg_backward(ctx, x, dpre):
     """Weight (+ bias) gradients of a dense layer on the weight-gradient kernel: every segment (q|k|v) in one
     launch straight into the fp32 slots, bias column sums fused (not in deterministic mode: the per-split sums
@@ -418,9 +441,15 @@ class _Dense(torch.autograd.Function):
                     d2 = _hand_dgrad(dpre, w) if hand else None
                     xs.written((d2 if d2 is not None else torch.mm(dpre, w.t())).view(ctx.x_shape))
         ws, bs = ctx.like[:ctx.nw], ctx.like[ctx.nw:]
+        with _wgrad_section(ctx, x, dpre):
+            gws, gbs = _Dense._weight_grads(ctx, x, dpre, ws, bs)
+        return (dx, None, None, None, None, None, None, None) + tuple(gws) + tuple(gbs)
+
+    @staticmethod
+    def _weight_grads(ctx, x, dpre, ws, bs):
         if _wg_backward(ctx, x, dpre):
-            return ((dx, None, None, None, None, None, None, None) + tuple(V.grad_marker(w) for w in ws)
-                    + tuple(V.grad_marker(b) for b in bs if ctx.has_b) + ((None,) * ctx.nw if not ctx.has_b else ()))
+            return ([V.grad_marker(w) for w in ws],
+                    [V.grad_marker(b) for b in bs] if ctx.has_b else [None] * ctx.nw)
         gws, gbs = [], []
         bias_done = [False] * ctx.nw
         col = 0
@@ -479,7 +508,55 @@ class _Dense(torch.autograd.Function):
                         gbs.append(part.to(bs[j].dtype))
         else:
             gbs = [None] * ctx.nw
-        return (dx, None, None, None, None, None, None, None) + tuple(gws) + tuple(gbs)
+        return gws, gbs
+
+
+def _pp_weight_grads(ctx, x, dpre, ws, bs):
+    """Weight (+ bias) gradients of the core backward, straight into the fp32 slots."""
+    wsinks, bsinks = ctx.wsinks, ctx.bsinks
+    gws, gbs = [None] * ctx.nw, [None] * ctx.nw
+    all_w = all(sk is not None for sk in wsinks)
+    all_b = ctx.has_b and all(sk is not None for sk in bsinks)
+    done = False
+    if _wg_backward(ctx, x, dpre):
+        done = True
+    elif all_w and (all_b or not ctx.has_b) and PP_WGRAD == "all":
+        if ctx.trans:                                   # w [N, K]: g += dy^T x  (C rows = N)
+            done = ctx.nw == 1 and mm.wgrad_into([wsinks[0].grad], dpre, x, dbs=None)
+            if done and ctx.has_b:
+                kernels.colsum_into(dpre, bsinks[0].grad)
+        else:
+            done = mm.wgrad_into([sk.grad for sk in wsinks], x, dpre,
+                                 dbs=[sk.grad for sk in bsinks] if ctx.has_b else None)
+    if done:
+        gws = [V.grad_marker(w) for w in ws]
+        if ctx.has_b:
+            gbs = [V.grad_marker(b) for b in bs]
+    else:
+        col = 0
+        for j, n in enumerate(ctx.widths):
+            d = dpre[:, col:col + n] if ctx.nw > 1 else dpre
+            col += n
+            sink = wsinks[j]
+            bias_done = False
+            if sink is not None:
+                if ctx.trans:
+                    _accum_mm(sink.grad, d.t(), x)
+                else:                                   # conv-kernel wgrad, bias gradient fused in
+                    bsk = bsinks[j] if ctx.has_b else None
+                    bias_done = wgrad_into(sink.grad, x, d, bsk.grad if bsk is not None else None)
+                gws[j] = V.grad_marker(ws[j])
+            elif ctx.needs_input_grad[8 + j]:
+                g = torch.mm(d.t(), x) if ctx.trans else torch.mm(x.t(), d)
+                gws[j] = g.to(ws[j].dtype)
+            if ctx.has_b and bias_done:
+                gbs[j] = V.grad_marker(bs[j])
+            elif ctx.has_b and bsinks[j] is not None:
+                kernels.colsum_into(d, bsinks[j].grad) if d.is_contiguous() else bsinks[j].grad.add_(d.float().sum(0))
+                gbs[j] = V.grad_marker(bs[j])
+            elif ctx.has_b:
+                gbs[j] = d.float().sum(0).to(bs[j].dtype)
+    return gws, gbs
 
 
 def _backward_pp(ctx, dy):
@@ -533,49 +610,8 @@ def _backward_pp(ctx, dy):
                     d2 = torch.mm(dpre, torch.cat(ws, 1).t() if ctx.nw > 1 else ws[0].t())
                 xs.written(d2.view(ctx.x_shape))
     # weight (+ bias) gradients straight into the fp32 slots
-    wsinks, bsinks = ctx.wsinks, ctx.bsinks
-    gws, gbs = [None] * ctx.nw, [None] * ctx.nw
-    all_w = all(sk is not None for sk in wsinks)
-    all_b = ctx.has_b and all(sk is not None for sk in bsinks)
-    done = False
-    if _wg_backward(ctx, x, dpre):
-        done = True
-    elif all_w and (all_b or not ctx.has_b) and PP_WGRAD == "all":
-        if ctx.trans:                                   # w [N, K]: g += dy^T x  (C rows = N)
-            done = ctx.nw == 1 and mm.wgrad_into([wsinks[0].grad], dpre, x, dbs=None)
-            if done and ctx.has_b:
-                kernels.colsum_into(dpre, bsinks[0].grad)
-        else:
-            done = mm.wgrad_into([sk.grad for sk in wsinks], x, dpre,
-                                 dbs=[sk.grad for sk in bsinks] if ctx.has_b else None)
-    if done:
-        gws = [V.grad_marker(w) for w in ws]
-        if ctx.has_b:
-            gbs = [V.grad_marker(b) for b in bs]
-    else:
-        col = 0
-        for j, n in enumerate(ctx.widths):
-            d = dpre[:, col:col + n] if ctx.nw > 1 else dpre
-            col += n
-            sink = wsinks[j]
-            bias_done = False
-            if sink is not None:
-                if ctx.trans:
-                    _accum_mm(sink.grad, d.t(), x)
-                else:                                   # conv-kernel wgrad, bias gradient fused in
-                    bsk = bsinks[j] if ctx.has_b else None
-                    bias_done = wgrad_into(sink.grad, x, d, bsk.grad if bsk is not None else None)
-                gws[j] = V.grad_marker(ws[j])
-            elif ctx.needs_input_grad[8 + j]:
-                g = torch.mm(d.t(), x) if ctx.trans else torch.mm(x.t(), d)
-                gws[j] = g.to(ws[j].dtype)
-            if ctx.has_b and bias_done:
-                gbs[j] = V.grad_marker(bs[j])
-            elif ctx.has_b and bsinks[j] is not None:
-                kernels.colsum_into(d, bsinks[j].grad) if d.is_contiguous() else bsinks[j].grad.add_(d.float().sum(0))
-                gbs[j] = V.grad_marker(bs[j])
-            elif ctx.has_b:
-                gbs[j] = d.float().sum(0).to(bs[j].dtype)
+    with _wgrad_section(ctx, x, dpre):
+        gws, gbs = _pp_weight_grads(ctx, x, dpre, ws, bs)
     return (dx, None, None, None, None, None, None, None) + tuple(gws) + tuple(gbs)
 
 

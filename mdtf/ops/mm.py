@@ -163,10 +163,13 @@ _TICKETS = {}
 
 
 def _tickets(device, n):
-    t = _TICKETS.get(device)
+    """Zeroed per-tile arrival tickets, one buffer per (device, stream): launches on one stream are ordered, and
+    every launch leaves its tickets at zero (the last arriver resets them)."""
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    t = _TICKETS.get(key)
     if t is None or t.numel() < n:
         t = torch.zeros(max(n, 4096), dtype=torch.int32, device=device)
-        _TICKETS[device] = t
+        _TICKETS[key] = t
     return t
 
 
