@@ -15,6 +15,7 @@ Tile codes: 0 = 256x256, 1 = 256x128, 2 = 128x256, 3 = 128x128, 4 = 256x192, 5 =
 ``TILES`` pins measured per-shape choices (``bench/gemm_pp_probe.py`` on an MI355X).
 """
 import ctypes
+import os
 
 import torch
 
@@ -160,6 +161,9 @@ WG_TILES = {(768, 2304, 8192): (256, 2, 4), (768, 3072, 8192): (256, 2, 3), (307
             (768, 768, 8192): (128, 2, 6), (1024, 3072, 8192): (256, 2, 2), (1024, 4096, 8192): (256, 2, 2),
             (4096, 1024, 8192): (256, 2, 2)}
 _TICKETS = {}
+# MDTF_WG_STAGES: force the ring depth of the table entries (in-step A/B: the operands of the step are HBM-cold,
+# the graph-timed probe's are MALL-resident)
+_WG_STAGES = int(os.environ["MDTF_WG_STAGES"]) if os.environ.get("MDTF_WG_STAGES") else None
 
 
 def _tickets(device, n):
@@ -179,7 +183,7 @@ def wg_pick(M, Nn, K):
     round of workgroups costs more than it saves), keeping >= 16 K-tiles per split."""
     t = WG_TILES.get((M, Nn, K))
     if t is not None:
-        return t
+        return t if _WG_STAGES is None else (t[0], _WG_STAGES, t[2])
     kt = K // 64
     bm = 256 if M % 256 == 0 else 128
     tiles = (M // bm) * (Nn // 128)
