@@ -139,7 +139,9 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
       gm[i][4] = g1.x; gm[i][5] = g1.y; gm[i][6] = g1.z; gm[i][7] = g1.w;
     }
   }
-  auto load_row = [&](long long row, uint4 (&gr)[NV], uint4 (&sr)[NV]) {
+  auto load_row = [&](long long row, uint4 (&gr)[NV], uint4 (&sr)[NV], float& mu, float& rs) {
+    mu = mean[row];       // issued with the row's vectors, not behind the previous row's stores
+    rs = rstd[row];
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = lane + i * 64;
@@ -149,8 +151,7 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
       }
     }
   };
-  auto do_row = [&](long long row, const uint4 (&gr)[NV], const uint4 (&sr)[NV]) {
-    const float mu = mean[row], rs = rstd[row];
+  auto do_row = [&](long long row, const uint4 (&gr)[NV], const uint4 (&sr)[NV], const float mu, const float rs) {
     float g[NV][8], xh[NV][8];
     float a = 0.f, b = 0.f;
 #pragma unroll
@@ -195,12 +196,13 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
   constexpr int W = kT / 64, RIF = NV <= 2 ? 4 : 1;
   for (long long row = r0 + wave; row < r1; row += RIF * W) {
     uint4 gr[RIF][NV], sr[RIF][NV];
+    float mu[RIF], rs[RIF];
 #pragma unroll
     for (int j = 0; j < RIF; ++j)
-      if (row + j * W < r1) load_row(row + j * W, gr[j], sr[j]);
+      if (row + j * W < r1) load_row(row + j * W, gr[j], sr[j], mu[j], rs[j]);
 #pragma unroll
     for (int j = 0; j < RIF; ++j)
-      if (row + j * W < r1) do_row(row + j * W, gr[j], sr[j]);
+      if (row + j * W < r1) do_row(row + j * W, gr[j], sr[j], mu[j], rs[j]);
   }
   // combine the 4 waves through LDS; block partials -> ws[block][2][H] (plain stores)
   __shared__ __attribute__((aligned(16))) float L[2][kT / 64][64 * 8];   // one 512-column slab per pass over NV
