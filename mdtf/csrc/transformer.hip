@@ -37,7 +37,17 @@ __device__ __forceinline__ uint32_t step_seed(uint32_t seed, const long long* se
   return seed_off ? seed ^ ((uint32_t)(*seed_off) * 0x85EBCA6Bu) : seed;
 }
 
-template <int NV>
+// sum over the LPR lanes that share a row (LPR = 64: the wave; 32: each half-wave holds its own row)
+template <int LPR>
+__device__ __forceinline__ float row_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// LPR lanes per row: 64 (a wave per row) or 32 (two rows per wave: H = 768 is 96 vectors = 32 lanes x 3, where a
+// whole wave would leave half its lanes idle on the second vector)
+template <int NV, int LPR>
 __global__ void __launch_bounds__(kT) ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                                    bf16_t* __restrict__ y, bf16_t* __restrict__ s_out,
@@ -45,15 +55,15 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const bf16_t* __restrict__ x
                                                    long long rows, int H, float eps, uint32_t thr, float inv_keep,
                                                    uint32_t seed, const long long* __restrict__ seed_off) {
   seed = step_seed(seed, seed_off);
-  const int lane = threadIdx.x & 63;
-  const long long row = (long long)blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  const int lane = threadIdx.x & (LPR - 1);
+  const long long row = (long long)blockIdx.x * (kT / LPR) + (threadIdx.x / LPR);
+  if (row >= rows) return;      // (LPR = 32: the row sums shuffle inside each 32-lane half only)
   const int nvec = H / 8;
   float v[NV][8];
   float sum = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int c = (lane + i * 64);
+    const int c = (lane + i * LPR);
     if (c < nvec) {
       load_bf8(x + row * H + c * 8, v[i]);
       if (thr) {      // fused dropout on the branch input (before the residual add)
@@ -71,11 +81,11 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const bf16_t* __restrict__ x
       for (int k = 0; k < 8; ++k) sum += v[i][k];
     }
   }
-  const float mean = wave_sum(sum) / (float)H;
+  const float mean = row_sum<LPR>(sum) / (float)H;
   float sq = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int c = (lane + i * 64);
+    const int c = (lane + i * LPR);
     if (c < nvec) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -84,10 +94,10 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const bf16_t* __restrict__ x
       }
     }
   }
-  const float rstd = rsqrtf(wave_sum(sq) / (float)H + eps);
+  const float rstd = rsqrtf(row_sum<LPR>(sq) / (float)H + eps);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int c = (lane + i * 64);
+    const int c = (lane + i * LPR);
     if (c < nvec) {
       if (s_out) store_bf8(s_out + row * H + c * 8, v[i]);
       const float4 g0 = *reinterpret_cast<const float4*>(gamma + c * 8);
@@ -108,8 +118,9 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const bf16_t* __restrict__ x
   }
 }
 
-// each block (4 waves) walks rows_per_block rows; dgamma/dbeta partials live in registers
-template <int NV>
+// each block (kT / LPR row slices: whole waves, or half-waves for LPR = 32) walks rows_per_block rows;
+// dgamma/dbeta partials live in registers
+template <int NV, int LPR>
 __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
                                                    const float* __restrict__ gamma, const float* __restrict__ mean,
                                                    const float* __restrict__ rstd, bf16_t* __restrict__ dx,
@@ -118,7 +129,8 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
                                                    uint32_t thr, float inv_keep, uint32_t seed,
                                                    const long long* __restrict__ seed_off) {
   seed = step_seed(seed, seed_off);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int W = kT / LPR;                 // row slices per block
+  const int lane = threadIdx.x & (LPR - 1), slice = threadIdx.x / LPR;
   const int nvec = H / 8;
   float dg[NV][8], db[NV][8];
 #pragma unroll
@@ -131,7 +143,7 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
   float gm[NV][8];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int c = lane + i * 64;
+    const int c = lane + i * LPR;
     if (c < nvec) {
       const float4 g0 = *reinterpret_cast<const float4*>(gamma + c * 8);
       const float4 g1 = *reinterpret_cast<const float4*>(gamma + c * 8 + 4);
@@ -144,7 +156,7 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
     rs = rstd[row];
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      const int c = lane + i * 64;
+      const int c = lane + i * LPR;
       if (c < nvec) {
         gr[i] = *reinterpret_cast<const uint4*>(dy + row * H + c * 8);
         sr[i] = *reinterpret_cast<const uint4*>(s + row * H + c * 8);
@@ -156,7 +168,7 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      const int c = lane + i * 64;
+      const int c = lane + i * LPR;
       if (c < nvec) {
         const uint32_t gw[4] = {gr[i].x, gr[i].y, gr[i].z, gr[i].w};
         const uint32_t sw[4] = {sr[i].x, sr[i].y, sr[i].z, sr[i].w};
@@ -173,11 +185,11 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
         }
       }
     }
-    a = wave_sum(a) / (float)H;
-    b = wave_sum(b) / (float)H;
+    a = row_sum<LPR>(a) / (float)H;
+    b = row_sum<LPR>(b) / (float)H;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      const int c = lane + i * 64;
+      const int c = lane + i * LPR;
       if (c < nvec) {
         float o[8];
 #pragma unroll
@@ -192,9 +204,9 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
       }
     }
   };
-  // RIF rows per wave per iteration, all their loads in flight before the first is reduced
-  constexpr int W = kT / 64, RIF = NV <= 2 ? 4 : 1;
-  for (long long row = r0 + wave; row < r1; row += RIF * W) {
+  // RIF rows per slice per iteration, all their loads in flight before the first is reduced
+  constexpr int RIF = NV <= 2 ? 4 : (NV == 3 ? 2 : 1);
+  for (long long row = r0 + slice; row < r1; row += RIF * W) {
     uint4 gr[RIF][NV], sr[RIF][NV];
     float mu[RIF], rs[RIF];
 #pragma unroll
@@ -204,26 +216,27 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
     for (int j = 0; j < RIF; ++j)
       if (row + j * W < r1) do_row(row + j * W, gr[j], sr[j], mu[j], rs[j]);
   }
-  // combine the 4 waves through LDS; block partials -> ws[block][2][H] (plain stores)
-  __shared__ __attribute__((aligned(16))) float L[2][kT / 64][64 * 8];   // one 512-column slab per pass over NV
+  // combine the W slices through LDS; block partials -> ws[block][2][H] (plain stores)
+  constexpr int SPAN = LPR * 8;               // columns one pass over i covers
+  __shared__ __attribute__((aligned(16))) float L[2][W][SPAN];
   float* wg = ws + (long long)blockIdx.x * 2 * H;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     // 16-B stores: 8 consecutive lanes cover all 64 banks (scalar stores at an 8-float stride hit 4 of them)
-    float4* l0 = reinterpret_cast<float4*>(&L[0][wave][lane * 8]);
-    float4* l1 = reinterpret_cast<float4*>(&L[1][wave][lane * 8]);
+    float4* l0 = reinterpret_cast<float4*>(&L[0][slice][lane * 8]);
+    float4* l1 = reinterpret_cast<float4*>(&L[1][slice][lane * 8]);
     l0[0] = make_float4(dg[i][0], dg[i][1], dg[i][2], dg[i][3]);
     l0[1] = make_float4(dg[i][4], dg[i][5], dg[i][6], dg[i][7]);
     l1[0] = make_float4(db[i][0], db[i][1], db[i][2], db[i][3]);
     l1[1] = make_float4(db[i][4], db[i][5], db[i][6], db[i][7]);
     __syncthreads();
-    for (int j = threadIdx.x; j < 2 * 512; j += kT) {
-      const int which = j >> 9, cc = j & 511;       // 0: dgamma, 1: dbeta
-      const int col = i * 512 + cc;
+    for (int j = threadIdx.x; j < 2 * SPAN; j += kT) {
+      const int which = j / SPAN, cc = j % SPAN;       // 0: dgamma, 1: dbeta
+      const int col = i * SPAN + cc;
       if (col < H) {
         float t = 0.f;
 #pragma unroll
-        for (int w = 0; w < kT / 64; ++w) t += L[which][w][cc];
+        for (int w = 0; w < W; ++w) t += L[which][w][cc];
         wg[(which ^ beta_first) * H + col] = t;      // partial rows follow the grad slots' order
       }
     }
@@ -379,6 +392,25 @@ inline int gcap(long long work) {
 
 }  // namespace
 
+// LayerNorm: 32 lanes per row when the row's vectors fill 32-lane slices exactly but not whole waves (H = 768:
+// 96 vectors = 3 x 32), else a wave per row
+#define LN_DISPATCH(H, KERNEL, GRID32, GRID64, ...)                                                        \
+  do {                                                                                                     \
+    const int nvec_ = (H) / 8;                                                                             \
+    if (nvec_ % 64 != 0 && nvec_ % 32 == 0 && nvec_ / 32 <= 3) {                                           \
+      if (nvec_ == 32) hipLaunchKernelGGL((KERNEL<1, 32>), GRID32, dim3(kT), 0, st, __VA_ARGS__);         \
+      else hipLaunchKernelGGL((KERNEL<3, 32>), GRID32, dim3(kT), 0, st, __VA_ARGS__);                     \
+      break;                                                                                               \
+    }                                                                                                      \
+    const int nv_ = static_cast<int>(ceil_div(nvec_, 64));                                                 \
+    if (nv_ <= 1) hipLaunchKernelGGL((KERNEL<1, 64>), GRID64, dim3(kT), 0, st, __VA_ARGS__);               \
+    else if (nv_ <= 2) hipLaunchKernelGGL((KERNEL<2, 64>), GRID64, dim3(kT), 0, st, __VA_ARGS__);          \
+    else if (nv_ <= 4) hipLaunchKernelGGL((KERNEL<4, 64>), GRID64, dim3(kT), 0, st, __VA_ARGS__);          \
+    else if (nv_ <= 8) hipLaunchKernelGGL((KERNEL<8, 64>), GRID64, dim3(kT), 0, st, __VA_ARGS__);          \
+    else if (nv_ <= 16) hipLaunchKernelGGL((KERNEL<16, 64>), GRID64, dim3(kT), 0, st, __VA_ARGS__);        \
+    else return MDTF_EUNSUPPORTED;                                                                         \
+  } while (0)
+
 #define NV_DISPATCH(H, KERNEL, GRID, ...)                                                                  \
   do {                                                                                                     \
     const int nv_ = static_cast<int>(ceil_div((H) / 8, 64));                                               \
@@ -404,8 +436,9 @@ MDTF_EXPORT int mdtf_ln_fwd(const void* x, const void* res, const float* gamma, 
   if (rows * H > 0xffffffffLL && p_drop > 0.f) return MDTF_EUNSUPPORTED;
   const uint32_t thr = drop_thr(p_drop);
   const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-  NV_DISPATCH(H, ln_fwd_kernel, dim3(ceil_div(rows, kT / 64)), (const bf16_t*)x, (const bf16_t*)res, gamma, beta,
-              (bf16_t*)y, (bf16_t*)s, mean, rstd, rows, H, eps, thr, inv_keep, (uint32_t)seed, seed_off);
+  LN_DISPATCH(H, ln_fwd_kernel, dim3(ceil_div(rows, kT / 32)), dim3(ceil_div(rows, kT / 64)), (const bf16_t*)x,
+              (const bf16_t*)res, gamma, beta, (bf16_t*)y, (bf16_t*)s, mean, rstd, rows, H, eps, thr, inv_keep,
+              (uint32_t)seed, seed_off);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
@@ -443,8 +476,8 @@ MDTF_EXPORT int mdtf_ln_bwd(const void* dy, const void* s, const float* gamma, c
   const int beta_first = (dgamma == dbeta + H) ? 1 : 0;
   const uint32_t thr = drop_thr(p_drop);
   const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-  NV_DISPATCH(H, ln_bwd_kernel, dim3(blocks), (const bf16_t*)dy, (const bf16_t*)s, gamma, mean, rstd, (bf16_t*)dx,
-              (bf16_t*)dx_branch, ws, rows, H, rpb, beta_first, thr, inv_keep, (uint32_t)seed, seed_off);
+  LN_DISPATCH(H, ln_bwd_kernel, dim3(blocks), dim3(blocks), (const bf16_t*)dy, (const bf16_t*)s, gamma, mean, rstd,
+              (bf16_t*)dx, (bf16_t*)dx_branch, ws, rows, H, rpb, beta_first, thr, inv_keep, (uint32_t)seed, seed_off);
   MDTF_LAUNCH_CHECK();
   if (beta_first) return mdtf_reduce_partials(ws, blocks, 2 * H, dbeta, st);
   // ws rows are [dgamma(H) | dbeta(H)]: reduce as a [blocks, 2H] matrix when the

@@ -578,12 +578,15 @@ def test_stem_conv_bn_relu_maxpool_fused_vs_unfused(monkeypatch):
         assert e_u < 1e-1 and e_f <= 1.3 * e_u + 1e-2, (key, e_f, e_u)
 
 
-@pytest.mark.parametrize("H,res", [(768, True), (1024, False), (64, True)])
-def test_layernorm_kernel(H, res):
+@pytest.mark.parametrize("H,res,rows", [(768, True, 37), (1024, False, 37), (64, True, 37), (256, True, 37),
+                                        (768, False, 4099)])
+def test_layernorm_kernel(H, res, rows):
+    """Forward + backward vs fp32 CPU: a wave per row (1024, 64) and 32 lanes per row (768 = 3 x 32 vectors,
+    256 = 1 x 32), odd row counts (partial blocks, half-filled waves)."""
     from mdtf.ops import transformer as T
     torch.manual_seed(11)
-    x = torch.randn(37, H) * 2 + 1
-    r = torch.randn(37, H) if res else None
+    x = torch.randn(rows, H) * 2 + 1
+    r = torch.randn(rows, H) if res else None
     g = torch.rand(H) + 0.5
     b = torch.randn(H)
     outs = {}
@@ -593,7 +596,7 @@ def test_layernorm_kernel(H, res):
         gg = g.to(dev).requires_grad_(True)
         bb = b.to(dev).requires_grad_(True)
         y = T.layer_norm(xx, gg, bb, 1e-12, residual=rr)
-        y.backward(torch.randn(37, H, generator=torch.Generator().manual_seed(2)).to(dev).to(dt))
+        y.backward(torch.randn(rows, H, generator=torch.Generator().manual_seed(2)).to(dev).to(dt))
         outs[dev] = (y.detach(), xx.grad, gg.grad, bb.grad, rr.grad if res else None)
     for i in range(4):
         assert _rel(outs[DEV][i], outs["cpu"][i]) < 2e-2, i
