@@ -825,6 +825,48 @@ __global__ void __launch_bounds__(256) transpose16_multi(const TDesc* __restrict
   }
 }
 
+// Batched 2-D copies (16-B vectors): dst[r][0:cols] = src[r][0:cols] for every record, each record a block range.
+// The q|k|v weight concatenation of every transformer layer in one launch per step (ops.gemm _WeightCats).
+struct CDesc {
+  const uint4* src;
+  uint4* dst;
+  int rows, vcols;            // rows, 16-B vectors per row
+  int src_ld, dst_ld;         // row strides in 16-B vectors
+  int block0, pad;
+};
+
+__global__ void __launch_bounds__(256) copy2d_multi(const CDesc* __restrict__ desc, int count) {
+  int i = 0;
+  while (i + 1 < count && desc[i + 1].block0 <= (int)blockIdx.x) ++i;
+  const CDesc d = desc[i];
+  // each block: 256 threads x 4 vectors, rows walked in row-major vector order
+  const long long base = (long long)(blockIdx.x - d.block0) * 1024 + threadIdx.x;
+  const long long n = (long long)d.rows * d.vcols;
+  uint4 v[4];
+  long long idx[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    idx[u] = base + u * 256;
+    if (idx[u] < n) {
+      const long long r = idx[u] / d.vcols, c = idx[u] - r * d.vcols;
+      v[u] = d.src[r * d.src_ld + c];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (idx[u] < n) {
+      const long long r = idx[u] / d.vcols, c = idx[u] - r * d.vcols;
+      d.dst[r * d.dst_ld + c] = v[u];
+    }
+}
+
+MDTF_EXPORT int mdtf_copy2d_multi(const void* desc, int count, int total_blocks, hipStream_t st) {
+  if (count <= 0 || total_blocks <= 0) return 0;
+  hipLaunchKernelGGL(copy2d_multi, dim3(total_blocks), dim3(256), 0, st, (const CDesc*)desc, count);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
 MDTF_EXPORT int mdtf_transpose_multi(const void* desc, int count, int total_tiles, hipStream_t st) {
   if (count <= 0 || total_tiles <= 0) return 0;
   hipLaunchKernelGGL(transpose16_multi, dim3(total_tiles), dim3(256), 0, st, (const TDesc*)desc, count);

@@ -313,6 +313,7 @@ class TrainOp(Fetchable):
     def _run_step(self, ctx, step, dyn=None):
         """forward + backward of every tower program, reduction, fused update (one step)."""
         from ..ops import conv as _conv
+        from ..ops import gemm as _gemm
         red = self.reducer
         red.begin_step()
         lr = self.optimizer.learning_rate(step)
@@ -323,6 +324,7 @@ class TrainOp(Fetchable):
         else:
             red.set_update_fn(None)
         _conv._WT.step_begin()                 # conv filters' K-contiguous copies: one batched refresh per step
+        _gemm._CATS.step_begin()               # q|k|v weight concatenations: one batched copy per step
         try:
             for prog in self.programs:
                 out = prog.forward(ctx, grad=True)
@@ -330,6 +332,7 @@ class TrainOp(Fetchable):
                 loss.backward()
         finally:
             _conv._WT.step_end()
+            _gemm._CATS.step_end()
         scale = red.end_backward(step) * self.grad_scale_extra
         with torch.no_grad():
             for target in red.update_targets():
@@ -383,7 +386,9 @@ def release_graphs():
     for op in _TRAIN_OPS:
         op.release_graph()
     from ..ops import conv as _conv
+    from ..ops import gemm as _gemm
     _conv._WT.clear()               # the filter-transpose cache holds the released space's shadows
+    _gemm._CATS.clear()
 
 
 def reset():

@@ -662,6 +662,44 @@ def test_bert_tiny_train_step_gpu():
     assert ls[-1] < 0.5 * ls[0], ls
 
 
+def test_weight_cat_cache_matches_torch_cat(monkeypatch):
+    """q|k|v weight concatenations refreshed by one batched copy per step (ops.gemm._WeightCats) train exactly like
+    a torch.cat per layer: same losses over several steps (the weights change every step)."""
+    import mdtf
+    from mdtf.models import Bert, BertPretrainingLoss, SyntheticBertLoader
+    from mdtf.ops import gemm as G
+    from mdtf.runtime import Net, Tower
+    from mdtf.train import step as S
+    from mdtf.train import variables as V
+    runs = {}
+    for cache in ("1", "0"):
+        monkeypatch.setenv("MDTF_WEIGHT_CAT_CACHE", cache)
+        V.reset_default_graph()
+        S.reset()
+        store = V.get_store()
+        store.device = torch.device(DEV)
+        store.compute_dtype = torch.bfloat16
+        store.generator.manual_seed(99)
+        ld = SyntheticBertLoader(seq_len=32, max_predictions=5, vocab=512, seed=4)
+        ld.batch_size = 8
+        raw, gt = ld.load_train_batch()
+        opt = mdtf.train.AdamWeightDecayOptimizer(1e-3)
+        tg = []
+        t = Tower(Net(Bert("tiny", vocab_size=512, seq_len=32, max_predictions=5, dropout=0.0)), "tower_0/", tg, raw,
+                  gt, BertPretrainingLoss(5), opt, batch_size=8)
+        _, loss, _ = t.process()
+        op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
+        sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
+        ls = []
+        for _ in range(5):
+            _, l = sess.run([op, loss])
+            ls.append(float(l))
+        runs[cache] = (ls, len(G._CATS.entries))
+    assert runs["1"][1] > 0, "no q|k|v group was registered"
+    for a, b in zip(runs["1"][0], runs["0"][0]):
+        assert abs(a - b) <= 1e-3 * max(1.0, abs(b)), (runs["1"][0], runs["0"][0])
+
+
 def _bert_step(dev, dt, raw, gt, seq=32, heads_dim=None, dropout=0.0):
     import mdtf
     from mdtf.models import Bert, BertPretrainingLoss
