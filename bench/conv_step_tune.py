@@ -161,6 +161,8 @@ def main():
     p.add_argument("--top", type=int, default=3, help="isolated-fastest candidates kept per kernel family")
     p.add_argument("--passes", default="fwd,dgrad,wgrad")
     p.add_argument("--budget_s", type=float, default=900.0, help="stop trying new keys after this long")
+    p.add_argument("--reverse", action="store_true", help="tune the keys last-seen first (continues a budget-capped "
+                   "earlier run from the other end of the step)")
     p.add_argument("--out", default="gpurun_out/conv_table_step.json")
     p.add_argument("--report", default="gpurun_out/conv_step_tune.md")
     args = p.parse_args()
@@ -183,6 +185,8 @@ def main():
     table = C.table()
     keys = [k for k in seen if k in table and k.split(":")[0] in args.passes.split(",")
             and table[k].get("backend") == "mdtf"]
+    if args.reverse:
+        keys = keys[::-1]
     base = [step_ms(sess, op, args.steps, args.warm) for _ in range(6)]
     noise = statistics.pstdev(base)
     t0 = statistics.median(base)

@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 TAG=${1:-st1}
-timeout -k 10 900 python -u bench/conv_step_tune.py --budget_s ${BUDGET:-600} --out gpurun_out/conv_table_$TAG.json \
+timeout -k 10 1000 python -u bench/conv_step_tune.py --budget_s ${BUDGET:-600} ${TUNE_ARGS} --out gpurun_out/conv_table_$TAG.json \
     --report gpurun_out/conv_step_tune_$TAG.md > gpurun_out/step_tune_$TAG.log 2>&1 \
   || { echo "step tune failed"; tail -30 gpurun_out/step_tune_$TAG.log; exit 1; }
 tail -3 gpurun_out/step_tune_$TAG.log
