@@ -663,6 +663,41 @@ __device__ __forceinline__ void pool_grad8(const bf16_t* __restrict__ dy, const 
                                            const PoolG& g, int n, int h, int w, int c8, float (&acc)[8]) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  if (g.KH <= 2 * g.SH && g.KW <= 2 * g.SW) {
+    // at most 2 x 2 windows hold this input (ResNet's 3x3 / 2 pool): their 4 (argmax, gradient) pairs are loaded
+    // unconditionally from clamped addresses first -- one memory round trip instead of one per window -- and the
+    // windows that do not cover (h, w) are masked afterwards
+    const int oh1 = min((h + g.PT) / g.SH, g.OH - 1), ow1 = min((w + g.PL) / g.SW, g.OW - 1);
+    uint2 pk[2][2];
+    uint4 gr[2][2];
+    uint32_t me[2][2];
+    bool ok[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int oh = oh1 - a, ow = ow1 - b;
+        const int kh = h - (oh * g.SH - g.PT), kw = w - (ow * g.SW - g.PL);
+        ok[a][b] = oh >= 0 && ow >= 0 && kh >= 0 && kh < g.KH && kw >= 0 && kw < g.KW;
+        me[a][b] = static_cast<uint32_t>(kh * g.KW + kw);
+        const long long o = ok[a][b] ? ((long long)(n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8 : 0;
+        pk[a][b] = *reinterpret_cast<const uint2*>(arg + o);
+        gr[a][b] = *reinterpret_cast<const uint4*>(dy + o);
+      }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        float gv[8];
+        unpack8(gr[a][b], gv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t id = ((k < 4 ? pk[a][b].x : pk[a][b].y) >> (8 * (k & 3))) & 0xffu;
+          if (ok[a][b] && id == me[a][b]) acc[k] += gv[k];
+        }
+      }
+    return;
+  }
   int oh0 = h + g.PT - g.KH + g.SH;
   oh0 = oh0 < 0 ? 0 : oh0 / g.SH;
   int oh1 = (h + g.PT) / g.SH;

@@ -123,13 +123,14 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
   const int stepA = (int)(64 * a.lda * 2), stepB = (int)(64 * a.ldb * 2);
   const int jA = (int)(RJA * a.lda * 2), jB = (int)(RJB * a.ldb * 2);
 
-  auto issue = [&](int t) {
-    const unsigned slot = lds0 + (t % STAGES) * SLOT;
+  auto issue_to = [&](int t, int sl) {
+    const unsigned slot = lds0 + sl * SLOT;
 #pragma unroll
     for (int j = 0; j < IA; ++j) dma16(ra, slot + (j * NW + wave) * 1024, vA, t * stepA + j * jA);
 #pragma unroll
     for (int j = 0; j < IB; ++j) dma16(rb, slot + BYTES_A + (j * NW + wave) * 1024, vB, t * stepB + j * jB);
   };
+  auto issue = [&](int t) { issue_to(t, t % STAGES); };
 
   // fragment reads: lane (fr, fq) gets X[k = 32 s + 8 fq + 0..7][col = c0 + fr] (the 16x16x32 operand map)
   const int fq = lane >> 4;
@@ -176,19 +177,26 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
   for (int p = 0; p < STAGES - 1; ++p)
     if (p < T) issue(p);
   if constexpr (!PIPE) {
-    for (int t = 0; t < T; ++t) {
-      // tile t landed: the tiles issued after it (up to STAGES - 2) may stay in flight
-      if (t + STAGES - 2 < T) wait_vmcnt<(STAGES - 2) * PER_TILE>();
-      else wait_vmcnt<0>();
-      barrier();
-      // every wave has finished reading tile t - 1: its slot takes tile t + STAGES - 1
-      if (t + STAGES - 1 < T) issue(t + STAGES - 1);
-      const char* slotp = smem + (t % STAGES) * SLOT;
+    // unrolled by the ring depth: every slot address is a compile-time offset
+    for (int t0 = 0; t0 < T; t0 += STAGES) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8_t fa[4], fb[4];
-        load_frags(slotp, s, fa, fb);
-        mfmas(fa, fb);
+      for (int u = 0; u < STAGES; ++u) {
+        const int t = t0 + u;
+        if (t < T) {
+          // tile t landed: the tiles issued after it (up to STAGES - 2) may stay in flight
+          if (t + STAGES - 2 < T) wait_vmcnt<(STAGES - 2) * PER_TILE>();
+          else wait_vmcnt<0>();
+          barrier();
+          // every wave has finished reading tile t - 1: its slot takes tile t + STAGES - 1
+          if (t + STAGES - 1 < T) issue_to(t + STAGES - 1, (u + STAGES - 1) % STAGES);
+          const char* slotp = smem + u * SLOT;
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            bf16x8_t fa[4], fb[4];
+            load_frags(slotp, s, fa, fb);
+            mfmas(fa, fb);
+          }
+        }
       }
     }
   } else {
