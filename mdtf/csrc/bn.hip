@@ -667,7 +667,9 @@ __device__ __forceinline__ void pool_grad8(const bf16_t* __restrict__ dy, const 
     // at most 2 x 2 windows hold this input (ResNet's 3x3 / 2 pool): their 4 (argmax, gradient) pairs are loaded
     // unconditionally from clamped addresses first -- one memory round trip instead of one per window -- and the
     // windows that do not cover (h, w) are masked afterwards
-    const int oh1 = min((h + g.PT) / g.SH, g.OH - 1), ow1 = min((w + g.PL) / g.SW, g.OW - 1);
+    const int hp = h + g.PT, wp = w + g.PL;            // >= 0
+    const int oh1 = min(g.SH == 2 ? hp >> 1 : hp / g.SH, g.OH - 1);
+    const int ow1 = min(g.SW == 2 ? wp >> 1 : wp / g.SW, g.OW - 1);
     uint2 pk[2][2];
     uint4 gr[2][2];
     uint32_t me[2][2];
@@ -873,6 +875,93 @@ __global__ void __launch_bounds__(kThreads)
   store_bf8(dx + (long long)i * 8, o);
 }
 
+// Same as maxpool_bn_dx, one workgroup per input row (n, h): a thread keeps one 8-channel vector c8 (its BN
+// coefficients loaded once) and walks the row's pixels w = w0, w0 + 256 / cv, ...; no per-element integer
+// divisions (cv = C / 8 a power of two, 2^cvs).
+__global__ void __launch_bounds__(kThreads)
+    maxpool_bn_dx_rows(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ x,
+                       const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ k1,
+                       const float* __restrict__ k2, const float* __restrict__ k3, bf16_t* __restrict__ dx, PoolG g,
+                       int cvs) {
+  const int row = blockIdx.x;
+  const int n = row / g.H, h = row - n * g.H;
+  const int cv = 1 << cvs;
+  const int c8 = threadIdx.x & (cv - 1);
+  const int wstep = kThreads >> cvs;
+  float sc[8], sh[8], A[8], B[8], E[8];
+  load_coef8(scale, c8 * 8, sc);
+  load_coef8(shift, c8 * 8, sh);
+  load_coef8(k1, c8 * 8, A);
+  load_coef8(k2, c8 * 8, B);
+  load_coef8(k3, c8 * 8, E);
+  for (int w = threadIdx.x >> cvs; w < g.W; w += wstep) {
+    const long long i = ((long long)row * g.W + w) * cv + c8;
+    float xv[8], gv[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + i * 8), xv);
+    pool_grad8(dy, arg, g, n, h, w, c8, gv);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float gm = (xv[k] * sc[k] + sh[k] > 0.f) ? gv[k] : 0.f;
+      o[k] = A[k] * gm + B[k] * xv[k] + E[k];
+    }
+    store_bf8(dx + i * 8, o);
+  }
+}
+
+// Σ g·m and Σ g·m·x by input rows (the maxpool_bn_dx_rows mapping): block b sums image rows [b rpb, (b+1) rpb),
+// a thread one channel vector over pixels w0, w0 + 256 / cv, ...; the threads of a channel vector are combined in
+// LDS -> partials [gridDim.x][C]
+__global__ void __launch_bounds__(kThreads)
+    maxpool_bn_bwd_reduce_rows(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                               const bf16_t* __restrict__ x, const float* __restrict__ scale,
+                               const float* __restrict__ shift, PoolG g, int cvs, int rpb, float* __restrict__ p0,
+                               float* __restrict__ p1) {
+  __shared__ __attribute__((aligned(16))) float L[2][kThreads * 8];
+  const int cv = 1 << cvs;
+  const int c8 = threadIdx.x & (cv - 1);
+  const int wstep = kThreads >> cvs;
+  const int nrows = g.N * g.H;
+  const int r0 = blockIdx.x * rpb, r1 = min(r0 + rpb, nrows);
+  float sc[8], sh[8], s0[8], s1[8];
+  load_coef8(scale, c8 * 8, sc);
+  load_coef8(shift, c8 * 8, sh);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s0[k] = s1[k] = 0.f;
+  for (int row = r0; row < r1; ++row) {
+    const int n = row / g.H, h = row - n * g.H;
+    for (int w = threadIdx.x >> cvs; w < g.W; w += wstep) {
+      const long long i = ((long long)row * g.W + w) * cv + c8;
+      float xv[8], gv[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + i * 8), xv);
+      pool_grad8(dy, arg, g, n, h, w, c8, gv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gm = (xv[k] * sc[k] + sh[k] > 0.f) ? gv[k] : 0.f;
+        s0[k] += gm;
+        s1[k] += gm * xv[k];
+      }
+    }
+  }
+  float4* l0 = reinterpret_cast<float4*>(&L[0][threadIdx.x * 8]);
+  float4* l1 = reinterpret_cast<float4*>(&L[1][threadIdx.x * 8]);
+  l0[0] = make_float4(s0[0], s0[1], s0[2], s0[3]);
+  l0[1] = make_float4(s0[4], s0[5], s0[6], s0[7]);
+  l1[0] = make_float4(s1[0], s1[1], s1[2], s1[3]);
+  l1[1] = make_float4(s1[4], s1[5], s1[6], s1[7]);
+  __syncthreads();
+  for (int c = threadIdx.x; c < g.C; c += kThreads) {
+    const int cc = c >> 3, k = c & 7;
+    float a = 0.f, b = 0.f;
+    for (int j = 0; j < wstep; ++j) {
+      a += L[0][(j * cv + cc) * 8 + k];
+      b += L[1][(j * cv + cc) * 8 + k];
+    }
+    p0[(long long)blockIdx.x * g.C + c] = a;
+    p1[(long long)blockIdx.x * g.C + c] = b;
+  }
+}
+
 bool pool_geo_ok(const PoolG& g) {
   return g.C % 8 == 0 && g.KH * g.KW <= 255 && (long long)g.N * g.H * g.W * g.C < (1LL << 31) &&
          g.OH > 0 && g.OW > 0;
@@ -914,14 +1003,36 @@ MDTF_EXPORT int mdtf_maxpool_bn_bwd(const void* dy, const uint8_t* arg, const vo
   float* k1 = p1 + (long long)ge.gx * C;
   float* k2 = k1 + C;
   float* k3 = k2 + C;
-  const size_t lds = 2 * sizeof(float) * ge.rg * ge.tpr * 8;
-  hipLaunchKernelGGL(maxpool_bn_bwd_reduce, dim3(ge.gx, ge.gy), dim3(kThreads), lds, st, (const bf16_t*)dy, arg,
-                     (const bf16_t*)x, ss, ss + C, g, ge.tpr, ge.rg, p0, p1);
-  hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, p0, p1, ge.gx, M,
+  const int cv = C / 8;
+  const bool rows_path = (cv & (cv - 1)) == 0 && cv <= kThreads;
+  int parts = ge.gx;
+  if (rows_path) {
+    int cvs = 0;
+    while ((1 << cvs) < cv) ++cvs;
+    const int nrows = N * H;
+    int gx = ge.gx < nrows ? ge.gx : nrows;           // partial rows fit the workspace's ge.gx
+    const int rpb = (nrows + gx - 1) / gx;
+    gx = (nrows + rpb - 1) / rpb;
+    parts = gx;
+    hipLaunchKernelGGL(maxpool_bn_bwd_reduce_rows, dim3(gx), dim3(kThreads), 0, st, (const bf16_t*)dy, arg,
+                       (const bf16_t*)x, ss, ss + C, g, cvs, rpb, p0, p1);
+  } else {
+    const size_t lds = 2 * sizeof(float) * ge.rg * ge.tpr * 8;
+    hipLaunchKernelGGL(maxpool_bn_bwd_reduce, dim3(ge.gx, ge.gy), dim3(kThreads), lds, st, (const bf16_t*)dy, arg,
+                       (const bf16_t*)x, ss, ss + C, g, ge.tpr, ge.rg, p0, p1);
+  }
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, p0, p1, parts, M,
                      C, gamma, mean, invstd, dgamma, dbeta, k1, k2, k3, 0);
-  const int total = (int)(M * (C / 8));
-  hipLaunchKernelGGL(maxpool_bn_dx, dim3(ceil_div(total, kThreads)), dim3(kThreads), 0, st, (const bf16_t*)dy, arg,
-                     (const bf16_t*)x, ss, ss + C, k1, k2, k3, (bf16_t*)dx, g, total);
+  if (rows_path) {
+    int cvs = 0;
+    while ((1 << cvs) < cv) ++cvs;
+    hipLaunchKernelGGL(maxpool_bn_dx_rows, dim3(N * H), dim3(kThreads), 0, st, (const bf16_t*)dy, arg,
+                       (const bf16_t*)x, ss, ss + C, k1, k2, k3, (bf16_t*)dx, g, cvs);
+  } else {
+    const int total = (int)(M * cv);
+    hipLaunchKernelGGL(maxpool_bn_dx, dim3(ceil_div(total, kThreads)), dim3(kThreads), 0, st, (const bf16_t*)dy, arg,
+                       (const bf16_t*)x, ss, ss + C, k1, k2, k3, (bf16_t*)dx, g, total);
+  }
   MDTF_LAUNCH_CHECK();
   return 0;
 }
