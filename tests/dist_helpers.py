@@ -5,6 +5,17 @@ import os
 import torch
 
 
+def _teardown(server):
+    """Server.from_env leaves the process group to its launcher (torchrun); these spawned ranks have none, so
+    destroy it here: a gloo group torn down by interpreter exit can abort the process ("terminate called without
+    an active exception") after the test's work is done."""
+    import torch.distributed as dist
+    server.shutdown()
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def _linear_setup(rank, world, batch, seed=0):
     import mdtf
     from mdtf.runtime import Loss, Model, Net, Tower
@@ -59,7 +70,7 @@ def sync_worker(rank, world, port, mode, steps, out_dir, replicas=None, batch=4,
     w = {v.name: v.master.tolist() for v in V.get_store().trainable_variables()}
     with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
         json.dump({"weights": w, "contributed": contributed, "step": gs.value()}, f)
-    server.shutdown()
+    _teardown(server)
 
 
 def single_process_reference(world, steps, batch=4):
@@ -109,7 +120,7 @@ def sharded_ckpt_worker(rank, world, port, steps, out_dir, save_steps=None):
             sess.run(op, feed_dict={x_ph: xs[lo:hi], y_ph: ys[lo:hi]})
     with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
         json.dump({"step": gs.value()}, f)
-    server.shutdown()
+    _teardown(server)
 
 
 def hidden_ckpt_restore_worker(rank, world, port, out_dir):
@@ -144,7 +155,7 @@ def hidden_ckpt_restore_worker(rank, world, port, out_dir):
     with open(os.path.join(out_dir, "resume%d.json" % rank), "w") as f:
         json.dump({"step": step, "weights": w, "adam_m": m, "restored": sess.restored_from}, f)
     sess.close()
-    server.shutdown()
+    _teardown(server)
 
 
 def recovery_worker(rank, world, port, steps, out_dir, fault_step=None, fault_task="worker:1", mode="abort"):
@@ -182,7 +193,7 @@ def recovery_worker(rank, world, port, steps, out_dir, fault_step=None, fault_ta
     w = {v.name: v.master.tolist() for v in V.get_store().trainable_variables()}
     with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
         json.dump({"step": gs.value(), "recoveries": rec, "runs": runs, "weights": w}, f)
-    server.shutdown()
+    _teardown(server)
 
 
 def backup_gpu_worker(rank, world, port, steps, out_dir, replicas):
@@ -216,4 +227,4 @@ def backup_gpu_worker(rank, world, port, steps, out_dir, replicas):
     w = {v.name: v.master.tolist() for v in V.get_store().trainable_variables()}
     with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
         json.dump({"weights": w, "contributed": contributed, "device_mask": bool(op.reducer.backup_device)}, f)
-    server.shutdown()
+    _teardown(server)
