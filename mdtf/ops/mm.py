@@ -159,7 +159,8 @@ N.register("mdtf_gemm_wg_slab_floats", [N.I, N.I, N.I, N.I], N.L)
 # the 3/4-stage rings and the mid-tile-barrier loop (stages < 0) measured slower than the 2-stage ring on every shape)
 # In the BERT-base step the 256-row kernels gain from the third ring stage (HBM-cold saved activations; graph-timed
 # with MALL-resident operands 2 and 3 stages tie): MDTF_WG_STAGES=3 vs 2, alternating: 6485 / 6530 vs 6378 / 6420 seq/s
-WG_TILES = {(768, 2304, 8192): (256, 3, 4), (768, 3072, 8192): (256, 3, 3), (3072, 768, 8192): (128, 2, 3),
+# (FFN-out 3072 x 768: 256-row 3-stage 6368 / 6362 vs 128-row 2-stage 6356 / 6336 seq/s)
+WG_TILES = {(768, 2304, 8192): (256, 3, 4), (768, 3072, 8192): (256, 3, 3), (3072, 768, 8192): (256, 3, 3),
             (768, 768, 8192): (128, 2, 6), (1024, 3072, 8192): (256, 2, 2), (1024, 4096, 8192): (256, 2, 2),
             (4096, 1024, 8192): (256, 2, 2)}
 _TICKETS = {}
@@ -184,8 +185,8 @@ def wg_pick(M, Nn, K):
     2-stage ring beats the 128-row pairs; split until the tiles x splits grid just fills the 256 CUs (a second
     round of workgroups costs more than it saves), keeping >= 16 K-tiles per split."""
     t = WG_TILES.get((M, Nn, K))
-    if t is not None and os.environ.get("MDTF_WG_FFN_OUT") == "256" and (M, Nn, K) == (3072, 768, 8192):
-        t = (256, 3, 3)                                  # (A/B switch)
+    if t is not None and os.environ.get("MDTF_WG_FFN_OUT") == "128" and (M, Nn, K) == (3072, 768, 8192):
+        t = (128, 2, 3)                                  # (A/B switch)
     if t is not None:
         return t if (_WG_STAGES is None or t[0] != 256) else (t[0], _WG_STAGES, t[2])   # 128-row rings stay 2-deep
     kt = K // 64
