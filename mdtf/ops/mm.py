@@ -161,8 +161,8 @@ N.register("mdtf_gemm_wg_slab_floats", [N.I, N.I, N.I, N.I], N.L)
 # with MALL-resident operands 2 and 3 stages tie): MDTF_WG_STAGES=3 vs 2, alternating: 6485 / 6530 vs 6378 / 6420 seq/s
 # (FFN-out 3072 x 768: 256-row 3-stage 6368 / 6362 vs 128-row 2-stage 6356 / 6336 seq/s)
 WG_TILES = {(768, 2304, 8192): (256, 3, 4), (768, 3072, 8192): (256, 3, 3), (3072, 768, 8192): (256, 3, 3),
-            (768, 768, 8192): (128, 2, 6), (1024, 3072, 8192): (256, 2, 2), (1024, 4096, 8192): (256, 2, 2),
-            (4096, 1024, 8192): (256, 2, 2)}
+            (768, 768, 8192): (128, 2, 6), (1024, 3072, 8192): (256, 3, 2), (1024, 4096, 8192): (256, 3, 2),
+            (4096, 1024, 8192): (256, 3, 2)}
 _TICKETS = {}
 # MDTF_WG_STAGES: force the ring depth of the table entries (in-step A/B: the operands of the step are HBM-cold,
 # the graph-timed probe's are MALL-resident)
@@ -182,7 +182,7 @@ def _tickets(device, n):
 
 def wg_pick(M, Nn, K):
     """(bm, stages, splits) for C[M][Nn] += over K tokens.  Measured: one 256-row workgroup per CU with a
-    2-stage ring beats the 128-row pairs; split until the tiles x splits grid just fills the 256 CUs (a second
+    3-stage ring (in the step) beats the 128-row pairs; split until the tiles x splits grid just fills the 256 CUs (a second
     round of workgroups costs more than it saves), keeping >= 16 K-tiles per split."""
     t = WG_TILES.get((M, Nn, K))
     if t is not None and os.environ.get("MDTF_WG_FFN_OUT") == "128" and (M, Nn, K) == (3072, 768, 8192):
@@ -192,7 +192,7 @@ def wg_pick(M, Nn, K):
     kt = K // 64
     bm = 256 if M % 256 == 0 else 128
     tiles = (M // bm) * (Nn // 128)
-    return bm, 2, max(1, min(kt // 16, CUS // tiles))
+    return bm, (3 if bm == 256 else 2), max(1, min(kt // 16, CUS // tiles))
 
 
 def wg_into(gws, x, dy, dbs=None, bm=None, stages=None, splits=None):
