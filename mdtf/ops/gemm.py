@@ -98,7 +98,8 @@ def _wg_ok(x, d):
     weight gradient is 10 % faster there)."""
     T, K = x.shape
     Nn = d.shape[1]
-    return T >= 4096 and K % 128 == 0 and Nn % 128 == 0 and K * Nn > 768 * 768 and T % 64 == 0
+    small_ok = os.environ.get("MDTF_WG_SQUARE", "0") == "1"        # (A/B switch: the 768 x 768 product too)
+    return T >= 4096 and K % 128 == 0 and Nn % 128 == 0 and (K * Nn > 768 * 768 or small_ok) and T % 64 == 0
 
 
 _ACT = {None: 0, "relu": 1, "gelu": 2}
