@@ -95,6 +95,8 @@ def fwd(x, ws, biases=None, act=0, pre=None, out=None, tile=None):
     M, K = x.shape
     ns = ws[0].shape[1]
     Nn = ns * len(ws)
+    if tile is None and os.environ.get("MDTF_PP_FWD_TILE"):        # (A/B switch: force the forward tile code)
+        tile = int(os.environ["MDTF_PP_FWD_TILE"])
     t = (tile, 1) if tile is not None else pick_tile(0, M, Nn, K, ns if len(ws) > 1 else None)
     if t is None:
         return None
