@@ -55,3 +55,26 @@ def test_apply_multi_equals_sequential_updates():
         optim.apply_multi_(kind, a, grads, sa1, sa2, None, lrs, lrts, **kw)
         _sequential(kind, b, grads, sb1, sb2, lrs, lrts, **kw)
         assert torch.allclose(a, b, atol=1e-6), kind
+
+
+def test_wg_pick_table_and_fallback_fill_the_cus():
+    # measured table entries come back as stored (256-row tiles: 3-stage ring; 128-row: 2-stage)
+    for key, val in mm.WG_TILES.items():
+        if mm._WG_STAGES is None:
+            assert mm.wg_pick(*key) == val
+    # fallback: 256-row tiles when the rows allow it, split so tiles x splits <= 256 CUs, >= 16 K-tiles per split
+    for (M, Nn, K) in [(512, 1024, 8192), (640, 384, 4096), (2048, 2048, 4096), (128, 128, 64 * 8)]:
+        bm, st, sp = mm.wg_pick(M, Nn, K)
+        assert bm == (256 if M % 256 == 0 else 128) and st == (3 if bm == 256 else 2)
+        tiles = (M // bm) * (Nn // 128)
+        assert sp >= 1 and (sp == 1 or (tiles * sp <= mm.CUS and (K // 64) // sp >= 16)), (M, Nn, K, sp)
+
+
+def test_wg_route_shape_gate():
+    from mdtf.ops import gemm
+    x = torch.empty(8192, 768, dtype=torch.bfloat16)
+    assert gemm._wg_ok(x, torch.empty(8192, 2304, dtype=torch.bfloat16))       # q|k|v
+    assert gemm._wg_ok(torch.empty(8192, 3072, dtype=torch.bfloat16), torch.empty(8192, 768, dtype=torch.bfloat16))
+    assert not gemm._wg_ok(x, torch.empty(8192, 100, dtype=torch.bfloat16))    # N not a 128-multiple
+    assert not gemm._wg_ok(x[:2048], torch.empty(2048, 2304, dtype=torch.bfloat16))   # too few tokens
+    assert not gemm._wg_ok(torch.empty(8032, 768, dtype=torch.bfloat16), torch.empty(8032, 2304, dtype=torch.bfloat16))
