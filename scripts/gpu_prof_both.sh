@@ -11,5 +11,6 @@ cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof_resnet_$TAG" -o run --output-format csv \
     -- python3 "$ROOT/bench.py" --steps 5 --warmup 3 --bert 0 > "$ROOT/gpurun_out/prof_resnet_$TAG.log" 2>&1 \
   || { echo "resnet prof failed"; tail -20 "$ROOT/gpurun_out/prof_resnet_$TAG.log"; exit 1; }
-python3 "$ROOT/scripts/step_breakdown.py" "$ROOT/gpurun_out/prof_resnet_$TAG/run_kernel_trace.csv" | head -12
+python3 "$ROOT/scripts/step_breakdown.py" "$ROOT/gpurun_out/prof_resnet_$TAG/run_kernel_trace.csv" > "$ROOT/gpurun_out/resnet_steps_$TAG.txt"
+head -12 "$ROOT/gpurun_out/resnet_steps_$TAG.txt"
 python3 "$ROOT/scripts/prof_summary.py" "$ROOT/gpurun_out/prof_resnet_$TAG/run_kernel_stats.csv" 8 > "$ROOT/gpurun_out/resnet_prof_$TAG.txt"
