@@ -150,8 +150,23 @@ class FaultInjectionHook(H.SessionRunHook):
         h = cls(job_name, task_index)
         return h if h.armed else None
 
+    def before_run(self, run_context):
+        if not self.armed or not self.mode.endswith("_in_step") or V.get_global_step().value() < self.step:
+            return None
+        # raise from INSIDE the train op (after its collectives and update), not from a hook
+        from .. import errors
+        from ..train import step as S
+        self.armed = False
+        cls = errors.AbortedError if self.mode.startswith("abort") else errors.UnavailableError
+
+        def fault(step):
+            logger.error("injected in-step fault at global step %d (%s)" % (step, self.mode))
+            raise cls(message="injected %s inside the step at global step %d" % (self.mode, step))
+        S.STEP_FAULTS.append(fault)
+        return None
+
     def after_run(self, run_context, run_values):
-        if not self.armed or V.get_global_step().value() < self.step:
+        if not self.armed or self.mode.endswith("_in_step") or V.get_global_step().value() < self.step:
             return
         logger.error("injected fault at global step %d (%s)" % (V.get_global_step().value(), self.mode))
         if self.mode in ("abort", "unavailable"):

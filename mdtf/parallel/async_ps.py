@@ -91,29 +91,110 @@ K_PULL, K_PUSH, K_DONE, K_MASTER = 0, 1, 2, 3
 class _Posted(object):
     """A posted receive whose completion is polled without blocking, on both backends.  An RCCL work answers
     ``is_completed()`` from its HIP event; a gloo receive completes only inside ``wait()`` (its
-    ``is_completed()`` stays False), so a helper thread waits on it and the poll reads a flag."""
-    __slots__ = ("work", "ev")
+    ``is_completed()`` stays False), so a helper thread waits on it and the poll reads a flag.  A failed
+    receive (peer died, gloo timeout) is re-raised from ``done()`` / ``wait()`` in the service loop, so the PS
+    fails for the supervisor to restart instead of polling forever."""
+    __slots__ = ("work", "ev", "err", "wake")
 
-    def __init__(self, work, threaded):
+    def __init__(self, work, threaded, wake=None):
         self.work = work
         self.ev = None
+        self.err = None
+        self.wake = wake
         if threaded:
             import threading
             self.ev = threading.Event()
             threading.Thread(target=self._wait, daemon=True).start()
 
     def _wait(self):
-        self.work.wait()
-        self.ev.set()
+        try:
+            self.work.wait()
+        except BaseException as e:  # noqa: BLE001 - handed to the service loop
+            self.err = e
+        finally:
+            self.ev.set()
+            if self.wake is not None:
+                self.wake.set()
 
     def done(self):
-        return self.ev.is_set() if self.ev is not None else self.work.is_completed()
+        if self.ev is not None:
+            if not self.ev.is_set():
+                return False
+            if self.err is not None:
+                raise self.err
+            return True
+        return self.work.is_completed()
 
     def wait(self):
         if self.ev is not None:
             self.ev.wait()
+            if self.err is not None:
+                raise self.err
         else:
             self.work.wait()
+
+
+def service_loop(workers, post_header, read_header, post_payload, serve, apply_batch, threaded, st,
+                 idle_wait_s=0.002):
+    """The PS request loop, backend-independent (RCCL: ``threaded=False``, works polled with
+    ``is_completed()``; gloo: helper threads).
+
+    ``post_header(w)`` / ``post_payload(w)`` post the receives of worker ``w``'s next header / push payload
+    (works; a list for the payload); ``read_header(w)`` -> ``(kind, version)`` of the header that completed;
+    ``serve(w, kind, version)`` handles a non-push request (False once ``w`` is done); ``apply_batch(batch)``
+    applies the completed pushes ``[(w, version), ...]``.  Returns when every worker is done.  ``st["idle"]``
+    accumulates the seconds spent waiting with nothing to do."""
+    wake = None
+    if threaded:
+        import threading
+        wake = threading.Event()
+
+    def posted(work):
+        return _Posted(work, threaded, wake)
+
+    req = {w: posted(post_header(w)) for w in workers}
+    inflight = {}
+    done = 0
+    while done < len(workers):
+        if wake is not None:
+            wake.clear()                  # any completion after this point is seen by the wait below
+        progressed = False
+        for w in workers:
+            r = req.get(w)
+            if r is None or not r.done():
+                continue
+            progressed = True
+            r.wait()
+            kind, wver = read_header(w)
+            if kind == K_PUSH:
+                inflight[w] = ([posted(x) for x in post_payload(w)], wver)
+                req[w] = None                 # re-posted once the update is applied
+                continue
+            if serve(w, kind, wver):
+                req[w] = posted(post_header(w))
+            else:
+                req[w] = None
+                done += 1
+        ready = [w for w, (rs, _) in inflight.items() if all(x.done() for x in rs)]
+        if ready:
+            progressed = True
+            batch = []
+            for w in ready:
+                rs, wver = inflight.pop(w)
+                for x in rs:
+                    x.wait()
+                batch.append((w, wver))
+            apply_batch(batch)
+            for w, _ in batch:
+                req[w] = posted(post_header(w))
+        if not progressed:
+            ti = time.time()
+            if wake is not None:
+                wake.wait(idle_wait_s)        # woken by the helper thread of the next completed receive
+            else:
+                os.sched_yield()              # RCCL: the next poll is an event query, no GIL contention
+            st["idle"] += time.time() - ti
+    return st
 
 
 class _TimedStore(object):
@@ -242,38 +323,8 @@ def run_parameter_server(op, server):
     # ONE service loop for RCCL and gloo: a posted header receive per worker, polled; a push's payload receives
     # stay in flight while other workers are served; completed payloads are applied together
     threaded = dist.get_backend() != "nccl"
-    req = {w: _Posted(dist.irecv(hdr[w], src=w), threaded) for w in workers}
-    inflight = {}
-    while st["done"] < len(workers):
-        progressed = False
-        for w in workers:
-            r = req.get(w)
-            if r is None or not r.done():
-                continue
-            progressed = True
-            r.wait()
-            kind, wver = hdr[w].tolist()      # one device->host read per header
-            if kind == K_PUSH:
-                inflight[w] = ([_Posted(dist.irecv(b, src=w), threaded) for b in bufs(w)], wver)
-                req[w] = None                 # re-posted once the update is applied
-                continue
-            req[w] = _Posted(dist.irecv(hdr[w], src=w), threaded) if serve(w, kind, wver) else None
-        ready = [w for w, (rs, _) in inflight.items() if all(x.done() for x in rs)]
-        if ready:
-            progressed = True
-            batch = []
-            for w in ready:
-                rs, wver = inflight.pop(w)
-                for x in rs:
-                    x.wait()
-                batch.append((w, wver))
-            apply_batch(batch)
-            for w, _ in batch:
-                req[w] = _Posted(dist.irecv(hdr[w], src=w), threaded)
-        if not progressed:
-            ti = time.time()
-            os.sched_yield()
-            st["idle"] += time.time() - ti
+    service_loop(workers, lambda w: dist.irecv(hdr[w], src=w), lambda w: tuple(hdr[w].tolist()),
+                 lambda w: [dist.irecv(b, src=w) for b in bufs(w)], serve, apply_batch, threaded, st)
     server.store = store
     updates = st["updates"]
     stale_sum, stale_max = st["stale_sum"], st["stale_max"]

@@ -37,7 +37,8 @@ replicas to finish backward are aggregated, the rest contribute zeros (TF
 drops them as stale).  On GPUs the arrival order is decided ON THE DEVICE: each
 replica stamps the device clock when its backward has finished (a kernel on the
 compute stream), the stamps are all-gathered and every replica ranks itself
-(``csrc/backup.hip``; clock origins calibrated once against the host clock).
+(``csrc/backup.hip``; clock origins calibrated against the node's monotonic host clock, re-measured
+every 1000 steps; single-node groups only, a multi-node group takes the store ticket).
 The 0/1 mask scales the flat gradients before the bucket all-reduces, with no
 host synchronize and no store round trip, so the step stays hipGraph-capturable.
 On the CPU the order is an atomic counter in the cluster store.  Overlap is
@@ -131,8 +132,12 @@ class GradReducer(object):
         self.eager_update = None
         self._upd_stream = None
         # backup workers decided on the device (GPU replicas): see the module docstring
+        # device clocks are calibrated against ONE host clock, so only for a single-node group; multi-node
+        # groups take the store ticket
+        single_node = int(os.environ.get("LOCAL_WORLD_SIZE", self.world)) >= int(
+            os.environ.get("WORLD_SIZE", self.world))
         self.backup_device = (self.world > 1 and self.R < self.world and space.device is not None
-                              and torch.device(space.device).type == "cuda")
+                              and torch.device(space.device).type == "cuda" and single_node)
         self._bk = None
         if mode not in ("allreduce", "sharded"):
             raise ValueError("mode must be 'allreduce' or 'sharded'")
@@ -285,10 +290,10 @@ class GradReducer(object):
         best = None
         for _ in range(5):                  # the tightest of a few host brackets around one device stamp
             torch.cuda.synchronize(dev)
-            t0 = time.time_ns()
+            t0 = time.monotonic_ns()        # one system-wide clock for every rank of the node
             N.check(N.fn("mdtf_stamp_realtime")(N.ptr(stamp), N.stream_ptr()), "stamp_realtime")
             torch.cuda.synchronize(dev)
-            t1 = time.time_ns()
+            t1 = time.monotonic_ns()
             if best is None or t1 - t0 < best[0]:
                 best = (t1 - t0, int(stamp.item()) * 10 - (t0 + t1) // 2)
         off = torch.tensor([best[1]], dtype=torch.int64, device=dev)
@@ -298,9 +303,14 @@ class GradReducer(object):
                     "offsets": offsets, "mask": torch.ones(1, dtype=torch.float32, device=dev)}
         return self._bk
 
-    def _backup_mask_device(self):
+    BACKUP_RECALIBRATE_STEPS = 1000      # device-clock offsets re-measured this often (refclk drift)
+
+    def _backup_mask_device(self, step=0):
         from ..ops import _native as N
+        if self._bk is not None and step - self._bk.get("at", step) >= self.BACKUP_RECALIBRATE_STEPS:
+            self._bk = None                     # every rank reaches the same global step: a collective re-measure
         bk = self._backup_buffers()
+        bk.setdefault("at", step)
         N.check(N.fn("mdtf_stamp_realtime")(N.ptr(bk["stamp"]), N.stream_ptr()), "stamp_realtime")
         dist.all_gather(list(bk["stamps"].view(self.world, 1).unbind(0)), bk["stamp"], group=self.pg)
         N.check(N.fn("mdtf_backup_mask")(N.ptr(bk["stamps"]), N.ptr(bk["offsets"]), self.world, self.rank, self.R,
@@ -314,7 +324,7 @@ class GradReducer(object):
         from ..ops import conv as _conv
         _conv.join_side_streams()          # every weight gradient is in the flat buffer
         if self.backup_device:
-            self.contributed = self._backup_mask_device()      # device 0/1 (read only when someone asks)
+            self.contributed = self._backup_mask_device(step)  # device 0/1 (read only when someone asks)
             self.num_contributors = self.R
         elif self.world > 1 and self.R < self.world:
             # the ticket is taken after this replica's backward has COMPLETED on the device (not

@@ -288,13 +288,27 @@ class SyncReplicasHook(SessionRunHook):
     def __init__(self, opt, is_chief):
         self._opt = opt
         self.is_chief = is_chief
-        self.dropped_steps = 0
+        self._dropped = 0
+        self._dropped_dev = None       # device-side count when the contributor mask lives on the GPU
+
+    @property
+    def dropped_steps(self):
+        """Steps whose gradients were not aggregated (a host read only when asked for)."""
+        extra = int(self._dropped_dev.item()) if self._dropped_dev is not None else 0
+        return self._dropped + extra
 
     def after_run(self, run_context, run_values):
         from . import step as step_mod
         for op in step_mod.train_ops():
-            if op.optimizer is self._opt and not op.last_contributed:
-                self.dropped_steps += 1
+            if op.optimizer is not self._opt:
+                continue
+            c = op.last_contributed
+            if isinstance(c, torch.Tensor):
+                # GPU backup workers: count on the device, no host sync per step
+                miss = (c.reshape(-1)[:1] == 0).to(torch.int64)
+                self._dropped_dev = miss if self._dropped_dev is None else self._dropped_dev + miss
+            elif not c:
+                self._dropped += 1
 
 
 class ProfilerHook(SessionRunHook):

@@ -26,12 +26,19 @@ chief's broadcast state), hooks' ``after_create_session`` called again — and r
 With several replicas the restore is a collective, so the replicas first AGREE, at a step boundary, that
 one of them failed (reference ``distribute_train.py:169-180``: TF re-creates every worker's session when
 a PS restart aborts them).  Every ``run`` does, on every replica and in the same place:
-``before_run`` hooks -> one host all-reduce(MAX) of a "recovery needed" bit over a gloo group of the
-replicas -> the step -> ``after_run`` hooks.  A recoverable error raised by a hook on ONE replica (the
-step's collectives have all been issued, or none of them) is held and its bit set at the next agreement;
-then every replica re-creates its session from the chief's latest checkpoint in process and they continue
-from the same global step.  An error raised inside the step itself (mid-collective) cannot be agreed on
-safely and is re-raised, for the job supervisor's restart (``mdtf.cluster.health.supervise``).
+``before_run`` hooks -> one host all-reduce(MAX) of a code (0 ok, 1 recovery needed, 2 fatal) over a gloo
+group of the replicas -> the step -> ``after_run`` hooks.  A recoverable error raised on ONE replica by a
+hook, or inside the step once the step's collectives have been issued (a device error, a store failure), is
+held and its code sent at the next agreement; then every replica re-creates its session from the chief's
+latest checkpoint in process and they continue from the same global step (the failing replica retries the
+run that raised).  A non-recoverable error in ``before_run`` still joins the agreement with code 2, so every
+replica stops at that boundary instead of waiting in the next step's collectives.  An error that stops a
+replica before it issues the step's collectives leaves its peers inside them: that ends in the collective
+timeout / heartbeat watchdog and the job supervisor's restart (``mdtf.cluster.health.supervise``).
+
+Multi-replica ``run`` calls must stay in lockstep (every replica calls ``run`` the same number of times, in the
+same order): the agreement is a collective.  Fetch-only runs on one replica (the chief reading a variable)
+belong outside the session (``Variable.value()``, ``Saver``).
 """
 import os
 import time
@@ -157,7 +164,12 @@ class MonitoredSession(Session):
         self._stop = False
         self.restored_from = None
         self._agree_pg = None          # gloo group of the replicas for the recovery agreement (world > 1)
-        self._pending = None           # recoverable error a hook raised, held for the next agreement
+        self._pending = None           # recoverable error (hook or step) held for the next agreement
+        self._agree_buf = None
+        self.agreements = 0
+        self._agree_async = os.environ.get("MDTF_AGREE", "async") != "sync"
+        self._agree_work = None        # async agreement in flight: (work, result tensor)
+        self._posted_err = None
         for h in self._hooks:
             h.begin()
         self._create()
@@ -244,12 +256,19 @@ class MonitoredSession(Session):
             [dist.get_global_rank(pg, i) for i in range(dist.get_world_size(pg))]
         return dist.new_group(ranks, backend="gloo", use_local_synchronization=True)
 
-    def _agree(self, bad):
-        """All-reduce(MAX) of this replica's "recovery needed" bit: True if any replica needs it."""
+    AGREE_OK, AGREE_RECOVER, AGREE_FATAL = 0, 1, 2
+
+    def _agree(self, code):
+        """All-reduce(MAX) of this replica's code (0 ok, 1 recovery needed, 2 non-recoverable error): the
+        worst code of any replica.  One 4-byte gloo all-reduce per step; its cost at 8 ranks is in
+        ``profiles/agree_cost_r4.json`` (``bench/agree_cost.py``)."""
         import torch.distributed as dist
-        t = torch.tensor([1 if bad else 0], dtype=torch.int32)
+        t = self._agree_buf
+        if t is None:
+            t = self._agree_buf = torch.zeros(1, dtype=torch.int32)
+        t.fill_(int(code))
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._agree_pg)
-        return bool(t.item())
+        return int(t.item())
 
     @staticmethod
     def _visible_everywhere(ckpt, pg):
@@ -299,31 +318,78 @@ class MonitoredSession(Session):
                 self._recreate()
 
     def _run_agreed(self, fetches, feed_dict):
-        """Multi-replica run: hooks, step-boundary agreement, step (see the module docstring)."""
+        """Multi-replica run: hooks, step-boundary agreement, step (see the module docstring).
+
+        ``MDTF_AGREE=async`` (default): the boundary's all-reduce is POSTED and the step runs while it travels;
+        its result is read at the next boundary (one step later), where every replica sees the same code and
+        acts on it together: the per-step cost is a post and a wait on a completed work instead of a blocking
+        host round trip (``profiles/agree_cost_r4.json``).  A replica that must stop or recover still runs the
+        step it posted the code with, so no peer is left inside that step's collectives.
+        ``MDTF_AGREE=sync``: the all-reduce completes before the step (acted on at the same boundary)."""
         from .. import errors
+        async_mode = self._agree_async
         while True:
             if self._stop:
                 raise RuntimeError("Run called even after should_stop requested.")
+            if async_mode and self._agree_work is not None:
+                agreed = self._agree_result()        # the code posted one boundary ago
+                if agreed >= self.AGREE_FATAL:
+                    raise RuntimeError("a peer replica stopped on a non-recoverable error (agreed one step boundary "
+                                       "later)")
+                if agreed == self.AGREE_RECOVER:
+                    self._recover_agreed()
+                    continue
             pre = None
+            fatal = None
             try:
                 pre = self._before_run(fetches, feed_dict)
             except Exception as e:  # noqa: BLE001 - classified below
                 err = errors.as_recoverable(e)
                 if err is None:
+                    fatal = e                # still join the agreement, so the peers stop too (no hang)
+                else:
+                    self._pending = self._pending or err
+            code = self.AGREE_FATAL if fatal is not None else (
+                self.AGREE_RECOVER if self._pending is not None else self.AGREE_OK)
+            if async_mode:
+                self._agree_post(code)
+                if code == self.AGREE_RECOVER:
+                    self._posted_err = self._posted_err or self._pending
+                    self._pending = None     # posted; acted on when the result is read
+            else:
+                agreed = self._agree(code)
+                self.agreements += 1
+                if fatal is not None:
+                    raise fatal
+                if agreed >= self.AGREE_FATAL:
+                    raise RuntimeError("a peer replica stopped on a non-recoverable error at this step boundary")
+                if agreed == self.AGREE_RECOVER:
+                    self._recover_agreed()
+                    continue                 # retry this run on the restored state
+            if pre is None:
+                rc, extra, feed = None, {}, dict(feed_dict or {})
+            else:
+                rc, extra, feed = pre
+            try:
+                results = self.run_raw(self._all_fetches(fetches, extra), feed)
+            except Exception as e:  # noqa: BLE001 - classified below
+                err = errors.as_recoverable(e)
+                if err is None:
                     raise
-                self._pending = self._pending or err
-            if self._agree(self._pending is not None):
-                err = self._pending or errors.AbortedError(message="a peer replica requested session recovery")
-                self._pending = None
-                if self.recoveries >= self.max_recoveries:
-                    raise err
-                self.recoveries += 1
-                logger.warn("replica recovery agreed (%s: %s); re-creating the session from the chief's checkpoint "
-                            "(recovery %d of %d)" % (type(err).__name__, err, self.recoveries, self.max_recoveries))
-                self._recreate()
-                continue                     # retry this run on the restored state
-            rc, extra, feed = pre
-            results = self.run_raw(self._all_fetches(fetches, extra), feed)
+                # a recoverable error inside the step on this replica (e.g. a device or store error detected
+                # once the step's collectives were issued): hold it, agree with the peers at their next step
+                # boundary, recover there together and retry this run.  An error that stops this replica
+                # BEFORE it issues the step's collectives leaves the peers waiting in them: that case ends in
+                # the collective timeout / heartbeat watchdog and the supervisor's restart
+                # (mdtf.cluster.health), as in TF when a worker dies mid-step.
+                self._pending = err
+                logger.warn("%s inside the step on this replica; recovery is agreed at the next step boundary"
+                            % type(err).__name__)
+                continue
+            if fatal is not None:
+                # async: the step ran (its collectives are matched on every replica); the peers stop at the next
+                # boundary when they read code 2.  This replica stops now.
+                raise fatal
             try:
                 self._after_run(rc, extra, results)
             except Exception as e:  # noqa: BLE001 - classified below
@@ -336,6 +402,31 @@ class MonitoredSession(Session):
             if rc.stop_requested:
                 self._stop = True
             return results["__user__"]
+
+    def _agree_post(self, code):
+        import torch.distributed as dist
+        t = torch.full((1,), int(code), dtype=torch.int32)
+        self._agree_work = (dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._agree_pg, async_op=True), t)
+        self.agreements += 1
+
+    def _agree_result(self):
+        work, t = self._agree_work
+        self._agree_work = None
+        work.wait()
+        return int(t.item())
+
+    def _recover_agreed(self):
+        from .. import errors
+        err = self._posted_err or self._pending or errors.AbortedError(
+            message="a peer replica requested session recovery")
+        self._pending = None
+        self._posted_err = None
+        if self.recoveries >= self.max_recoveries:
+            raise err
+        self.recoveries += 1
+        logger.warn("replica recovery agreed (%s: %s); re-creating the session from the chief's checkpoint "
+                    "(recovery %d of %d)" % (type(err).__name__, err, self.recoveries, self.max_recoveries))
+        self._recreate()
 
     def _recreate(self):
         """Drop per-session device state and create again: restore the latest checkpoint, re-broadcast."""
@@ -390,10 +481,22 @@ class MonitoredSession(Session):
     def should_stop(self):
         return self._stop
 
+    def _drain_agreement(self):
+        """The last posted agreement (every replica posted one in its last run): complete it."""
+        if self._agree_work is None:
+            return
+        try:
+            if self._agree_result() != self.AGREE_OK:
+                logger.warn("a recovery / stop request agreed at the last step boundary is dropped: the session "
+                            "is closing")
+        except Exception as e:  # noqa: BLE001 - closing anyway
+            logger.warn("agreement drain at close failed: %s" % e)
+
     def close(self):
         if self._closed:
             return
         self._closed = True
+        self._drain_agreement()
         for h in self._hooks:
             h.end(self)
         if torch.cuda.is_available():

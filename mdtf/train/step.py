@@ -361,8 +361,15 @@ class TrainOp(Fetchable):
             self.graph.run(ctx, step)
         else:
             self._run_step(ctx, step)
+        if STEP_FAULTS:
+            # fault injection inside the step, after its collectives and update (mdtf.cluster.health
+            # FaultInjectionHook mode "abort_in_step"): a one-shot callable that raises
+            STEP_FAULTS.pop(0)(step)
         c = self.reducer.contributed
-        # (a device 0/1 mask for GPU backup workers: converted lazily by whoever reads it)
+        # (a device 0/1 mask for GPU backup workers: a per-step snapshot of the persistent mask buffer, which
+        # the next step / graph replay rewrites in place; converted lazily by whoever reads it)
+        if isinstance(c, torch.Tensor):
+            c = c.clone()
         self.last_contributed = c
         self.step_count += 1
         if self.global_step is not None:
@@ -372,6 +379,7 @@ class TrainOp(Fetchable):
 
 
 _TRAIN_OPS = []
+STEP_FAULTS = []        # one-shot callables(step) raised from inside TrainOp.evaluate (fault injection)
 
 
 def _register(op):

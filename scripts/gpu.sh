@@ -1,0 +1,85 @@
+#!/bin/bash
+# One entry point for the GPU-box runs (gpurun -- bash scripts/gpu.sh <what> [tag] [extra args]).
+#   tests   : pytest -m gpu (one process, per-test timeout)
+#   bench   : bench.py (ResNet-50 + BERT-base line), three times
+#   prof    : rocprofv3 --kernel-trace --stats of the captured ResNet-50 and BERT-base steps
+#   profr   : the same, ResNet-50 only
+#   pmc     : SQ / FETCH / WRITE+L2 counter passes over both steps (eager), each its own run
+#   envab   : alternating A/B of bench.py under two env settings: gpu.sh envab TAG "A=1" "A=0" [steps]
+#   py      : run a python script under a time limit: gpu.sh py TAG path/to/script.py [args]
+# Every GPU step runs under its own time limit and the script stops at the first failure.
+set -o pipefail
+ROOT="${GRAFT_REPO_ROOT:-/root/repo}"
+OUT="$ROOT/gpurun_out"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+WHAT=${1:-bench}
+TAG=${2:-x}
+shift 2 2>/dev/null
+fail() { echo "$1 failed"; tail -30 "$2"; exit 1; }
+
+prof_one() {   # name script args...
+  local name=$1; shift
+  (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_${name}_$TAG" -o run \
+      --output-format csv -- python3 "$@") > "$OUT/prof_${name}_$TAG.log" 2>&1 || fail "prof $name" "$OUT/prof_${name}_$TAG.log"
+  echo "prof $name ok"
+}
+
+case "$WHAT" in
+  tests)
+    cd "$ROOT"
+    timeout -k 10 1000 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread "$@" \
+        > "$OUT/pytest_gpu_$TAG.log" 2>&1
+    rc=$?
+    tail -15 "$OUT/pytest_gpu_$TAG.log"
+    exit $rc ;;
+  bench)
+    cd "$ROOT"
+    for i in 1 2 3; do
+      timeout -k 10 300 python bench.py "$@" > "$OUT/bench_${TAG}_$i.log" 2>&1 || fail "bench $i" "$OUT/bench_${TAG}_$i.log"
+      tail -1 "$OUT/bench_${TAG}_$i.log"
+    done ;;
+  prof)
+    prof_one resnet "$ROOT/bench.py" --steps 5 --warmup 3 --bert 0 "$@"
+    prof_one bert "$ROOT/bench/bert_bench.py" --steps 5 --warmup 3
+    cd "$ROOT" && python scripts/step_breakdown.py "$OUT/prof_resnet_$TAG" --calls > "$OUT/summary_resnet_$TAG.txt" 2>&1
+    python scripts/step_breakdown.py "$OUT/prof_bert_$TAG" > "$OUT/summary_bert_$TAG.txt" 2>&1
+    head -30 "$OUT/summary_resnet_$TAG.txt" ;;
+  profr)
+    prof_one resnet "$ROOT/bench.py" --steps 5 --warmup 3 --bert 0 "$@"
+    cd "$ROOT" && python scripts/step_breakdown.py "$OUT/prof_resnet_$TAG" --calls > "$OUT/summary_resnet_$TAG.txt" 2>&1
+    head -40 "$OUT/summary_resnet_$TAG.txt" ;;
+  pmc)
+    P1="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CU_CYCLES SQ_WAVES GRBM_GUI_ACTIVE"
+    P2="FETCH_SIZE GRBM_GUI_ACTIVE"
+    P3="WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"
+    i=0
+    for P in "$P1" "$P2" "$P3"; do
+      i=$((i+1))
+      (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $P --kernel-trace -d "$OUT/pmcr_${TAG}_p$i" -o run \
+          --output-format csv -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --hip_graph 0 --bert 0) \
+          > "$OUT/pmcr_${TAG}_p$i.log" 2>&1 || fail "resnet pmc $i" "$OUT/pmcr_${TAG}_p$i.log"
+      (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $P --kernel-trace -d "$OUT/pmcb_${TAG}_p$i" -o run \
+          --output-format csv -- python3 "$ROOT/bench/bert_bench.py" --steps 2 --warmup 1 --hip_graph 0) \
+          > "$OUT/pmcb_${TAG}_p$i.log" 2>&1 || fail "bert pmc $i" "$OUT/pmcb_${TAG}_p$i.log"
+      echo "pmc pass $i ok"
+    done ;;
+  envab)
+    A=$1; B=$2; STEPS=${3:-30}
+    cd "$ROOT"
+    for i in 1 2 3; do
+      for arm in A B; do
+        if [ $arm = A ]; then E=$A; else E=$B; fi
+        env $E timeout -k 10 300 python bench.py --steps $STEPS --warmup 5 --bert 0 > "$OUT/ab_${TAG}_${arm}_$i.log" 2>&1 \
+          || fail "ab $arm $i" "$OUT/ab_${TAG}_${arm}_$i.log"
+        echo "$arm($E) $(tail -1 "$OUT/ab_${TAG}_${arm}_$i.log" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+      done
+    done ;;
+  py)
+    cd "$ROOT"
+    S=$1; shift
+    timeout -k 10 600 python -u "$S" "$@" > "$OUT/py_$TAG.log" 2>&1 || fail "py $S" "$OUT/py_$TAG.log"
+    tail -40 "$OUT/py_$TAG.log" ;;
+  *)
+    echo "unknown: $WHAT"; exit 2 ;;
+esac

@@ -158,12 +158,13 @@ def hidden_ckpt_restore_worker(rank, world, port, out_dir):
     _teardown(server)
 
 
-def recovery_worker(rank, world, port, steps, out_dir, fault_step=None, fault_task="worker:1", mode="abort"):
+def recovery_worker(rank, world, port, steps, out_dir, fault_step=None, fault_task="worker:1", mode="abort",
+                    agree="async"):
     """Sync replicas under MonitoredTrainingSession with a chief checkpoint every 2 steps; ``fault_task``
     raises an in-process AbortedError after ``fault_step`` (one replica only): every replica must agree on
     the recovery, restore the chief's checkpoint in process and finish at the same global step."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), MDTF_AGREE=agree)
     import mdtf
     from mdtf.cluster import Server
     from mdtf.cluster.health import FaultInjectionHook
@@ -190,9 +191,46 @@ def recovery_worker(rank, world, port, steps, out_dir, fault_step=None, fault_ta
             sess.run(op, feed_dict={x_ph: xs[lo:hi], y_ph: ys[lo:hi]})
             runs += 1
         rec = sess.recoveries
+        agreements = sess.agreements
     w = {v.name: v.master.tolist() for v in V.get_store().trainable_variables()}
     with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
-        json.dump({"step": gs.value(), "recoveries": rec, "runs": runs, "weights": w}, f)
+        json.dump({"step": gs.value(), "recoveries": rec, "runs": runs, "weights": w, "agreements": agreements}, f)
+    _teardown(server)
+
+
+def fatal_hook_worker(rank, world, port, out_dir):
+    """Replica 1's hook raises a non-recoverable ValueError in before_run at global step 3."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    import mdtf
+    from mdtf.cluster import Server
+    from mdtf.train import hooks as H
+    server = Server.from_env(backend="gloo")
+    batch = 4
+    Lin, MSE, xs, ys, x_ph, y_ph, Tower, Net = _linear_setup(rank, world, batch)
+    base = mdtf.train.MomentumOptimizer(0.1, 0.9)
+    tg = []
+    Tower(Net(Lin()), "tower_0/", tg, x_ph, y_ph, MSE(), base, batch_size=batch).process()
+    opt = mdtf.train.SyncReplicasOptimizer(base, replicas_to_aggregate=world, total_num_replicas=world)
+    gs = mdtf.train.get_or_create_global_step()
+    op = opt.apply_gradients(Tower.average_gradients(tg), global_step=gs)
+
+    class Bug(H.SessionRunHook):
+        def before_run(self, rc):
+            if rank == 1 and gs.value() == 3:
+                raise ValueError("bug in a hook")
+
+    lo, hi = rank * batch, (rank + 1) * batch
+    err = None
+    sess = mdtf.train.MonitoredTrainingSession(is_chief=rank == 0, hooks=[H.StopAtStepHook(last_step=8), Bug()],
+                                               log_step_count_steps=0, server=server)
+    try:
+        while not sess.should_stop():
+            sess.run(op, feed_dict={x_ph: xs[lo:hi], y_ph: ys[lo:hi]})
+    except Exception as e:  # noqa: BLE001 - recorded for the test
+        err = "%s: %s" % (type(e).__name__, e)
+    with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
+        json.dump({"step": gs.value(), "error": err}, f)
     _teardown(server)
 
 

@@ -245,24 +245,70 @@ def test_restore_when_checkpoint_visible_only_on_chief(tmp_path):
     assert any(abs(x) > 0 for x in res[0]["adam_m"])
 
 
-def test_coordinated_recovery_one_replica_aborts(tmp_path):
+@pytest.mark.parametrize("agree", ["sync", "async"])
+def test_coordinated_recovery_one_replica_aborts(tmp_path, agree):
     """ONE of two sync replicas raises AbortedError after step 5 (reference distribute_train.py:169-180: the
-    recoverable MonitoredTrainingSession).  Both replicas agree on the recovery at the next step boundary,
-    re-create their sessions in process from the chief's step-4 checkpoint, and finish at the same global
-    step with the weights of an uninterrupted run."""
+    recoverable MonitoredTrainingSession).  Both replicas agree on the recovery at a step boundary (sync: the
+    next one; async: the code posted at the next boundary is read one boundary later), re-create their sessions
+    in process from the chief's latest checkpoint, and finish at the same global step with the weights of an
+    uninterrupted run."""
     sys.path.insert(0, os.path.dirname(__file__))
     import dist_helpers
     res = {}
     for tag, fault in (("ref", None), ("run", 5)):
         d = tmp_path / tag
         d.mkdir()
-        mp.start_processes(dist_helpers.recovery_worker, args=(2, free_port(), 8, str(d), fault),
+        mp.start_processes(dist_helpers.recovery_worker, args=(2, free_port(), 8, str(d), fault, "worker:1", "abort",
+                                                               agree),
                            nprocs=2, join=True, start_method="spawn")
         res[tag] = [json.load(open(str(d / ("rank%d.json" % r)))) for r in range(2)]
     ref, run = res["ref"], res["run"]
     assert [r["step"] for r in run] == [8, 8] and [r["recoveries"] for r in run] == [1, 1]
     assert [r["recoveries"] for r in ref] == [0, 0]
-    assert run[0]["runs"] == run[1]["runs"] == ref[0]["runs"] + 1     # step 5 re-runs from the step-4 state
+    assert run[0]["runs"] == run[1]["runs"]
+    if agree == "sync":
+        assert run[0]["runs"] == ref[0]["runs"] + 1     # step 5 re-runs from the step-4 state
     for k, w in ref[0]["weights"].items():
         for r in run:
             assert torch.allclose(torch.tensor(r["weights"][k]), torch.tensor(w), atol=1e-6), k
+
+
+def test_coordinated_recovery_error_inside_the_step(tmp_path):
+    """ONE of two sync replicas raises AbortedError from INSIDE its train op (after the step's collectives and
+    update: ``FaultInjectionHook`` mode ``abort_in_step``), not from a hook.  The failing replica holds the
+    error, both replicas agree at the next step boundary, restore the chief's step-4 checkpoint in process and
+    finish at the same global step with the weights of an uninterrupted run (reference
+    distribute_train.py:169-180)."""
+    sys.path.insert(0, os.path.dirname(__file__))
+    import dist_helpers
+    res = {}
+    for tag, fault in (("ref", None), ("run", 5)):
+        d = tmp_path / tag
+        d.mkdir()
+        mp.start_processes(dist_helpers.recovery_worker, args=(2, free_port(), 8, str(d), fault, "worker:1",
+                                                               "abort_in_step"),
+                           nprocs=2, join=True, start_method="spawn")
+        res[tag] = [json.load(open(str(d / ("rank%d.json" % r)))) for r in range(2)]
+    ref, run = res["ref"], res["run"]
+    assert [r["step"] for r in run] == [8, 8] and [r["recoveries"] for r in run] == [1, 1]
+    assert [r["agreements"] for r in run] == [run[0]["agreements"]] * 2       # lockstep boundaries
+    # the failing replica retried its run inside the same call, so its peer made one call more
+    assert run[1]["runs"] == run[0]["runs"] - 1
+    for k, w in ref[0]["weights"].items():
+        for r in run:
+            assert torch.allclose(torch.tensor(r["weights"][k]), torch.tensor(w), atol=1e-6), k
+
+
+def test_fatal_hook_error_stops_every_replica(tmp_path):
+    """A non-recoverable error in one replica's before_run still joins the step-boundary agreement: the peer
+    stops at that boundary with an error instead of waiting in the next step's collectives."""
+    sys.path.insert(0, os.path.dirname(__file__))
+    import dist_helpers
+    d = tmp_path / "fatal"
+    d.mkdir()
+    mp.start_processes(dist_helpers.fatal_hook_worker, args=(2, free_port(), str(d)), nprocs=2, join=True,
+                       start_method="spawn")
+    out = [json.load(open(str(d / ("rank%d.json" % r)))) for r in range(2)]
+    assert out[1]["error"].startswith("ValueError") and "bug in a hook" in out[1]["error"]
+    assert out[0]["error"].startswith("RuntimeError") and "non-recoverable" in out[0]["error"]
+    assert out[0]["step"] == out[1]["step"] == 4        # async agreement: the posted step still ran everywhere
