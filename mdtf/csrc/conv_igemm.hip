@@ -1499,6 +1499,78 @@ int dispatch_wgrad_v2(ConvArgs& a, int bm, int bn, int stages, int w8, int split
   return MDTF_EUNSUPPORTED;
 }
 
+// Strided dgrad, the stride-parity classes whose filter-tap set is empty (3 of the 4 classes of a 1x1 stride-2
+// conv): DX there is 0 + the accumulate source, so these pixels are a streaming pass, not a GEMM.  One launch
+// covers every such class.  Thread = one 16-B channel chunk of one DX pixel; with C8 = Cin / 8 dividing the block,
+// a thread keeps one chunk for the whole grid-stride walk, so the BN-backward partials (Σ g·mask, Σ g·mask·x)
+// stay in registers and are reduced once per block.  Pixels of classes with taps are skipped (their GEMM
+// launch writes them).  out = acc ? (acc_src ? acc_src * acc_mask : out) : 0.
+template <bool BSTAT>
+__global__ void __launch_bounds__(256) dgrad_zero_classes(ConvArgs a, int C8) {
+  const int tid = threadIdx.x;
+  const int ppb = 256 / C8;                          // pixels per block iteration
+  const int c8 = tid % C8, pl = tid / C8;
+  const long long P = (long long)a.N * a.H * a.W;
+  float s0[8], s1[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s0[k] = s1[k] = 0.f;
+  for (long long p = (long long)blockIdx.x * ppb + pl; p < P; p += (long long)gridDim.x * ppb) {
+    const int w = static_cast<int>(p % a.W);
+    const int h = static_cast<int>((p / a.W) % a.H);
+    const int rh = (h + a.PH) % a.SH, rw = (w + a.PW) % a.SW;
+    if (rh < a.KH && rw < a.KW) continue;            // this class has taps: the GEMM launch owns it
+    const long long off = p * a.Ncol + c8 * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (a.accumulate) {
+      v = *reinterpret_cast<const uint4*>((a.acc_src ? a.acc_src : a.out) + off);
+      if (a.acc_mask) v = mask_bf8(v, a.acc_mask[off >> 3]);
+    }
+    if (a.acc_src || !a.accumulate) *reinterpret_cast<uint4*>(a.out + off) = v;
+    if constexpr (BSTAT) {
+      const uint4 x4 = *reinterpret_cast<const uint4*>(a.bx + off);
+      const uint32_t mb = a.bmask ? a.bmask[off >> 3] : 0xffu;
+      const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float g = (k & 1) ? __uint_as_float(vw[k >> 1] & 0xffff0000u) : __uint_as_float(vw[k >> 1] << 16);
+        const float xk = (k & 1) ? __uint_as_float(xw[k >> 1] & 0xffff0000u) : __uint_as_float(xw[k >> 1] << 16);
+        const float gm = ((mb >> k) & 1u) ? g : 0.f;
+        s0[k] += gm;
+        s1[k] += gm * xk;
+      }
+    }
+  }
+  if constexpr (BSTAT) {
+    __shared__ float red[2][8][256];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[0][k][tid] = s0[k];
+      red[1][k][tid] = s1[k];
+    }
+    __syncthreads();
+    const long long slot = (long long)(blockIdx.x % a.bslots) * a.Ncol;
+    for (int ch = tid; ch < a.Ncol; ch += 256) {
+      const int cc = ch >> 3, k = ch & 7;
+      float sv = 0.f, q = 0.f;
+      for (int t = cc; t < 256; t += C8) {
+        sv += red[0][k][t];
+        q += red[1][k][t];
+      }
+      atomicAdd(a.bsum + slot + ch, sv);
+      atomicAdd(a.bsq + slot + ch, q);
+    }
+  }
+}
+
+// MDTF_ZERO_CLASS=gemm: the tap-less classes run the GEMM kernel with K = 0 as before (A/B switch)
+bool zero_class_gemm() {
+  static const bool g = [] {
+    const char* e = getenv("MDTF_ZERO_CLASS");
+    return e && e[0] == 'g';
+  }();
+  return g;
+}
+
 ConvArgs make_args(int N, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int SH, int SW, int PH,
                    int PW, int DH, int DW) {
   ConvArgs a{};
@@ -1633,7 +1705,11 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
     a.K = KH * KW * Cout;
     return dispatch_fd_v2<1, false>(a, bm, bn, stages, st);
   }
-  // strided: one launch per stride-parity class (rh, rw) = ((h + PH) % SH, (w + PW) % SW)
+  // strided: one launch per stride-parity class (rh, rw) = ((h + PH) % SH, (w + PW) % SW); the classes without
+  // taps go to one streaming launch (dgrad_zero_classes) when their pixels must be written or counted
+  const int C8 = Cin / 8;
+  const bool zero_stream = C8 <= 256 && 256 % C8 == 0 && !zero_class_gemm();
+  bool zero_pending = false;
   for (int rh = 0; rh < SH; ++rh)
     for (int rw = 0; rw < SW; ++rw) {
       ConvArgs c = a;
@@ -1652,10 +1728,23 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
       // no pixels / nothing to add (unless the BN statistics need every pixel)
       // (with a separate accumulate source the class's pixels must still be written)
       if (c.M == 0 || (c.K == 0 && accumulate && !bsum && !acc_src)) continue;
+      if (c.K == 0 && zero_stream) {
+        zero_pending = true;
+        continue;
+      }
       const int cs = c.K > 64 && stages == 1 ? 2 : stages;
       const int rc = dispatch_fd_v2<2, false>(c, bm, bn, cs, st);
       if (rc) return rc;
     }
+  if (zero_pending) {
+    const long long chunks = (long long)N * H * W * C8;
+    const int blocks = static_cast<int>(ceil_div(chunks, 256) < 4096 ? ceil_div(chunks, 256) : 4096);
+    if (bsum)
+      hipLaunchKernelGGL(dgrad_zero_classes<true>, dim3(blocks), dim3(256), 0, st, a, C8);
+    else
+      hipLaunchKernelGGL(dgrad_zero_classes<false>, dim3(blocks), dim3(256), 0, st, a, C8);
+    MDTF_LAUNCH_CHECK();
+  }
   return 0;
 }
 

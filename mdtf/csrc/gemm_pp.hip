@@ -43,6 +43,37 @@ typedef __attribute__((address_space(3))) v4s lds_v4s;
 constexpr unsigned kOOB = 0x80000000u;   // buffer offset past num_records: the DMA writes zeros
 constexpr int kCUs = 256;                 // MI355X compute units: one 512-thread GEMM block each
 
+// Implicit-GEMM convolution on the same core (CONV = 1 forward, 2 stride-1 data gradient).  A is gathered: GEMM
+// row m = one pixel of the row grid (fwd: output pixel, dgrad: DX pixel), K-tile t = 64 channels c0 of filter tap
+// `tap` (taps in HWIO order, GC / 64 K-tiles per tap), read from the gathered tensor (fwd X, dgrad DY) at
+//   fwd   (oh SH - PH + kh DH, ow SW - PW + kw DW)      dgrad (h + PH - kh DH, w + PW - kw DW)
+// Each DMA lane keeps its row's element offset of tap (0, 0) and a bitmask of the taps that stay inside the image
+// (computed once per tile with magic-number divisions); a K-tile adds a wave-uniform tap offset and tests one bit,
+// taps outside the image get an offset past the buffer range (zero fill).  B is the filter, K-contiguous rows:
+// fwd Wt[co][(tap, ci)] (the gemm layout), dgrad W[tap][ci][co] (row ci, tap stride Cin Cout).
+struct ConvGeo {
+  int GH, GW, GC;              // gathered tensor dims (per image)
+  int RH, RW;                  // row-pixel grid per image
+  unsigned mag_rw, mag_rh, mag_kw;
+  int sh_rw, sh_rh, sh_kw;
+  int SH, SW, PH, PW, DH, DW, KH, KW;
+  int cpt_lg;                  // log2(GC / 64): K-tiles per tap
+  long long wtap_bytes;        // dgrad: bytes per filter tap of B (Cin Cout 2)
+  // forward epilogue: per-channel BatchNorm partials sum y, sum y^2 into row (tile_m % stat_slots)
+  float* stat_sum;
+  float* stat_sq;
+  int stat_slots;
+  // dgrad epilogue: out = result + (acc_src ? acc_src * acc_mask bit : out) when accumulating; BN-backward
+  // statistics sum g m, sum g m x of the stored gradient g (m: bmask bit, x: bx) into row (tile_m % bslots)
+  const bf16_t* acc_src;
+  const uint8_t* acc_mask;
+  const bf16_t* bx;
+  const uint8_t* bmask;
+  float* bsum;
+  float* bsq;
+  int bslots;
+};
+
 struct GemmArgs {
   const bf16_t* A;
   const bf16_t* B;
@@ -73,7 +104,17 @@ struct GemmArgs {
   const bf16_t* act_pre;     // dgrad: C = acc * act'(act_pre) (the producer's activation backward), null: none
   int act_bwd;
   int persistent;            // 1: grid = min(tiles, CUs) blocks loop over the tiles
+  ConvGeo cv;                // CONV != 0
 };
+
+// n / d for n < 2^31 with a host-computed magic pair (umulhi + add + shift)
+__device__ __forceinline__ unsigned fdiv(unsigned n, unsigned mag, int sh) { return (__umulhi(n, mag) + n) >> sh; }
+
+void magic_u32(unsigned d, unsigned& mag, int& sh) {
+  sh = 0;
+  while ((1ull << sh) < d) ++sh;
+  mag = static_cast<unsigned>(((1ull << 32) * ((1ull << sh) - d)) / d + 1);
+}
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
   if (act == 1) return fmaxf(v, 0.f);
@@ -144,8 +185,9 @@ struct Unit {
 // Tile geometry.  Eight waves = group G (M half) x 4 column strips; each wave owns (BM/2) x (BN/4).
 //   BM = 256: four quadrant phases per 64-deep K-tile, 2 LDS stages, unit-level DMA schedule;
 //   BM = 128: two k-substep phases per K-tile, 3 LDS stages, whole-tile DMA one tile further ahead.
-template <int BM, int BN, bool ATR, bool BTR, int EPI>
+template <int BM, int BN, bool ATR, bool BTR, int EPI, int CONV = 0>
 __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
+  static_assert(CONV == 0 || (!ATR && !BTR && EPI == 0), "conv: K-contiguous operands, bf16 output");
   constexpr int RW = BM / 2, CW = BN / 4;
   constexpr int FM = RW / 16, FN = CW / 16;
   constexpr int FMH = FM / 2, FNL = (FN + 1) / 2;
@@ -202,7 +244,45 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
   // a 192-B-pitch transposed image: instruction j = 1 does not start on a row boundary -> its own offsets
   constexpr bool B_J1 = BTR && UB::PITCH == 192;
   unsigned vA = 0, vB = 0, vB1 = 0;
+  // CONV: per (unit half u, instruction j) the lane's row offset of tap (0, 0) (elements, channel chunk included)
+  // and its in-image tap mask.  Row = u WA + (8 j + wave) 8 + lane / 8; its 16-B chunk swizzle does not depend
+  // on u or j (WA and 64 j are multiples of 16 rows).
+  constexpr int JA = (UA::NI + 7) / 8;
+  unsigned cA[2][JA], mA[2][JA];
+  auto conv_rows = [&]() {
+    const ConvGeo& g = a.cv;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < JA; ++j) {
+        const int row = u * WA + (8 * j + wave) * 8 + (lane >> 3);
+        const int lc = (lane & 7) ^ ((row >> 1) & 7);
+        const int m = m0 + row;
+        unsigned mask = 0, base = 0;
+        if (m < a.M && (8 * j + wave) < UA::NI) {
+          const unsigned t1 = fdiv(m, g.mag_rw, g.sh_rw);
+          const int ow = m - static_cast<int>(t1) * g.RW;
+          const unsigned n = fdiv(t1, g.mag_rh, g.sh_rh);
+          const int oh = static_cast<int>(t1 - n * g.RH);
+          const int y0 = CONV == 1 ? oh * g.SH - g.PH : oh + g.PH;
+          const int x0 = CONV == 1 ? ow * g.SW - g.PW : ow + g.PW;
+          unsigned wm = 0;
+          for (int kw = 0; kw < g.KW; ++kw) {
+            const int ix = CONV == 1 ? x0 + kw * g.DW : x0 - kw * g.DW;
+            wm |= (ix >= 0 && ix < g.GW) ? (1u << kw) : 0u;
+          }
+          for (int kh = 0; kh < g.KH; ++kh) {
+            const int iy = CONV == 1 ? y0 + kh * g.DH : y0 - kh * g.DH;
+            if (iy >= 0 && iy < g.GH) mask |= wm << (kh * g.KW);
+          }
+          base = ((n * g.GH + y0) * g.GW + x0) * g.GC + lc * 8;
+        }
+        cA[u][j] = base;
+        mA[u][j] = mask;
+      }
+  };
   auto set_offsets = [&]() {
+    if constexpr (CONV != 0) conv_rows();
     vA = src_off(ATR, UA::PITCH, a.lda, m0, a.M, wave);
     vB = src_off(BTR, UB::PITCH, a.ldb, n0, a.N, wave);
     vB1 = B_J1 ? src_off(true, UB::PITCH, a.ldb, n0, a.N, 8 + wave) : 0u;
@@ -218,6 +298,23 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
   // this wave's (group-uniform) share of unit u of K-tile t, into slot t % STAGES
   auto issue_unit = [&](int u, int t) {
     const unsigned slot = lds0 + (t % STAGES) * SLOT;
+    if (CONV != 0 && u < 2) {
+      const ConvGeo& g = a.cv;
+      const int tap = t >> g.cpt_lg;
+      const int c0 = (t & ((1 << g.cpt_lg) - 1)) * 64;
+      const int kh = static_cast<int>(fdiv(tap, g.mag_kw, g.sh_kw)), kw = tap - kh * g.KW;
+      const int sp = (kh * g.DH * g.GW + kw * g.DW) * g.GC;
+      const unsigned te = static_cast<unsigned>((CONV == 1 ? sp : -sp) + c0);
+      const int cnt = G == 0 ? UA::template per_wave<0>() : UA::template per_wave<1>();
+#pragma unroll
+      for (int j = 0; j < JA; ++j)
+        if (j < cnt) {
+          const unsigned c = u == 0 ? cA[0][j] : cA[1][j];
+          const unsigned m = u == 0 ? mA[0][j] : mA[1][j];
+          dma16(ra, slot + u * UA::BYTES + (j * 8 + wave) * 1024, ((m >> tap) & 1u) ? (c + te) * 2u : kOOB, 0);
+        }
+      return;
+    }
     if (u < 2) {
       const int cnt = G == 0 ? UA::template per_wave<0>() : UA::template per_wave<1>();
 #pragma unroll
@@ -230,7 +327,11 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
       // segment rebasing folded into the descriptor (a negative soffset would break the range check): the
       // column / reduction index counts from the first segment's origin
       const i32x4_t rb = buffer_rsrc(a.bseg[seg] - seg * a.seg_cols, a.bytes_b + seg * a.seg_cols * 2);
-      const int sb = t * stepB + (u - 2) * duB;
+      int sb = t * stepB + (u - 2) * duB;
+      if constexpr (CONV == 2) {      // W[tap][ci][co]: the K-tile's tap block, then its 64 output channels
+        const int tap = t >> a.cv.cpt_lg;
+        sb = static_cast<int>(tap * a.cv.wtap_bytes) + (t & ((1 << a.cv.cpt_lg) - 1)) * 128 + (u - 2) * duB;
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         if (j < cnt)
@@ -491,7 +592,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
       bpre[j] = *reinterpret_cast<const uint2*>(a.biasseg[sg] + (col - sg * a.seg_cols));
     }
   }
-  const bool early = !(a.act_bwd || a.accumulate || (EPI == 1 && !a.atomic));
+  const bool early = !(a.act_bwd || a.accumulate || (EPI == 1 && !a.atomic) || (CONV == 2 && a.cv.bsum));
   if (more && early) {
     set_tile(nxt);
     set_offsets();
@@ -511,6 +612,90 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
       for (int e = 0; e < 4; ++e) unsafeAtomicAdd(db + e, accb[j][e]);
     }
   }
+  if constexpr (CONV != 0) {
+    // ---- convolution epilogue: bf16 store (dgrad: + accumulate source), BN statistics of the tile's columns
+    const ConvGeo& g = a.cv;
+    const bool st = CONV == 1 ? g.stat_sum != nullptr : g.bsum != nullptr;
+    float s0[FN][4], s1[FN][4];
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s0[j][e] = s1[j][e] = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = rbase + 16 * i;
+      if (row >= a.M) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = cbase + 16 * j;
+        if (col >= a.N) continue;
+        const long long off = (long long)row * a.ldc + col;
+        float4v v = acc[i][j];
+        if (CONV == 2 && a.accumulate) {
+          uint2 o = *reinterpret_cast<const uint2*>((g.acc_src ? g.acc_src : a.C) + off);
+          if (g.acc_mask) {
+            const unsigned nb = (g.acc_mask[off >> 3] >> (off & 7)) & 15u;
+            o.x &= ((nb & 1u) ? 0x0000ffffu : 0u) | ((nb & 2u) ? 0xffff0000u : 0u);
+            o.y &= ((nb & 4u) ? 0x0000ffffu : 0u) | ((nb & 8u) ? 0xffff0000u : 0u);
+          }
+          v[0] += __uint_as_float(o.x << 16);
+          v[1] += __uint_as_float(o.x & 0xffff0000u);
+          v[2] += __uint_as_float(o.y << 16);
+          v[3] += __uint_as_float(o.y & 0xffff0000u);
+        }
+        const uint2 pk = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+        *reinterpret_cast<uint2*>(a.C + off) = pk;
+        if (CONV == 1 && st) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            s0[j][e] += v[e];
+            s1[j][e] += v[e] * v[e];
+          }
+        } else if (CONV == 2 && st) {
+          const uint2 xq = *reinterpret_cast<const uint2*>(g.bx + off);
+          const unsigned nb = g.bmask ? (g.bmask[off >> 3] >> (off & 7)) & 15u : 15u;
+          const float gv[4] = {__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
+                               __uint_as_float(pk.y << 16), __uint_as_float(pk.y & 0xffff0000u)};
+          const float xv[4] = {__uint_as_float(xq.x << 16), __uint_as_float(xq.x & 0xffff0000u),
+                               __uint_as_float(xq.y << 16), __uint_as_float(xq.y & 0xffff0000u)};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float gm = ((nb >> e) & 1u) ? gv[e] : 0.f;
+            s0[j][e] += gm;
+            s1[j][e] += gm * xv[e];
+          }
+        }
+      }
+    }
+    if (st) {
+      // the 16 lanes of a 4-column group hold 16 rows each: butterfly over lane bits 0..3, then lanes fr = e
+      // (e < 4) add column e of every group
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            s0[j][e] += __shfl_xor(s0[j][e], o, 64);
+            s1[j][e] += __shfl_xor(s1[j][e], o, 64);
+          }
+      float* psum = CONV == 1 ? g.stat_sum : g.bsum;
+      float* psq = CONV == 1 ? g.stat_sq : g.bsq;
+      const int slots = CONV == 1 ? g.stat_slots : g.bslots;
+      const long long srow = (long long)((em0 / BM) % slots) * a.N;
+      if (fr < 4) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int col = cbase + 16 * j + fr;
+          if (col >= a.N) continue;
+          const float v0 = fr == 0 ? s0[j][0] : fr == 1 ? s0[j][1] : fr == 2 ? s0[j][2] : s0[j][3];
+          const float v1 = fr == 0 ? s1[j][0] : fr == 1 ? s1[j][1] : fr == 2 ? s1[j][2] : s1[j][3];
+          atomicAdd(psum + srow + col, v0);
+          atomicAdd(psq + srow + col, v1);
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int row = rbase + 16 * i;
@@ -570,6 +755,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
       }
     }
   }
+  }
   if (!more) break;
   if (!early) {
     set_tile(nxt);
@@ -581,7 +767,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
   }
 }
 
-template <int BM, int BN, bool ATR, bool BTR, int EPI>
+template <int BM, int BN, bool ATR, bool BTR, int EPI, int CONV = 0>
 int launch_pp(const GemmArgs& a0, int splits, hipStream_t st) {
   GemmArgs a = a0;
   // a transposed (k-major) operand's tile must not straddle its edge (see src_off)
@@ -595,7 +781,7 @@ int launch_pp(const GemmArgs& a0, int splits, hipStream_t st) {
   splits = (KT + a.kt_split - 1) / a.kt_split;
   if (EPI == 1) a.atomic = splits > 1 ? 1 : a.atomic;
   constexpr int lds = (BM == 256 ? 2 : 3) * (BM + BN) * 128;
-  auto k = gemm_pp_kernel<BM, BN, ATR, BTR, EPI>;
+  auto k = gemm_pp_kernel<BM, BN, ATR, BTR, EPI, CONV>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -695,5 +881,78 @@ MDTF_EXPORT int mdtf_gemm_pp(const bf16_t* A, long long lda, const bf16_t* const
     case 1: return dispatch<false, false, 1>(tile, a, splits, st);
     case 2: return dispatch<true, true, 1>(tile, a, splits, st);
   }
+  return MDTF_EINVAL;
+}
+
+// Convolution on the ping-pong core (CONV 1 = forward, 2 = stride-1 data gradient), NHWC bf16, fp32 accumulate.
+//   fwd  : y[N,OH,OW,Cout] = conv(x[N,H,W,Cin], Wt[Cout][(kh,kw,ci)])      (+ BN partials stat_sum/sq[slots][Cout])
+//   dgrad: dx[N,H,W,Cin]   = dgrad(dy[N,OH,OW,Cout], W[kh][kw][Cin][Cout]) (+ accumulate source, BN-bwd partials)
+// The gathered channels (fwd Cin, dgrad Cout) must be 64 * 2^p; <= 32 taps; dgrad Cin % (tile cols) == 0.
+// tile: gemm tile code (0 = 256x256, 1 = 256x128, 2 = 128x256, 3 = 128x128, 4 = 256x192, 5 = 128x192).
+MDTF_EXPORT int mdtf_conv_pp(int pass, const void* src, const void* wgt, void* out, int N, int H, int W, int Cin,
+                             int OH, int OW, int Cout, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW,
+                             int tile, float* stat_sum, float* stat_sq, int stat_slots, int accumulate,
+                             const void* acc_src, const void* acc_mask, const void* bx, const void* bmask, float* bsum,
+                             float* bsq, int bslots, void* stream) {
+  if (pass != 1 && pass != 2) return MDTF_EINVAL;
+  const int GC = pass == 1 ? Cin : Cout, NC = pass == 1 ? Cout : Cin;
+  if (GC % 64 || NC % 8 || KH * KW > 32 || KH < 1 || KW < 1) return MDTF_EUNSUPPORTED;
+  int lg = 0;
+  while ((64 << lg) < GC) ++lg;
+  if ((64 << lg) != GC) return MDTF_EUNSUPPORTED;
+  if (pass == 2 && (SH != 1 || SW != 1)) return MDTF_EUNSUPPORTED;
+  static const int tile_cols[6] = {256, 128, 256, 128, 192, 192};
+  if (tile < 0 || tile > 5) return MDTF_EINVAL;
+  if (pass == 2 && NC % tile_cols[tile]) return MDTF_EUNSUPPORTED;   // filter rows past Cin would alias a tap
+  const long long gbytes = (long long)N * (pass == 1 ? H * W : OH * OW) * GC * 2;
+  const long long M = (long long)N * (pass == 1 ? OH * OW : H * W);
+  if (gbytes >= (1ll << 31) || M * NC >= (1ll << 31) || (long long)KH * KW * Cin * Cout * 2 >= (1ll << 31))
+    return MDTF_EUNSUPPORTED;
+  if ((acc_src || acc_mask) && !accumulate) return MDTF_EINVAL;
+  GemmArgs a{};
+  a.A = (const bf16_t*)src;
+  a.B = (const bf16_t*)wgt;
+  a.lda = GC;
+  a.ldb = pass == 1 ? (long long)KH * KW * Cin : Cout;
+  a.M = (int)M;
+  a.N = NC;
+  a.K = KH * KW * GC;
+  a.bytes_a = (int)gbytes;
+  a.bytes_b = (int)((long long)KH * KW * Cin * Cout * 2);
+  a.nseg = 1;
+  a.seg_cols = pass == 1 ? NC : a.K;
+  for (int i = 0; i < 4; ++i) a.bseg[i] = a.B;
+  a.C = (bf16_t*)out;
+  a.ldc = NC;
+  a.accumulate = pass == 2 ? accumulate : 0;
+  ConvGeo& g = a.cv;
+  g.GH = pass == 1 ? H : OH;
+  g.GW = pass == 1 ? W : OW;
+  g.GC = GC;
+  g.RH = pass == 1 ? OH : H;
+  g.RW = pass == 1 ? OW : W;
+  magic_u32(g.RW, g.mag_rw, g.sh_rw);
+  magic_u32(g.RH, g.mag_rh, g.sh_rh);
+  magic_u32(KW, g.mag_kw, g.sh_kw);
+  g.SH = SH; g.SW = SW; g.PH = PH; g.PW = PW; g.DH = DH; g.DW = DW; g.KH = KH; g.KW = KW;
+  g.cpt_lg = lg;
+  g.wtap_bytes = (long long)Cin * Cout * 2;
+  g.stat_sum = stat_sum;
+  g.stat_sq = stat_sq;
+  g.stat_slots = stat_slots > 0 ? stat_slots : 1;
+  g.acc_src = (const bf16_t*)acc_src;
+  g.acc_mask = (const uint8_t*)acc_mask;
+  g.bx = (const bf16_t*)bx;
+  g.bmask = (const uint8_t*)bmask;
+  g.bsum = bsum;
+  g.bsq = bsq;
+  g.bslots = bslots > 0 ? bslots : 1;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+#define CPP(T_, BM_, BN_) \
+  case T_: return pass == 1 ? launch_pp<BM_, BN_, false, false, 0, 1>(a, 1, st) : launch_pp<BM_, BN_, false, false, 0, 2>(a, 1, st);
+  switch (tile) {
+    CPP(0, 256, 256) CPP(1, 256, 128) CPP(2, 128, 256) CPP(3, 128, 128) CPP(4, 256, 192) CPP(5, 128, 192)
+  }
+#undef CPP
   return MDTF_EINVAL;
 }

@@ -125,6 +125,14 @@ def choose(pass_, x_shape, w_shape, stride, pads, dil):
     if forced == "auto" and ent is not None:
         if ent["backend"] in ("miopen", "winograd"):
             return (ent["backend"],)
+        if ent.get("ver") == 5:                  # ping-pong core (csrc/gemm_pp.hip mdtf_conv_pp)
+            if pp_ok(pass_, c, co, stride, kh, kw, ent["tile"]):
+                return ("pp", ent["tile"])
+            ent = ent.get("prev")
+            if ent is None:
+                return ("mdtf",) + _default_tile(co if pass_ == "fwd" else ci) + (0, 2, 2)
+            if ent["backend"] in ("miopen", "winograd"):
+                return (ent["backend"],)
         if ent.get("ver") == 4:
             if N.deterministic():                # cross-block statistics atomics: use the v2 kernels
                 return ("mdtf", 128, 128 if (co if pass_ == "fwd" else c) % 128 == 0 else 64, 0, 2, 2)
@@ -478,6 +486,48 @@ def ws_dgrad(dy, w, x_shape, pads, dil, tile, out=None, accumulate=False, bn_sta
     return dx
 
 
+N.register("mdtf_conv_pp", [N.I, N.P, N.P, N.P] + [N.I] * 15 + [N.I, N.P, N.P, N.I, N.I] + [N.P] * 6 + [N.I, N.P])
+PP_TILES = {0: (256, 256), 1: (256, 128), 2: (128, 256), 3: (128, 128), 4: (256, 192), 5: (128, 192)}
+
+
+def pp_ok(pass_, c, co, stride, kh, kw, tile=None):
+    """Shapes the ping-pong conv kernel (csrc/gemm_pp.hip mdtf_conv_pp) takes: the gathered channels are 64 * 2^p,
+    <= 32 taps; dgrad stride 1 with Cin a multiple of the tile's columns."""
+    g = c if pass_ == "fwd" else co
+    if pass_ not in ("fwd", "dgrad") or g < 64 or g & (g - 1) or kh * kw > 32:
+        return False
+    if pass_ == "fwd":
+        return co % 8 == 0
+    return tuple(stride) == (1, 1) and (tile is None or c % PP_TILES[tile][1] == 0)
+
+
+def pp_fwd(x, w, out_hw, stride, pads, dil, tile, stats=None, out=None):
+    """Y = conv(X, W) on the ping-pong core (+ BN partials ``stats = (psum, psq)`` [slots][Cout])."""
+    n = x.shape[0]
+    co = w.shape[3]
+    y = out if out is not None else torch.empty((n, out_hw[0], out_hw[1], co), dtype=x.dtype, device=x.device)
+    s_sum, s_sq = stats if stats is not None else (None, None)
+    slots = s_sum.shape[0] if s_sum is not None else 0
+    N.check(N.fn("mdtf_conv_pp")(1, N.ptr(x), N.ptr(transpose_filter(w)), N.ptr(y), *_geo(x, w, out_hw, stride, pads, dil),
+                                 int(tile), N.ptr(s_sum), N.ptr(s_sq), slots, 0, None, None, None, None, None, None, 0,
+                                 N.stream_ptr()), "conv_pp_fwd")
+    return y
+
+
+def pp_dgrad(dy, w, x_shape, pads, dil, tile, out=None, accumulate=False, bn_stats=None, acc_src=None):
+    """DX of a stride-1 conv on the ping-pong core; ``bn_stats`` / ``acc_src`` as in :func:`mdtf_dgrad`."""
+    dx = out if out is not None else torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
+    n, h, wd, c = x_shape
+    kh, kw, ci, co = w.shape
+    geo = [n, h, wd, c, dy.shape[1], dy.shape[2], co, kh, kw, 1, 1, pads[0], pads[2], dil[0], dil[1]]
+    bx, bmask, bsum, bsq, bslots = bn_stats if bn_stats is not None else (None, None, None, None, 0)
+    ag, am = acc_src if acc_src is not None else (None, None)
+    N.check(N.fn("mdtf_conv_pp")(2, N.ptr(dy), N.ptr(w), N.ptr(dx), *geo, int(tile), None, None, 0,
+                                 int(bool(accumulate) or acc_src is not None), N.ptr(ag), N.ptr(am), N.ptr(bx),
+                                 N.ptr(bmask), N.ptr(bsum), N.ptr(bsq), int(bslots), N.stream_ptr()), "conv_pp_dgrad")
+    return dx
+
+
 def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=1, stages=2):
     """fp32 HWIO weight gradient; accumulates into ``out`` when given (must be zeroed or a grad slot)."""
     dw = torch.zeros(w_shape, dtype=torch.float32, device=x.device) if out is None else out
@@ -606,6 +656,13 @@ class _Conv(torch.autograd.Function):
                 buf = sbuf(co, x.device, slots)
                 stats = (buf[0], buf[1])
             y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2], stats, ch[4], ch[5])
+        elif ch[0] == "pp":
+            if want_stats:
+                co = w.shape[3]
+                slots = stat_slots(-(-x.shape[0] * out_hw[0] * out_hw[1] // PP_TILES[ch[1]][0]))
+                buf = sbuf(co, x.device, slots)
+                stats = (buf[0], buf[1])
+            y = pp_fwd(x, w, out_hw, stride, pads, dil, ch[1], stats)
         elif ch[0] == "stem":
             if want_stats:
                 buf = sbuf(w.shape[3], x.device, STAT_SLOTS)
@@ -680,6 +737,21 @@ class _Conv(torch.autograd.Function):
                     xs.stats = sbuf
             else:
                 dx = ws_dgrad(dy, w, x.shape, pads, dil, tile)
+        elif need_dx and cd[0] == "pp":
+            if xs is not None:
+                buf, acc, pend = xs.target_ex()
+                bst = None
+                if xs.stat_req is not None and xs.completing() and BWD_STATS and not N.deterministic():
+                    bx, bmask = xs.stat_req
+                    sbuf = bwd_stats_acquire(x.device, x.shape[3],
+                                             stat_slots(-(-x.numel() // x.shape[3] // PP_TILES[cd[1]][0])))
+                    bst = (bx, bmask, sbuf[0], sbuf[1], sbuf.shape[1])
+                xs.written(pp_dgrad(dy, w, x.shape, pads, dil, cd[1], out=buf, accumulate=acc, bn_stats=bst,
+                                    acc_src=pend))
+                if bst is not None:
+                    xs.stats = sbuf
+            else:
+                dx = pp_dgrad(dy, w, x.shape, pads, dil, cd[1])
         elif need_dx and not lib_dx:
             if xs is not None and cd[4] in (2, 3):
                 buf, acc, pend = xs.target_ex()

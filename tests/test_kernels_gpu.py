@@ -1057,6 +1057,116 @@ def test_conv_v2_strided_dgrad(k, s, h, w, pads, stages):
     assert _rel(out, ref + base.float()) < 1e-2
 
 
+def _bits(b):
+    """bool [..., C] -> the kernels' 1-bit-per-element mask bytes (element 8i + k = bit k of byte i)."""
+    w = (1 << torch.arange(8, device=b.device)).to(torch.int32)
+    return (b.reshape(-1, 8).to(torch.int32) * w).sum(-1).to(torch.uint8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", [64, 256])
+@pytest.mark.parametrize("mode", ["plain", "acc_src_stats"])
+def test_strided_dgrad_zero_tap_classes_streamed(c, mode):
+    """1x1 stride-2 dgrad: 3 of the 4 stride-parity classes have no filter taps.  Their pixels are written by
+    one streaming launch (csrc/conv_igemm.hip dgrad_zero_classes), with the masked accumulate source and the
+    BN-backward statistics (sum g*mask, sum g*mask*x) of every pixel, vs an fp32 reference."""
+    from mdtf.ops import conv as C
+    torch.manual_seed(c)
+    n, h, w, co = 4, 14, 14, 128
+    wt = (torch.randn(1, 1, c, co, device=DEV) / c ** 0.5).bfloat16()
+    dy = torch.randn(n, 7, 7, co, device=DEV).bfloat16()
+    ref = torch.zeros(n, h, w, c, device=DEV)
+    ref[:, ::2, ::2] = (dy.float().reshape(-1, co) @ wt.float().reshape(c, co).t()).reshape(n, 7, 7, c)
+    if mode == "plain":
+        dx = C.mdtf_dgrad(dy, wt, (n, h, w, c), (2, 2), (0, 0, 0, 0), (1, 1), 64, 128, 2, 2)
+        assert _rel(dx, ref) < 1e-2
+        assert dx.float()[:, 1::2].abs().max().item() == 0 and dx.float()[:, :, 1::2].abs().max().item() == 0
+        return
+    g = torch.randn(n, h, w, c, device=DEV).bfloat16()
+    gm = torch.rand(n, h, w, c, device=DEV) > 0.3
+    x = torch.randn(n, h, w, c, device=DEV).bfloat16()
+    xm = torch.rand(n, h, w, c, device=DEV) > 0.5
+    slots = 4
+    ps = torch.zeros(2, slots, c, device=DEV)
+    out = torch.empty(n, h, w, c, device=DEV, dtype=torch.bfloat16)
+    C.mdtf_dgrad(dy, wt, (n, h, w, c), (2, 2), (0, 0, 0, 0), (1, 1), 64, 128, 2, 2, out=out,
+                 bn_stats=(x, _bits(xm), ps[0], ps[1], slots), acc_src=(g, _bits(gm)))
+    full = ref + g.float() * gm
+    assert _rel(out, full) < 1e-2
+    o = out.float() * xm
+    assert _rel(ps[0].sum(0), o.sum((0, 1, 2))) < 1e-3
+    assert _rel(ps[1].sum(0), (o * x.float()).sum((0, 1, 2))) < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("k,s,pad,c,co", [(3, 1, 1, 64, 192), (3, 2, 1, 128, 64), (1, 2, 0, 256, 512),
+                                          (1, 1, 0, 64, 256), (7, 1, 3, 64, 64)])
+def test_conv_pp_forward_with_bn_stats(tile, k, s, pad, c, co):
+    """Forward conv on the ping-pong core (csrc/gemm_pp.hip mdtf_conv_pp): padding taps, strides, tile tails;
+    output and the epilogue's per-channel sum y / sum y^2 vs an fp32 reference.  Every tile must accept."""
+    from mdtf.ops import conv as C
+    torch.manual_seed(k * 7 + s + tile)
+    n, h, w = 3, 17, 15
+    assert C.pp_ok("fwd", c, co, (s, s), k, k, tile)
+    x = torch.randn(n, h, w, c, device=DEV).bfloat16()
+    wt = (torch.randn(k, k, c, co, device=DEV) / (k * k * c) ** 0.5).bfloat16()
+    oh, ow = (h + 2 * pad - k) // s + 1, (w + 2 * pad - k) // s + 1
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wt.float().permute(3, 2, 0, 1), stride=s,
+                                     padding=pad).permute(0, 2, 3, 1)
+    slots = 8
+    st = torch.zeros(2, slots, co, device=DEV)
+    y = C.pp_fwd(x, wt, (oh, ow), (s, s), (pad, pad, pad, pad), (1, 1), tile, (st[0], st[1]))
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 1e-2
+    assert _rel(st[0].sum(0), ref.sum((0, 1, 2))) < 1e-3
+    assert _rel(st[1].sum(0), (ref * ref).sum((0, 1, 2))) < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [1, 3, 5])
+@pytest.mark.parametrize("k,pad,c,co", [(3, 1, 128, 64), (1, 0, 256, 128), (3, 1, 384, 256)])
+@pytest.mark.parametrize("mode", ["plain", "accumulate", "acc_src_stats"])
+def test_conv_pp_dgrad(tile, k, pad, c, co, mode):
+    """Stride-1 data gradient on the ping-pong core: plain, accumulating into out, and with a masked accumulate
+    source + the BN-backward statistics epilogue, vs fp32.  Every listed tile must accept these shapes."""
+    from mdtf.ops import conv as C
+    if c % C.PP_TILES[tile][1]:
+        pytest.skip("Cin not a multiple of the tile's columns (host refuses: filter rows would alias a tap)")
+    torch.manual_seed(k + c + tile)
+    n, h, w = 2, 13, 11
+    assert C.pp_ok("dgrad", c, co, (1, 1), k, k, tile)
+    wt = (torch.randn(k, k, c, co, device=DEV) / (k * k * co) ** 0.5).bfloat16()
+    dy = torch.randn(n, h, w, co, device=DEV).bfloat16()
+    xr = torch.zeros(n, c, h, w, device=DEV, requires_grad=True)
+    yr = torch.nn.functional.conv2d(xr, wt.float().permute(3, 2, 0, 1), padding=pad)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    ref = xr.grad.permute(0, 2, 3, 1)
+    if mode == "plain":
+        dx = C.pp_dgrad(dy, wt, (n, h, w, c), (pad, pad, pad, pad), (1, 1), tile)
+        assert _rel(dx, ref) < 1e-2
+        return
+    if mode == "accumulate":
+        base = torch.randn(n, h, w, c, device=DEV).bfloat16()
+        out = base.clone()
+        C.pp_dgrad(dy, wt, (n, h, w, c), (pad, pad, pad, pad), (1, 1), tile, out=out, accumulate=True)
+        assert _rel(out, ref + base.float()) < 1e-2
+        return
+    g = torch.randn(n, h, w, c, device=DEV).bfloat16()
+    gm = torch.rand(n, h, w, c, device=DEV) > 0.3
+    x = torch.randn(n, h, w, c, device=DEV).bfloat16()
+    xm = torch.rand(n, h, w, c, device=DEV) > 0.5
+    ps = torch.zeros(2, 4, c, device=DEV)
+    out = torch.empty(n, h, w, c, device=DEV, dtype=torch.bfloat16)
+    C.pp_dgrad(dy, wt, (n, h, w, c), (pad, pad, pad, pad), (1, 1), tile, out=out,
+               bn_stats=(x, _bits(xm), ps[0], ps[1], 4), acc_src=(g, _bits(gm)))
+    full = ref + g.float() * gm
+    assert _rel(out, full) < 1e-2
+    o = out.float() * xm
+    assert _rel(ps[0].sum(0), o.sum((0, 1, 2))) < 1e-3
+    assert _rel(ps[1].sum(0), (o * x.float()).sum((0, 1, 2))) < 1e-3
+
+
 class _TinyRes(object):
     """Fan-out activations as in ResNet: a BN output feeding a conv AND a residual (identity block),
     then a block input feeding two convs (projection shortcut) -- exercises the activation-gradient sinks."""
