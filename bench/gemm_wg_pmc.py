@@ -1,5 +1,5 @@
 """A few launches of weight-gradient kernel configs on BERT-base FFN-in (768 x 3072 over 8192 tokens) for a
-rocprofv3 --pmc pass (scripts/gpu_wg_pmc.sh)."""
+rocprofv3 --pmc pass (scripts/gpu.sh py)."""
 import os
 import sys
 

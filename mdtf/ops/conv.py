@@ -27,7 +27,7 @@ N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P, N.P, 
 N.register("mdtf_conv_wgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.I, N.P])
 
 # split-K weight gradients: per-split partial slabs + one reduction pass (plain stores) instead of fp32
-# atomics into DW.  Measured on MI355X (scripts/gpu_envab.sh): +0.4 % BERT-base (dense GEMM weight
+# atomics into DW.  Measured on MI355X (scripts/gpu.sh envab): +0.4 % BERT-base (dense GEMM weight
 # gradients), -0.3 % ResNet-50 (conv tiles were autotuned with atomics) -> default: dense layers only.
 # MDTF_WGRAD_SLAB = dense (default) | 1 (conv too) | 0 (atomics everywhere)
 _SLAB_MODE = os.environ.get("MDTF_WGRAD_SLAB", "dense")
@@ -596,7 +596,7 @@ def stat_slots(mtiles):
 # gradient buffer), so it runs on its own HIP stream beside the dgrad -> BN-backward chain and fills
 # the CUs that chain's memory-bound and small kernels leave idle.  Captured hipGraphs keep the two
 # streams as concurrent branches.  The gradient buffer is read only after join_side_streams()
-# (bucket all-reduce launch, end of backward).  Measured on ResNet-50 (scripts/gpu_envab.sh): -0.3 %
+# (bucket all-reduce launch, end of backward).  Measured on ResNet-50 (scripts/gpu.sh envab): -0.3 %
 # (the chain's kernels already keep HBM busy), so it is opt-in: MDTF_WGRAD_STREAM=1.
 WGRAD_STREAM = os.environ.get("MDTF_WGRAD_STREAM", "0") == "1"
 _SIDE = {}        # device -> side stream

@@ -3,7 +3,7 @@
 The dense layers' plain GEMMs (BERT's QKV / output / FFN projections, the tied MLM decoder) go to
 the vendor libraries through ``torch.mm`` / ``torch.addmm``.  The library heuristics do not pick
 the fastest solution for every shape. ``tunableop_gfx950.csv`` holds the choices timed on an
-MI355X with this image's PyTorch / HIP / hipBLASLt / rocBLAS (``scripts/gpu_tunableop.sh``).
+MI355X with this image's PyTorch / HIP / hipBLASLt / rocBLAS (the TunableOp tuning run; its launcher is in the git history before round 4).
 They are loaded read-only before the first GEMM, so a captured step graph replays the tuned
 kernels (BERT-base: +3.5% seq/s in an alternating A/B).
 

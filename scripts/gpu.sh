@@ -7,6 +7,10 @@
 #   pmc     : SQ / FETCH / WRITE+L2 counter passes over both steps (eager), each its own run
 #   envab   : alternating A/B of bench.py under two env settings: gpu.sh envab TAG "A=1" "A=0" [steps]
 #   py      : run a python script under a time limit: gpu.sh py TAG path/to/script.py [args]
+#   bertab  : alternating A/B of bench/bert_bench.py under two env settings: gpu.sh bertab TAG "A=1" "A=0" [steps]
+#   rehearse2: 2-rank gloo rehearsal of bench.py on the one GPU (allreduce and sharded/bf16 modes; not a scaling run)
+# (Round 4 replaced the per-experiment scripts/gpu_*.sh launchers that older profiles/ notes name with these modes;
+#  their exact commands are in the git history.)
 # Every GPU step runs under its own time limit and the script stops at the first failure.
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-/root/repo}"
@@ -75,6 +79,25 @@ case "$WHAT" in
         echo "$arm($E) $(tail -1 "$OUT/ab_${TAG}_${arm}_$i.log" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
       done
     done ;;
+  bertab)
+    A=$1; B=$2; STEPS=${3:-30}
+    cd "$ROOT"
+    for i in 1 2 3; do
+      for arm in A B; do
+        if [ $arm = A ]; then E=$A; else E=$B; fi
+        env $E timeout -k 10 300 python bench/bert_bench.py --steps $STEPS --warmup 5 > "$OUT/bab_${TAG}_${arm}_$i.log" 2>&1 \
+          || fail "bert ab $arm $i" "$OUT/bab_${TAG}_${arm}_$i.log"
+        echo "$arm($E) $(tail -1 "$OUT/bab_${TAG}_${arm}_$i.log" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+      done
+    done ;;
+  rehearse2)
+    cd "$ROOT"
+    MDTF_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 --bert 0 \
+        > "$OUT/rehearse2_$TAG.json" 2> "$OUT/rehearse2_$TAG.err" || fail "rehearsal" "$OUT/rehearse2_$TAG.err"
+    tail -1 "$OUT/rehearse2_$TAG.json" | cut -c1-400
+    MDTF_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 --bert 0 --mode sharded \
+        --comm_dtype bf16 > "$OUT/rehearse2s_$TAG.json" 2> "$OUT/rehearse2s_$TAG.err" || fail "sharded rehearsal" "$OUT/rehearse2s_$TAG.err"
+    tail -1 "$OUT/rehearse2s_$TAG.json" | cut -c1-400 ;;
   py)
     cd "$ROOT"
     S=$1; shift

@@ -1714,6 +1714,8 @@ def test_gemm_core_three_layouts_vs_fp32(tile, M, N, K):
     x, w, b = rnd(M, K), rnd(K, N), rnd(N)
     pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     y = mm.fwd(x, w, biases=[b], act=2, pre=pre, tile=tile)
+    # the forward declines exactly the tiles whose column width does not divide N (transposed B), no others
+    assert (y is not None) == mm._valid(0, tile, M, N), (tile, M, N)
     if y is not None:
         ref = x.float() @ w.float() + b.float()
         assert _rel(pre, ref) < 1e-2
@@ -1728,7 +1730,9 @@ def test_gemm_core_three_layouts_vs_fp32(tile, M, N, K):
     for sp in (1, 2):
         gw = torch.randn(M, N, device=DEV)
         ref = gw + xt.float().t() @ dyt.float()
-        if mm.wgrad_into(gw, xt, dyt, tile=tile, splits=sp):
+        ok = mm.wgrad_into(gw, xt, dyt, tile=tile, splits=sp)
+        assert ok == mm._valid(2, tile, M, N), (tile, M, N, sp)     # declines only transposed-edge straddles
+        if ok:
             assert _rel(gw, ref) < 1e-4
 
 
