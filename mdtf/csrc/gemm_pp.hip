@@ -141,10 +141,13 @@ __device__ __forceinline__ int seg_of(int col, int seg_cols, int nseg) {
 
 // LDS-DMA of 16 B per lane: LDS destination = m0 (wave-uniform) + 16 * lane, source = rsrc + voff + soff.
 // Issued from inline asm so the compiler neither sees an LDS write (no vmcnt(0) before our ds_reads) nor
-// counts it: the kernel's own wait_vmcnt<N> + s_barrier order every read after it.
+// counts it: the kernel's own wait_vmcnt<N> + s_barrier order every read after it.  The s_nop 4 covers the VALU ->
+// SGPR -> VMEM hazard the compiler does not pad before inline asm: an soffset / descriptor SGPR restored by
+// v_readlane (SGPR spill) right before the DMA was read stale (the 256x192 conv tile loaded B rows 64..79 from
+// rows 0..15), and M0 written by the SALU just before.
 __device__ __forceinline__ void dma16(i32x4_t rsrc, unsigned lds_addr, unsigned voff, int soff) {
   const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
-  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc), "s"(soff), "{m0}"(m0)
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc), "s"(soff), "{m0}"(m0)
                : "memory");
 }
 
@@ -404,7 +407,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
     if (first && T > 1) {
       if constexpr (QUAD) {
         if (G == 0) wait_vmcnt<CB0>();
-        else wait_vmcnt<CB0 + CB1>();
+        else wait_vmcnt<2 * CB1>();    // its own B0(1) + B1(1) (CB0 != CB1 when a B unit is 96 wide)
       } else {
         if (G == 0) wait_vmcnt<CT0>();
         else wait_vmcnt<CT1>();
@@ -920,7 +923,7 @@ MDTF_EXPORT int mdtf_conv_pp(int pass, const void* src, const void* wgt, void* o
   a.bytes_a = (int)gbytes;
   a.bytes_b = (int)((long long)KH * KW * Cin * Cout * 2);
   a.nseg = 1;
-  a.seg_cols = pass == 1 ? NC : a.K;
+  a.seg_cols = a.K;                 // non-transposed B: segments run along the reduction (one)
   for (int i = 0; i < 4; ++i) a.bseg[i] = a.B;
   a.C = (bf16_t*)out;
   a.ldc = NC;

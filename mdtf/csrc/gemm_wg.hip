@@ -50,7 +50,7 @@ struct WgArgs {
 
 __device__ __forceinline__ void dma16(i32x4_t rsrc, unsigned lds_addr, unsigned voff, int soff) {
   const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
-  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc), "s"(soff), "{m0}"(m0)
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc), "s"(soff), "{m0}"(m0)
                : "memory");
 }
 

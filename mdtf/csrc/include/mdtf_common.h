@@ -100,7 +100,7 @@ __device__ __forceinline__ i32x4_t buffer_rsrc(const void* base, int nbytes) {
 __device__ __forceinline__ void dma16_asm(i32x4_t rsrc, const char* lds, unsigned voff) {
   const unsigned m0 = __builtin_amdgcn_readfirstlane(
       static_cast<unsigned>(reinterpret_cast<unsigned long long>((__attribute__((address_space(3))) const char*)lds)));
-  asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "{m0}"(m0) : "memory");
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "{m0}"(m0) : "memory");
 }
 
 // s_waitcnt vmcnt(N) leaving lgkm/exp counters alone (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14)

@@ -175,8 +175,24 @@ class GradReducer(object):
                 sh["master"][b.shard_offset:b.shard_offset + b.shard_len].copy_(g.master[s:s + b.shard_len])
 
     # -- step protocol ---------------------------------------------------
+    # MDTF_ZERO_SIDE=1: zero the flat fp32 gradient buffer on a side stream beside the forward pass (nothing reads or
+    # writes gradients before backward; join_zero() makes the compute stream wait for it before the first backward
+    # kernel).  Off by default: measured slower on both steps (ResNet-50 11241 vs 11389 img/s, BERT-base 6330 vs 6441
+    # seq/s, alternating A/B, profiles/ab_r4.md) -- the fill's blocks take CU slots and HBM from the forward kernels.
+    ZERO_SIDE = os.environ.get("MDTF_ZERO_SIDE", "0") == "1"
+
     def begin_step(self):
-        self.space.zero_grad()
+        dev = self.space.device
+        if self.ZERO_SIDE and dev is not None and torch.device(dev).type == "cuda":
+            if getattr(self, "_zero_stream", None) is None:
+                self._zero_stream = torch.cuda.Stream(dev)
+            zs = self._zero_stream
+            zs.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(zs):
+                self.space.zero_grad()
+            self._zero_pending = zs
+        else:
+            self.space.zero_grad()
         for v in self.space.variables:
             v.uses = 0
         for b in self.space.buckets:
@@ -185,6 +201,13 @@ class GradReducer(object):
             b.launched = False
             b.updated = False
             b.gather = None
+
+    def join_zero(self):
+        """The compute stream waits for the side-stream gradient zeroing (before any gradient is written)."""
+        zs = getattr(self, "_zero_pending", None)
+        if zs is not None:
+            torch.cuda.current_stream(self.space.device).wait_stream(zs)
+            self._zero_pending = None
 
     def _on_grad_ready(self, var):
         b = var.bucket
@@ -199,7 +222,8 @@ class GradReducer(object):
         # (not while a hipGraph captures the step: ending that capture with the side-stream updates and the
         # in-backward gathers segfaulted in hipStreamEndCapture on ROCm 7.0 -- a captured sharded step gathers
         # after the update as before)
-        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        capturing = (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+                     and os.environ.get("MDTF_SHARDED_CAPTURE_OVERLAP", "0") != "1")
         self.eager_update = fn if (self.mode == "sharded" and self.overlap and self.collective
                                    and self.R == self.world and not capturing) else None
 
@@ -208,6 +232,8 @@ class GradReducer(object):
         sh = self._shards[id(g)]
         cuda = torch.device(g.device).type == "cuda"
         us = None
+        if cuda and os.environ.get("MDTF_SHARDED_UPD_STREAM", "1") == "0":
+            cuda = False                        # (diagnostic) update + gather issued from the compute stream
         if cuda:
             if self._upd_stream is None:
                 self._upd_stream = torch.cuda.Stream(g.device)
@@ -322,6 +348,7 @@ class GradReducer(object):
     def end_backward(self, step=0):
         """Finish all reductions; returns the gradient scale (1/contributors)."""
         from ..ops import conv as _conv
+        self.join_zero()
         _conv.join_side_streams()          # every weight gradient is in the flat buffer
         if self.backup_device:
             self.contributed = self._backup_mask_device(step)  # device 0/1 (read only when someone asks)

@@ -329,6 +329,7 @@ class TrainOp(Fetchable):
             for prog in self.programs:
                 out = prog.forward(ctx, grad=True)
                 loss = out[self.loss_key]
+                red.join_zero()                # the side-stream gradient zeroing ran beside the forward
                 loss.backward()
         finally:
             _conv._WT.step_end()

@@ -1101,7 +1101,7 @@ def test_strided_dgrad_zero_tap_classes_streamed(c, mode):
 @pytest.mark.gpu
 @pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("k,s,pad,c,co", [(3, 1, 1, 64, 192), (3, 2, 1, 128, 64), (1, 2, 0, 256, 512),
-                                          (1, 1, 0, 64, 256), (7, 1, 3, 64, 64)])
+                                          (1, 1, 0, 64, 256), (5, 1, 2, 64, 64)])
 def test_conv_pp_forward_with_bn_stats(tile, k, s, pad, c, co):
     """Forward conv on the ping-pong core (csrc/gemm_pp.hip mdtf_conv_pp): padding taps, strides, tile tails;
     output and the epilogue's per-channel sum y / sum y^2 vs an fp32 reference.  Every tile must accept."""
