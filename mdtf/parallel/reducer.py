@@ -128,7 +128,8 @@ class GradReducer(object):
         self.num_contributors = self.world
         self._shards = {}
         # sharded + overlap: each bucket's shard is updated and all-gathered as soon as its reduce-scatter
-        # lands, on a side stream, while backward continues (set per step by the TrainOp: set_update_fn)
+        # lands, on a side stream (the capture stream inside a hipGraph capture), while backward continues (set per
+        # step by the TrainOp: set_update_fn)
         self.eager_update = None
         self._upd_stream = None
         # backup workers decided on the device (GPU replicas): see the module docstring
@@ -219,21 +220,33 @@ class GradReducer(object):
         """``fn(target)`` runs the fused optimizer on one update target.  In sharded mode with overlapped
         reductions the reducer then updates and all-gathers every bucket during backward (the gather of the
         refreshed weights no longer waits for the whole backward, and never for the host)."""
-        # (not while a hipGraph captures the step: ending that capture with the side-stream updates and the
-        # in-backward gathers segfaulted in hipStreamEndCapture on ROCm 7.0 -- a captured sharded step gathers
-        # after the update as before)
-        capturing = (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
-                     and os.environ.get("MDTF_SHARDED_CAPTURE_OVERLAP", "0") != "1")
+        # Inside a hipGraph capture the per-bucket update and its all-gather are issued from the capturing (compute)
+        # stream.  Cause of the round-2 segfault: ending a capture in which a side stream, forked from the capture
+        # stream inside the autograd engine's device thread, ran the updates and issued the RCCL all-gathers made
+        # hipStreamEndCapture segfault (reproduced in round 4 with MDTF_SHARDED_UPD_STREAM=1 inside capture,
+        # gpurun_out/sharded_capture_r4c.log: SIGSEGV in torch.cuda.graphs capture_end); the same work issued from
+        # the capture stream captures and replays bitwise equal to eager (tests/test_hip_graph.py).  The collectives
+        # still run on RCCL's own stream beside backward; only the small fused update kernels run in line.
+        # MDTF_SHARDED_CAPTURE_OVERLAP=0: no in-backward update inside a capture (gathers after the update).
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        self._capturing = capturing
+        allowed = not capturing or os.environ.get("MDTF_SHARDED_CAPTURE_OVERLAP", "1") != "0"
         self.eager_update = fn if (self.mode == "sharded" and self.overlap and self.collective
-                                   and self.R == self.world and not capturing) else None
+                                   and self.R == self.world and allowed) else None
 
     def _update_bucket(self, b):
         g = b.group
         sh = self._shards[id(g)]
         cuda = torch.device(g.device).type == "cuda"
         us = None
-        if cuda and os.environ.get("MDTF_SHARDED_UPD_STREAM", "1") == "0":
-            cuda = False                        # (diagnostic) update + gather issued from the compute stream
+        # eager steps: a side stream; inside a capture: the capture stream (see set_update_fn)
+        # (MDTF_SHARDED_UPD_STREAM=1 forces the side stream in capture too: reproduces the EndCapture segfault)
+        capt = getattr(self, "_capturing", False)
+        env = os.environ.get("MDTF_SHARDED_UPD_STREAM", "")
+        cuda = cuda and (env == "1" if capt else env != "0")
+        self.bucket_updates = getattr(self, "bucket_updates", 0) + 1
+        if capt:
+            self.captured_bucket_updates = getattr(self, "captured_bucket_updates", 0) + 1
         if cuda:
             if self._upd_stream is None:
                 self._upd_stream = torch.cuda.Stream(g.device)

@@ -214,6 +214,10 @@ def test_hip_graph_captures_rccl_collectives(mode, monkeypatch):
             _native.set_deterministic(False)
         assert op_e.reducer.collective and op_e.reducer.overlap and len(op_e.space.buckets) > 1
         assert op.graph.replays == 3 and op.graph.fallbacks == 0
+        if mode == "sharded":
+            # every bucket was updated + all-gathered during backward INSIDE the capture (not after the update)
+            assert getattr(op.reducer, "captured_bucket_updates", 0) == len(op.space.buckets), \
+                (getattr(op.reducer, "captured_bucket_updates", 0), len(op.space.buckets))
         from mdtf.train import graph as G
         assert G.LAST_DRAIN[0] == "recorder", G.LAST_DRAIN
         assert l_e == l_g, (l_e, l_g)
