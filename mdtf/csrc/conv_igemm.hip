@@ -676,17 +676,16 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < RB; ++i)
       dma16(wbase, bytes_b, ldsb + (wave + NW * i) * 1024, b_off[i], sb);
-    // advance the K walk by 64
+    // advance the K walk by 64 (scalar selects)
     s_k0 += 64;
     s_c0 += 64;
-    if (s_c0 == GC) {
-      s_c0 = 0;
-      ++s_t;
-      if (++s_kw == TKW) {
-        s_kw = 0;
-        ++s_kh;
-      }
-    }
+    const int wrap = s_c0 == GC ? 1 : 0;
+    s_c0 = wrap ? 0 : s_c0;
+    s_t += wrap;
+    s_kw += wrap;
+    const int wrap2 = s_kw == TKW ? 1 : 0;
+    s_kw = wrap2 ? 0 : s_kw;
+    s_kh += wrap2;
   };
 
   float4v acc[TM][TN];
@@ -810,7 +809,8 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   // statistics) is issued for all of this thread's rows before the first store: one latency, not ITER
   constexpr int ITER = BM * (BN / 8) / NT;
   static_assert(ITER * NT == BM * (BN / 8), "copy-out rows per thread");
-  constexpr int PF = ITER < 4 ? ITER : 4;      // rows in flight (register budget of the 256-row tiles)
+  // rows in flight (register budget of the 256-row tiles; the 448-row tile's 14 rows per thread go in pairs)
+  constexpr int PF = ITER < 4 ? ITER : (ITER % 4 == 0 ? 4 : 2);
   static_assert(ITER % PF == 0, "prefetch groups");
 #pragma unroll
   for (int g0 = 0; g0 < ITER; g0 += PF) {
@@ -1031,6 +1031,12 @@ int dispatch_fd_v2w8(ConvArgs& a, int bm, int bn, int stages, hipStream_t st) {
   if (bm == BM_ && bn == BN_ && stages == S_) return launch_fd_v2<BM_, BN_, MODE, STATS, S_, 8>(a, st);
   FD8(256, 256, 1) FD8(256, 256, 2) FD8(256, 128, 1) FD8(256, 128, 2) FD8(256, 128, 3) FD8(256, 64, 2)
   FD8(256, 64, 3) FD8(256, 64, 4) FD8(128, 256, 2) FD8(128, 256, 3)
+  // 448 = 7 x 64 rows: at batch 256 every row count is 49 * 4^k * 256, so 256-row tiles leave 196 * 4^k * (N / BN)
+  // tiles = 0.77 of a 256-CU wave; 448-row tiles give 112 * 4^k * (N / 128) = 0.875 of one (4 x 2 waves of 112 x 64)
+  // (not the dense act-backward mode: its 14 pre-activation vectors per thread spill)
+  if constexpr (MODE != 4) {
+    FD8(448, 128, 1) FD8(448, 128, 2)
+  }
 #undef FD8
   return MDTF_EUNSUPPORTED;
 }

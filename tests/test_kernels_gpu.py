@@ -1057,6 +1057,36 @@ def test_conv_v2_strided_dgrad(k, s, h, w, pads, stages):
     assert _rel(out, ref + base.float()) < 1e-2
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("stages", [1, 2])
+@pytest.mark.parametrize("k,s,pad,c,co", [(3, 1, 1, 64, 128), (1, 1, 0, 128, 256), (3, 2, 1, 128, 128),
+                                          (1, 2, 0, 64, 128)])
+def test_conv_v2_448_row_tile(stages, k, s, pad, c, co):
+    """The 448 x 128 8-wave tile (0.875-wave tile counts at ResNet shapes): forward with the BN-statistics epilogue
+    and (strided) data gradient vs fp32; row counts that leave a partial 448-row tile."""
+    from mdtf.ops import conv as C
+    # a one-stage ring takes K == 64 only (the strided dgrad launcher adapts per class by itself)
+    stages_fwd = 2 if (stages == 1 and k * k * c > 64) else stages
+    torch.manual_seed(k + c + s)
+    n, h, w = 3, 19, 17
+    x = torch.randn(n, h, w, c, device=DEV).bfloat16()
+    wt = (torch.randn(k, k, c, co, device=DEV) / (k * k * c) ** 0.5).bfloat16()
+    oh, ow = (h + 2 * pad - k) // s + 1, (w + 2 * pad - k) // s + 1
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wt.float().permute(3, 2, 0, 1), stride=s,
+                                     padding=pad).permute(0, 2, 3, 1)
+    st = torch.zeros(2, 8, co, device=DEV)
+    y = C.mdtf_fwd(x, wt, (oh, ow), (s, s), (pad,) * 4, (1, 1), 448, 128, (st[0], st[1]), 3, stages_fwd)
+    assert _rel(y, ref) < 1e-2
+    assert _rel(st[0].sum(0), ref.sum((0, 1, 2))) < 1e-3
+    dy = torch.randn(n, oh, ow, co, device=DEV).bfloat16()
+    xr = torch.zeros(n, c, h, w, device=DEV, requires_grad=True)
+    torch.nn.functional.conv2d(xr, wt.float().permute(3, 2, 0, 1), stride=s, padding=pad).backward(
+        dy.float().permute(0, 3, 1, 2))
+    dstages = 2 if (s == 1 and k * k * co > 64 and stages == 1) else stages
+    dx = C.mdtf_dgrad(dy, wt, (n, h, w, c), (s, s), (pad,) * 4, (1, 1), 448, 128, 3, dstages)
+    assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
 def _bits(b):
     """bool [..., C] -> the kernels' 1-bit-per-element mask bytes (element 8i + k = bit k of byte i)."""
     w = (1 << torch.arange(8, device=b.device)).to(torch.int32)
