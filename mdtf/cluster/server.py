@@ -54,7 +54,7 @@ class Server(object):
         cluster.task_address(job_name, self.task_index)  # validates
         if async_ps is None:
             from ..config.flags import FLAGS
-            async_ps = FLAGS.ps_mode == "async"
+            async_ps = FLAGS.ps_mode in ("async", "sync_ps")
         self.layout = RankLayout(cluster, gpu_num if gpu_num is not None else 0, async_ps=async_ps)
         if local_rank is None:
             local_rank = int(os.environ.get("MDTF_LOCAL_RANK", "0"))

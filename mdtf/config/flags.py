@@ -149,7 +149,9 @@ DEFINE_float('train_learning_rate', 0.001, "Value of initial learning rate.")
 DEFINE_string('learning_rate_json', 'YOUR LEARNING RATE SAVING PATH', "Path of the learning-rate json file.")
 # framework extensions
 DEFINE_string("data_load_option", "tfrecords", "DistributeExperiment input mode: tfrecords | placeholder | datapath | synthetic.")
-DEFINE_string('ps_mode', 'sync', "Parameter-server mode: sync (RCCL reduce-scatter/all-gather) or async.")
+DEFINE_string('ps_mode', 'sync', "Parameter-server mode: sync (RCCL reduce-scatter/all-gather), async, or sync_ps "
+              "(dedicated PS ranks aggregating the first replicas_to_aggregate pushes per version; late pushes of "
+              "backup workers are dropped, so a straggler does not stall the step).")
 DEFINE_string('model_dir', '', "Override @model_dir (checkpoint directory).")
 DEFINE_string('data_dir', '', "Override @data_dir (input data).")
 DEFINE_string('mode', '', "Override @current_mode (Train / Eval).")

@@ -233,8 +233,15 @@ def _hdr(device):
 # ---------------------------------------------------------------------------
 # parameter-server side
 # ---------------------------------------------------------------------------
-def run_parameter_server(op, server):
-    """PS role of the Train operator in async mode: a store-free request loop over all workers."""
+def run_parameter_server(op, server, sync_replicas=None, total_step=None):
+    """PS role of the Train operator in async mode: a store-free request loop over all workers.
+
+    ``sync_replicas = R`` (ps_mode ``sync_ps``): SyncReplicasOptimizer semantics on the same data plane
+    (distribute_train.py:146-160): the PS accumulates the pushes computed on its CURRENT version, applies their
+    mean as ONE update once R have arrived, and only then replies to those R workers.  A push computed on an
+    older version -- a backup worker that lost the race -- is dropped (TF discards stale gradients) and answered at
+    once with the current weights, so a straggler never holds the other workers back: that is the latency hiding
+    of ``replicas_to_aggregate < total_num_replicas``.  From ``total_step`` on every push is answered at once."""
     from ..runtime.train import configure_store_for
     import os
     store = server.store
@@ -267,7 +274,8 @@ def run_parameter_server(op, server):
     gbuf = {}                             # worker -> per-group wire buffers (payloads of several workers in flight)
     vt = torch.zeros(1, dtype=torch.int64, device=cdev)
     st = {"version": 0, "done": 0, "stale_sum": 0, "stale_max": 0, "updates": 0, "apply": 0.0, "idle": 0.0,
-          "applies": 0, "batched_max": 0}
+          "applies": 0, "batched_max": 0, "dropped": 0}
+    accepted = []                         # sync_ps: workers whose push on the current version waits for the mean
     timed_store = _TimedStore(store)
     server.store = timed_store            # any store call made while serving is timed (the data plane makes none)
     t0 = time.time()
@@ -284,10 +292,41 @@ def run_parameter_server(op, server):
         for g in groups:
             dist.send(g.shadow if g.shadow is not None else g.master, dst=w)
 
+    def apply_sync(batch):
+        """sync_ps: accept pushes on the current version until R are in, apply their mean once, reply to them;
+        drop (and answer at once) every push computed on an older version or after the last step."""
+        ta = time.time()
+        for w, wver in batch:
+            if wver == st["version"] and len(accepted) < sync_replicas and (total_step is None
+                                                                           or st["version"] < total_step):
+                accepted.append(w)
+            else:
+                st["dropped"] += 1
+                reply(w)
+        if len(accepted) >= sync_replicas:
+            step = st["version"]
+            with torch.no_grad():
+                for gi, g in enumerate(groups):
+                    g.grad.copy_(gbuf[accepted[0]][gi])
+                    for w in accepted[1:]:
+                        g.grad.add_(gbuf[w][gi])
+                    optimizer.update(UpdateTarget(g, g.master, g.grad, g.shadow, "full"),
+                                     optimizer.learning_rate(step), 1.0 / len(accepted), step)
+            st["version"] += 1
+            st["updates"] += 1
+            st["applies"] += 1
+            st["batched_max"] = max(st["batched_max"], len(accepted))
+            for w in accepted:
+                reply(w)
+            del accepted[:]
+        st["apply"] += time.time() - ta
+
     def apply_batch(batch):
         """Every payload that completed since the last apply, as consecutive updates in ONE fused pass per group
         (chunks of MAX_MULTI); then one reply per worker with the weights after the chunk."""
         from ..ops.optim import MAX_MULTI
+        if sync_replicas:
+            return apply_sync(batch)
         ta = time.time()
         for c0 in range(0, len(batch), MAX_MULTI):
             chunk = batch[c0:c0 + MAX_MULTI]
@@ -334,7 +373,8 @@ def run_parameter_server(op, server):
              "updates_per_sec": updates / max(dt, 1e-9), "apply_s": round(t_apply, 3), "idle_s": round(t_idle, 3),
              "wall_s": round(dt, 3), "store_wait_s": round(timed_store.wait_s, 6), "store_calls": timed_store.calls,
              "applies": st["applies"], "batched_max": st["batched_max"], "wire": str(wire).replace("torch.", ""),
-             "poll": "threaded-gloo" if threaded else "rccl-is_completed"}
+             "poll": "threaded-gloo" if threaded else "rccl-is_completed",
+             "mode": "sync_ps R=%d" % sync_replicas if sync_replicas else "async", "dropped": st["dropped"]}
     store.set("%s/ps%d/stats" % (_PREFIX, ps), json.dumps(stats))
     out_dir = os.environ.get("MDTF_BENCH_OUT")
     if out_dir:
@@ -349,8 +389,9 @@ def run_parameter_server(op, server):
 # worker side
 # ---------------------------------------------------------------------------
 class AsyncWorker(object):
-    def __init__(self, op, server, tower, grads_and_vars, total_step):
+    def __init__(self, op, server, tower, grads_and_vars, total_step, sync=False):
         self.op = op
+        self.sync = sync                  # sync_ps: wait for the PS reply before the next step (no pipelining)
         self.server = server
         self.tower = tower
         self.total_step = total_step
@@ -447,6 +488,9 @@ class AsyncWorker(object):
         last = None
         import os
         bench_warmup = int(os.environ.get("MDTF_BENCH_WARMUP", "0"))
+        # fault injection for tests: MDTF_STRAGGLER=worker:<task>:<seconds> makes that worker sleep every step
+        slow = os.environ.get("MDTF_STRAGGLER", "").split(":")
+        delay = float(slow[2]) if len(slow) == 3 and slow[0] == "worker" and int(slow[1]) == self.op.task_index else 0.0
         t_bench = None
         pending = None                    # (push send requests, reply receive requests) of the previous step
         step = 0
@@ -455,6 +499,8 @@ class AsyncWorker(object):
                 if V.get_store().device.type == "cuda":
                     torch.cuda.synchronize()
                 t_bench = time.time()
+            if self.sync and self.version[0] >= self.total_step:
+                break                         # sync_ps: the last answer already carried the final version
             ctx = S.RunContext({})
             for v in self.vars:
                 v.uses = 0
@@ -462,6 +508,8 @@ class AsyncWorker(object):
             # forward/backward of this step overlaps the previous push and its reply (into staging)
             out = loss_h.forward(ctx, grad=True)
             out["loss"].backward()
+            if delay:
+                time.sleep(delay)
             from ..ops import conv as _conv
             _conv.join_side_streams()
             used = list(self.version)         # the weights this gradient was computed on
@@ -474,6 +522,13 @@ class AsyncWorker(object):
                 pending = None
                 break
             pending = (self._push(used), self._post_reply(True))
+            if self.sync:
+                # synchronous replicas: the next step runs on the weights the PS answers with (the mean of the
+                # first R pushes of this version, or the current weights if this push came too late)
+                for r in pending[0]:
+                    r.wait()
+                self._finish_reply(pending[1], True)
+                pending = None
             self.steps_done += 1
             last = out["loss"]
             if self.steps_done % 10 == 0:
@@ -482,7 +537,7 @@ class AsyncWorker(object):
                 logger.info("async step %d (local %d), loss = %.8f (%.1f examples/sec local)" % (
                     step, self.steps_done, lv, 10 * self.op.batch_size / max(now - window, 1e-9)))
                 window = now
-            if step + 1 >= self.total_step:
+            if step + 1 >= self.total_step and pending is not None:
                 for r in pending[0]:
                     r.wait()
                 self._finish_reply(pending[1], True)
@@ -496,7 +551,7 @@ class AsyncWorker(object):
             timed = self.steps_done - bench_warmup
             with open(os.path.join(out_dir, "worker%d.json" % self.op.task_index), "w") as f:
                 json.dump({"steps": timed, "seconds": time.time() - t_bench, "batch": self.op.batch_size,
-                           "staleness": getattr(self, "staleness", None)}, f)
+                           "staleness": getattr(self, "staleness", None), "steps_done": self.steps_done}, f)
         if is_chief and self.op.model_dir:
             self.pull_masters()
             V.get_or_create_global_step().assign(self.version[0])

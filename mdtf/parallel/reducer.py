@@ -46,7 +46,10 @@ disabled in this mode because the mask is only known after backward.  Unlike
 TF's accumulators, stragglers are NOT skipped in time: every replica still joins
 every collective (its contribution zeroed), so a slow replica delays the step;
 backup workers here reproduce the gradient math (exactly R contributions per
-step), not the latency hiding.
+step), not the latency hiding.  ``ps_mode='sync_ps'`` (``parallel/async_ps.py``)
+reproduces both on dedicated PS ranks: each version is the mean of the first R
+pushes computed on it and a late push is dropped, so a straggler never stalls
+the other workers (``tests/test_distributed.py``, sync_ps straggler test).
 """
 import os
 

@@ -64,7 +64,7 @@ def run_from_annotations(main, module=None):
     cluster = ClusterSpec.from_hosts(ps_hosts, worker_hosts)
     gpu_num = int(_maybe(main, "gpu_num", 0) or 0)
     launcher.maybe_spawn_towers(job_name, gpu_num)     # no return if this process became a launcher
-    if job_name == "ps" and (_maybe(main, "ps_mode", None) or FLAGS.ps_mode) != "async":
+    if job_name == "ps" and (_maybe(main, "ps_mode", None) or FLAGS.ps_mode) not in ("async", "sync_ps"):
         os.environ["HIP_VISIBLE_DEVICES"] = ""          # sync-mode PS hosts no GPU work (distribute.py:61-62)
 
     optimizer = _maybe(main, "optimizer", None)
@@ -80,7 +80,7 @@ def run_from_annotations(main, module=None):
         os.makedirs(model_dir, exist_ok=True)                  # create instead of failing
     loss = annotations.get_instance_from_annotation(main, "loss", module)
     server = Server(cluster, job_name=job_name, task_index=task_index, gpu_num=gpu_num,
-                    async_ps=(_maybe(main, "ps_mode", None) or FLAGS.ps_mode) == "async")
+                    async_ps=(_maybe(main, "ps_mode", None) or FLAGS.ps_mode) in ("async", "sync_ps"))
 
     data_loader = annotations.get_instance_from_annotation(main, "input", module)
     ltype = getattr(data_loader, "type", None)

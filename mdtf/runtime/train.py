@@ -53,8 +53,8 @@ def configure_store_for(server):
 class Train(object):
     def _ps_mode(self):
         mode = getattr(self, "ps_mode", None) or FLAGS.ps_mode
-        if mode == "async":
-            return "async"
+        if mode in ("async", "sync_ps"):
+            return mode
         if mode in ("allreduce", "sharded"):
             return mode
         # 'sync': PS tasks present -> PS-shard semantics; else plain all-reduce DP
@@ -73,9 +73,12 @@ class Train(object):
 
         # ------------------------------------------------------------ PS role
         if self.job_name == "ps":
-            if ps_mode == "async":
+            if ps_mode in ("async", "sync_ps"):
                 from ..parallel.async_ps import run_parameter_server
-                run_parameter_server(self, server)
+                r = None
+                if ps_mode == "sync_ps":
+                    r = replicas_to_aggregate or num_replicas
+                run_parameter_server(self, server, sync_replicas=r, total_step=total_step)
                 return
             server.join()
             return
@@ -99,9 +102,10 @@ class Train(object):
         grads = Tower.average_gradients(tower_grads)
         loss = tower_losses[0]
 
-        if ps_mode == "async":
+        if ps_mode in ("async", "sync_ps"):
             from ..parallel.async_ps import AsyncWorker
-            return AsyncWorker(self, server, tower, grads, total_step).run(post_fn, args, kwargs)
+            return AsyncWorker(self, server, tower, grads, total_step, sync=ps_mode == "sync_ps").run(
+                post_fn, args, kwargs)
 
         if replicas_to_aggregate is None:
             replicas_to_aggregate = num_replicas

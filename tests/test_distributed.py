@@ -142,6 +142,29 @@ def test_async_ps_two_ps_two_workers(tmp_path):
     assert int(r.get_tensor("global_step")) >= 100
 
 
+def test_sync_ps_backup_workers_do_not_wait_for_a_straggler(tmp_path):
+    """ps_mode=sync_ps, 3 workers, replicas_to_aggregate=2 (distribute_train.py:146-160): each PS version is the
+    mean of the first 2 pushes computed on it; worker 2 sleeps 0.3 s per step, so its pushes are mostly late and
+    dropped, and the two fast workers reach the last step without waiting for it (latency hiding)."""
+    md = str(tmp_path / "syncps")
+    out = str(tmp_path / "stats")
+    os.makedirs(out)
+    script = os.path.join(ROOT, "distribute.py")
+    codes = launch_local_cluster([script, "--model_dir=%s" % md, "--ps_mode=sync_ps", "--replicas_to_aggregate=2"],
+                                 num_ps=1, num_workers=3, timeout_s=400,
+                                 extra_env={"MDTF_STRAGGLER": "worker:2:0.3", "MDTF_BENCH_OUT": out})
+    assert codes == [0, 0, 0, 0]
+    ps = json.load(open(os.path.join(out, "ps0.json")))
+    assert ps["mode"] == "sync_ps R=2" and ps["batched_max"] == 2
+    assert ps["updates"] == 100                 # one update per global step, each the mean of exactly 2 pushes
+    assert ps["dropped"] >= 10, ps              # the straggler's late pushes were discarded, not waited for
+    w = [json.load(open(os.path.join(out, "worker%d.json" % i))) for i in range(3)]
+    assert w[2]["steps_done"] < min(w[0]["steps_done"], w[1]["steps_done"]), w
+    from mdtf.train.saver import latest_checkpoint
+    from mdtf.ckpt.tensor_bundle import BundleReader
+    assert int(BundleReader(latest_checkpoint(md)).get_tensor("global_step")) == 100
+
+
 @pytest.mark.slow
 def test_fault_injection_restart_resumes_from_checkpoint(tmp_path):
     """Kill worker 1 at global step 37; the heartbeat watchdog stops the surviving tasks, the supervisor
