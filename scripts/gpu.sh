@@ -98,6 +98,11 @@ case "$WHAT" in
     MDTF_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 --bert 0 --mode sharded \
         --comm_dtype bf16 > "$OUT/rehearse2s_$TAG.json" 2> "$OUT/rehearse2s_$TAG.err" || fail "sharded rehearsal" "$OUT/rehearse2s_$TAG.err"
     tail -1 "$OUT/rehearse2s_$TAG.json" | cut -c1-400 ;;
+  pmcpy)   # gpu.sh pmcpy TAG "COUNTERS" script.py [args]: one counter pass over a python script
+    C=$1; S=$2; shift 2
+    (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $C --kernel-trace -d "$OUT/pmcpy_$TAG" -o run \
+        --output-format csv -- python3 "$ROOT/$S" "$@") > "$OUT/pmcpy_$TAG.log" 2>&1 || fail "pmc $S" "$OUT/pmcpy_$TAG.log"
+    echo "pmcpy $TAG ok" ;;
   py)
     cd "$ROOT"
     S=$1; shift
