@@ -19,7 +19,6 @@
 //   3. bn_dx_kernel: dx (and d(residual) = dz) in one pass.
 // All passes are HBM-bound; workspaces are caller-allocated (graph-capture safe).
 #include "mdtf_common.h"
-#include "bn_fin.h"
 
 using namespace mdtf;
 
@@ -428,19 +427,11 @@ __device__ __forceinline__ void dx8(const uint4& gr, const uint4& xr, uint32_t m
 }
 
 // Same chunked structure as bn_apply_kernel (k1..k3 loaded once when C | 2048).
-// dgdb (optional): dγ, dβ ([2][C]) of an in-kernel finalize (bn_fin.h) that block 0 adds into dgamma / dbeta.
 template <bool RELU, bool WRITE_DRES>
 __global__ void __launch_bounds__(kThreads)
     bn_dx_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const uint8_t* __restrict__ mk,
                  bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long n8, int C, const float* __restrict__ k1,
-                 const float* __restrict__ k2, const float* __restrict__ k3, int accum_dres,
-                 const float* __restrict__ dgdb, float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  if (dgdb && blockIdx.x == 0) {
-    for (int c = threadIdx.x; c < C; c += kThreads) {
-      if (dgamma) dgamma[c] += dgdb[c];
-      if (dbeta) dbeta[c] += dgdb[C + c];
-    }
-  }
+                 const float* __restrict__ k2, const float* __restrict__ k3, int accum_dres) {
   const long long base = (long long)blockIdx.x * (kThreads * kVpt) + threadIdx.x;
   const uint4 z4 = make_uint4(0, 0, 0, 0);
   const bool acc = WRITE_DRES && accum_dres;
@@ -477,8 +468,7 @@ __global__ void __launch_bounds__(kThreads)
 
 inline int ew_grid(long long n8);
 void launch_dx(const void* dy, const void* x, const void* mask, void* dx, void* dres, long long M, int C,
-               const float* k1, const float* k2, const float* k3, int relu, int accum_dres, hipStream_t st,
-               const float* dgdb = nullptr, float* dgamma = nullptr, float* dbeta = nullptr);
+               const float* k1, const float* k2, const float* k3, int relu, int accum_dres, hipStream_t st);
 
 void launch_apply(const void* x, const void* res, void* y, uint8_t* mask, long long n8, int C, const float* scale,
                   const float* shift, int relu, hipStream_t st) {
@@ -636,107 +626,22 @@ MDTF_EXPORT int mdtf_bn_bwd_stats(const void* dy, const void* x, const void* mas
 
 namespace {
 void launch_dx(const void* dy, const void* x, const void* mask, void* dx, void* dres, long long M, int C,
-               const float* k1, const float* k2, const float* k3, int relu, int accum_dres, hipStream_t st,
-               const float* dgdb, float* dgamma, float* dbeta) {
+               const float* k1, const float* k2, const float* k3, int relu, int accum_dres, hipStream_t st) {
   long long n8 = M * C / 8;
   if (relu && dres)
     hipLaunchKernelGGL((bn_dx_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, (const uint8_t*)mask, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3, accum_dres,
-                       dgdb, dgamma, dbeta);
+                       (const bf16_t*)x, (const uint8_t*)mask, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3, accum_dres);
   else if (relu)
     hipLaunchKernelGGL((bn_dx_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, (const uint8_t*)mask, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3, 0, dgdb, dgamma,
-                       dbeta);
+                       (const bf16_t*)x, (const uint8_t*)mask, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3, 0);
   else if (dres)
     hipLaunchKernelGGL((bn_dx_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, nullptr, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3, accum_dres, dgdb,
-                       dgamma, dbeta);
+                       (const bf16_t*)x, nullptr, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3, accum_dres);
   else
     hipLaunchKernelGGL((bn_dx_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, nullptr, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3, 0, dgdb, dgamma, dbeta);
+                       (const bf16_t*)x, nullptr, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3, 0);
 }
-
-thread_local BnFin g_fin_armed{};
 }  // namespace
-
-namespace mdtf {
-BnFin bn_fin_take() {
-  BnFin f = g_fin_armed;
-  g_fin_armed = BnFin{};
-  return f;
-}
-}  // namespace mdtf
-
-// Arm the in-kernel finalize (bn_fin.h) of the next stats-producing conv launch of this host thread.
-// ticket: one zeroed int (device); bwd 0: gamma, beta, moving mean / variance (null: none), decay, eps -> out
-// [4][C] mean, invstd, scale, shift;  bwd 1: gamma, the forward's mean / invstd -> out [5][C] k1, k2, k3, dγ, dβ.
-MDTF_EXPORT int mdtf_bn_fin_arm(int* ticket, int bwd, long long count, const float* gamma, const float* beta,
-                                float* mmean, float* mvar, float decay, float eps, const float* mean,
-                                const float* invstd, float* out) {
-  if (!ticket || !out || count < 1 || (bwd && (!mean || !invstd))) return MDTF_EINVAL;
-  BnFin f{};
-  f.ticket = ticket;
-  f.bwd = bwd;
-  f.count = count;
-  f.gamma = gamma;
-  f.beta = beta;
-  f.mmean = mmean;
-  f.mvar = mvar;
-  f.decay = decay;
-  f.eps = eps;
-  f.mean = mean;
-  f.invstd = invstd;
-  f.out = out;
-  g_fin_armed = f;
-  return 0;
-}
-
-// The finalize launch alone (for producers that did not finalize in-kernel): [P][C] partials (re-zeroed) ->
-// fwd out [4][C] mean, invstd, scale, shift (+ moving averages);  bwd out [5][C] k1, k2, k3, dγ, dβ (out[3:5]
-// accumulated: pass it zeroed).
-MDTF_EXPORT int mdtf_bn_finalize(int bwd, float* psum, float* psq, int P, long long M, int C, const float* gamma,
-                                 const float* beta, float* mmean, float* mvar, float decay, float eps,
-                                 const float* mean, const float* invstd, float* out, hipStream_t st) {
-  if (C % 8 || P < 1 || !out) return MDTF_EINVAL;
-  if (!bwd)
-    hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M,
-                       C, gamma, beta, mmean, mvar, decay, eps, out, out + C, out + 2 * C, out + 3 * C, 1);
-  else
-    hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M,
-                       C, gamma, mean, invstd, out + 3 * C, out + 4 * C, out, out + C, out + 2 * C, 1);
-  MDTF_LAUNCH_CHECK();
-  return 0;
-}
-
-// The apply pass alone, with scale / shift from an in-kernel finalize.
-MDTF_EXPORT int mdtf_bn_apply(const void* x, const void* res, void* y, uint8_t* mask, long long M, int C,
-                              const float* scale, const float* shift, int relu, hipStream_t st) {
-  if (C % 8) return MDTF_EINVAL;
-  launch_apply(x, res, y, mask, M * C / 8, C, scale, shift, relu, st);
-  MDTF_LAUNCH_CHECK();
-  return 0;
-}
-
-MDTF_EXPORT int mdtf_bn_apply_dual(const void* x, const void* r, void* y, uint8_t* mask, long long M, int C,
-                                   const float* scale, const float* shift, const float* scale2, const float* shift2,
-                                   hipStream_t st) {
-  if (C % 8 || !mask) return MDTF_EINVAL;
-  const long long n8 = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_dual_kernel, dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
-                     (const bf16_t*)r, (bf16_t*)y, mask, n8, C, scale, shift, scale2, shift2);
-  MDTF_LAUNCH_CHECK();
-  return 0;
-}
-
-// The input-gradient pass alone, with the coefficients of an in-kernel finalize: fin = [5][C] k1, k2, k3, dγ, dβ
-// (dγ / dβ added into dgamma / dbeta, either may be null).
-MDTF_EXPORT int mdtf_bn_dx(const void* dy, const void* x, const void* mask, void* dx, void* dres, long long M, int C,
-                           const float* fin, float* dgamma, float* dbeta, int relu, int accum_dres, hipStream_t st) {
-  if (C % 8 || !fin) return MDTF_EINVAL;
-  launch_dx(dy, x, mask, dx, dres, M, C, fin, fin + C, fin + 2 * C, relu, accum_dres, st, fin + 3 * C, dgamma, dbeta);
-  MDTF_LAUNCH_CHECK();
-  return 0;
-}
 
 // ------------------------------------------------------------------------------------------------------------
 // Stem: BatchNorm + ReLU + max pool fused (ResNet's conv1 -> bn -> relu -> 3x3/2 max pool).  The normalised

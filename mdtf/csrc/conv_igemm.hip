@@ -23,7 +23,6 @@
 // so the N-tiles of one M-tile share an L2.  Forward can emit per-channel
 // Σy / Σy² partials for the following BatchNorm (bn.hip consumes them).
 #include "mdtf_common.h"
-#include "bn_fin.h"
 
 using namespace mdtf;
 
@@ -90,8 +89,6 @@ struct ConvArgs {
   const bf16_t* bias;    // bf16 [Ncol], added to the fp32 accumulators (null: none)
   bf16_t* pre_out;       // act != 0: the bf16 pre-activation is also stored here (null: not kept)
   int act;               // 0 none, 1 relu, 2 gelu (tanh form)
-  // the BN finalize of the statistics this launch emits, by its last-arriving block (bn_fin.h; ticket null: off)
-  BnFin fin;
 };
 
 // zero the bf16 elements of an 8-element vector whose mask bit (element k: bit k) is clear
@@ -996,7 +993,6 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
       }
     }
   }
-  if (STATS || bstat) bn_fin_arrive<NT>(a.fin, smem_raw);
 }
 
 template <int BM, int BN, int MODE, bool STATS, int STAGES, int NW = 4>
@@ -1011,7 +1007,6 @@ int launch_fd_v2(ConvArgs& a, hipStream_t st) {
   if (lds < (size_t)(NT + 8) * 16 * sizeof(float)) lds = (size_t)(NT + 8) * 16 * sizeof(float);   // BN-stat reduction
   if (STAGES == 1 && a.K > 64) return MDTF_EINVAL;      // single buffer: one K step only
   if (lds > 160 * 1024) return MDTF_EUNSUPPORTED;
-  a.fin.nwg = static_cast<int>(nblk);
   hipLaunchKernelGGL((conv_fd_v2<BM, BN, MODE, STATS, STAGES, NW>), dim3((unsigned)nblk), dim3(NT), lds, st, a);
   MDTF_LAUNCH_CHECK();
   return 0;
@@ -1570,7 +1565,6 @@ __global__ void __launch_bounds__(256) dgrad_zero_classes(ConvArgs a, int C8) {
       atomicAdd(a.bsum + slot + ch, sv);
       atomicAdd(a.bsq + slot + ch, q);
     }
-    bn_fin_arrive<256>(a.fin, reinterpret_cast<char*>(&red[0][0][0]));
   }
 }
 
@@ -1665,7 +1659,6 @@ MDTF_EXPORT int mdtf_conv_fwd_v2(const void* x, const void* wt, void* y, float* 
                                  int stat_slots, int N, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
                                  int SH, int SW, int PH, int PW, int DH, int DW, int bm, int bn, int* mtiles_out,
                                  hipStream_t st) {
-  const BnFin fin = bn_fin_take();     // an armed finalize is consumed (or dropped) by this call, never the next
   if (Cin % 64 || Cout % 8) return MDTF_EINVAL;
   if (KH * KW > 32 || (long long)N * H * W * Cin * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
   ConvArgs a = make_args(N, H, W, Cin, OH, OW, Cout, KH, KW, SH, SW, PH, PW, DH, DW);
@@ -1678,13 +1671,6 @@ MDTF_EXPORT int mdtf_conv_fwd_v2(const void* x, const void* wt, void* y, float* 
   a.M = (long long)N * OH * OW;
   a.Ncol = Cout;
   a.K = KH * KW * Cin;
-  if (stat_sum && fin.ticket) {
-    a.fin = fin;
-    a.fin.p0 = stat_sum;
-    a.fin.p1 = stat_sq;
-    a.fin.slots = a.stat_slots;
-    a.fin.C = Cout;
-  }
   // bm = 10000 (8 waves) + stages * 1000 + tile rows
   const int w8 = bm / 10000, stages = (bm % 10000) / 1000 ? (bm % 10000) / 1000 : 2;
   bm = w8 * 10000 + bm % 1000;
@@ -1699,7 +1685,6 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
                                    int bm, int bn, int accumulate, const void* bx, const void* bmask,
                                    float* bsum, float* bsq, int bslots, const void* acc_src, const void* acc_mask,
                                    hipStream_t st) {
-  BnFin fin = bn_fin_take();           // an armed finalize is consumed (or dropped) by this call, never the next
   if (Cout % 64 || Cin % 8) return MDTF_EINVAL;
   if ((acc_src || acc_mask) && !accumulate) return MDTF_EINVAL;
   if ((long long)N * OH * OW * Cout * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
@@ -1719,21 +1704,11 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
   a.bsq = bsq;
   a.bslots = bslots > 0 ? bslots : 1;
   a.Ncol = Cin;
-  // the BN finalize rides on the last launch that emits statistics (the earlier ones precede it in the stream)
-  if (bsum && fin.ticket) {
-    fin.p0 = bsum;
-    fin.p1 = bsq;
-    fin.slots = a.bslots;
-    fin.C = Cin;
-  } else {
-    fin = BnFin{};
-  }
   const int w8 = bm / 10000, stages = (bm % 10000) / 1000 ? (bm % 10000) / 1000 : 2;
   bm = w8 * 10000 + bm % 1000;
   if (SH == 1 && SW == 1) {
     a.M = (long long)N * H * W;
     a.K = KH * KW * Cout;
-    a.fin = fin;
     return dispatch_fd_v2<1, false>(a, bm, bn, stages, st);
   }
   // strided: one launch per stride-parity class (rh, rw) = ((h + PH) % SH, (w + PW) % SW); the classes without
@@ -1741,11 +1716,8 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
   const int C8 = Cin / 8;
   const bool zero_stream = C8 <= 256 && 256 % C8 == 0 && !zero_class_gemm();
   bool zero_pending = false;
-  ConvArgs cls[64];
-  int ncls = 0;
   for (int rh = 0; rh < SH; ++rh)
     for (int rw = 0; rw < SW; ++rw) {
-      if (ncls == 64) return MDTF_EUNSUPPORTED;
       ConvArgs c = a;
       c.cls_h0 = ((rh - PH) % SH + SH) % SH;
       c.cls_w0 = ((rw - PW) % SW + SW) % SW;
@@ -1766,20 +1738,13 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
         zero_pending = true;
         continue;
       }
-      cls[ncls++] = c;
+      const int cs = c.K > 64 && stages == 1 ? 2 : stages;
+      const int rc = dispatch_fd_v2<2, false>(c, bm, bn, cs, st);
+      if (rc) return rc;
     }
-  if (fin.ticket && !zero_pending && ncls == 0) return MDTF_EINVAL;   // nothing would finalize
-  if (!zero_pending && ncls > 0) cls[ncls - 1].fin = fin;
-  for (int i = 0; i < ncls; ++i) {
-    const int cs = cls[i].K > 64 && stages == 1 ? 2 : stages;
-    const int rc = dispatch_fd_v2<2, false>(cls[i], bm, bn, cs, st);
-    if (rc) return rc;
-  }
   if (zero_pending) {
     const long long chunks = (long long)N * H * W * C8;
     const int blocks = static_cast<int>(ceil_div(chunks, 256) < 4096 ? ceil_div(chunks, 256) : 4096);
-    a.fin = fin;
-    a.fin.nwg = blocks;
     if (bsum)
       hipLaunchKernelGGL(dgrad_zero_classes<true>, dim3(blocks), dim3(256), 0, st, a, C8);
     else

@@ -74,7 +74,6 @@ int conv_ws_impl(const void* src, const void* wgt, void* out, int N, int H, int 
                  int grid_cap, float* ssum, float* ssq, int sslots, const void* bx, const void* bmask, float* bsum,
                  float* bsq, int bslots, int accumulate, const void* acc_src, const void* acc_mask,
                  hipStream_t st) {
-  const BnFin fin = bn_fin_take();     // an armed finalize is consumed (or dropped) by this call, never the next
   WsArgs a{};
   a.cs = cs;
   a.src = (const bf16_t*)src;
@@ -105,13 +104,6 @@ int conv_ws_impl(const void* src, const void* wgt, void* out, int N, int H, int 
   if (nw % cg) return MDTF_EINVAL;
   a.dbg = ws_debug;
   const bool stats = ssum != nullptr, bstat = bsum != nullptr;
-  if ((stats || bstat) && fin.ticket) {
-    a.fin = fin;
-    a.fin.p0 = stats ? ssum : bsum;
-    a.fin.p1 = stats ? ssq : bsq;
-    a.fin.slots = stats ? a.sslots : a.bslots;
-    a.fin.C = Ncol;
-  }
   if (stats && bstat) return MDTF_EINVAL;
   if (stats) return accumulate ? MDTF_EINVAL : dispatch_ws<1>(a, tp, nw, cg, d, grid_cap, st);
   if (bstat) return accumulate ? dispatch_ws<4>(a, tp, nw, cg, d, grid_cap, st)

@@ -30,7 +30,7 @@ class ActGradSink(object):
     producing BatchNorm needs for its backward statistics, ``(x, relu_mask)``.  The contributor that
     completes the sum (the ``consumers``-th) may emit the statistics in its epilogue into ``stats``
     (the v2 conv dgrad does)."""
-    __slots__ = ("buf", "count", "consumers", "stat_req", "stats", "pend", "fin_req", "fin")
+    __slots__ = ("buf", "count", "consumers", "stat_req", "stats", "pend")
 
     def __init__(self):
         self.buf = None
@@ -39,8 +39,6 @@ class ActGradSink(object):
         self.stat_req = None
         self.stats = None
         self.pend = None
-        self.fin_req = None      # (gamma_f32, mean, invstd, count): the producer may also finalize the statistics
-        self.fin = None          # [5][C] k1, k2, k3, dγ, dβ of that in-kernel finalize
 
     def defer_masked(self, g, mask):
         """Contribute ``g * mask`` without materialising it (only as the first contribution)."""
@@ -112,11 +110,6 @@ class ActGradSink(object):
         """The emitted BN statistics ``(psum, psq, slots)`` or None (cleared)."""
         st, self.stats = self.stats, None
         return st
-
-    def take_fin(self):
-        """The in-kernel finalize's [5][C] coefficients of those statistics, or None (cleared)."""
-        f, self.fin = self.fin, None
-        return f
 
 
 ENABLED = os.environ.get("MDTF_ACT_SINKS", "1") != "0"      # switch for A/B tests and benches

@@ -20,11 +20,6 @@ N.register("mdtf_bn_relu_maxpool_fwd", [N.P, N.P, N.P] + [N.I] * 12 + [N.P] * 4 
            + [N.P, N.P])
 N.register("mdtf_maxpool_bn_bwd", [N.P] * 4 + [N.I] * 12 + [N.P] * 7 + [N.P])
 N.register("mdtf_bn_bwd_dual", [N.P] * 6 + [N.L, N.I] + [N.P] * 7 + [N.I] + [N.P] * 6 + [N.P])
-N.register("mdtf_bn_fin_arm", [N.P, N.I, N.L, N.P, N.P, N.P, N.P, N.F, N.F, N.P, N.P, N.P])
-N.register("mdtf_bn_finalize", [N.I, N.P, N.P, N.I, N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.P, N.P, N.P, N.P])
-N.register("mdtf_bn_apply", [N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.I, N.P])
-N.register("mdtf_bn_apply_dual", [N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.P, N.P])
-N.register("mdtf_bn_dx", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.I, N.I, N.P])
 
 
 FUSED_BWD = [0]      # backward passes that took their statistics from the dgrad epilogue (tests)
@@ -52,70 +47,6 @@ DUAL_FUSED = os.environ.get("MDTF_DUAL_BWD_FUSED", "1") != "0"
 DUAL_BWD = [0]       # one-pass dual backward launches (tests)
 
 
-# In-kernel finalize (csrc/include/bn_fin.h): the conv that emits a BN's statistics partials (forward: the
-# producing conv's epilogue; backward: the dgrad that completes the BN output's gradient) also turns them into
-# the BN coefficients in its last-arriving workgroup, so no separate finalize launch runs.  MDTF_BN_FIN=0: the
-# finalize launch (mdtf_bn_finalize) between the producer and the apply / input-gradient pass.
-IN_KERNEL_FIN = os.environ.get("MDTF_BN_FIN", "0") != "0"
-FIN_ARMED = [0, 0]   # forward / backward finalizes armed onto a conv launch (tests)
-_TICKETS = {}
-
-
-def _ticket(device):
-    t = _TICKETS.get(device)
-    if t is None:
-        t = torch.zeros(16, dtype=torch.int32, device=device)   # word 0: 0 between launches (self-resetting)
-        _TICKETS[device] = t
-    return t
-
-
-def fin_enabled():
-    return IN_KERNEL_FIN and not N.deterministic()
-
-
-class FwdFin(object):
-    """A training BN's forward finalize, to be armed onto the conv launch that emits its statistics:
-    ``out`` [4][C] receives mean, invstd, scale, shift; the moving averages are updated in-kernel."""
-
-    def __init__(self, gamma, beta, moving_mean, moving_var, decay, epsilon, count, C, device):
-        self.g, self.b = _f32(gamma), _f32(beta)
-        self.mm, self.mv = moving_mean, moving_var
-        self.decay, self.eps, self.count = float(decay), float(epsilon), int(count)
-        self.out = torch.empty((4, C), dtype=torch.float32, device=device)
-        self.armed = False
-
-    def arm(self):
-        N.check(N.fn("mdtf_bn_fin_arm")(N.ptr(_ticket(self.out.device)), 0, self.count, N.ptr(self.g), N.ptr(self.b),
-                                        N.ptr(self.mm), N.ptr(self.mv), self.decay, self.eps, None, None,
-                                        N.ptr(self.out)), "bn_fin_arm")
-        self.armed = True
-        FIN_ARMED[0] += 1
-
-
-def arm_bwd_fin(req, C, device):
-    """Arm the backward finalize ``req = (gamma_f32, mean, invstd, count)`` onto the next dgrad launch; returns
-    its [5][C] output (k1, k2, k3, dγ, dβ)."""
-    g, mean, invstd, count = req
-    out = torch.empty((5, C), dtype=torch.float32, device=device)
-    N.check(N.fn("mdtf_bn_fin_arm")(N.ptr(_ticket(device)), 1, int(count), N.ptr(g), None, None, None, 0.0, 0.0,
-                                    N.ptr(mean), N.ptr(invstd), N.ptr(out)), "bn_fin_arm")
-    FIN_ARMED[1] += 1
-    return out
-
-
-def _finalize_fwd(stats, gamma_f, beta_f, mm, mv, decay, eps, M, C, device):
-    """[4][C] mean, invstd, scale, shift of conv-epilogue statistics: in-kernel already (a 4-tuple) or one
-    finalize launch now (the partials are re-zeroed either way)."""
-    if len(stats) == 4:
-        return stats[3]
-    psum, psq, P = stats
-    out = torch.empty((4, C), dtype=torch.float32, device=device)
-    N.check(N.fn("mdtf_bn_finalize")(0, N.ptr(psum), N.ptr(psq), int(P), M, C, N.ptr(gamma_f), N.ptr(beta_f),
-                                     N.ptr(mm), N.ptr(mv), float(decay), float(eps), None, None, N.ptr(out),
-                                     N.stream_ptr()), "bn_finalize")
-    return out
-
-
 class _BNTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, mm, mv, decay, eps, relu, stats):
@@ -128,21 +59,23 @@ class _BNTrain(torch.autograd.Function):
         C = x.shape[-1]
         M = x.numel() // C
         y = torch.empty_like(x)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
         # ReLU: 1-bit-per-element mask for the backward (instead of keeping / re-reading y)
         mask = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device) if relu else None
         g, b = _f32(gamma), _f32(beta)
         res = residual.contiguous() if residual is not None else None
         if stats is not None:
-            # Σx / Σx² already produced by the conv epilogue (finalized there too, or by one launch here): apply only
-            fo = _finalize_fwd(stats, g, b, mm, mv, decay, eps, M, C, x.device)
-            mean, invstd = fo[0], fo[1]
-            N.check(N.fn("mdtf_bn_apply")(N.ptr(x), N.ptr(res), N.ptr(y), N.ptr(mask), M, C, N.ptr(fo[2]),
-                                          N.ptr(fo[3]), int(relu), N.stream_ptr()), "bn_apply")
+            # Σx / Σx² already produced by the conv epilogue: finalize + apply only
+            psum, psq, P = stats
+            ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+            N.check(N.fn("mdtf_bn_fwd_stats")(N.ptr(x), N.ptr(res), N.ptr(y), N.ptr(mask), M, C, N.ptr(g), N.ptr(b),
+                                              N.ptr(mm), N.ptr(mv), float(decay), float(eps), int(relu), N.ptr(mean),
+                                              N.ptr(invstd), N.ptr(psum), N.ptr(psq), int(P), N.ptr(ws),
+                                              N.stream_ptr()), "bn_fwd_stats")
             from . import conv as _conv
-            _conv.stats_consumed(x.device)           # the finalize re-zeroed the partials
+            _conv.stats_consumed(x.device)           # the finalize kernel re-zeroed the partials
         else:
-            mean = torch.empty(C, dtype=torch.float32, device=x.device)
-            invstd = torch.empty_like(mean)
             ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(M, C)), dtype=torch.float32, device=x.device)
             N.check(N.fn("mdtf_bn_fwd_train")(N.ptr(x), N.ptr(res), N.ptr(y), N.ptr(mask), M, C, N.ptr(g), N.ptr(b),
                                               N.ptr(mm), N.ptr(mv), float(decay), float(eps), int(relu), N.ptr(mean),
@@ -157,31 +90,26 @@ class _BNTrain(torch.autograd.Function):
         ctx.like = (gamma, beta)
         ctx.out_sink = actsink.attach(y)             # this output's consumers may accumulate here
         if ctx.out_sink is not None:
-            # the consumer that completes dy may emit Σ dy·mask, Σ dy·mask·x for this backward (and finalize them)
+            # the consumer that completes dy may emit Σ dy·mask, Σ dy·mask·x for this backward
             ctx.out_sink.stat_req = (x, mask)
-            ctx.out_sink.fin_req = (g, mean, invstd, M)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mask, g, mean, invstd = ctx.saved_tensors
         pstats = None
-        fin = None
         why = "no_sink"
         if ctx.out_sink is not None:
             pstats = ctx.out_sink.take_stats()
-            fin = ctx.out_sink.take_fin()
             why = "no_epilogue_stats" if pstats is None else "fused"
             if pstats is not None and dy is not None:
-                # part of dy came through plain autograd: the epilogue statistics (and an in-kernel finalize of
-                # them) are incomplete
+                # part of dy came through plain autograd: the epilogue statistics are incomplete
                 from . import conv as _conv
                 _conv.bwd_stats_release(pstats, False)
-                pstats, fin = None, None
+                pstats = None
                 why = "autograd_part"
             dy = ctx.out_sink.take(dy)
             ctx.out_sink.stat_req = None
-            ctx.out_sink.fin_req = None
         if BWD_TRACE is not None:
             BWD_TRACE.append((tuple(x.shape), ctx.has_res, why))
         if dy is None:
@@ -212,14 +140,11 @@ class _BNTrain(torch.autograd.Function):
         dbeta = sb.grad if sb is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
         if pstats is not None:
             from . import conv as _conv
-            if fin is None:                              # the producer did not finalize: one launch here
-                fin = torch.zeros((5, C), dtype=torch.float32, device=x.device)
-                N.check(N.fn("mdtf_bn_finalize")(1, N.ptr(pstats[0]), N.ptr(pstats[1]), int(pstats.shape[1]), M, C,
-                                                 N.ptr(g), None, None, None, 0.0, 0.0, N.ptr(mean), N.ptr(invstd),
-                                                 N.ptr(fin), N.stream_ptr()), "bn_finalize")
-            N.check(N.fn("mdtf_bn_dx")(N.ptr(dy), N.ptr(x), N.ptr(mask if ctx.relu else None), N.ptr(dx), N.ptr(dres),
-                                       M, C, N.ptr(fin), N.ptr(dgamma), N.ptr(dbeta), int(ctx.relu), accum,
-                                       N.stream_ptr()), "bn_dx")
+            ws = torch.empty(3 * C, dtype=torch.float32, device=x.device)
+            N.check(N.fn("mdtf_bn_bwd_stats")(N.ptr(dy), N.ptr(x), N.ptr(mask if ctx.relu else None), N.ptr(dx),
+                                              N.ptr(dres), M, C, N.ptr(g), N.ptr(mean), N.ptr(invstd), N.ptr(dgamma),
+                                              N.ptr(dbeta), int(ctx.relu), N.ptr(pstats[0]), N.ptr(pstats[1]),
+                                              int(pstats.shape[1]), N.ptr(ws), accum, N.stream_ptr()), "bn_bwd_stats")
             _conv.bwd_stats_release(pstats, True)        # the finalize re-zeroed it
             FUSED_BWD[0] += 1
         else:
@@ -268,14 +193,17 @@ class _BNTrainDual(torch.autograd.Function):
         C = x.shape[-1]
         M = x.numel() // C
         y = torch.empty_like(x)
+        mean, invstd = (torch.empty(C, dtype=torch.float32, device=x.device) for _ in range(2))
+        mean2, invstd2 = (torch.empty(C, dtype=torch.float32, device=x.device) for _ in range(2))
         mask = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device)
         g, b, g2, b2 = _f32(gamma), _f32(beta), _f32(gamma2), _f32(beta2)
-        fo = _finalize_fwd(stats, g, b, mm, mv, decay, eps, M, C, x.device)
-        fo2 = _finalize_fwd(stats2, g2, b2, mm2, mv2, decay, eps, M, C, x.device)
-        mean, invstd, mean2, invstd2 = fo[0], fo[1], fo2[0], fo2[1]
-        N.check(N.fn("mdtf_bn_apply_dual")(N.ptr(x), N.ptr(r), N.ptr(y), N.ptr(mask), M, C, N.ptr(fo[2]),
-                                           N.ptr(fo[3]), N.ptr(fo2[2]), N.ptr(fo2[3]), N.stream_ptr()),
-                "bn_apply_dual")
+        ws = torch.empty(4 * C, dtype=torch.float32, device=x.device)
+        (ps, pq, P), (ps2, pq2, P2) = stats, stats2
+        N.check(N.fn("mdtf_bn_fwd_dual")(N.ptr(x), N.ptr(r), N.ptr(y), N.ptr(mask), M, C, N.ptr(g), N.ptr(b),
+                                         N.ptr(mm), N.ptr(mv), N.ptr(ps), N.ptr(pq), int(P), N.ptr(mean),
+                                         N.ptr(invstd), N.ptr(g2), N.ptr(b2), N.ptr(mm2), N.ptr(mv2), N.ptr(ps2),
+                                         N.ptr(pq2), int(P2), N.ptr(mean2), N.ptr(invstd2), float(decay), float(eps),
+                                         N.ptr(ws), N.stream_ptr()), "bn_fwd_dual")
         from . import conv as _conv
         _conv.stats_consumed(x.device)               # both finalizes re-zeroed their partials
         ctx.save_for_backward(x, mask, g, mean, invstd, r, g2, mean2, invstd2)

@@ -618,26 +618,6 @@ def join_side_streams():
     _PENDING.clear()
 
 
-def fin_slots(C, slots):
-    """Partial rows when the producing kernel also finalizes them (csrc/include/bn_fin.h): slots x C <= 4096
-    floats (16 KiB per partial array), so the last workgroup reads them in one or two trips per thread."""
-    cap = 1
-    while cap * 2 * C <= 4096:
-        cap *= 2
-    return max(1, min(slots, cap))
-
-
-def _fin_ok(ch):
-    """The backends whose launch takes an armed in-kernel BN finalize."""
-    from . import bn as _bn
-    return _bn.fin_enabled() and ((ch[0] == "mdtf" and ch[4] in (2, 3)) or ch[0] == "ws")
-
-
-def _bn_mod():
-    from . import bn as _bn
-    return _bn
-
-
 _BSTATS = {}      # (device, C, slots) -> free zeroed [2, slots, C] buffers (BN backward statistics)
 
 
@@ -655,7 +635,7 @@ def bwd_stats_release(buf, zeroed):
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pads, dil, out_hw, want_stats, fin=None):
+    def forward(ctx, x, w, stride, pads, dil, out_hw, want_stats):
         from . import actsink
         ctx.set_materialize_grads(False)      # no zero-filled grads for the (non-differentiable) stats outputs
         ctx.x_sink = actsink.sink_of(x)       # fanned-out input: dgrad accumulates into the producer's sink
@@ -669,18 +649,12 @@ class _Conv(torch.autograd.Function):
         # deferred shortcut BN), else the persistent per-device one
         sbuf = _stats_buffer if want_stats != 2 else (
             lambda co, dev, slots=STAT_SLOTS: torch.zeros((2, slots, co), dtype=torch.float32, device=dev))
-        if fin is not None and not (want_stats and _fin_ok(ch)):
-            fin = None
         if ch[0] == "mdtf":
             if want_stats:
                 co = w.shape[3]
                 slots = stat_slots(-(-x.shape[0] * out_hw[0] * out_hw[1] // ch[1]))
-                if fin is not None:
-                    slots = fin_slots(co, slots)
                 buf = sbuf(co, x.device, slots)
                 stats = (buf[0], buf[1])
-            if fin is not None:
-                fin.arm()
             y = mdtf_fwd(x, w, out_hw, stride, pads, dil, ch[1], ch[2], stats, ch[4], ch[5])
         elif ch[0] == "pp":
             if want_stats:
@@ -698,13 +672,9 @@ class _Conv(torch.autograd.Function):
             ctx.stem_x4 = keep[0]
         elif ch[0] == "ws":
             if want_stats:
-                co = w.shape[3]
-                buf = sbuf(co, x.device, fin_slots(co, STAT_SLOTS) if fin is not None else STAT_SLOTS)
+                buf = sbuf(w.shape[3], x.device, STAT_SLOTS)
                 stats = (buf[0], buf[1])
-            wt = transpose_filter(w)
-            if fin is not None:
-                fin.arm()
-            y = ws_fwd(x, wt, w.shape[0], w.shape[1], out_hw, stride, pads, dil, ch[1], stats)
+            y = ws_fwd(x, transpose_filter(w), w.shape[0], w.shape[1], out_hw, stride, pads, dil, ch[1], stats)
         elif ch[0] == "winograd":
             y = winograd.winograd_fwd(x, w, out_hw, pads)
         else:
@@ -726,7 +696,7 @@ class _Conv(torch.autograd.Function):
     def backward(ctx, dy, *unused):
         x, w = ctx.saved_tensors
         if dy is None:
-            return None, None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         stride, pads, dil = ctx.args
         dy = dy.contiguous()
         need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
@@ -756,21 +726,15 @@ class _Conv(torch.autograd.Function):
             if xs is not None:
                 buf, acc, pend = xs.target_ex()
                 bst = None
-                fo = None
                 if xs.stat_req is not None and xs.completing() and BWD_STATS:
                     bx, bmask = xs.stat_req
-                    fr = xs.fin_req if _bn_mod().fin_enabled() else None
-                    c = x.shape[3]
-                    sbuf = bwd_stats_acquire(x.device, c, fin_slots(c, STAT_SLOTS) if fr is not None else STAT_SLOTS)
+                    sbuf = bwd_stats_acquire(x.device, x.shape[3], STAT_SLOTS)
                     bst = (bx, bmask, sbuf[0], sbuf[1], sbuf.shape[1])
                     tile = (2,) + tuple(tile[1:])      # the statistics epilogue's register budget
-                    if fr is not None:
-                        fo = _bn_mod().arm_bwd_fin(fr, c, x.device)
                 xs.written(ws_dgrad(dy, w, x.shape, pads, dil, tile, out=buf, accumulate=acc, bn_stats=bst,
                                     acc_src=pend))
                 if bst is not None:
                     xs.stats = sbuf
-                    xs.fin = fo
             else:
                 dx = ws_dgrad(dy, w, x.shape, pads, dil, tile)
         elif need_dx and cd[0] == "pp":
@@ -792,23 +756,15 @@ class _Conv(torch.autograd.Function):
             if xs is not None and cd[4] in (2, 3):
                 buf, acc, pend = xs.target_ex()
                 bst = None
-                fo = None
                 if xs.stat_req is not None and xs.completing() and BWD_STATS and not N.deterministic():
-                    # this dgrad completes the BN output's gradient: emit the BN backward statistics (and finalize
-                    # them in its last workgroup)
+                    # this dgrad completes the BN output's gradient: emit the BN backward statistics
                     bx, bmask = xs.stat_req
-                    fr = xs.fin_req if _bn_mod().fin_enabled() else None
-                    c = x.shape[3]
-                    slots = stat_slots(-(-x.numel() // c // cd[1]))
-                    sbuf = bwd_stats_acquire(x.device, c, fin_slots(c, slots) if fr is not None else slots)
+                    sbuf = bwd_stats_acquire(x.device, x.shape[3], stat_slots(-(-x.numel() // x.shape[3] // cd[1])))
                     bst = (bx, bmask, sbuf[0], sbuf[1], sbuf.shape[1])
-                    if fr is not None:
-                        fo = _bn_mod().arm_bwd_fin(fr, c, x.device)
                 xs.written(mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5], out=buf,
                                       accumulate=acc, bn_stats=bst, acc_src=pend))
                 if bst is not None:
                     xs.stats = sbuf
-                    xs.fin = fo
                 dx = None
             else:
                 dx = mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5])
@@ -844,7 +800,7 @@ class _Conv(torch.autograd.Function):
                 dw = mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], ver=cw[4], stages=cw[5])
                 if dw.dtype != ctx.w_dtype:
                     dw = dw.to(ctx.w_dtype)
-        return dx, dw, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 def _out_hw(x, w, stride, pads, dil):
@@ -867,21 +823,17 @@ def conv2d_nhwc(x, w, stride, pads, dil, bias=None, act=None):
     return y
 
 
-def conv2d_stats_nhwc(x, w, stride, pads, dil, private=False, fin=None):
+def conv2d_stats_nhwc(x, w, stride, pads, dil, private=False):
     """conv2d that also returns fused BN statistics partials ``(psum, psq, P)`` (or None); ``private``: in a
-    buffer of their own (consumed after later convs have run) instead of the shared per-device one.  ``fin``
-    (:class:`bn.FwdFin`): finalize them in the conv's last workgroup where the kernel can, then the statistics
-    are ``(psum, psq, P, [4][C] mean/invstd/scale/shift)``."""
+    buffer of their own (consumed after later convs have run) instead of the shared per-device one."""
     if x.dtype != torch.bfloat16:
         raise TypeError("mdtf conv kernels take bf16 activations, got %s" % x.dtype)
     if w.dtype != x.dtype:
         w = w.to(x.dtype)
     y, psum, psq = _Conv.apply(x, w, tuple(stride), tuple(pads), tuple(dil), _out_hw(x, w, stride, pads, dil),
-                               2 if private else True, fin)
+                               2 if private else True)
     if psum.numel() == 0:
         return y, None
-    if fin is not None and fin.armed:
-        return y, (psum, psq, psum.shape[0], fin.out)
     return y, (psum, psq, psum.shape[0])
 
 

@@ -250,10 +250,7 @@ def conv_bn(x, w, gamma, beta, moving_mean, moving_var, strides=1, padding="SAME
         from . import conv as conv_mod
         from . import bn
         defer = defer and not relu and residual is None and bn.DEFER_SHORTCUT
-        # the BN finalize rides on the conv's last workgroup (not for the fused stem pass)
-        fin = (bn.FwdFin(gamma, beta, moving_mean, moving_var, decay, epsilon, n * oh * ow, co, x.device)
-               if pool is None and bn.fin_enabled() else None)
-        y, stats = conv_mod.conv2d_stats_nhwc(x, w, (sh, sw), (pt, pb, pl, pr), (1, 1), private=defer, fin=fin)
+        y, stats = conv_mod.conv2d_stats_nhwc(x, w, (sh, sw), (pt, pb, pl, pr), (1, 1), private=defer)
         if defer and stats is not None:
             return bn.DeferredBN(y, gamma, beta, moving_mean, moving_var, decay, epsilon, stats)
         if pool is not None and relu and residual is None and stats is not None and bn.FUSED_STEM:

@@ -1260,42 +1260,6 @@ def test_bn_backward_stats_from_dgrad_epilogue(model, monkeypatch):
         assert _rel(gf[k], go[k]) < 1e-2, (k, _rel(gf[k], go[k]))
 
 
-@pytest.mark.parametrize("model,conv_backend", [("res", "mdtf2"), ("strided", "mdtf2"), ("res", "ws"),
-                                                ("dual", "auto"), ("dual_strided", "auto")])
-def test_bn_finalize_in_kernel_matches_finalize_launch(model, conv_backend, monkeypatch):
-    """BN statistics finalized by the producing conv's last-arriving workgroup (csrc/include/bn_fin.h: forward
-    from the conv epilogue, backward from the completing dgrad, ticket reset by the last arriver) == the separate
-    finalize launch: losses over two steps (the ticket must have reset), gradients, moving statistics.  Both
-    in-kernel paths must actually have been armed."""
-    from mdtf.ops import bn as B
-    if conv_backend == "mdtf2":
-        monkeypatch.setenv("MDTF_CONV", conv_backend)
-    global _Tiny
-    saved = _Tiny
-    _Tiny = {"res": _TinyRes, "strided": _TinyStrided, "dual": _TinyDual, "dual_strided": _TinyDualStrided}[model]
-    try:
-        torch.manual_seed(8)
-        # "ws": ResNet-50's 56 x 56 x 64 shapes, which conv_table.json runs on the weight-stationary kernel
-        x = torch.randn(4, 56, 56, 64) if conv_backend == "ws" else torch.randn(16, 12, 12, 64)
-        y = torch.randint(0, 16, (16,))
-        monkeypatch.setattr(B, "IN_KERNEL_FIN", True)
-        f0, b0 = B.FIN_ARMED
-        lf, gf = _tiny_step(DEV, torch.bfloat16, x, y)
-        lf2, _ = _tiny_step(DEV, torch.bfloat16, x, y)
-        assert B.FIN_ARMED[0] - f0 >= 4
-        if model in ("res", "strided"):
-            assert B.FIN_ARMED[1] - b0 >= 2
-        monkeypatch.setattr(B, "IN_KERNEL_FIN", False)
-        f1 = list(B.FIN_ARMED)
-        lo, go = _tiny_step(DEV, torch.bfloat16, x, y)
-        assert B.FIN_ARMED == f1
-    finally:
-        _Tiny = saved
-    assert abs(lf - lo) / abs(lo) < 1e-3 and abs(lf2 - lo) / abs(lo) < 1e-3, (lf, lf2, lo)
-    for k in go:
-        assert _rel(gf[k], go[k]) < 2e-2, (k, _rel(gf[k], go[k]))
-
-
 class _TinyDual(object):
     """A projection-shortcut block as ResNet builds it: the shortcut BN deferred into the residual BN
     (relu(BN(x) + BN2(r)), ops.bn.DeferredBN); ``stride`` 2 makes both the shortcut and the 3x3 strided."""
