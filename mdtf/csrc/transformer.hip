@@ -224,17 +224,20 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
   float* wg = ws ? ws + (long long)blockIdx.x * 2 * H : nullptr;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    // 16-B stores: 8 consecutive lanes cover all 64 banks (scalar stores at an 8-float stride hit 4 of them)
-    float4* l0 = reinterpret_cast<float4*>(&L[0][slice][lane * 8]);
-    float4* l1 = reinterpret_cast<float4*>(&L[1][slice][lane * 8]);
-    l0[0] = make_float4(dg[i][0], dg[i][1], dg[i][2], dg[i][3]);
-    l0[1] = make_float4(dg[i][4], dg[i][5], dg[i][6], dg[i][7]);
-    l1[0] = make_float4(db[i][0], db[i][1], db[i][2], db[i][3]);
-    l1[1] = make_float4(db[i][4], db[i][5], db[i][6], db[i][7]);
+    // a lane's 8 columns as two 16-B halves, each half-set lane-contiguous (position h * 4 LPR + 4 lane + e holds
+    // column 8 lane + 4 h + e): the 16 lanes one ds_write_b128 cycle serves write 256 contiguous bytes -- all 64
+    // banks once.  (Both halves at 8 lane, 8 lane + 4 put lanes l and l + 8 on the same banks: 2-way conflicts.)
+    float4* l0 = reinterpret_cast<float4*>(&L[0][slice][0]);
+    float4* l1 = reinterpret_cast<float4*>(&L[1][slice][0]);
+    l0[lane] = make_float4(dg[i][0], dg[i][1], dg[i][2], dg[i][3]);
+    l0[LPR + lane] = make_float4(dg[i][4], dg[i][5], dg[i][6], dg[i][7]);
+    l1[lane] = make_float4(db[i][0], db[i][1], db[i][2], db[i][3]);
+    l1[LPR + lane] = make_float4(db[i][4], db[i][5], db[i][6], db[i][7]);
     __syncthreads();
     for (int j = threadIdx.x; j < 2 * SPAN; j += kT) {
       const int which = j / SPAN, cc = j % SPAN;       // 0: dgamma, 1: dbeta
-      const int col = i * SPAN + cc;
+      const int h = cc / (4 * LPR), ln = (cc / 4) % LPR, e = cc % 4;
+      const int col = i * SPAN + ln * 8 + h * 4 + e;
       if (col < H) {
         float t = 0.f;
 #pragma unroll
