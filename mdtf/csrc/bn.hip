@@ -962,6 +962,125 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
+// Σ g·m and Σ g·m·x of the stem BN from the POOLED tensors (pooled rows M' = N OH OW instead of the 4x larger
+// input): every pooled output's gradient dy lands on its window's argmax input, and it passes the ReLU exactly when
+// the pooled value y = relu(x scale + shift) is > 0, where that input's BN input is x = (y - shift) / scale.  So
+// Σ g·m = Σ dy [y > 0] and Σ g·m·x = Σ dy [y > 0] (y - shift) / scale -- the 411 MB input x is not read (ResNet-50,
+// batch 256); for a channel with scale == 0 the argmax element is gathered from x instead.  Block geometry and
+// output ([gx][C] partials) as bn_reduce_kernel.
+__global__ void __launch_bounds__(kThreads)
+    maxpool_bn_bwd_reduce_pooled(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                 const uint8_t* __restrict__ arg, const bf16_t* __restrict__ x,
+                                 const float* __restrict__ scale, const float* __restrict__ shift, PoolG g, int tpr,
+                                 int rg, float* __restrict__ p0, float* __restrict__ p1) {
+  extern __shared__ float smem[];
+  const int t = threadIdx.x;
+  const int lane_c = t % tpr;
+  const int rgi = t / tpr;
+  const int c8 = blockIdx.y * tpr + lane_c;
+  const long long M = (long long)g.N * g.OH * g.OW;
+  float s0[8], s1[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s0[k] = s1[k] = 0.f;
+  if (c8 * 8 < g.C) {
+    float sc[8], sh[8], isc[8];
+    load_coef8(scale, c8 * 8, sc);
+    load_coef8(shift, c8 * 8, sh);
+    bool any_zero = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      isc[k] = sc[k] != 0.f ? 1.f / sc[k] : 0.f;
+      any_zero |= sc[k] == 0.f;
+    }
+    const long long span = ceil_div(ceil_div(M, (long long)gridDim.x), (long long)rg) * rg;
+    const long long rbeg = (long long)blockIdx.x * span;
+    const long long rend = rbeg + span < M ? rbeg + span : M;
+    long long r = rbeg + rgi;
+    // 4 pooled rows per trip: all 8 loads in flight before the first use
+    for (; r + 3 * rg < rend; r += 4 * rg) {
+      uint4 gr[4], yr[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long off = (r + u * rg) * g.C + c8 * 8;
+        gr[u] = *reinterpret_cast<const uint4*>(dy + off);
+        yr[u] = *reinterpret_cast<const uint4*>(y + off);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float gv[8], yv[8];
+        unpack8(gr[u], gv);
+        unpack8(yr[u], yv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float gm = yv[k] > 0.f ? gv[k] : 0.f;
+          s0[k] += gm;
+          s1[k] += gm * (yv[k] - sh[k]) * isc[k];
+        }
+      }
+    }
+    for (; r < rend; r += rg) {
+      const long long off = r * g.C + c8 * 8;
+      float gv[8], yv[8];
+      load_bf8(dy + off, gv);
+      load_bf8(y + off, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gm = yv[k] > 0.f ? gv[k] : 0.f;
+        s0[k] += gm;
+        s1[k] += gm * (yv[k] - sh[k]) * isc[k];
+      }
+    }
+    if (any_zero) {
+      // channels with scale == 0: x of each pooled output's argmax input, gathered (a second, rare sweep)
+      for (long long q = rbeg + rgi; q < rend; q += rg) {
+        const long long off = q * g.C + c8 * 8;
+        const int ow = static_cast<int>(q % g.OW);
+        const long long t2 = q / g.OW;
+        const int oh = static_cast<int>(t2 % g.OH);
+        const int n = static_cast<int>(t2 / g.OH);
+        const uint2 pk = *reinterpret_cast<const uint2*>(arg + off);
+        float gv[8], yv[8];
+        load_bf8(dy + off, gv);
+        load_bf8(y + off, yv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (sc[k] != 0.f || !(yv[k] > 0.f)) continue;
+          const int id = static_cast<int>(((k < 4 ? pk.x : pk.y) >> (8 * (k & 3))) & 0xffu);
+          const int h = oh * g.SH - g.PT + id / g.KW, w = ow * g.SW - g.PL + id % g.KW;
+          s1[k] += gv[k] * bf2f(x[(((long long)n * g.H + h) * g.W + w) * g.C + c8 * 8 + k]);
+        }
+      }
+    }
+  }
+  const int W = tpr * 8;
+  float* L0 = smem;
+  float* L1 = smem + rg * W;
+  {
+    float4* d0 = reinterpret_cast<float4*>(L0 + rgi * W + lane_c * 8);
+    float4* d1 = reinterpret_cast<float4*>(L1 + rgi * W + lane_c * 8);
+    d0[0] = make_float4(s0[0], s0[1], s0[2], s0[3]);
+    d0[1] = make_float4(s0[4], s0[5], s0[6], s0[7]);
+    d1[0] = make_float4(s1[0], s1[1], s1[2], s1[3]);
+    d1[1] = make_float4(s1[4], s1[5], s1[6], s1[7]);
+  }
+  __syncthreads();
+  for (int step = rg / 2; step > 0; step >>= 1) {
+    for (int e = t; e < step * W; e += kThreads) {
+      const int gi = e / W, k = e % W;
+      L0[gi * W + k] += L0[(gi + step) * W + k];
+      L1[gi * W + k] += L1[(gi + step) * W + k];
+    }
+    __syncthreads();
+  }
+  for (int k = t; k < W; k += kThreads) {
+    const int c = blockIdx.y * W + k;
+    if (c < g.C) {
+      p0[(long long)blockIdx.x * g.C + c] = L0[k];
+      p1[(long long)blockIdx.x * g.C + c] = L1[k];
+    }
+  }
+}
+
 bool pool_geo_ok(const PoolG& g) {
   return g.C % 8 == 0 && g.KH * g.KW <= 255 && (long long)g.N * g.H * g.W * g.C < (1LL << 31) &&
          g.OH > 0 && g.OW > 0;
@@ -989,11 +1108,12 @@ MDTF_EXPORT int mdtf_bn_relu_maxpool_fwd(const void* x, void* y, uint8_t* arg, i
 }
 
 // Backward of mdtf_bn_relu_maxpool_fwd: dy = gradient of the pooled output, ss = the forward's scale/shift,
-// ws = mdtf_bn_workspace_floats(N*H*W, C) floats.  dgamma/dbeta accumulate.
+// ws = mdtf_bn_workspace_floats(N*H*W, C) floats.  dgamma/dbeta accumulate.  y (optional): the pooled output, whose
+// values give the statistics without re-reading x (maxpool_bn_bwd_reduce_pooled).
 MDTF_EXPORT int mdtf_maxpool_bn_bwd(const void* dy, const uint8_t* arg, const void* x, void* dx, int N, int H, int W,
                                     int C, int OH, int OW, int KH, int KW, int SH, int SW, int PT, int PL,
                                     const float* gamma, const float* mean, const float* invstd, float* dgamma,
-                                    float* dbeta, const float* ss, float* ws, hipStream_t st) {
+                                    float* dbeta, const float* ss, float* ws, const void* y, hipStream_t st) {
   PoolG g{N, H, W, C, OH, OW, KH, KW, SH, SW, PT, PL};
   if (!pool_geo_ok(g)) return MDTF_EUNSUPPORTED;
   const long long M = (long long)N * H * W;
@@ -1006,7 +1126,14 @@ MDTF_EXPORT int mdtf_maxpool_bn_bwd(const void* dy, const uint8_t* arg, const vo
   const int cv = C / 8;
   const bool rows_path = (cv & (cv - 1)) == 0 && cv <= kThreads;
   int parts = ge.gx;
-  if (rows_path) {
+  if (y) {
+    // statistics from the pooled output (y: the forward's pooled tensor), maxpool_bn_bwd_reduce_pooled
+    const Geo gp = make_geo((long long)N * OH * OW, C);       // gp.gx <= ge.gx: fits the workspace rows
+    parts = gp.gx;
+    const size_t lds = 2 * sizeof(float) * gp.rg * gp.tpr * 8;
+    hipLaunchKernelGGL(maxpool_bn_bwd_reduce_pooled, dim3(gp.gx, gp.gy), dim3(kThreads), lds, st, (const bf16_t*)dy,
+                       (const bf16_t*)y, arg, (const bf16_t*)x, ss, ss + C, g, gp.tpr, gp.rg, p0, p1);
+  } else if (rows_path) {
     int cvs = 0;
     while ((1 << cvs) < cv) ++cvs;
     const int nrows = N * H;

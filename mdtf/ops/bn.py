@@ -18,7 +18,7 @@ N.register("mdtf_bn_fwd_stats", [N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.
                                  N.I, N.P, N.P])
 N.register("mdtf_bn_relu_maxpool_fwd", [N.P, N.P, N.P] + [N.I] * 12 + [N.P] * 4 + [N.F, N.F] + [N.P] * 4 + [N.I]
            + [N.P, N.P])
-N.register("mdtf_maxpool_bn_bwd", [N.P] * 4 + [N.I] * 12 + [N.P] * 7 + [N.P])
+N.register("mdtf_maxpool_bn_bwd", [N.P] * 4 + [N.I] * 12 + [N.P] * 8 + [N.P])
 N.register("mdtf_bn_bwd_dual", [N.P] * 6 + [N.L, N.I] + [N.P] * 7 + [N.I] + [N.P] * 6 + [N.P])
 
 
@@ -283,6 +283,9 @@ class _BNTrainDual(torch.autograd.Function):
 
 # the stem's BN + ReLU + max pool as one pass (bn_relu_maxpool_nhwc); MDTF_FUSED_STEM=0: BN apply + max pool
 FUSED_STEM = os.environ.get("MDTF_FUSED_STEM", "1") != "0"
+# its backward's BN statistics from the pooled tensors (dy, pooled y: x recovered from y at each window's argmax)
+# instead of a gather pass over the 4x larger input; MDTF_STEM_POOLED_STATS=0: the input-row pass
+STEM_POOLED_STATS = os.environ.get("MDTF_STEM_POOLED_STATS", "1") != "0"
 
 
 class _BNReluMaxPool(torch.autograd.Function):
@@ -309,7 +312,7 @@ class _BNReluMaxPool(torch.autograd.Function):
                                                  int(P), N.ptr(ss), N.stream_ptr()), "bn_relu_maxpool_fwd")
         from . import conv as _conv
         _conv.stats_consumed(x.device)
-        ctx.save_for_backward(x, arg, g, mean, invstd, ss)
+        ctx.save_for_backward(x, arg, g, mean, invstd, ss, y if STEM_POOLED_STATS else None)
         ctx.geo = geo
         ctx.sinks = (V.grad_sink(gamma) if gamma is not None else None,
                      V.grad_sink(beta) if beta is not None else None)
@@ -323,7 +326,7 @@ class _BNReluMaxPool(torch.autograd.Function):
             dy = ctx.out_sink.take(dy)
         if dy is None:
             return (None,) * 9
-        x, arg, g, mean, invstd, ss = ctx.saved_tensors
+        x, arg, g, mean, invstd, ss, yp = ctx.saved_tensors
         dy = dy.contiguous()
         n, h, w, c = x.shape
         oh, ow, kh, kw, sh, sw, pt, pl = ctx.geo
@@ -334,7 +337,8 @@ class _BNReluMaxPool(torch.autograd.Function):
         ws = torch.empty(int(N.fn("mdtf_bn_workspace_floats")(n * h * w, c)), dtype=torch.float32, device=x.device)
         N.check(N.fn("mdtf_maxpool_bn_bwd")(N.ptr(dy), N.ptr(arg), N.ptr(x), N.ptr(dx), n, h, w, c, oh, ow, kh, kw,
                                             sh, sw, pt, pl, N.ptr(g), N.ptr(mean), N.ptr(invstd), N.ptr(dgamma),
-                                            N.ptr(dbeta), N.ptr(ss), N.ptr(ws), N.stream_ptr()), "maxpool_bn_bwd")
+                                            N.ptr(dbeta), N.ptr(ss), N.ptr(ws), N.ptr(yp), N.stream_ptr()),
+                "maxpool_bn_bwd")
         gamma, beta = ctx.like
         rg = (V.grad_marker(gamma) if sg is not None else dgamma) if gamma is not None else None
         rb = (V.grad_marker(beta) if sb is not None else dbeta) if beta is not None else None

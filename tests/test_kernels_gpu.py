@@ -540,6 +540,36 @@ def test_bert_embeddings_fused_vs_fp32(monkeypatch):
         assert _rel(a, r) < 2e-2
 
 
+@pytest.mark.parametrize("zero_gamma", [False, True])
+def test_stem_bn_backward_statistics_from_pooled_tensors(zero_gamma, monkeypatch):
+    """The fused stem's BN backward statistics from the pooled tensors (csrc/bn.hip maxpool_bn_bwd_reduce_pooled:
+    x recovered from the pooled y at each window's argmax; channels with gamma == 0 gather x instead) == the
+    input-row pass over x: filter / gamma / beta gradients."""
+    from mdtf.ops import bn as B
+    torch.manual_seed(14)
+    x = torch.randn(8, 38, 38, 3)
+    w = torch.randn(7, 7, 3, 64) * (1.0 / 147 ** 0.5)
+    g = torch.rand(64) + 0.5
+    if zero_gamma:
+        g[::7] = 0.0
+    b = torch.randn(64) * 0.2
+    dy0 = torch.randn(8, 10, 10, 64, generator=torch.Generator().manual_seed(5))
+    outs = {}
+    monkeypatch.setattr(B, "FUSED_STEM", True)
+    for pooled in (True, False):
+        monkeypatch.setattr(B, "STEM_POOLED_STATS", pooled)
+        xx = x.to(DEV).bfloat16()
+        ww = w.to(DEV).bfloat16().requires_grad_(True)
+        gg = g.to(DEV).requires_grad_(True)
+        bb = b.to(DEV).requires_grad_(True)
+        y = ops.conv_bn(xx, ww, gg, bb, torch.zeros(64, device=DEV), torch.ones(64, device=DEV), 2, (3, 3), True,
+                        0.9, 1e-5, True, None, pool=(3, 2, "SAME"))
+        y.backward(dy0.to(DEV).bfloat16())
+        outs[pooled] = dict(dw=ww.grad.float(), dg=gg.grad.float(), db=bb.grad.float())
+    for key in ("dw", "dg", "db"):
+        assert _rel(outs[True][key], outs[False][key]) < 1e-2, (key, _rel(outs[True][key], outs[False][key]))
+
+
 def test_stem_conv_bn_relu_maxpool_fused_vs_unfused(monkeypatch):
     """ResNet stem conv 7x7/2 -> BN -> ReLU -> max pool 3x3/2 SAME: the fused BN+ReLU+pool kernels
     (csrc/bn.hip mdtf_bn_relu_maxpool_fwd / mdtf_maxpool_bn_bwd) vs the unfused GPU passes on the same bf16
