@@ -222,23 +222,27 @@ __global__ void __launch_bounds__(1024)
                     float* __restrict__ mvar, float decay, float eps, float* __restrict__ mean_out,
                     float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift,
                     int zero_after) {
+  // the per-channel parameters are loaded before the partial sums, in the same memory round trip
+  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  const bool own = threadIdx.x < kFinCh && c < C;
+  const float g = own && gamma ? gamma[c] : 1.f;
+  const float bt = own && beta ? beta[c] : 0.f;
+  const float mm0 = own && mmean ? mmean[c] : 0.f;
+  const float mv0 = own && mvar ? mvar[c] : 0.f;
   double s, q;
   if (!sum_partials(p0, p1, gx, C, s, q, zero_after != 0)) return;
-  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
   double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
   if (var < 0) var = 0;
   float inv = rsqrtf((float)var + eps);
-  float g = gamma ? gamma[c] : 1.f;
-  float bt = beta ? beta[c] : 0.f;
   mean_out[c] = (float)mean;
   invstd_out[c] = inv;
   scale[c] = g * inv;
   shift[c] = bt - (float)mean * g * inv;
   if (mmean) {
     double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    mmean[c] = decay * mmean[c] + (1.f - decay) * (float)mean;
-    mvar[c] = decay * mvar[c] + (1.f - decay) * (float)unbiased;
+    mmean[c] = decay * mm0 + (1.f - decay) * (float)mean;
+    mvar[c] = decay * mv0 + (1.f - decay) * (float)unbiased;
   }
 }
 
@@ -380,15 +384,19 @@ __global__ void __launch_bounds__(1024)
                     const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
                     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ k1,
                     float* __restrict__ k2, float* __restrict__ k3, int zero_after) {
+  // the per-channel parameters are loaded before the partial sums, in the same memory round trip
+  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  const bool own = threadIdx.x < kFinCh && c < C;
+  const float mu = own ? mean[c] : 0.f, inv = own ? invstd[c] : 0.f;
+  const float g = own && gamma ? gamma[c] : 1.f;
+  const float dg0 = own && dgamma ? dgamma[c] : 0.f;
+  const float db0 = own && dbeta ? dbeta[c] : 0.f;
   double sdz, sdzx;
   if (!sum_partials(p0, p1, gx, C, sdz, sdzx, zero_after != 0)) return;
-  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
-  float mu = mean[c], inv = invstd[c];
-  float g = gamma ? gamma[c] : 1.f;
   float db = (float)sdz;
   float dg = (float)((sdzx - (double)mu * sdz) * inv);
-  if (dgamma) dgamma[c] += dg;     // accumulate: zeroed buffer or the variable's fp32 grad slot
-  if (dbeta) dbeta[c] += db;
+  if (dgamma) dgamma[c] = dg0 + dg;   // accumulate: zeroed buffer or the variable's fp32 grad slot
+  if (dbeta) dbeta[c] = db0 + db;
   float a = g * inv;
   float invM = 1.f / (float)M;
   // dx = a*(dz - db/M - xhat*dg/M), xhat = (x-mu)*inv
