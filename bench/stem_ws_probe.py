@@ -40,7 +40,8 @@ def main():
     xa = torch.empty(256, 230, 230, 4, device=dev, dtype=torch.bfloat16)
     from mdtf.ops import _native as N
     res["pack_ms"] = round(timeit(lambda: N.fn("mdtf_stem_pack4")(N.ptr(x), N.ptr(xa), 256, 224, 224, 3, 3, 3, 230,
-                                                                   230, N.stream_ptr())), 4)
+                                                                   230, None, None, 0, 0, 0, 0,
+                                                                   N.stream_ptr())), 4)
     print(json.dumps(res), flush=True)
 
 

@@ -130,31 +130,78 @@ MDTF_EXPORT int mdtf_conv_ws(const void* src, const void* wgt, void* out, int N,
 // fragments straight from x4: no im2col, no library call.
 // ---------------------------------------------------------------------------------------------
 namespace {
-__global__ void __launch_bounds__(256) stem_pack4(const bf16_t* __restrict__ x, uint2* __restrict__ x4, int N, int H,
-                                                  int W, int C, int pt, int pl, int H4, int W4) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long total = (long long)N * H4 * W4;
-  if (i >= total) return;
-  const int xw = (int)(i % W4);
-  const long long q = i / W4;
-  const int yh = (int)(q % H4);
-  const int n = (int)(q / H4);
-  const int ih = yh - pt, iw = xw - pl;
+// One 128-thread block per x4 image row: the source row (W * C bf16) is staged through LDS with 16-byte loads
+// when it is 16-byte aligned, then written out two pixels (16 bytes) per thread; the blocks past the rows repack
+// the HWIO filter into wt[co][KHp][32] (tap kw, channel c at element 4 kw + c; zero past KH / KW / C), so the
+// stem's operands are ready after a single launch.
+constexpr int kPackThreads = 128;
+constexpr int kStemRowMax = 16384;            // W * C bf16 staged per row (32 KB of LDS)
+
+__device__ __forceinline__ uint2 stem_pixel(const bf16_t* row, int iw, int W, int C) {
   uint32_t v[4] = {0u, 0u, 0u, 0u};
-  if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
-    const bf16_t* p = x + (((long long)n * H + ih) * W + iw) * C;
-    for (int c = 0; c < C; ++c) v[c] = p[c];
+  if (iw >= 0 && iw < W)
+    for (int c = 0; c < C; ++c) v[c] = row[iw * C + c];
+  return make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(kPackThreads) stem_pack4(const bf16_t* __restrict__ x, uint2* __restrict__ x4,
+                                                           int N, int H, int W, int C, int pt, int pl, int H4,
+                                                           int W4, const bf16_t* __restrict__ w,
+                                                           bf16_t* __restrict__ wt, int KH, int KW, int CO, int KHP) {
+  extern __shared__ __align__(16) bf16_t row_s[];
+  const int rows = N * H4;
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (b >= rows) {
+    const int i = (b - rows) * kPackThreads + t;
+    if (i >= CO * KHP * 32) return;
+    const int co = i / (KHP * 32), r = i % (KHP * 32);
+    const int kh = r >> 5, kw = (r & 31) >> 2, c = r & 3;
+    wt[i] = (kh < KH && kw < KW && c < C) ? w[((kh * KW + kw) * C + c) * CO + co] : bf16_t(0);
+    return;
   }
-  x4[i] = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+  const int n = b / H4, ih = b - n * H4 - pt;
+  const bool live = ih >= 0 && ih < H;                 // block-uniform
+  if (live) {
+    const bf16_t* src = x + ((long long)n * H + ih) * W * C;
+    if (VEC) {
+      const uint4* s4 = reinterpret_cast<const uint4*>(src);
+      uint4* d4 = reinterpret_cast<uint4*>(row_s);
+      for (int i = t; i < W * C / 8; i += kPackThreads) d4[i] = s4[i];
+    } else {
+      for (int i = t; i < W * C; i += kPackThreads) row_s[i] = src[i];
+    }
+    __syncthreads();
+  }
+  uint2* dst = x4 + (long long)b * W4;
+  if ((W4 & 1) == 0) {
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    for (int p = t; p < W4 / 2; p += kPackThreads) {
+      uint2 a = make_uint2(0u, 0u), c = a;
+      if (live) {
+        a = stem_pixel(row_s, 2 * p - pl, W, C);
+        c = stem_pixel(row_s, 2 * p + 1 - pl, W, C);
+      }
+      d4[p] = make_uint4(a.x, a.y, c.x, c.y);
+    }
+  } else {
+    for (int p = t; p < W4; p += kPackThreads) dst[p] = live ? stem_pixel(row_s, p - pl, W, C) : make_uint2(0u, 0u);
+  }
 }
 }  // namespace
 
+// x -> zero-haloed x4 [N][H4][W4][4]; with w non-null also the filter rows wt (see stem_pack4).
 MDTF_EXPORT int mdtf_stem_pack4(const void* x, void* x4, int N, int H, int W, int C, int pt, int pl, int H4, int W4,
-                                hipStream_t st) {
-  if (C < 1 || C > 4) return MDTF_EINVAL;
-  const long long total = (long long)N * H4 * W4;
-  hipLaunchKernelGGL(stem_pack4, dim3((unsigned)ceil_div(total, 256LL)), dim3(256), 0, st, (const bf16_t*)x,
-                     (uint2*)x4, N, H, W, C, pt, pl, H4, W4);
+                                const void* w, void* wt, int KH, int KW, int CO, int KHP, hipStream_t st) {
+  if (C < 1 || C > 4 || KH > KHP || KW > 8 || W * C > kStemRowMax) return MDTF_EINVAL;
+  const long long rows = (long long)N * H4;
+  const long long wblocks = w ? ceil_div((long long)CO * KHP * 32, (long long)kPackThreads) : 0;
+  if (rows + wblocks >= (1LL << 31)) return MDTF_EINVAL;
+  const bool vec = (W * C) % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  const size_t lds = (size_t)W * C * sizeof(bf16_t);
+  auto k = vec ? stem_pack4<true> : stem_pack4<false>;
+  hipLaunchKernelGGL(k, dim3((unsigned)(rows + wblocks)), dim3(kPackThreads), lds, st, (const bf16_t*)x,
+                     (uint2*)x4, N, H, W, C, pt, pl, H4, W4, (const bf16_t*)w, (bf16_t*)wt, KH, KW, CO, KHP);
   MDTF_LAUNCH_CHECK();
   return 0;
 }

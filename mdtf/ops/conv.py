@@ -384,10 +384,11 @@ def ws_ok(pass_, c, co, stride, kh, kw, dil=(1, 1)):
             and 64 * kh * kw * red * 2 <= 160 * 1024)
 
 
-N.register("mdtf_stem_pack4", [N.P, N.P] + [N.I] * 8 + [N.P])
+N.register("mdtf_stem_pack4", [N.P, N.P] + [N.I] * 8 + [N.P, N.P] + [N.I] * 4 + [N.P])
 N.register("mdtf_conv_ws_stem", [N.P, N.P, N.P] + [N.I] * 10 + [N.P, N.P, N.I, N.P])
 N.register("mdtf_stem_wgrad", [N.P, N.P, N.P] + [N.I] * 11 + [N.P])
 STEM = os.environ.get("MDTF_STEM", "mdtf")          # mdtf: hand-written stem forward | miopen
+_STEM_PACK_W = os.environ.get("MDTF_STEM_PACK_W", "1") != "0"     # filter rows packed in the x4 launch
 STEM_TILE = (4, 4, 1, 4)          # bench/stem_ws_probe.py: 0.329 ms vs MIOpen 0.487 (batch 256)
 
 
@@ -395,6 +396,7 @@ def stem_ok(x_shape, w_shape, dil):
     """Few-channel stems (Cin <= 4, KW <= 8, undilated): csrc/conv_ws.hip mdtf_conv_ws_stem."""
     kh, kw, ci, co = w_shape
     return (STEM != "miopen" and ci <= 4 and kw <= 8 and co % 64 == 0 and tuple(dil) == (1, 1)
+            and x_shape[2] * ci <= 16384                          # source row staged in LDS (stem_pack4)
             and os.environ.get("MDTF_CONV", "auto") != "miopen")
 
 
@@ -410,8 +412,8 @@ def stem_wgrad(x4, dy, w_shape, stride, out=None, blocks=0):
 
 
 def stem_fwd(x, w, out_hw, stride, pads, stats=None, tile=None, keep_x4=None):
-    """Stem forward: repack x into a zero-haloed 4-channel image (one kernel), then the weight-stationary
-    GEMM with one 32-deep k-step per filter row (filter rows packed [co][row][kw*4 + c], zero-padded)."""
+    """Stem forward: repack x into a zero-haloed 4-channel image and the filter into rows [co][row][kw*4 + c]
+    (zero-padded; one kernel for both), then the weight-stationary GEMM with one 32-deep k-step per row."""
     n, h, wd, c = x.shape
     kh, kw, ci, co = w.shape
     pt, pb, pl, pr = pads
@@ -419,10 +421,17 @@ def stem_fwd(x, w, out_hw, stride, pads, stats=None, tile=None, keep_x4=None):
     h4 = max(h + pt + pb, (out_hw[0] - 1) * stride[0] + khp)
     w4 = max(wd + pl + pr, (out_hw[1] - 1) * stride[1] + 8)
     x4 = torch.empty((n, h4, w4, 4), dtype=x.dtype, device=x.device)
-    N.check(N.fn("mdtf_stem_pack4")(N.ptr(x), N.ptr(x4), n, h, wd, c, pt, pl, h4, w4, N.stream_ptr()), "stem_pack4")
-    wp = torch.zeros((khp, 8, 4, co), dtype=x.dtype, device=x.device)
-    wp[:kh, :kw, :ci].copy_(w)
-    wt = wp.view(khp * 32, co).t().contiguous()              # [co][row][kw*4 + c]
+    assert ci == c, "stem filter channels %d != input channels %d" % (ci, c)
+    w = w.to(x.dtype).contiguous()
+    if _STEM_PACK_W:
+        wt = torch.empty((co, khp * 32), dtype=x.dtype, device=x.device)      # [co][row][kw*4 + c]
+    else:
+        wp = torch.zeros((khp, 8, 4, co), dtype=x.dtype, device=x.device)
+        wp[:kh, :kw, :ci].copy_(w)
+        wt = wp.view(khp * 32, co).t().contiguous()
+    N.check(N.fn("mdtf_stem_pack4")(N.ptr(x), N.ptr(x4), n, h, wd, c, pt, pl, h4, w4,
+                                    N.ptr(w if _STEM_PACK_W else None), N.ptr(wt), kh, kw, co, khp,
+                                    N.stream_ptr()), "stem_pack4")
     y = torch.empty((n, out_hw[0], out_hw[1], co), dtype=x.dtype, device=x.device)
     s_sum, s_sq = stats if stats is not None else (None, None)
     slots = s_sum.shape[0] if s_sum is not None else 0
