@@ -37,6 +37,7 @@ def main():
     for tile in [(4, 8, 1, 4), (2, 8, 1, 4), (4, 4, 1, 4), (2, 4, 1, 4)]:
         res["stem_%d%d%d%d_ms" % tile] = round(timeit(lambda: C.stem_fwd(x, w, (112, 112), (2, 2), pads,
                                                                           (sbuf[0], sbuf[1]), tile)), 4)
+    res["stem_rows_ms"] = round(timeit(lambda: C.stem_fwd(x, w, (112, 112), (2, 2), pads, (sbuf[0], sbuf[1]))), 4)
     xa = torch.empty(256, 230, 230, 4, device=dev, dtype=torch.bfloat16)
     from mdtf.ops import _native as N
     res["pack_ms"] = round(timeit(lambda: N.fn("mdtf_stem_pack4")(N.ptr(x), N.ptr(xa), 256, 224, 224, 3, 3, 3, 230,

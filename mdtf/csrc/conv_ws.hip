@@ -215,3 +215,226 @@ MDTF_EXPORT int mdtf_conv_ws_stem(const void* x4, const void* wt, void* out, int
   return conv_ws_impl(x4, wt, out, N, H4, W4, 32, 4, OH, OW, Ncol, KHp, 1, SH, SW, 0, 0, 1, 1, 0, tile, 0, ssum,
                       ssq, sslots, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, nullptr, st);
 }
+
+// ---------------------------------------------------------------------------------------------
+// Row-staged stem convolution.  The streamed kernel above reads each B fragment from x4 in global
+// memory with only a 4-k-step ring in flight at two waves per SIMD: the stem's 8 KB-per-output-row
+// reads are latency bound there (259 us for ResNet's 7x7/2, against ~45 us of MFMA work).  Here a
+// 4-wave block owns kStemRows consecutive output rows of one image (one row per wave, all 64
+// channels of its channel group): it stages the KH filter rows (fragment order, 1 KiB per fragment)
+// and the (kStemRows-1)*SH + KH input rows it reads into LDS with every load issued before the
+// first wait, then each wave runs KH k-steps of 4 x TP MFMAs with both operands from LDS and stores
+// its row.  Three blocks fit a CU (52 KB of LDS at W4 = 230), so one block's staging overlaps the
+// others' MFMAs.  Forward BN statistics are reduced per wave and added to [sslots][Ncol] slots.
+// ---------------------------------------------------------------------------------------------
+namespace {
+constexpr int kStemRows = 4;
+constexpr int kStemStage = 8;          // 16-B staging loads in flight per thread per batch
+
+// Σ over the 16 lanes of a DPP row (lane & 15), valid in the row's lane 15: four v_add_f32 with row_shr
+// operands -- no LDS crossbar traffic (the __shfl_xor version cost ~45 us in this kernel's 28k waves).
+__device__ __forceinline__ float row_sum16(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
+  return v;
+}
+
+// AL16: SW even, so every B fragment (16 B at pixel ow*SW + 2g) is 16-B aligned: one ds_read_b128
+// (two 8-B reads per lane at a 16-B lane stride conflict 2-way)
+template <int TP, bool AL16>
+__global__ void __launch_bounds__(256, 3) stem_conv_rows(const bf16_t* __restrict__ x4, const bf16_t* __restrict__ wt,
+                                                         bf16_t* __restrict__ out, int H4, int W4, int OH, int OW,
+                                                         int Ncol, int KH, int KHP, int SH, int SW, int rblocks,
+                                                         int ngroups, float* __restrict__ ssum,
+                                                         float* __restrict__ ssq, int sslots) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int cgroups = Ncol / 64;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int cblk = bid % cgroups;                          // fixed per block: gridDim.x % cgroups == 0
+  const int nrows = (kStemRows - 1) * SH + KH;
+  const int pitch = W4 * 8;                                // bytes per staged row (W4 even: 16-B aligned)
+  const int chunks_w = KH * 4 * 64, chunks_r = nrows * (W4 / 2);
+  char* rows_s = lds + chunks_w * 16;
+  float* stat_s = reinterpret_cast<float*>(rows_s + chunks_r * 16);   // [2][64] block partials (LDS atomics)
+  const int n0 = cblk * 64;
+  if (threadIdx.x < 128) stat_s[threadIdx.x] = 0.f;
+
+  // ---- filter fragments once per block (f = ks*4 + i: lane l holds channel chan_of(i, l&15), k = 32 ks + 8 (l>>4))
+  for (int q = threadIdx.x; q < chunks_w; q += 256) {
+    const int f = q >> 6, l = q & 63;
+    const int ch = n0 + chan_of(f & 3, l & 15);
+    reinterpret_cast<uint4*>(lds)[q] =
+        *reinterpret_cast<const uint4*>(wt + (long long)ch * (KHP * 32) + (f >> 2) * 32 + 8 * (l >> 4));
+  }
+
+  const int rp = lane >> 2, rc = lane & 3;
+  const int xsrc = (16 * rc + rp) * 4;
+  auto xpose = [&](const uint4& v) {
+    return make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute(xsrc, (int)v.x),
+                      (uint32_t)__builtin_amdgcn_ds_bpermute(xsrc, (int)v.y),
+                      (uint32_t)__builtin_amdgcn_ds_bpermute(xsrc, (int)v.z),
+                      (uint32_t)__builtin_amdgcn_ds_bpermute(xsrc, (int)v.w));
+  };
+
+  for (int grp = bid; grp < ngroups; grp += gridDim.x) {
+    const int rb = grp / cgroups;
+    const int n = rb / rblocks, oh0 = (rb - n * rblocks) * kStemRows;
+    __syncthreads();                                       // the previous group's rows are consumed
+    // ---- input rows oh0*SH .. + nrows-1 (zero past H4): a batch of loads before its LDS writes
+    {
+      const uint4* src4 = reinterpret_cast<const uint4*>(x4) + ((long long)n * H4 + (long long)oh0 * SH) * (W4 / 2);
+      const int avail = (H4 - oh0 * SH) * (W4 / 2);        // chunks of the staged rows that exist in x4
+      for (int base = 0; base < chunks_r; base += kStemStage * 256) {
+        uint4 v[kStemStage];
+#pragma unroll
+        for (int u = 0; u < kStemStage; ++u) {
+          const int q = base + u * 256 + threadIdx.x;
+          v[u] = q < chunks_r && q < avail ? src4[q] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < kStemStage; ++u) {
+          const int q = base + u * 256 + threadIdx.x;
+          if (q < chunks_r) reinterpret_cast<uint4*>(rows_s)[q] = v[u];
+        }
+      }
+    }
+    __syncthreads();
+
+    const int oh = oh0 + wave;
+    if (oh >= OH) continue;                                // wave-uniform; the loop's barriers stay matched
+    float4v acc[4][TP];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < TP; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < KH; ++ks) {
+      bf16x8_t af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(lds + (ks * 4 + i) * 1024 + lane * 16));
+      const char* row = rows_s + (wave * SH + ks) * pitch;
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int ow = 16 * j + li;
+        uint4 bv = make_uint4(0u, 0u, 0u, 0u);
+        if (ow < OW) {
+          if (AL16) {
+            bv = *reinterpret_cast<const uint4*>(row + (ow * SW + 2 * g) * 8);
+          } else {
+            const uint2* p = reinterpret_cast<const uint2*>(row + (ow * SW + 2 * g) * 8);
+            const uint2 lo = p[0], hi = p[1];
+            bv = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          }
+        }
+        const bf16x8_t b = __builtin_bit_cast(bf16x8_t, bv);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = mfma(af[i], b, acc[i][j]);
+      }
+    }
+
+    // ---- epilogue: fragment layout (channel chunk g, pixel li) -> row layout (pixel rp, chunk rc) and
+    // 2 x 16-B stores per pixel (a full 128-B output row); statistics from the fp32 accumulators (pixels
+    // past OW hold zeros), row-reduced and added to the block's LDS partials
+    float s0[16], s1[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s0[e] = s1[e] = 0.f;
+    const long long prow = ((long long)n * OH + oh) * OW;
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      float v0[8], v1[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v0[r] = acc[0][j][r];
+        v0[4 + r] = acc[1][j][r];
+        v1[r] = acc[2][j][r];
+        v1[4 + r] = acc[3][j][r];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s0[e] += v0[e];
+        s1[e] += v0[e] * v0[e];
+        s0[8 + e] += v1[e];
+        s1[8 + e] += v1[e] * v1[e];
+      }
+      const uint4 w0 = xpose(pack8(v0)), w1 = xpose(pack8(v1));
+      const int ow = 16 * j + rp;
+      if (ow < OW) {
+        bf16_t* o = out + (prow + ow) * Ncol + n0 + 8 * rc;
+        *reinterpret_cast<uint4*>(o) = w0;
+        *reinterpret_cast<uint4*>(o + 32) = w1;
+      }
+    }
+    if (ssum) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        s0[e] = row_sum16(s0[e]);
+        s1[e] = row_sum16(s1[e]);
+      }
+      if (li == 15) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int c = e < 8 ? 8 * g + e : 32 + 8 * g + (e - 8);
+          atomicAdd(stat_s + c, s0[e]);                    // LDS atomics: the block's partials
+          atomicAdd(stat_s + 64 + c, s1[e]);
+        }
+      }
+    }
+  }
+  if (ssum) {
+    __syncthreads();
+    if (threadIdx.x < 128) {
+      const int c = threadIdx.x & 63;
+      float* dst = (threadIdx.x < 64 ? ssum : ssq) + (long long)(blockIdx.x % sslots) * Ncol + n0 + c;
+      atomicAdd(dst, stat_s[threadIdx.x]);
+    }
+  }
+}
+
+template <int TP>
+void launch_stem_rows(const void* x4, const void* wt, void* out, int N, int H4, int W4, int OH, int OW, int Ncol,
+                      int KH, int KHP, int SH, int SW, float* ssum, float* ssq, int sslots, size_t lds, hipStream_t st) {
+  const int rblocks = (OH + kStemRows - 1) / kStemRows;
+  const int cgroups = Ncol / 64;
+  const long long ngroups = (long long)N * rblocks * cgroups;
+  // persistent: as many blocks as fit (LDS-bound, <= 3 per CU), a multiple of the channel groups
+  long long per_cu = (160 * 1024) / (long long)lds;
+  if (per_cu > 3) per_cu = 3;
+  long long nblk = 256 * per_cu / cgroups * cgroups;
+  if (nblk < cgroups) nblk = cgroups;
+  if (nblk > ngroups) nblk = ngroups;
+  auto k = (SW & 1) ? stem_conv_rows<TP, false> : stem_conv_rows<TP, true>;
+  hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(256), lds, st, (const bf16_t*)x4, (const bf16_t*)wt,
+                     (bf16_t*)out, H4, W4, OH, OW, Ncol, KH, KHP, SH, SW, rblocks, (int)ngroups, ssum, ssq,
+                     sslots > 0 ? sslots : 1);
+}
+}  // namespace
+
+// Row-staged stem forward (see above): same operands as mdtf_conv_ws_stem plus KH, the filter rows actually
+// used (rows KH..KHp-1 of wt are zero and skipped).  Needs W4 even, OW <= 128, Ncol % 64 == 0.
+MDTF_EXPORT int mdtf_stem_conv_rows(const void* x4, const void* wt, void* out, int N, int H4, int W4, int OH, int OW,
+                                    int Ncol, int KH, int KHp, int SH, int SW, float* ssum, float* ssq, int sslots,
+                                    hipStream_t st) {
+  if ((W4 & 1) || OW < 1 || OW > 128 || Ncol % 64 || KH < 1 || KH > KHp || (OW - 1) * SW + 8 > W4 ||
+      (OH - 1) * SH + KH > H4)
+    return MDTF_EINVAL;
+  const size_t lds = (size_t)KH * 4 * 1024 + (size_t)((kStemRows - 1) * SH + KH) * W4 * 8 + 128 * sizeof(float);
+  if (lds > 160 * 1024) return MDTF_EUNSUPPORTED;
+  if ((long long)N * ((OH + kStemRows - 1) / kStemRows) * (Ncol / 64) >= (1LL << 31)) return MDTF_EUNSUPPORTED;
+  switch ((OW + 15) / 16) {
+    case 1: launch_stem_rows<1>(x4, wt, out, N, H4, W4, OH, OW, Ncol, KH, KHp, SH, SW, ssum, ssq, sslots, lds, st); break;
+    case 2: launch_stem_rows<2>(x4, wt, out, N, H4, W4, OH, OW, Ncol, KH, KHp, SH, SW, ssum, ssq, sslots, lds, st); break;
+    case 3: launch_stem_rows<3>(x4, wt, out, N, H4, W4, OH, OW, Ncol, KH, KHp, SH, SW, ssum, ssq, sslots, lds, st); break;
+    case 4: launch_stem_rows<4>(x4, wt, out, N, H4, W4, OH, OW, Ncol, KH, KHp, SH, SW, ssum, ssq, sslots, lds, st); break;
+    case 5: launch_stem_rows<5>(x4, wt, out, N, H4, W4, OH, OW, Ncol, KH, KHp, SH, SW, ssum, ssq, sslots, lds, st); break;
+    case 6: launch_stem_rows<6>(x4, wt, out, N, H4, W4, OH, OW, Ncol, KH, KHp, SH, SW, ssum, ssq, sslots, lds, st); break;
+    case 7: launch_stem_rows<7>(x4, wt, out, N, H4, W4, OH, OW, Ncol, KH, KHp, SH, SW, ssum, ssq, sslots, lds, st); break;
+    default: launch_stem_rows<8>(x4, wt, out, N, H4, W4, OH, OW, Ncol, KH, KHp, SH, SW, ssum, ssq, sslots, lds, st); break;
+  }
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}

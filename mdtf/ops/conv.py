@@ -386,8 +386,11 @@ def ws_ok(pass_, c, co, stride, kh, kw, dil=(1, 1)):
 
 N.register("mdtf_stem_pack4", [N.P, N.P] + [N.I] * 8 + [N.P, N.P] + [N.I] * 4 + [N.P])
 N.register("mdtf_conv_ws_stem", [N.P, N.P, N.P] + [N.I] * 10 + [N.P, N.P, N.I, N.P])
+N.register("mdtf_stem_conv_rows", [N.P, N.P, N.P] + [N.I] * 10 + [N.P, N.P, N.I, N.P])
 N.register("mdtf_stem_wgrad", [N.P, N.P, N.P] + [N.I] * 11 + [N.P])
 STEM = os.environ.get("MDTF_STEM", "mdtf")          # mdtf: hand-written stem forward | miopen
+# rows: row-staged kernel (both operands from LDS, one output row per wave) | ws: streamed weight-stationary kernel
+STEM_KERNEL = os.environ.get("MDTF_STEM_KERNEL", "rows")
 _STEM_PACK_W = os.environ.get("MDTF_STEM_PACK_W", "1") != "0"     # filter rows packed in the x4 launch
 STEM_TILE = (4, 4, 1, 4)          # bench/stem_ws_probe.py: 0.329 ms vs MIOpen 0.487 (batch 256)
 
@@ -420,6 +423,7 @@ def stem_fwd(x, w, out_hw, stride, pads, stats=None, tile=None, keep_x4=None):
     khp = -(-kh // 4) * 4
     h4 = max(h + pt + pb, (out_hw[0] - 1) * stride[0] + khp)
     w4 = max(wd + pl + pr, (out_hw[1] - 1) * stride[1] + 8)
+    w4 += w4 & 1                                   # even: 16-B aligned rows for the row-staged kernel
     x4 = torch.empty((n, h4, w4, 4), dtype=x.dtype, device=x.device)
     assert ci == c, "stem filter channels %d != input channels %d" % (ci, c)
     w = w.to(x.dtype).contiguous()
@@ -435,9 +439,14 @@ def stem_fwd(x, w, out_hw, stride, pads, stats=None, tile=None, keep_x4=None):
     y = torch.empty((n, out_hw[0], out_hw[1], co), dtype=x.dtype, device=x.device)
     s_sum, s_sq = stats if stats is not None else (None, None)
     slots = s_sum.shape[0] if s_sum is not None else 0
-    N.check(N.fn("mdtf_conv_ws_stem")(N.ptr(x4), N.ptr(wt), N.ptr(y), n, h4, w4, out_hw[0], out_hw[1], co, khp,
-                                      stride[0], stride[1], _ws_code(*(tile or STEM_TILE)), N.ptr(s_sum), N.ptr(s_sq),
-                                      slots, N.stream_ptr()), "conv_ws_stem")
+    if STEM_KERNEL == "rows" and tile is None and out_hw[1] <= 128:
+        N.check(N.fn("mdtf_stem_conv_rows")(N.ptr(x4), N.ptr(wt), N.ptr(y), n, h4, w4, out_hw[0], out_hw[1], co, kh,
+                                            khp, stride[0], stride[1], N.ptr(s_sum), N.ptr(s_sq), slots,
+                                            N.stream_ptr()), "stem_conv_rows")
+    else:
+        N.check(N.fn("mdtf_conv_ws_stem")(N.ptr(x4), N.ptr(wt), N.ptr(y), n, h4, w4, out_hw[0], out_hw[1], co, khp,
+                                          stride[0], stride[1], _ws_code(*(tile or STEM_TILE)), N.ptr(s_sum),
+                                          N.ptr(s_sq), slots, N.stream_ptr()), "conv_ws_stem")
     if keep_x4 is not None:
         keep_x4.append(x4)                    # the weight gradient reads the packed image again
     return y

@@ -1533,9 +1533,11 @@ def test_conv_weight_stationary(tile, geo):
 
 @pytest.mark.parametrize("geo", [(2, 30, 31, 3, 7, 64, 2, 3), (3, 17, 16, 1, 5, 128, 1, 2), (2, 24, 24, 4, 3, 64, 2, 1),
                                  (1, 224, 224, 3, 7, 64, 2, 3)])
-def test_stem_conv_forward(geo):
-    """Few-channel stem forward (repack to a haloed 4-channel image + weight-stationary GEMM) with the fused
-    BN-statistics epilogue vs the fp32 reference; ResNet's 7x7/2 RGB stem included."""
+@pytest.mark.parametrize("kernel", ["rows", "ws"])
+def test_stem_conv_forward(geo, kernel):
+    """Few-channel stem forward (repack to a haloed 4-channel image + the row-staged kernel, or the streamed
+    weight-stationary GEMM) with the fused BN-statistics epilogue vs the fp32 reference; ResNet's 7x7/2 RGB
+    stem included."""
     from mdtf.ops import conv as C
     n, h, w, c, k, co, s, p = geo
     torch.manual_seed(sum(geo))
@@ -1548,7 +1550,8 @@ def test_stem_conv_forward(geo):
                                     padding=p).permute(0, 2, 3, 1)
     sbuf = torch.zeros(2, 8, co, device=DEV)
     keep = []
-    y = C.stem_fwd(x.to(DEV), wt.to(DEV), (oh, ow), (s, s), (p, p, p, p), (sbuf[0], sbuf[1]), keep_x4=keep)
+    y = C.stem_fwd(x.to(DEV), wt.to(DEV), (oh, ow), (s, s), (p, p, p, p), (sbuf[0], sbuf[1]),
+                   tile=C.STEM_TILE if kernel == "ws" else None, keep_x4=keep)
     assert y.shape == yr.shape
     assert _rel(y, yr) < 1e-2
     yf = yr.reshape(-1, co)
