@@ -917,6 +917,94 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
+// Same math, one workgroup per PAIR of input rows sharing their pooled rows (2 x 2 stride, windows <= 4: input
+// row h is covered by pooled rows k = (h + PT) / 2 and k - 1 only): the two pooled rows' gradient + argmax are
+// staged in LDS once (every input pixel reads up to 4 windows' (argmax, gradient) -- from LDS instead of L2),
+// and the thread's x vectors are loaded before the staging barrier.  Needs 2 W cv <= kThreads * kPairVec.
+constexpr int kPairVec = 8;
+
+__global__ void __launch_bounds__(kThreads)
+    maxpool_bn_dx_pairs(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ x,
+                        const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ k1,
+                        const float* __restrict__ k2, const float* __restrict__ k3, bf16_t* __restrict__ dx, PoolG g,
+                        int cvs, int kmin, int nk) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  const int t = threadIdx.x;
+  const int n = blockIdx.x / nk, k = kmin + (int)(blockIdx.x - n * nk);
+  const int cv = 1 << cvs, c8 = t & (cv - 1);
+  const int rowv = g.W << cvs, prowv = g.OW << cvs;      // 8-channel vectors per input / pooled row
+  const int h0 = 2 * k - g.PT;                            // input rows h0, h0 + 1
+  uint4* dys = reinterpret_cast<uint4*>(sm);                              // [2][OW][cv]: rows k-1, k
+  uint2* ags = reinterpret_cast<uint2*>(sm + 2 * prowv * sizeof(uint4));  // same layout, argmax bytes
+  const uint4* x4 = reinterpret_cast<const uint4*>(x);
+  uint4 xr[kPairVec];
+#pragma unroll
+  for (int u = 0; u < kPairVec; ++u) {
+    const int q = u * kThreads + t, r = q >= rowv ? 1 : 0, h = h0 + r;
+    const bool ok = q < 2 * rowv && h >= 0 && h < g.H;
+    xr[u] = ok ? x4[((long long)n * g.H + h) * rowv + (q - r * rowv)] : make_uint4(0u, 0u, 0u, 0u);
+  }
+  const uint4* dy4 = reinterpret_cast<const uint4*>(dy);
+  const uint2* ag2 = reinterpret_cast<const uint2*>(arg);
+  for (int q = t; q < 2 * prowv; q += kThreads) {
+    const int s = q >= prowv ? 1 : 0, oh = k - 1 + s;
+    uint4 d = make_uint4(0u, 0u, 0u, 0u);
+    uint2 a = make_uint2(0u, 0u);
+    if (oh >= 0 && oh < g.OH) {
+      const long long o = ((long long)n * g.OH + oh) * prowv + (q - s * prowv);
+      d = dy4[o];
+      a = ag2[o];
+    }
+    dys[q] = d;
+    ags[q] = a;
+  }
+  float sc[8], sh[8], A[8], B[8], E[8];
+  load_coef8(scale, c8 * 8, sc);
+  load_coef8(shift, c8 * 8, sh);
+  load_coef8(k1, c8 * 8, A);
+  load_coef8(k2, c8 * 8, B);
+  load_coef8(k3, c8 * 8, E);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kPairVec; ++u) {
+    const int q = u * kThreads + t, r = q >= rowv ? 1 : 0, h = h0 + r;
+    if (q >= 2 * rowv || h < 0 || h >= g.H) continue;
+    const int w = (q - r * rowv) >> cvs;
+    const int wp = w + g.PL, ow1 = wp >> 1;
+    float gv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gv[e] = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int oh = k - a, kh = r + 2 * a;                // window row oh covers h at tap kh
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int ow = ow1 - b, kw = wp - 2 * ow;
+        const bool ok = oh >= 0 && oh < g.OH && kh < g.KH && ow >= 0 && ow < g.OW && kw < g.KW;
+        const int idx = ((1 - a) * g.OW + min(max(ow, 0), g.OW - 1)) * cv + c8;
+        const uint4 gr = dys[idx];
+        const uint2 pk = ags[idx];
+        const uint32_t me = static_cast<uint32_t>(kh * g.KW + kw);
+        float gw[8];
+        unpack8(gr, gw);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t id = ((e < 4 ? pk.x : pk.y) >> (8 * (e & 3))) & 0xffu;
+          if (ok && id == me) gv[e] += gw[e];
+        }
+      }
+    }
+    float xv[8], o[8];
+    unpack8(xr[u], xv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gm = (xv[e] * sc[e] + sh[e] > 0.f) ? gv[e] : 0.f;
+      o[e] = A[e] * gm + B[e] * xv[e] + E[e];
+    }
+    store_bf8(dx + (((long long)n * g.H + h) * rowv + (q - r * rowv)) * 8, o);
+  }
+}
+
 // Σ g·m and Σ g·m·x by input rows (the maxpool_bn_dx_rows mapping): block b sums image rows [b rpb, (b+1) rpb),
 // a thread one channel vector over pixels w0, w0 + 256 / cv, ...; the threads of a channel vector are combined in
 // LDS -> partials [gridDim.x][C]
@@ -1118,6 +1206,12 @@ MDTF_EXPORT int mdtf_bn_relu_maxpool_fwd(const void* x, void* y, uint8_t* arg, i
 // Backward of mdtf_bn_relu_maxpool_fwd: dy = gradient of the pooled output, ss = the forward's scale/shift,
 // ws = mdtf_bn_workspace_floats(N*H*W, C) floats.  dgamma/dbeta accumulate.  y (optional): the pooled output, whose
 // values give the statistics without re-reading x (maxpool_bn_bwd_reduce_pooled).
+namespace {
+int pool_dx_pairs = -1;     // -1: from MDTF_POOL_DX_PAIRS (default on); tests switch it with mdtf_bn_pool_dx_pairs
+}  // namespace
+
+MDTF_EXPORT void mdtf_bn_pool_dx_pairs(int on) { pool_dx_pairs = on ? 1 : 0; }
+
 MDTF_EXPORT int mdtf_maxpool_bn_bwd(const void* dy, const uint8_t* arg, const void* x, void* dx, int N, int H, int W,
                                     int C, int OH, int OW, int KH, int KW, int SH, int SW, int PT, int PL,
                                     const float* gamma, const float* mean, const float* invstd, float* dgamma,
@@ -1158,7 +1252,20 @@ MDTF_EXPORT int mdtf_maxpool_bn_bwd(const void* dy, const uint8_t* arg, const vo
   }
   hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, p0, p1, parts, M,
                      C, gamma, mean, invstd, dgamma, dbeta, k1, k2, k3, 0);
-  if (rows_path) {
+  if (pool_dx_pairs < 0) {
+    const char* e = getenv("MDTF_POOL_DX_PAIRS");
+    pool_dx_pairs = (e && e[0] == '0') ? 0 : 1;
+  }
+  const bool pairs_on = pool_dx_pairs != 0;
+  const size_t pair_lds = (size_t)2 * OW * cv * (sizeof(uint4) + sizeof(uint2));
+  if (rows_path && pairs_on && SH == 2 && SW == 2 && KH <= 4 && KW <= 4 && PT >= 0 && PL >= 0 &&
+      2 * W * cv <= kThreads * kPairVec && pair_lds <= 64 * 1024) {
+    int cvs = 0;
+    while ((1 << cvs) < cv) ++cvs;
+    const int kmin = PT >> 1, nk = ((H - 1 + PT) >> 1) - kmin + 1;
+    hipLaunchKernelGGL(maxpool_bn_dx_pairs, dim3(N * nk), dim3(kThreads), pair_lds, st, (const bf16_t*)dy, arg,
+                       (const bf16_t*)x, ss, ss + C, k1, k2, k3, (bf16_t*)dx, g, cvs, kmin, nk);
+  } else if (rows_path) {
     int cvs = 0;
     while ((1 << cvs) < cv) ++cvs;
     hipLaunchKernelGGL(maxpool_bn_dx_rows, dim3(N * H), dim3(kThreads), 0, st, (const bf16_t*)dy, arg,

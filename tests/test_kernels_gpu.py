@@ -570,6 +570,37 @@ def test_stem_bn_backward_statistics_from_pooled_tensors(zero_gamma, monkeypatch
         assert _rel(outs[True][key], outs[False][key]) < 1e-2, (key, _rel(outs[True][key], outs[False][key]))
 
 
+@pytest.mark.parametrize("hw", [64, 38])
+def test_stem_pool_bn_input_gradient_row_pairs(hw, monkeypatch):
+    """The fused stem backward's input gradient by pairs of input rows with the pooled rows staged in LDS
+    (csrc/bn.hip maxpool_bn_dx_pairs) == the per-row kernel (maxpool_bn_dx_rows): filter / gamma / beta gradients
+    of the stem, even and odd conv-output sizes (first and last row pairs half outside the image)."""
+    from mdtf.ops import bn as B
+    from mdtf.ops import _native as N
+    N.register("mdtf_bn_pool_dx_pairs", [N.I], restype=None)
+    torch.manual_seed(15)
+    x = torch.randn(4, hw, hw, 3)
+    w = torch.randn(7, 7, 3, 64) * (1.0 / 147 ** 0.5)
+    g = torch.rand(64) + 0.5
+    b = torch.randn(64) * 0.2
+    monkeypatch.setattr(B, "FUSED_STEM", True)
+    outs = {}
+    try:
+        for pairs in (1, 0):
+            N.fn("mdtf_bn_pool_dx_pairs")(pairs)
+            ww = w.to(DEV).bfloat16().requires_grad_(True)
+            gg = g.to(DEV).requires_grad_(True)
+            bb = b.to(DEV).requires_grad_(True)
+            y = ops.conv_bn(x.to(DEV).bfloat16(), ww, gg, bb, torch.zeros(64, device=DEV),
+                            torch.ones(64, device=DEV), 2, (3, 3), True, 0.9, 1e-5, True, None, pool=(3, 2, "SAME"))
+            y.backward(torch.randn(y.shape, generator=torch.Generator().manual_seed(6)).to(DEV).bfloat16())
+            outs[pairs] = dict(dw=ww.grad.float(), dg=gg.grad.float(), db=bb.grad.float())
+    finally:
+        N.fn("mdtf_bn_pool_dx_pairs")(1)
+    for key in ("dw", "dg", "db"):
+        assert _rel(outs[1][key], outs[0][key]) < 1e-3, (key, _rel(outs[1][key], outs[0][key]))
+
+
 def test_stem_conv_bn_relu_maxpool_fused_vs_unfused(monkeypatch):
     """ResNet stem conv 7x7/2 -> BN -> ReLU -> max pool 3x3/2 SAME: the fused BN+ReLU+pool kernels
     (csrc/bn.hip mdtf_bn_relu_maxpool_fwd / mdtf_maxpool_bn_bwd) vs the unfused GPU passes on the same bf16
