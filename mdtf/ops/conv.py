@@ -403,6 +403,11 @@ def stem_ok(x_shape, w_shape, dil):
             and os.environ.get("MDTF_CONV", "auto") != "miopen")
 
 
+# blocks of the stem weight gradient: 3 per CU (78 VGPRs x 8 waves, 40 KB LDS) fill the chip in one round;
+# bench/stem_wgrad_probe.py: 256 / 512 / 768 / 1024 blocks -> 362 / 226 / 191 / 222 us
+STEM_WG_BLOCKS = int(os.environ.get("MDTF_STEM_WG_BLOCKS", "768"))
+
+
 def stem_wgrad(x4, dy, w_shape, stride, out=None, blocks=0):
     """Stem weight gradient from the forward's packed x4 (csrc/stem_wgrad.hip): fp32 HWIO, accumulated
     into ``out`` (a zeroed buffer or the variable's gradient slot)."""
@@ -410,7 +415,8 @@ def stem_wgrad(x4, dy, w_shape, stride, out=None, blocks=0):
     dw = out if out is not None else torch.zeros(w_shape, dtype=torch.float32, device=dy.device)
     n, h4, w4, _ = x4.shape
     N.check(N.fn("mdtf_stem_wgrad")(N.ptr(x4), N.ptr(dy), N.ptr(dw), n, h4, w4, dy.shape[1], dy.shape[2],
-                                    stride[0], stride[1], kh, kw, ci, int(blocks), N.stream_ptr()), "stem_wgrad")
+                                    stride[0], stride[1], kh, kw, ci, int(blocks or STEM_WG_BLOCKS),
+                                    N.stream_ptr()), "stem_wgrad")
     return dw
 
 
