@@ -216,34 +216,60 @@ __device__ __forceinline__ bool sum_partials(const float* __restrict__ p0, const
   return true;
 }
 
+struct FinFwd {
+  const float* p0;
+  const float* p1;
+  int gx;
+  const float* gamma;
+  const float* beta;
+  float* mmean;
+  float* mvar;
+  float* mean_out;
+  float* invstd_out;
+  float* scale;
+  float* shift;
+  int zero_after;
+};
+
+__device__ __forceinline__ void finalize_fwd(const FinFwd& a, long long M, int C, float decay, float eps) {
+  // the per-channel parameters are loaded before the partial sums, in the same memory round trip
+  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  const bool own = threadIdx.x < kFinCh && c < C;
+  const float g = own && a.gamma ? a.gamma[c] : 1.f;
+  const float bt = own && a.beta ? a.beta[c] : 0.f;
+  const float mm0 = own && a.mmean ? a.mmean[c] : 0.f;
+  const float mv0 = own && a.mvar ? a.mvar[c] : 0.f;
+  double s, q;
+  if (!sum_partials(a.p0, a.p1, a.gx, C, s, q, a.zero_after != 0)) return;
+  double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  if (var < 0) var = 0;
+  float inv = rsqrtf((float)var + eps);
+  a.mean_out[c] = (float)mean;
+  a.invstd_out[c] = inv;
+  a.scale[c] = g * inv;
+  a.shift[c] = bt - (float)mean * g * inv;
+  if (a.mmean) {
+    double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    a.mmean[c] = decay * mm0 + (1.f - decay) * (float)mean;
+    a.mvar[c] = decay * mv0 + (1.f - decay) * (float)unbiased;
+  }
+}
+
 __global__ void __launch_bounds__(1024)
     bn_finalize_fwd(const float* __restrict__ p0, const float* __restrict__ p1, int gx, long long M, int C,
                     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ mmean,
                     float* __restrict__ mvar, float decay, float eps, float* __restrict__ mean_out,
                     float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift,
                     int zero_after) {
-  // the per-channel parameters are loaded before the partial sums, in the same memory round trip
-  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
-  const bool own = threadIdx.x < kFinCh && c < C;
-  const float g = own && gamma ? gamma[c] : 1.f;
-  const float bt = own && beta ? beta[c] : 0.f;
-  const float mm0 = own && mmean ? mmean[c] : 0.f;
-  const float mv0 = own && mvar ? mvar[c] : 0.f;
-  double s, q;
-  if (!sum_partials(p0, p1, gx, C, s, q, zero_after != 0)) return;
-  double mean = s / (double)M;
-  double var = q / (double)M - mean * mean;
-  if (var < 0) var = 0;
-  float inv = rsqrtf((float)var + eps);
-  mean_out[c] = (float)mean;
-  invstd_out[c] = inv;
-  scale[c] = g * inv;
-  shift[c] = bt - (float)mean * g * inv;
-  if (mmean) {
-    double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    mmean[c] = decay * mm0 + (1.f - decay) * (float)mean;
-    mvar[c] = decay * mv0 + (1.f - decay) * (float)unbiased;
-  }
+  finalize_fwd(FinFwd{p0, p1, gx, gamma, beta, mmean, mvar, mean_out, invstd_out, scale, shift, zero_after}, M, C,
+               decay, eps);
+}
+
+// two BNs over the same M x C (a projection block's residual + shortcut BN): one launch, blockIdx.y picks
+__global__ void __launch_bounds__(1024) bn_finalize_fwd2(FinFwd a0, FinFwd a1, long long M, int C, float decay,
+                                                         float eps) {
+  finalize_fwd(blockIdx.y ? a1 : a0, M, C, decay, eps);
 }
 
 __global__ void bn_eval_coeffs(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -379,30 +405,54 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
+struct FinBwd {
+  const float* p0;
+  const float* p1;
+  int gx;
+  const float* gamma;
+  const float* mean;
+  const float* invstd;
+  float* dgamma;
+  float* dbeta;
+  float* k1;
+  float* k2;
+  float* k3;
+  int zero_after;
+};
+
+__device__ __forceinline__ void finalize_bwd(const FinBwd& a, long long M, int C) {
+  // the per-channel parameters are loaded before the partial sums, in the same memory round trip
+  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  const bool own = threadIdx.x < kFinCh && c < C;
+  const float mu = own ? a.mean[c] : 0.f, inv = own ? a.invstd[c] : 0.f;
+  const float g = own && a.gamma ? a.gamma[c] : 1.f;
+  const float dg0 = own && a.dgamma ? a.dgamma[c] : 0.f;
+  const float db0 = own && a.dbeta ? a.dbeta[c] : 0.f;
+  double sdz, sdzx;
+  if (!sum_partials(a.p0, a.p1, a.gx, C, sdz, sdzx, a.zero_after != 0)) return;
+  float db = (float)sdz;
+  float dg = (float)((sdzx - (double)mu * sdz) * inv);
+  if (a.dgamma) a.dgamma[c] = dg0 + dg;   // accumulate: zeroed buffer or the variable's fp32 grad slot
+  if (a.dbeta) a.dbeta[c] = db0 + db;
+  float ak = g * inv;
+  float invM = 1.f / (float)M;
+  // dx = a*(dz - db/M - xhat*dg/M), xhat = (x-mu)*inv
+  a.k1[c] = ak;
+  a.k2[c] = -ak * inv * dg * invM;
+  a.k3[c] = ak * (-db * invM + mu * inv * dg * invM);
+}
+
 __global__ void __launch_bounds__(1024)
     bn_finalize_bwd(const float* __restrict__ p0, const float* __restrict__ p1, int gx, long long M, int C,
                     const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
                     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ k1,
                     float* __restrict__ k2, float* __restrict__ k3, int zero_after) {
-  // the per-channel parameters are loaded before the partial sums, in the same memory round trip
-  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
-  const bool own = threadIdx.x < kFinCh && c < C;
-  const float mu = own ? mean[c] : 0.f, inv = own ? invstd[c] : 0.f;
-  const float g = own && gamma ? gamma[c] : 1.f;
-  const float dg0 = own && dgamma ? dgamma[c] : 0.f;
-  const float db0 = own && dbeta ? dbeta[c] : 0.f;
-  double sdz, sdzx;
-  if (!sum_partials(p0, p1, gx, C, sdz, sdzx, zero_after != 0)) return;
-  float db = (float)sdz;
-  float dg = (float)((sdzx - (double)mu * sdz) * inv);
-  if (dgamma) dgamma[c] = dg0 + dg;   // accumulate: zeroed buffer or the variable's fp32 grad slot
-  if (dbeta) dbeta[c] = db0 + db;
-  float a = g * inv;
-  float invM = 1.f / (float)M;
-  // dx = a*(dz - db/M - xhat*dg/M), xhat = (x-mu)*inv
-  k1[c] = a;
-  k2[c] = -a * inv * dg * invM;
-  k3[c] = a * (-db * invM + mu * inv * dg * invM);
+  finalize_bwd(FinBwd{p0, p1, gx, gamma, mean, invstd, dgamma, dbeta, k1, k2, k3, zero_after}, M, C);
+}
+
+// both BNs of a projection block's backward in one launch (blockIdx.y picks the set)
+__global__ void __launch_bounds__(1024) bn_finalize_bwd2(FinBwd a0, FinBwd a1, long long M, int C) {
+  finalize_bwd(blockIdx.y ? a1 : a0, M, C);
 }
 
 // One 8-channel vector of the BN backward: dz = dy (ReLU-masked), d(res) = dz, dx = k1*dz + k2*x + k3.
@@ -563,10 +613,10 @@ MDTF_EXPORT int mdtf_bn_fwd_dual(const void* x, const void* r, void* y, uint8_t*
   float* shift = ws + C;
   float* scale2 = ws + 2 * C;
   float* shift2 = ws + 3 * C;
-  hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M,
-                     C, gamma, beta, mmean, mvar, decay, eps, mean, invstd, scale, shift, 1);
-  hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum2, psq2, P2,
-                     M, C, gamma2, beta2, mmean2, mvar2, decay, eps, mean2, invstd2, scale2, shift2, 1);
+  hipLaunchKernelGGL(bn_finalize_fwd2, dim3(ceil_div(C, kFinCh), 2), dim3(kFinCh * kFinGroups), 0, st,
+                     FinFwd{psum, psq, P, gamma, beta, mmean, mvar, mean, invstd, scale, shift, 1},
+                     FinFwd{psum2, psq2, P2, gamma2, beta2, mmean2, mvar2, mean2, invstd2, scale2, shift2, 1}, M, C,
+                     decay, eps);
   const long long n8 = M * C / 8;
   hipLaunchKernelGGL(bn_apply_dual_kernel, dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
                      (const bf16_t*)r, (bf16_t*)y, mask, n8, C, scale, shift, scale2, shift2);
@@ -1362,14 +1412,16 @@ MDTF_EXPORT int mdtf_bn_bwd_dual(const void* dy, const void* x, const void* r, c
                        (const bf16_t*)x, mask, M, C, g.tpr, g.rg, p0, p1);
     hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, p0, p1, g.gx, M,
                        C, gamma, mean, invstd, dgamma, dbeta, kk, kk + C, kk + 2 * C, 0);
-  } else {
-    hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M,
-                       C, gamma, mean, invstd, dgamma, dbeta, kk, kk + C, kk + 2 * C, 1);
   }
   hipLaunchKernelGGL((bn_reduce_kernel<true, true>), dim3(g.gx, g.gy), dim3(kThreads), lds, st, (const bf16_t*)dy,
                      (const bf16_t*)r, mask, M, C, g.tpr, g.rg, q0, q1);
-  hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, q0, q1, g.gx, M, C,
-                     gamma2, mean2, invstd2, dgamma2, dbeta2, kk2, kk2 + C, kk2 + 2 * C, 0);
+  const FinBwd sc{q0, q1, g.gx, gamma2, mean2, invstd2, dgamma2, dbeta2, kk2, kk2 + C, kk2 + 2 * C, 0};
+  if (P > 0)   // the main BN's epilogue partials and the shortcut's: both finalizes in one launch
+    hipLaunchKernelGGL(bn_finalize_bwd2, dim3(ceil_div(C, kFinCh), 2), dim3(kFinCh * kFinGroups), 0, st,
+                       FinBwd{psum, psq, P, gamma, mean, invstd, dgamma, dbeta, kk, kk + C, kk + 2 * C, 1}, sc, M, C);
+  else
+    hipLaunchKernelGGL(bn_finalize_bwd2, dim3(ceil_div(C, kFinCh), 1), dim3(kFinCh * kFinGroups), 0, st, sc, sc, M,
+                       C);
   const long long n8 = M * C / 8;
   hipLaunchKernelGGL(bn_dx_dual_kernel, dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
                      (const bf16_t*)x, (const bf16_t*)r, mask, (bf16_t*)dx, (bf16_t*)dr, n8, C, kk, kk2);
