@@ -14,7 +14,7 @@ import re
 import sys
 
 WS = r"conv_ws_kernel<\d+, \d+, \d+, \d+, \d+, "     # ...<TP, NW, CG, D, KSC, EPI, DIRECT>
-CATS = [("conv_fwd", r"conv_fd_v2<\d+, \d+, 0, |conv_fd_kernel<\d+, \d+, 0,|conv_pp|" + WS + r"1,|stem_pack4"),
+CATS = [("conv_fwd", r"conv_fd_v2<\d+, \d+, 0, |conv_fd_kernel<\d+, \d+, 0,|conv_pp|" + WS + r"1,|stem_pack4|stem_conv_rows"),
         ("conv_dgrad", r"conv_fd_v2<\d+, \d+, [12], |conv_fd_kernel<\d+, \d+, [12],|" + WS + r"[234],"),
         ("conv_ws_plain", WS + r"0,"), ("conv_wgrad", r"conv_wgrad|stem_wgrad"),
         ("winograd", r"wino"),
