@@ -15,7 +15,7 @@ import sys
 
 WS = r"conv_ws_kernel<\d+, \d+, \d+, \d+, \d+, "     # ...<TP, NW, CG, D, KSC, EPI, DIRECT>
 CATS = [("conv_fwd", r"conv_fd_v2<\d+, \d+, 0, |conv_fd_kernel<\d+, \d+, 0,|conv_pp|" + WS + r"1,|stem_pack4|stem_conv_rows"),
-        ("conv_dgrad", r"conv_fd_v2<\d+, \d+, [12], |conv_fd_kernel<\d+, \d+, [12],|" + WS + r"[234],"),
+        ("conv_dgrad", r"conv_fd_v2<\d+, \d+, [12], |conv_fd_kernel<\d+, \d+, [12],|dgrad_zero_classes|" + WS + r"[234],"),
         ("conv_ws_plain", WS + r"0,"), ("conv_wgrad", r"conv_wgrad|stem_wgrad"),
         ("winograd", r"wino"),
         ("miopen", r"^(naive_conv|igemm|MIOpen|miopen|ck::|gridwise|sp3A|kernel_batched|SubTensor|_ZN2ck)"),
