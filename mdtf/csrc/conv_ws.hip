@@ -243,8 +243,10 @@ __device__ __forceinline__ float row_sum16(float v) {
 
 // AL16: SW even, so every B fragment (16 B at pixel ow*SW + 2g) is 16-B aligned: one ds_read_b128
 // (two 8-B reads per lane at a 16-B lane stride conflict 2-way)
-template <int TP, bool AL16>
-__global__ void __launch_bounds__(256, 3) stem_conv_rows(const bf16_t* __restrict__ x4, const bf16_t* __restrict__ wt,
+// PF: the next group's input rows are loaded into registers before this group's MFMAs and written to LDS after
+// them (2 blocks per CU with the registers that takes, instead of 3 blocks staging in turn)
+template <int TP, bool AL16, bool PF>
+__global__ void __launch_bounds__(256, PF ? 2 : 3) stem_conv_rows(const bf16_t* __restrict__ x4, const bf16_t* __restrict__ wt,
                                                          bf16_t* __restrict__ out, int H4, int W4, int OH, int OW,
                                                          int Ncol, int KH, int KHP, int SH, int SW, int rblocks,
                                                          int ngroups, float* __restrict__ ssum,
@@ -281,32 +283,29 @@ __global__ void __launch_bounds__(256, 3) stem_conv_rows(const bf16_t* __restric
                       (uint32_t)__builtin_amdgcn_ds_bpermute(xsrc, (int)v.w));
   };
 
-  for (int grp = bid; grp < ngroups; grp += gridDim.x) {
+  auto load_rows = [&](int grp, uint4 (&v)[kStemStage], int base) {
     const int rb = grp / cgroups;
     const int n = rb / rblocks, oh0 = (rb - n * rblocks) * kStemRows;
-    __syncthreads();                                       // the previous group's rows are consumed
-    // ---- input rows oh0*SH .. + nrows-1 (zero past H4): a batch of loads before its LDS writes
-    {
-      const uint4* src4 = reinterpret_cast<const uint4*>(x4) + ((long long)n * H4 + (long long)oh0 * SH) * (W4 / 2);
-      const int avail = (H4 - oh0 * SH) * (W4 / 2);        // chunks of the staged rows that exist in x4
-      for (int base = 0; base < chunks_r; base += kStemStage * 256) {
-        uint4 v[kStemStage];
+    const uint4* src4 = reinterpret_cast<const uint4*>(x4) + ((long long)n * H4 + (long long)oh0 * SH) * (W4 / 2);
+    const int avail = (H4 - oh0 * SH) * (W4 / 2);          // chunks of the staged rows that exist in x4
 #pragma unroll
-        for (int u = 0; u < kStemStage; ++u) {
-          const int q = base + u * 256 + threadIdx.x;
-          v[u] = q < chunks_r && q < avail ? src4[q] : make_uint4(0u, 0u, 0u, 0u);
-        }
-#pragma unroll
-        for (int u = 0; u < kStemStage; ++u) {
-          const int q = base + u * 256 + threadIdx.x;
-          if (q < chunks_r) reinterpret_cast<uint4*>(rows_s)[q] = v[u];
-        }
-      }
+    for (int u = 0; u < kStemStage; ++u) {
+      const int q = base + u * 256 + threadIdx.x;
+      v[u] = grp < ngroups && q < chunks_r && q < avail ? src4[q] : make_uint4(0u, 0u, 0u, 0u);
     }
-    __syncthreads();
-
+  };
+  auto store_rows = [&](const uint4 (&v)[kStemStage], int base) {
+#pragma unroll
+    for (int u = 0; u < kStemStage; ++u) {
+      const int q = base + u * 256 + threadIdx.x;
+      if (q < chunks_r) reinterpret_cast<uint4*>(rows_s)[q] = v[u];
+    }
+  };
+  auto run_group = [&](int grp) {
+    const int rb = grp / cgroups;
+    const int n = rb / rblocks, oh0 = (rb - n * rblocks) * kStemRows;
     const int oh = oh0 + wave;
-    if (oh >= OH) continue;                                // wave-uniform; the loop's barriers stay matched
+    if (oh >= OH) return;                                  // wave-uniform
     float4v acc[4][TP];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -384,6 +383,33 @@ __global__ void __launch_bounds__(256, 3) stem_conv_rows(const bf16_t* __restric
         }
       }
     }
+    };
+
+  if constexpr (PF) {
+    // chunks_r <= kStemStage * 256 (host-checked): one register batch holds a group's rows
+    uint4 pv[kStemStage];
+    load_rows(bid, pv, 0);
+    store_rows(pv, 0);
+    for (int grp = bid; grp < ngroups; grp += gridDim.x) {
+      __syncthreads();                                     // this group's rows (and the filter) are in LDS
+      const int nxt = grp + gridDim.x;
+      load_rows(nxt, pv, 0);                               // in flight during this group's MFMAs
+      run_group(grp);
+      __syncthreads();                                     // every wave is done with this group's rows
+      if (nxt < ngroups) store_rows(pv, 0);
+    }
+  } else {
+    for (int grp = bid; grp < ngroups; grp += gridDim.x) {
+      __syncthreads();                                     // the previous group's rows are consumed
+      // ---- input rows oh0*SH .. + nrows-1 (zero past H4): a batch of loads before its LDS writes
+      for (int base = 0; base < chunks_r; base += kStemStage * 256) {
+        uint4 v[kStemStage];
+        load_rows(grp, v, base);
+        store_rows(v, base);
+      }
+      __syncthreads();
+      run_group(grp);
+    }
   }
   if (ssum) {
     __syncthreads();
@@ -395,19 +421,31 @@ __global__ void __launch_bounds__(256, 3) stem_conv_rows(const bf16_t* __restric
   }
 }
 
+bool stem_rows_prefetch() {   // MDTF_STEM_PREFETCH=0: stage each group's rows in turn (3 blocks per CU)
+  static const bool on = [] {
+    const char* e = getenv("MDTF_STEM_PREFETCH");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int TP>
 void launch_stem_rows(const void* x4, const void* wt, void* out, int N, int H4, int W4, int OH, int OW, int Ncol,
                       int KH, int KHP, int SH, int SW, float* ssum, float* ssq, int sslots, size_t lds, hipStream_t st) {
   const int rblocks = (OH + kStemRows - 1) / kStemRows;
   const int cgroups = Ncol / 64;
   const long long ngroups = (long long)N * rblocks * cgroups;
-  // persistent: as many blocks as fit (LDS-bound, <= 3 per CU), a multiple of the channel groups
+  // persistent: as many blocks as fit (LDS-bound, <= 3 per CU; 2 with the register prefetch), a multiple of the
+  // channel groups
+  const int nrows = (kStemRows - 1) * SH + KH;
+  const bool pf = stem_rows_prefetch() && nrows * (W4 / 2) <= kStemStage * 256;
   long long per_cu = (160 * 1024) / (long long)lds;
-  if (per_cu > 3) per_cu = 3;
+  if (per_cu > (pf ? 2 : 3)) per_cu = pf ? 2 : 3;
   long long nblk = 256 * per_cu / cgroups * cgroups;
   if (nblk < cgroups) nblk = cgroups;
   if (nblk > ngroups) nblk = ngroups;
-  auto k = (SW & 1) ? stem_conv_rows<TP, false> : stem_conv_rows<TP, true>;
+  auto k = (SW & 1) ? (pf ? stem_conv_rows<TP, false, true> : stem_conv_rows<TP, false, false>)
+                     : (pf ? stem_conv_rows<TP, true, true> : stem_conv_rows<TP, true, false>);
   hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(256), lds, st, (const bf16_t*)x4, (const bf16_t*)wt,
                      (bf16_t*)out, H4, W4, OH, OW, Ncol, KH, KHP, SH, SW, rblocks, (int)ngroups, ssum, ssq,
                      sslots > 0 ? sslots : 1);
