@@ -151,7 +151,17 @@ class FaultInjectionHook(H.SessionRunHook):
         return h if h.armed else None
 
     def before_run(self, run_context):
-        if not self.armed or not self.mode.endswith("_in_step") or V.get_global_step().value() < self.step:
+        if not self.armed or V.get_global_step().value() < self.step:
+            return None
+        if self.mode.endswith("_before_run"):
+            # a recoverable error raised by a hook BEFORE the step (the async agreement still runs the step)
+            from .. import errors
+            self.armed = False
+            cls = errors.AbortedError if self.mode.startswith("abort") else errors.UnavailableError
+            logger.error("injected before_run fault at global step %d (%s)" % (V.get_global_step().value(),
+                                                                             self.mode))
+            raise cls(message="injected %s at global step %d" % (self.mode, V.get_global_step().value()))
+        if not self.mode.endswith("_in_step"):
             return None
         # raise from INSIDE the train op (after its collectives and update), not from a hook
         from .. import errors
@@ -166,7 +176,8 @@ class FaultInjectionHook(H.SessionRunHook):
         return None
 
     def after_run(self, run_context, run_values):
-        if not self.armed or self.mode.endswith("_in_step") or V.get_global_step().value() < self.step:
+        if (not self.armed or self.mode.endswith("_in_step") or self.mode.endswith("_before_run")
+                or V.get_global_step().value() < self.step):
             return
         logger.error("injected fault at global step %d (%s)" % (V.get_global_step().value(), self.mode))
         if self.mode in ("abort", "unavailable"):

@@ -1112,13 +1112,17 @@ __global__ void __launch_bounds__(kThreads)
 // input): every pooled output's gradient dy lands on its window's argmax input, and it passes the ReLU exactly when
 // the pooled value y = relu(x scale + shift) is > 0, where that input's BN input is x = (y - shift) / scale.  So
 // Σ g·m = Σ dy [y > 0] and Σ g·m·x = Σ dy [y > 0] (y - shift) / scale -- the 411 MB input x is not read (ResNet-50,
-// batch 256); for a channel with scale == 0 the argmax element is gathered from x instead.  Block geometry and
-// output ([gx][C] partials) as bn_reduce_kernel.
+// batch 256).  The reconstruction is only as good as bf16 y: its rounding error 2^-8 |y| ~ 2^-8 |shift| becomes
+// 2^-8 |shift / scale| in x, against x's own spread 1 / invstd.  For a channel where |scale| < 2^-3 |shift| invstd
+// (scale == 0 included: a tiny gamma beside a sizeable beta) that error would pass 2^-5 of the spread and bias
+// Σ g·m·x, so the argmax element is gathered from x instead.  Block geometry and output ([gx][C] partials) as
+// bn_reduce_kernel.
 __global__ void __launch_bounds__(kThreads)
     maxpool_bn_bwd_reduce_pooled(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                                  const uint8_t* __restrict__ arg, const bf16_t* __restrict__ x,
-                                 const float* __restrict__ scale, const float* __restrict__ shift, PoolG g, int tpr,
-                                 int rg, float* __restrict__ p0, float* __restrict__ p1) {
+                                 const float* __restrict__ scale, const float* __restrict__ shift,
+                                 const float* __restrict__ invstd, PoolG g, int tpr, int rg,
+                                 float* __restrict__ p0, float* __restrict__ p1) {
   extern __shared__ float smem[];
   const int t = threadIdx.x;
   const int lane_c = t % tpr;
@@ -1129,14 +1133,18 @@ __global__ void __launch_bounds__(kThreads)
 #pragma unroll
   for (int k = 0; k < 8; ++k) s0[k] = s1[k] = 0.f;
   if (c8 * 8 < g.C) {
-    float sc[8], sh[8], isc[8];
+    float sc[8], sh[8], isc[8], is[8];
     load_coef8(scale, c8 * 8, sc);
     load_coef8(shift, c8 * 8, sh);
-    bool any_zero = false;
+    load_coef8(invstd, c8 * 8, is);
+    bool any_gather = false;
+    unsigned gather = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      isc[k] = sc[k] != 0.f ? 1.f / sc[k] : 0.f;
-      any_zero |= sc[k] == 0.f;
+      const bool gx = fabsf(sc[k]) < 0.125f * fabsf(sh[k]) * is[k] || sc[k] == 0.f;
+      isc[k] = gx ? 0.f : 1.f / sc[k];
+      gather |= (gx ? 1u : 0u) << k;
+      any_gather |= gx;
     }
     const long long span = ceil_div(ceil_div(M, (long long)gridDim.x), (long long)rg) * rg;
     const long long rbeg = (long long)blockIdx.x * span;
@@ -1176,8 +1184,9 @@ __global__ void __launch_bounds__(kThreads)
         s1[k] += gm * (yv[k] - sh[k]) * isc[k];
       }
     }
-    if (any_zero) {
-      // channels with scale == 0: x of each pooled output's argmax input, gathered (a second, rare sweep)
+    if (any_gather) {
+      // channels whose x cannot be rebuilt from bf16 y: x of each pooled output's argmax input, gathered (a second,
+      // rare sweep)
       for (long long q = rbeg + rgi; q < rend; q += rg) {
         const long long off = q * g.C + c8 * 8;
         const int ow = static_cast<int>(q % g.OW);
@@ -1190,7 +1199,7 @@ __global__ void __launch_bounds__(kThreads)
         load_bf8(y + off, yv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          if (sc[k] != 0.f || !(yv[k] > 0.f)) continue;
+          if (!((gather >> k) & 1u) || !(yv[k] > 0.f)) continue;
           const int id = static_cast<int>(((k < 4 ? pk.x : pk.y) >> (8 * (k & 3))) & 0xffu);
           const int h = oh * g.SH - g.PT + id / g.KW, w = ow * g.SW - g.PL + id % g.KW;
           s1[k] += gv[k] * bf2f(x[(((long long)n * g.H + h) * g.W + w) * g.C + c8 * 8 + k]);
@@ -1284,7 +1293,7 @@ MDTF_EXPORT int mdtf_maxpool_bn_bwd(const void* dy, const uint8_t* arg, const vo
     parts = gp.gx;
     const size_t lds = 2 * sizeof(float) * gp.rg * gp.tpr * 8;
     hipLaunchKernelGGL(maxpool_bn_bwd_reduce_pooled, dim3(gp.gx, gp.gy), dim3(kThreads), lds, st, (const bf16_t*)dy,
-                       (const bf16_t*)y, arg, (const bf16_t*)x, ss, ss + C, g, gp.tpr, gp.rg, p0, p1);
+                       (const bf16_t*)y, arg, (const bf16_t*)x, ss, ss + C, invstd, g, gp.tpr, gp.rg, p0, p1);
   } else if (rows_path) {
     int cvs = 0;
     while ((1 << cvs) < cv) ++cvs;

@@ -488,9 +488,17 @@ class AsyncWorker(object):
         last = None
         import os
         bench_warmup = int(os.environ.get("MDTF_BENCH_WARMUP", "0"))
-        # fault injection for tests: MDTF_STRAGGLER=worker:<task>:<seconds> makes that worker sleep every step
+        # fault injection for tests: MDTF_STRAGGLER=worker:<task>:<seconds> makes that worker sleep every step;
+        # worker:<task>:x<k> sleeps k times its own forward/backward time of the step (slower by a factor k + 1
+        # whatever the machine's load, so a test's "late" does not depend on how busy the host is)
         slow = os.environ.get("MDTF_STRAGGLER", "").split(":")
-        delay = float(slow[2]) if len(slow) == 3 and slow[0] == "worker" and int(slow[1]) == self.op.task_index else 0.0
+        mine = len(slow) == 3 and slow[0] == "worker" and int(slow[1]) == self.op.task_index
+        delay, delay_x = 0.0, 0.0
+        if mine:
+            if slow[2].startswith("x"):
+                delay_x = float(slow[2][1:])
+            else:
+                delay = float(slow[2])
         t_bench = None
         pending = None                    # (push send requests, reply receive requests) of the previous step
         step = 0
@@ -506,10 +514,15 @@ class AsyncWorker(object):
                 v.uses = 0
             self.space.zero_grad()
             # forward/backward of this step overlaps the previous push and its reply (into staging)
+            t_fb = time.time()
             out = loss_h.forward(ctx, grad=True)
             out["loss"].backward()
             if delay:
                 time.sleep(delay)
+            elif delay_x:
+                if V.get_store().device.type == "cuda":
+                    torch.cuda.synchronize()
+                time.sleep(delay_x * (time.time() - t_fb))
             from ..ops import conv as _conv
             _conv.join_side_streams()
             used = list(self.version)         # the weights this gradient was computed on

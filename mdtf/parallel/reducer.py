@@ -107,6 +107,22 @@ class _NullCtx(object):
         return False
 
 
+def group_is_single_host(pg=None):
+    """True when every rank of ``pg`` runs on this host.  Decided by exchanging host names over the group (a
+    collective: every rank of ``pg`` calls it), not from torchrun's LOCAL_WORLD_SIZE / WORLD_SIZE, which the
+    ClusterSpec launcher does not set: a multi-host group must never take the device-clock backup path, whose
+    clocks are calibrated against one host's monotonic clock."""
+    import socket
+    if not (dist.is_available() and dist.is_initialized()):
+        return True
+    world = dist.get_world_size(pg)
+    if world == 1:
+        return True
+    names = [None] * world
+    dist.all_gather_object(names, socket.gethostname(), group=pg)
+    return len(set(names)) == 1
+
+
 class GradReducer(object):
     def __init__(self, space, process_group=None, mode="allreduce", overlap=True,
                  replicas_to_aggregate=None, store=None, comm_dtype=None):
@@ -138,10 +154,9 @@ class GradReducer(object):
         # backup workers decided on the device (GPU replicas): see the module docstring
         # device clocks are calibrated against ONE host clock, so only for a single-node group; multi-node
         # groups take the store ticket
-        single_node = int(os.environ.get("LOCAL_WORLD_SIZE", self.world)) >= int(
-            os.environ.get("WORLD_SIZE", self.world))
         self.backup_device = (self.world > 1 and self.R < self.world and space.device is not None
-                              and torch.device(space.device).type == "cuda" and single_node)
+                              and torch.device(space.device).type == "cuda"
+                              and group_is_single_host(process_group))
         self._bk = None
         if mode not in ("allreduce", "sharded"):
             raise ValueError("mode must be 'allreduce' or 'sharded'")
@@ -323,12 +338,26 @@ class GradReducer(object):
         against the (shared) host clock: offset = device_ns - host_ns, all-gathered."""
         if self._bk is not None:
             return self._bk
-        import time
         from ..ops import _native as N
         N.register("mdtf_stamp_realtime", [N.P, N.P])
         N.register("mdtf_backup_mask", [N.P, N.P, N.I, N.I, N.I, N.P, N.P])
         dev = torch.device(self.space.device)
         stamp = torch.zeros(1, dtype=torch.int64, device=dev)
+        offsets = torch.zeros(self.world, dtype=torch.int64, device=dev)
+        self._bk = {"stamp": stamp, "stamps": torch.zeros(self.world, dtype=torch.int64, device=dev),
+                    "offsets": offsets, "mask": torch.ones(1, dtype=torch.float32, device=dev)}
+        self._measure_clock_offsets()
+        return self._bk
+
+    def _measure_clock_offsets(self):
+        """(Re)measure every replica's device-clock origin into the existing ``offsets`` buffer, in place, so a
+        captured step graph that reads it sees the new values.  A collective over the group, host-synchronous:
+        never called while a hipGraph is being captured."""
+        import time
+        from ..ops import _native as N
+        bk = self._bk
+        dev = torch.device(self.space.device)
+        stamp = bk["stamp"]
         best = None
         for _ in range(5):                  # the tightest of a few host brackets around one device stamp
             torch.cuda.synchronize(dev)
@@ -339,20 +368,39 @@ class GradReducer(object):
             if best is None or t1 - t0 < best[0]:
                 best = (t1 - t0, int(stamp.item()) * 10 - (t0 + t1) // 2)
         off = torch.tensor([best[1]], dtype=torch.int64, device=dev)
-        offsets = torch.zeros(self.world, dtype=torch.int64, device=dev)
-        dist.all_gather(list(offsets.view(self.world, 1).unbind(0)), off, group=self.pg)
-        self._bk = {"stamp": stamp, "stamps": torch.zeros(self.world, dtype=torch.int64, device=dev),
-                    "offsets": offsets, "mask": torch.ones(1, dtype=torch.float32, device=dev)}
-        return self._bk
+        gathered = torch.zeros(self.world, dtype=torch.int64, device=dev)
+        dist.all_gather(list(gathered.view(self.world, 1).unbind(0)), off, group=self.pg)
+        bk["offsets"].copy_(gathered)
+        torch.cuda.synchronize(dev)
+        bk["at"] = None                         # set by the next step that uses the offsets
 
     BACKUP_RECALIBRATE_STEPS = 1000      # device-clock offsets re-measured this often (refclk drift)
 
+    def refresh_backup_clock(self, step):
+        """Host-side, between steps (also between hipGraph replays, which run no Python of the step): re-measure
+        the clock offsets every BACKUP_RECALIBRATE_STEPS global steps.  Every replica reaches the same global step,
+        so the collective re-measure is matched.  A step counter that went BACK (a restore after a recovery)
+        restarts the period."""
+        bk = self._bk
+        if bk is None or not self.backup_device:
+            return False
+        at = bk.get("at")
+        if at is None or step < at:
+            bk["at"] = step
+            return False
+        if step - at < self.BACKUP_RECALIBRATE_STEPS:
+            return False
+        self._measure_clock_offsets()
+        bk["at"] = step
+        return True
+
     def _backup_mask_device(self, step=0):
         from ..ops import _native as N
-        if self._bk is not None and step - self._bk.get("at", step) >= self.BACKUP_RECALIBRATE_STEPS:
-            self._bk = None                     # every rank reaches the same global step: a collective re-measure
+        if not torch.cuda.is_current_stream_capturing():
+            self.refresh_backup_clock(step)     # never inside a capture (host syncs and a collective)
         bk = self._backup_buffers()
-        bk.setdefault("at", step)
+        if bk.get("at") is None:
+            bk["at"] = step
         N.check(N.fn("mdtf_stamp_realtime")(N.ptr(bk["stamp"]), N.stream_ptr()), "stamp_realtime")
         dist.all_gather(list(bk["stamps"].view(self.world, 1).unbind(0)), bk["stamp"], group=self.pg)
         N.check(N.fn("mdtf_backup_mask")(N.ptr(bk["stamps"]), N.ptr(bk["offsets"]), self.world, self.rank, self.R,

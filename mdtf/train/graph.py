@@ -253,6 +253,8 @@ class StepGraph(object):
             self.fallbacks += 1
             return self.op._run_step(ctx, step)
         self._set_dyn(step)
+        if self.op.reducer.backup_device:
+            self.op.reducer.refresh_backup_clock(step)      # host-side, between replays (offsets updated in place)
         self.graph.replay()
         self.replays += 1
         for p in self.op.programs:

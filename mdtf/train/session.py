@@ -390,6 +390,11 @@ class MonitoredSession(Session):
                 # async: the step ran (its collectives are matched on every replica); the peers stop at the next
                 # boundary when they read code 2.  This replica stops now.
                 raise fatal
+            if rc is None:
+                # async: a hook raised a recoverable error in before_run.  The step ran so the peers' collectives
+                # are matched; this replica has no run context for it, so its after_run hooks are skipped, and the
+                # posted RECOVER code re-creates every replica together at the next boundary.
+                return results["__user__"]
             try:
                 self._after_run(rc, extra, results)
             except Exception as e:  # noqa: BLE001 - classified below

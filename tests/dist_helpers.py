@@ -266,3 +266,21 @@ def backup_gpu_worker(rank, world, port, steps, out_dir, replicas):
     with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
         json.dump({"weights": w, "contributed": contributed, "device_mask": bool(op.reducer.backup_device)}, f)
     _teardown(server)
+
+
+def host_check_worker(rank, world, port, out_dir, fake_hosts):
+    """group_is_single_host over a gloo group: real host names (one host) or faked per-rank host names (a
+    ClusterSpec job spread over two hosts, where LOCAL_WORLD_SIZE / WORLD_SIZE are not set)."""
+    import socket
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for k in ("LOCAL_WORLD_SIZE", "WORLD_SIZE"):
+        os.environ.pop(k, None)
+    dist.init_process_group("gloo", rank=rank, world_size=world, init_method="tcp://127.0.0.1:%d" % port)
+    if fake_hosts:
+        socket.gethostname = lambda: "host%d" % (rank % 2)
+    from mdtf.parallel.reducer import group_is_single_host
+    res = group_is_single_host(None)
+    with open(os.path.join(out_dir, "host%d.json" % rank), "w") as f:
+        json.dump({"single": res}, f)
+    dist.destroy_process_group()

@@ -58,3 +58,28 @@ def test_done_queue_barrier_waits_for_all_workers():
     client.add("mdtf/done_queue0", 1)
     t.join(10)
     assert got == [True]
+
+
+def test_backup_clock_refresh_is_host_side_and_restarts_after_restore():
+    """The device-clock offsets of the GPU backup-worker path are re-measured on the host between steps (also
+    between hipGraph replays), every BACKUP_RECALIBRATE_STEPS global steps; a global step that went back (a
+    restore after a recovery) restarts the period instead of re-measuring inside the next capture."""
+    from mdtf.parallel.reducer import GradReducer
+
+    class Fake(object):
+        BACKUP_RECALIBRATE_STEPS = 10
+        backup_device = True
+        measured = 0
+
+        def _measure_clock_offsets(self):
+            self.measured += 1
+
+    f = Fake()
+    f._bk = {"at": None}
+    refresh = GradReducer.refresh_backup_clock
+    assert refresh(f, 5) is False and f._bk["at"] == 5          # first use sets the period origin
+    assert refresh(f, 14) is False and f.measured == 0
+    assert refresh(f, 15) is True and f.measured == 1 and f._bk["at"] == 15
+    assert refresh(f, 3) is False and f._bk["at"] == 3           # restored to an earlier step: restart
+    assert refresh(f, 12) is False and f.measured == 1
+    assert refresh(f, 13) is True and f.measured == 2

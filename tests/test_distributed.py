@@ -89,14 +89,14 @@ def test_localhost_ps_worker_cluster_and_resume(tmp_path):
     md = str(tmp_path / "model")
     script = os.path.join(ROOT, "distribute.py")
     codes = launch_local_cluster([script, "--model_dir=%s" % md, "--epochs=1"], num_ps=1, num_workers=1,
-                                 timeout_s=300)
+                                 timeout_s=900)
     assert codes == [0, 0]
     from mdtf.train.saver import latest_checkpoint
     ck = latest_checkpoint(md)
     assert ck and ck.endswith("model.ckpt-100")
     # resume: epochs=2 -> continues from step 100 to 200
     codes = launch_local_cluster([script, "--model_dir=%s" % md, "--epochs=2"], num_ps=1, num_workers=1,
-                                 timeout_s=300)
+                                 timeout_s=900)
     assert codes == [0, 0]
     assert latest_checkpoint(md).endswith("model.ckpt-200")
     from mdtf.ckpt.tensor_bundle import BundleReader
@@ -109,18 +109,18 @@ def test_two_workers_one_ps_sharded(tmp_path):
     md = str(tmp_path / "model2")
     script = os.path.join(ROOT, "distribute.py")
     codes = launch_local_cluster([script, "--model_dir=%s" % md, "--epochs=1"], num_ps=1, num_workers=2,
-                                 timeout_s=300)
+                                 timeout_s=900)
     assert codes == [0, 0, 0]
 
 
 def test_eval_mode_restores_checkpoint(tmp_path):
     md = str(tmp_path / "model3")
     script = os.path.join(ROOT, "distribute.py")
-    assert launch_local_cluster([script, "--model_dir=%s" % md, "--epochs=1"], 1, 1, timeout_s=300) == [0, 0]
+    assert launch_local_cluster([script, "--model_dir=%s" % md, "--epochs=1"], 1, 1, timeout_s=900) == [0, 0]
     port = free_port()
     out = subprocess.run([sys.executable, script, "--job_name=worker", "--task_index=0", "--mode=Eval",
                           "--worker_hosts=127.0.0.1:%d" % port, "--ps_hosts=none", "--model_dir=%s" % md],
-                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=900)
     assert out.returncode == 0, out.stdout[-3000:]
     assert "Eval: {" in out.stdout and "model.ckpt-100" in out.stdout
 
@@ -130,7 +130,7 @@ def test_async_ps_two_ps_two_workers(tmp_path):
     md = str(tmp_path / "async")
     script = os.path.join(ROOT, "distribute.py")
     codes = launch_local_cluster([script, "--model_dir=%s" % md, "--ps_mode=async"], num_ps=2, num_workers=2,
-                                 timeout_s=300)
+                                 timeout_s=900)
     assert codes == [0, 0, 0, 0]
     from mdtf.ckpt.tensor_bundle import BundleReader
     from mdtf.train.saver import latest_checkpoint
@@ -144,15 +144,16 @@ def test_async_ps_two_ps_two_workers(tmp_path):
 
 def test_sync_ps_backup_workers_do_not_wait_for_a_straggler(tmp_path):
     """ps_mode=sync_ps, 3 workers, replicas_to_aggregate=2 (distribute_train.py:146-160): each PS version is the
-    mean of the first 2 pushes computed on it; worker 2 sleeps 0.3 s per step, so its pushes are mostly late and
-    dropped, and the two fast workers reach the last step without waiting for it (latency hiding)."""
+    mean of the first 2 pushes computed on it; worker 2 sleeps 4x its own forward/backward time per step (5x
+    slower whatever the host's load), so its pushes are mostly late and dropped, and the two fast workers reach the
+    last step without waiting for it (latency hiding)."""
     md = str(tmp_path / "syncps")
     out = str(tmp_path / "stats")
     os.makedirs(out)
     script = os.path.join(ROOT, "distribute.py")
     codes = launch_local_cluster([script, "--model_dir=%s" % md, "--ps_mode=sync_ps", "--replicas_to_aggregate=2"],
-                                 num_ps=1, num_workers=3, timeout_s=400,
-                                 extra_env={"MDTF_STRAGGLER": "worker:2:0.3", "MDTF_BENCH_OUT": out})
+                                 num_ps=1, num_workers=3, timeout_s=900,
+                                 extra_env={"MDTF_STRAGGLER": "worker:2:x4", "MDTF_BENCH_OUT": out})
     assert codes == [0, 0, 0, 0]
     ps = json.load(open(os.path.join(out, "ps0.json")))
     assert ps["mode"] == "sync_ps R=2" and ps["batched_max"] == 2
@@ -322,6 +323,30 @@ def test_coordinated_recovery_error_inside_the_step(tmp_path):
             assert torch.allclose(torch.tensor(r["weights"][k]), torch.tensor(w), atol=1e-6), k
 
 
+def test_coordinated_recovery_hook_error_in_before_run_async(tmp_path):
+    """ONE of two replicas' hooks raises a RECOVERABLE AbortedError from before_run under the async agreement
+    (``MDTF_AGREE=async``).  The step it posted the code with still runs on both replicas (no run context, so its
+    after_run hooks are skipped), every replica reads RECOVER at the next boundary, restores the chief's
+    checkpoint in process and finishes at the same global step with the weights of an uninterrupted run
+    (reference distribute_train.py:169-180)."""
+    sys.path.insert(0, os.path.dirname(__file__))
+    import dist_helpers
+    res = {}
+    for tag, fault in (("ref", None), ("run", 5)):
+        d = tmp_path / tag
+        d.mkdir()
+        mp.start_processes(dist_helpers.recovery_worker, args=(2, free_port(), 8, str(d), fault, "worker:1",
+                                                               "abort_before_run", "async"),
+                           nprocs=2, join=True, start_method="spawn")
+        res[tag] = [json.load(open(str(d / ("rank%d.json" % r)))) for r in range(2)]
+    ref, run = res["ref"], res["run"]
+    assert [r["step"] for r in run] == [8, 8] and [r["recoveries"] for r in run] == [1, 1]
+    assert [r["agreements"] for r in run] == [run[0]["agreements"]] * 2
+    for k, w in ref[0]["weights"].items():
+        for r in run:
+            assert torch.allclose(torch.tensor(r["weights"][k]), torch.tensor(w), atol=1e-6), k
+
+
 def test_fatal_hook_error_stops_every_replica(tmp_path):
     """A non-recoverable error in one replica's before_run still joins the step-boundary agreement: the peer
     stops at that boundary with an error instead of waiting in the next step's collectives."""
@@ -335,3 +360,16 @@ def test_fatal_hook_error_stops_every_replica(tmp_path):
     assert out[1]["error"].startswith("ValueError") and "bug in a hook" in out[1]["error"]
     assert out[0]["error"].startswith("RuntimeError") and "non-recoverable" in out[0]["error"]
     assert out[0]["step"] == out[1]["step"] == 4        # async agreement: the posted step still ran everywhere
+
+
+@pytest.mark.parametrize("fake", [False, True])
+def test_backup_device_path_only_on_one_host(tmp_path, fake):
+    """The device-clock backup-worker path (clocks calibrated against one host's monotonic clock) is taken only
+    when every rank of the group is on one host; that is decided from the ranks' host names, not from torchrun's
+    env, which the ClusterSpec launcher does not set (reference distribute.py:37-38: workers on several hosts)."""
+    sys.path.insert(0, os.path.dirname(__file__))
+    import dist_helpers
+    mp.start_processes(dist_helpers.host_check_worker, args=(2, free_port(), str(tmp_path), fake), nprocs=2,
+                       join=True, start_method="spawn")
+    out = [json.load(open(str(tmp_path / ("host%d.json" % r))))["single"] for r in range(2)]
+    assert out == [not fake, not fake]

@@ -540,19 +540,23 @@ def test_bert_embeddings_fused_vs_fp32(monkeypatch):
         assert _rel(a, r) < 2e-2
 
 
-@pytest.mark.parametrize("zero_gamma", [False, True])
+@pytest.mark.parametrize("zero_gamma", [False, True, "tiny"])
 def test_stem_bn_backward_statistics_from_pooled_tensors(zero_gamma, monkeypatch):
     """The fused stem's BN backward statistics from the pooled tensors (csrc/bn.hip maxpool_bn_bwd_reduce_pooled:
-    x recovered from the pooled y at each window's argmax; channels with gamma == 0 gather x instead) == the
-    input-row pass over x: filter / gamma / beta gradients."""
+    x recovered from the pooled y at each window's argmax; channels with gamma == 0, or a gamma so small beside a
+    large beta that bf16 y cannot give x back, gather x instead) == the input-row pass over x: filter / gamma /
+    beta gradients."""
     from mdtf.ops import bn as B
     torch.manual_seed(14)
     x = torch.randn(8, 38, 38, 3)
     w = torch.randn(7, 7, 3, 64) * (1.0 / 147 ** 0.5)
     g = torch.rand(64) + 0.5
-    if zero_gamma:
-        g[::7] = 0.0
     b = torch.randn(64) * 0.2
+    if zero_gamma == "tiny":
+        g[::5] = 1e-3              # |shift / scale| ~ 3000 std: bf16 y rounding would swamp x
+        b[::5] = 3.0
+    elif zero_gamma:
+        g[::7] = 0.0
     dy0 = torch.randn(8, 10, 10, 64, generator=torch.Generator().manual_seed(5))
     outs = {}
     monkeypatch.setattr(B, "FUSED_STEM", True)
