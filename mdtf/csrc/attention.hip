@@ -667,7 +667,404 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_v2(const bf16_t* __restrict__
   }
 }
 
+// ============================================================================ persistent forms (round 5)
+// The kernels above give each (batch, head) item its own workgroup: every workgroup pays one HBM load latency,
+// computes for ~1 us, then stores, so the chip streams at about half the HBM rate (attn_fwd 20 us for 50 MB,
+// attn_bwd_v2 39 us for 100 MB at BERT-base batch 64; 768 items on 512 backward slots also leave a half wave).
+// The persistent forms run ONE workgroup per CU that walks items bh = blockIdx.x, + gridDim.x, ...: the operands
+// of item i+1 go to the other half of a double-buffered LDS by LDS-DMA while item i computes, and item i's stores
+// drain under item i+1's loads.  The DMA is inline asm (invisible to the compiler, so it adds no vmcnt(0) in
+// front of the LDS reads); every wave waits for its own DMA with a counted vmcnt that leaves only the previous
+// item's stores (the youngest vector-memory operations) in flight, and an s_barrier then makes every wave's DMA
+// visible and frees the other buffer.  Numerics and dropout bits are those of the per-item kernels.
+constexpr int kImg = S * D * 2;                 // one [128][64] bf16 head slice
+constexpr int kFwdBuf = 3 * kImg + 1024;        // Q | K | V | key mask (512 B used)
+constexpr int kFwdPpLds = 2 * kFwdBuf;
+constexpr int kFwdPpStores = 5;                 // per wave and item: 4 context stores + 1 logsumexp store
+constexpr unsigned kOOBoff = 0x80000000u;
+
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// 8 waves, wave w = queries 16w .. 16w+15 of the item
+__global__ void __launch_bounds__(512) attn_fwd_pp(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+                                                   bf16_t* __restrict__ out, float* __restrict__ lse_out, int B,
+                                                   int nh, float scale, float p_drop, uint32_t seed,
+                                                   const long long* __restrict__ seed_off) {
+  seed = step_seed(seed, seed_off);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int H = nh * D, ld = 3 * H;
+  const int nitems = B * nh;
+  const i32x4_t rq = buffer_rsrc(qkv, (int)((long long)B * S * ld * 2));
+  const i32x4_t rm = buffer_rsrc(mask, mask ? B * S * 4 : 0);
+  const bool has_mask = mask != nullptr;
+
+  // this wave's share of item bh's loads: 1-KiB blocks j = wave, wave + 8 of Q, K (row-read swizzle) and V
+  // (transposed-read swizzle); the key mask (512 B) by wave 0
+  auto issue = [&](int bh, char* buf) {
+    const int b = bh / nh, h = bh - b * nh;
+    const long long row0 = (long long)b * S * ld;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = wave + 8 * jj;
+      const int r = 8 * j + (lane >> 3);
+      const unsigned base = (unsigned)((row0 + (long long)r * ld + h * D) * 2);
+      dma16_asm(rq, buf + j * 1024, base + (SwzA::f(r, lane & 7) << 4));
+      dma16_asm(rq, buf + kImg + j * 1024, base + H * 2 + (SwzA::f(r, lane & 7) << 4));
+      dma16_asm(rq, buf + 2 * kImg + j * 1024, base + H * 4 + (SwzV::f(r, lane & 7) << 4));
+    }
+    if (wave == 0 && has_mask) dma16_asm(rm, buf + 3 * kImg, lane < 32 ? (unsigned)(b * S * 4 + lane * 16) : kOOBoff);
+  };
+
+  const uint32_t thr = p_drop > 0.f ? (uint32_t)fminf(p_drop * 4294967296.f, 4294967295.f) : 0u;
+  const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const int q = 16 * wave + li;                  // this lane's query (column of S^T / O^T)
+  int bh = blockIdx.x;
+  if (bh < nitems) issue(bh, smem);
+  for (int it = 0; bh < nitems; ++it, bh += gridDim.x) {
+    // this wave's DMA of item bh landed (only the previous item's stores are younger), then every wave's
+    if (it == 0) wait_vmcnt<0>();
+    else wait_vmcnt<kFwdPpStores>();
+    pp_barrier();
+    char* buf = smem + (it & 1) * kFwdBuf;
+    if (bh + (int)gridDim.x < nitems) issue(bh + gridDim.x, smem + ((it + 1) & 1) * kFwdBuf);
+    const char* Qimg = buf;
+    const char* Kimg = buf + kImg;
+    const char* Vimg = buf + 2 * kImg;
+    const float* Mimg = reinterpret_cast<const float*>(buf + 3 * kImg);
+    const int b = bh / nh, h = bh - b * nh;
+
+    bf16x8_t qf[2];
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) qf[ds] = row_frag<SwzA>(Qimg, 16 * wave, 4 * ds, lane);
+    // S^T[k][q] = K Q^T
+    float4v sacc[8];
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) sacc[kt] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds)
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt) sacc[kt] = mfma(row_frag<SwzA>(Kimg, kt * 16, 4 * ds, lane), qf[ds], sacc[kt]);
+    // softmax over keys (scale, additive key mask), dropout, logsumexp
+    float m = -3.0e38f;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      const float4 m4 = has_mask ? *reinterpret_cast<const float4*>(Mimg + kt * 16 + 4 * g) : make_float4(0, 0, 0, 0);
+      const float mk[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float s = sacc[kt][i] * scale + mk[i];
+        sacc[kt][i] = s;
+        m = fmaxf(m, s);
+      }
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = __expf(sacc[kt][i] - m);
+        sacc[kt][i] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float p = sacc[kt][i] * inv;
+        if (thr) p = keep_elem(seed, bh, q, kt * 16 + 4 * g + i, thr) ? p * inv_keep : 0.f;
+        sacc[kt][i] = p;
+      }
+    // O^T[d][q] = V^T P^T (key order inside each 32-key step: {4g..4g+3, 16+4g..16+4g+3})
+    float4v oacc[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oacc[dt] = float4v{0.f, 0.f, 0.f, 0.f};
+    const int q4 = li >> 2, p4 = li & 3;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const float4v a0 = sacc[2 * ks], a1 = sacc[2 * ks + 1];
+      const bf16x8_t pf = __builtin_bit_cast(
+          bf16x8_t, make_uint4(pack2(a0[0], a0[1]), pack2(a0[2], a0[3]), pack2(a1[0], a1[1]), pack2(a1[2], a1[3])));
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        v4s lo = tr4<SwzV, 128>(Vimg, 32 * ks + 4 * g + q4, dt * 16 + 4 * p4);
+        v4s hi = tr4<SwzV, 128>(Vimg, 32 * ks + 16 + 4 * g + q4, dt * 16 + 4 * p4);
+        short8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        oacc[dt] = mfma(__builtin_bit_cast(bf16x8_t, f), pf, oacc[dt]);
+      }
+    }
+    // stores (kFwdPpStores vector-memory instructions per wave): logsumexp, then 4 x 8 B of context per lane
+    lse_out[(long long)bh * S + q] = m + __logf(sum);      // (every lane: lanes of one query store equal values)
+    bf16_t* o = out + ((long long)b * S + q) * H + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const float4v v = oacc[dt];
+      *reinterpret_cast<uint2*>(o + dt * 16 + 4 * g) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
+  }
+}
+
+// Backward: 16 waves.  Waves 0-7 = phase A of attn_bwd_v2 for keys 16w .. 16w+15 (dK, dV), waves 8-15 = its
+// phase B for queries 16(w-8) .. +15 (dQ), side by side instead of one after the other.  Per item: Q, K, V, dO
+// images (SwzV), logsumexp and key mask by LDS-DMA into a double buffer; D = rowsum(dO * O) from O (one more
+// LDS-DMA image, single-buffered: every wave reads back only the 1-KiB block its own lanes loaded, before it
+// issues the next item's block) and dO, published through a small LDS vector behind a second barrier.
+constexpr int kBwdBuf = 4 * kImg + 2048;        // Q | K | V | dO | lse (512 B used) | key mask (512 B used)
+constexpr int kBwdPpLds = 2 * kBwdBuf + kImg + S * 4;  // + O + D
+constexpr int kBwdStoresA = 8, kBwdStoresB = 4;
+
+__global__ void __launch_bounds__(1024) attn_bwd_pp(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+                                                    const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
+                                                    const float* __restrict__ lse, bf16_t* __restrict__ dqkv, int B,
+                                                    int nh, float scale, float p_drop, uint32_t seed,
+                                                    const long long* __restrict__ seed_off) {
+  seed = step_seed(seed, seed_off);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Obuf = smem + 2 * kBwdBuf;
+  float* DVs = reinterpret_cast<float*>(Obuf + kImg);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool phaseA = wave < 8;
+  const int g = lane >> 4, li = lane & 15;
+  const int H = nh * D, ld = 3 * H;
+  const int nitems = B * nh;
+  const i32x4_t rq = buffer_rsrc(qkv, (int)((long long)B * S * ld * 2));
+  const i32x4_t ro = buffer_rsrc(dout, (int)((long long)B * S * H * 2));
+  const i32x4_t rO = buffer_rsrc(out, (int)((long long)B * S * H * 2));
+  const i32x4_t rl = buffer_rsrc(lse, nitems * S * 4);
+  const i32x4_t rm = buffer_rsrc(mask, mask ? B * S * 4 : 0);
+  const bool has_mask = mask != nullptr;
+
+  // 64 1-KiB blocks (Q, K, V, dO; block j = 8-row block j & 15 of image j >> 4): wave w issues j = w + 16 t;
+  // + block w of O (linear layout: lane l holds row 8w + l / 8, columns 8 (l & 7) .. +7)
+  auto issue = [&](int bh, char* buf) {
+    const int b = bh / nh, h = bh - b * nh;
+    const long long row0 = (long long)b * S * ld, orow0 = (long long)b * S * H;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = wave + 16 * t;
+      const int img = j >> 4, rb = j & 15;
+      const int r = 8 * rb + (lane >> 3);
+      const int c = SwzV::f(r, lane & 7);
+      if (img < 3)
+        dma16_asm(rq, buf + img * kImg + rb * 1024,
+                  (unsigned)((row0 + (long long)r * ld + img * H + h * D + c * 8) * 2));
+      else
+        dma16_asm(ro, buf + 3 * kImg + rb * 1024, (unsigned)((orow0 + (long long)r * H + h * D + c * 8) * 2));
+    }
+    dma16_asm(rO, Obuf + wave * 1024,
+              (unsigned)((orow0 + (long long)(8 * wave + (lane >> 3)) * H + h * D + (lane & 7) * 8) * 2));
+    if (wave == 0) dma16_asm(rl, buf + 4 * kImg, lane < 32 ? (unsigned)(bh * S * 4 + lane * 16) : kOOBoff);
+    if (wave == 1 && has_mask)
+      dma16_asm(rm, buf + 4 * kImg + 1024, lane < 32 ? (unsigned)(b * S * 4 + lane * 16) : kOOBoff);
+  };
+  const int drow = 8 * wave + (lane >> 3), dc = lane & 7;
+
+  const uint32_t thr = p_drop > 0.f ? (uint32_t)fminf(p_drop * 4294967296.f, 4294967295.f) : 0u;
+  const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const int q4 = li >> 2, p4 = li & 3;
+  const int r = 16 * (wave & 7) + li;            // phase A: this lane's key; phase B: its query
+  int bh = blockIdx.x;
+  if (bh < nitems) issue(bh, smem);
+  for (int it = 0; bh < nitems; ++it, bh += gridDim.x) {
+    if (it == 0) wait_vmcnt<0>();
+    else if (phaseA) wait_vmcnt<kBwdStoresA>();
+    else wait_vmcnt<kBwdStoresB>();
+    pp_barrier();
+    const char* buf = smem + (it & 1) * kBwdBuf;
+    const char* OI = buf + 3 * kImg;             // dO
+    // D = rowsum(dO * O): 8 lanes per query row; O from this lane's own DMA slot (read before it is refilled)
+    float part = 0.f;
+    {
+      const uint4 ov = *reinterpret_cast<const uint4*>(Obuf + wave * 1024 + lane * 16);
+      const uint4 dv = *reinterpret_cast<const uint4*>(OI + drow * 128 + (SwzV::f(drow, dc) << 4));
+      const uint32_t ow[4] = {ov.x, ov.y, ov.z, ov.w}, dw[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        part += __uint_as_float(ow[e] << 16) * __uint_as_float(dw[e] << 16) +
+                __uint_as_float(ow[e] & 0xffff0000u) * __uint_as_float(dw[e] & 0xffff0000u);
+      part += __shfl_xor(part, 1, 64);
+      part += __shfl_xor(part, 2, 64);
+      part += __shfl_xor(part, 4, 64);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // the O slot has been read: it may be refilled
+    const int nb = bh + gridDim.x;
+    if (nb < nitems) issue(nb, smem + ((it + 1) & 1) * kBwdBuf);
+    if (dc == 0) DVs[drow] = part;
+    // raw barrier: a __syncthreads() fence would drain vmcnt, i.e. wait for the next item's DMA just issued
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_barrier();
+    const char* QI = buf;
+    const char* KI = buf + kImg;
+    const char* VI = buf + 2 * kImg;
+    const float* LS = reinterpret_cast<const float*>(buf + 4 * kImg);
+    const float* MK = reinterpret_cast<const float*>(buf + 4 * kImg + 1024);
+    const int b = bh / nh, h = bh - b * nh;
+    bf16x8_t rf0[2], rf1[2];                     // A: this wave's K / V rows; B: its Q / dO rows
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) {
+      rf0[ds] = row_frag<SwzV>(phaseA ? KI : QI, 16 * (wave & 7), 4 * ds, lane);
+      rf1[ds] = row_frag<SwzV>(phaseA ? VI : OI, 16 * (wave & 7), 4 * ds, lane);
+    }
+    bf16_t* rowp = dqkv + ((long long)b * S + r) * ld + h * D;
+    if (phaseA) {
+      // keys r (lane column): dV^T[d][k] = dO^T P, dK^T[d][k] = Q^T dS over all queries
+      const float mr = has_mask ? MK[r] : 0.f;
+      float4v dvacc[4], dkacc[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dvacc[dt] = dkacc[dt] = float4v{0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < 4; ++s) {                     // queries 32s .. 32s+31
+        float4v sc[2], dp[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) sc[t] = dp[t] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ds = 0; ds < 2; ++ds)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            sc[t] = mfma(row_frag<SwzV>(QI, 32 * s + 16 * t, 4 * ds, lane), rf0[ds], sc[t]);
+            dp[t] = mfma(row_frag<SwzV>(OI, 32 * s + 16 * t, 4 * ds, lane), rf1[ds], dp[t]);
+          }
+        float pv[8], sv[8];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int q0 = 32 * s + 16 * t + 4 * g;       // this lane's 4 queries of the tile
+          const float4 l4 = *reinterpret_cast<const float4*>(LS + q0);
+          const float4 d4 = *reinterpret_cast<const float4*>(DVs + q0);
+          const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = __expf(sc[t][i] * scale + mr - lv[i]);
+            float dpv = dp[t][i], pk = p;
+            if (thr) {
+              const bool keep = keep_elem(seed, bh, q0 + i, r, thr);
+              pk = keep ? p * inv_keep : 0.f;
+              dpv = keep ? dpv * inv_keep : 0.f;
+            }
+            pv[4 * t + i] = pk;
+            sv[4 * t + i] = p * (dpv - dv[i]);
+          }
+        }
+        const bf16x8_t pf = __builtin_bit_cast(bf16x8_t, make_uint4(pack2(pv[0], pv[1]), pack2(pv[2], pv[3]),
+                                                                    pack2(pv[4], pv[5]), pack2(pv[6], pv[7])));
+        const bf16x8_t sf = __builtin_bit_cast(bf16x8_t, make_uint4(pack2(sv[0], sv[1]), pack2(sv[2], sv[3]),
+                                                                    pack2(sv[4], sv[5]), pack2(sv[6], sv[7])));
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          v4s lo = tr4<SwzV, 128>(OI, 32 * s + 4 * g + q4, dt * 16 + 4 * p4);
+          v4s hi = tr4<SwzV, 128>(OI, 32 * s + 16 + 4 * g + q4, dt * 16 + 4 * p4);
+          short8 fo = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          dvacc[dt] = mfma(__builtin_bit_cast(bf16x8_t, fo), pf, dvacc[dt]);
+          lo = tr4<SwzV, 128>(QI, 32 * s + 4 * g + q4, dt * 16 + 4 * p4);
+          hi = tr4<SwzV, 128>(QI, 32 * s + 16 + 4 * g + q4, dt * 16 + 4 * p4);
+          short8 fq = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          dkacc[dt] = mfma(__builtin_bit_cast(bf16x8_t, fq), sf, dkacc[dt]);
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const float4v kv = dkacc[dt], vv = dvacc[dt];
+        *reinterpret_cast<uint2*>(rowp + H + dt * 16 + 4 * g) =
+            make_uint2(pack2(kv[0] * scale, kv[1] * scale), pack2(kv[2] * scale, kv[3] * scale));
+        *reinterpret_cast<uint2*>(rowp + 2 * H + dt * 16 + 4 * g) =
+            make_uint2(pack2(vv[0], vv[1]), pack2(vv[2], vv[3]));
+      }
+    } else {
+      // query r (lane column): dQ^T[d][q] = K^T dS^T over all keys
+      const float lq = LS[r], part = DVs[r];
+      float4v qacc[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) qacc[dt] = float4v{0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < 4; ++ks) {                  // keys 32ks .. 32ks+31
+        float4v sc[2], dp[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) sc[t] = dp[t] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ds = 0; ds < 2; ++ds)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            sc[t] = mfma(row_frag<SwzV>(KI, 32 * ks + 16 * t, 4 * ds, lane), rf0[ds], sc[t]);
+            dp[t] = mfma(row_frag<SwzV>(VI, 32 * ks + 16 * t, 4 * ds, lane), rf1[ds], dp[t]);
+          }
+        float sv[8];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int k0 = 32 * ks + 16 * t + 4 * g;       // this lane's 4 keys of the tile
+          const float4 m4 = has_mask ? *reinterpret_cast<const float4*>(MK + k0) : make_float4(0, 0, 0, 0);
+          const float mv[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = __expf(sc[t][i] * scale + mv[i] - lq);
+            float dpv = dp[t][i];
+            if (thr) dpv = keep_elem(seed, bh, r, k0 + i, thr) ? dpv * inv_keep : 0.f;
+            sv[4 * t + i] = p * (dpv - part);
+          }
+        }
+        const bf16x8_t sf = __builtin_bit_cast(bf16x8_t, make_uint4(pack2(sv[0], sv[1]), pack2(sv[2], sv[3]),
+                                                                    pack2(sv[4], sv[5]), pack2(sv[6], sv[7])));
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          v4s lo = tr4<SwzV, 128>(KI, 32 * ks + 4 * g + q4, dt * 16 + 4 * p4);
+          v4s hi = tr4<SwzV, 128>(KI, 32 * ks + 16 + 4 * g + q4, dt * 16 + 4 * p4);
+          short8 fk = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          qacc[dt] = mfma(__builtin_bit_cast(bf16x8_t, fk), sf, qacc[dt]);
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const float4v v = qacc[dt];
+        *reinterpret_cast<uint2*>(rowp + dt * 16 + 4 * g) =
+            make_uint2(pack2(v[0] * scale, v[1] * scale), pack2(v[2] * scale, v[3] * scale));
+      }
+    }
+  }
+}
+
 }  // namespace
+
+// persistent forms: 0 off, 1 on (one workgroup per CU), n >= 2 on with at most n workgroups (tests: several items per
+// workgroup at small sizes); -1: from MDTF_ATTN_PP at the first call.  Default off: graph-timed at BERT-base's
+// batch 64 x 12 heads they are slower than the per-item kernels (fwd 17.6 vs 16.7 us, bwd 37.1 vs 35.5 us,
+// bench/attn_probe.py, profiles/ab_r5.md) -- three per-item workgroups per CU already keep as many loads in flight
+// as the double buffer does.
+static int g_attn_pp = -1;
+
+// select the persistent S = 128 kernels (tests / A/B); returns the previous choice
+MDTF_EXPORT int mdtf_set_attn_pp(int on) {
+  const int prev = g_attn_pp;
+  g_attn_pp = on;
+  return prev;
+}
+
+static bool attn_pp_on() {
+  if (g_attn_pp < 0) {
+    const char* e = getenv("MDTF_ATTN_PP");
+    g_attn_pp = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_attn_pp >= 1;
+}
+
+static int pp_grid(int items) {
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n;
+  }();
+  int g = items < cus ? items : cus;
+  if (g_attn_pp >= 2 && g > g_attn_pp) g = g_attn_pp;
+  return g;
+}
 
 // ctx[B*S, H] = attention(qkv[B*S, 3H]); lse [B*nh, S] (fp32) saved for backward
 MDTF_EXPORT int mdtf_attn_fwd(const void* qkv, const float* mask, void* out, float* lse, int B, int seq, int nh,
@@ -680,7 +1077,10 @@ MDTF_EXPORT int mdtf_attn_fwd(const void* qkv, const float* mask, void* out, flo
     const char* e = getenv("MDTF_ATTN_FWD_MINW");
     return e && e[0] == '1';
   }();
-  if (w1)
+  if (attn_pp_on()) {
+    hipLaunchKernelGGL(attn_fwd_pp, dim3(pp_grid(B * nh)), dim3(512), kFwdPpLds, st, (const bf16_t*)qkv, mask, (bf16_t*)out, lse,
+                       B, nh, scale, p_drop, (uint32_t)seed, seed_off);
+  } else if (w1)
     hipLaunchKernelGGL(attn_fwd_kernel<1>, dim3(B * nh), dim3(NT), 0, st, (const bf16_t*)qkv, mask, (bf16_t*)out, lse,
                        B, nh, scale, p_drop, (uint32_t)seed, seed_off);
   else
@@ -716,6 +1116,13 @@ MDTF_EXPORT int mdtf_attn_bwd(const void* qkv, const float* mask, const void* ou
     const char* e = getenv("MDTF_ATTN_BWD_WAVES");
     return e && e[0] == '4';
   }();
+  if (!v1 && attn_pp_on()) {
+    hipLaunchKernelGGL(attn_bwd_pp, dim3(pp_grid(B * nh)), dim3(1024), kBwdPpLds, st, (const bf16_t*)qkv, mask,
+                       (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv, B, nh, scale, p_drop,
+                       (uint32_t)seed, seed_off);
+    MDTF_LAUNCH_CHECK();
+    return 0;
+  }
   if (!v1 && !w4) {
     hipLaunchKernelGGL(attn_bwd_v2, dim3(B * nh), dim3(512), kBwd2Lds, st, (const bf16_t*)qkv, mask,
                        (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv, B, nh, scale, p_drop,

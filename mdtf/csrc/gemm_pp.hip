@@ -403,6 +403,14 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
   };
   prologue_issue();
   bool first = true;
+  // stores of a whole in-range bf16 tile (EPI 0, no conv): one 8-B store per (i, j), plus the pre-activation's
+  // when it is kept.  A later tile's first wait leaves exactly those in flight (they are younger than its
+  // prologue loads), so the previous tile's store drain overlaps this tile's first K-steps instead of stalling it.
+  // (conv forward with BN statistics: + 2 atomics per column fragment)
+  // (GEMM: the 16-B paired stores, FN / 2 + FN % 2 per row fragment; conv: 8-B stores)
+  constexpr int NSTG = FM * (FN / 2 + FN % 2);
+  constexpr int NST1 = CONV == 0 ? NSTG : FM * FN, NST2 = 2 * NSTG, NST3 = FM * FN + 2 * FN;
+  int prev_st = 0;          // 0: the previous epilogue issued an unknown store count (or none after the prologue)
   while (true) {
     if (first && T > 1) {
       if constexpr (QUAD) {
@@ -412,6 +420,25 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
         if (G == 0) wait_vmcnt<CT0>();
         else wait_vmcnt<CT1>();
       }
+    } else if (EPI == 0 && prev_st != 0) {
+      // ops younger than this tile's prologue: its K-tile-1 units (T > 1) and the previous tile's stores; any count
+      // up to their number is safe (vmcnt: all but the n youngest are done), so the sums are capped at 63
+      constexpr int W0 = QUAD ? CB0 : CT0, W1 = QUAD ? 2 * CB1 : CT1;
+#define PP_WAIT(NS_)                                                        \
+  if (T > 1) {                                                              \
+    if (G == 0) wait_vmcnt<(W0 + NS_ < 63 ? W0 + NS_ : 63)>();              \
+    else wait_vmcnt<(W1 + NS_ < 63 ? W1 + NS_ : 63)>();                     \
+  } else {                                                                  \
+    wait_vmcnt<(NS_ < 63 ? NS_ : 63)>();                                    \
+  }
+      if (prev_st == 1) {
+        PP_WAIT(NST1)
+      } else if (prev_st == 2) {
+        PP_WAIT(NST2)
+      } else {
+        PP_WAIT(NST3)
+      }
+#undef PP_WAIT
     } else {
       wait_vmcnt<0>();       // (a later tile: the previous epilogue's stores were issued after these loads)
     }
@@ -601,6 +628,14 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
     set_offsets();
     prologue_issue();
   }
+  // the next tile may leave this epilogue's stores in flight when their count is known: every (i, j) in range
+  const bool whole = em0 + BM <= a.M && en0 + BN <= a.N;
+  int next_st = 0;
+  if (EPI == 0 && early && whole) {
+    if constexpr (CONV == 0) next_st = (a.act && a.pre) ? 2 : 1;     // (early: no accumulate, no act_bwd)
+    else if constexpr (CONV == 1) next_st = a.cv.stat_sum ? 3 : 1;
+    else next_st = 1;
+  }
   // ---- epilogue: lane holds C[row][col .. col+3] for each (i, j)
   const int rbase = em0 + G * (BM / 2) + fr;
   const int cbase = en0 + wc * CW + 4 * fq;
@@ -698,6 +733,80 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
         }
       }
     }
+  } else if (EPI == 0 && !a.accumulate) {
+    // bf16 epilogue with 16-B stores: a lane holds 4 consecutive columns of one row per (i, j); one
+    // v_permlane16_swap per dword of fragments j, j+1 gives lanes of 16-lane rows 0 / 2 columns 16j + 8 (fq / 2) ..
+    // +7 and lanes of rows 1 / 3 columns 16(j+1) + 8 (fq / 2) .. +7 (the partner lanes hold the same output row),
+    // so the tile goes out in half the store instructions (the epilogue is store-issue bound: bench/gemm_ksweep.py)
+    const int sbase = en0 + wc * CW;
+    const int pcol = 16 * (fq & 1) + 8 * (fq >> 1);      // this lane's column inside a 32-column pair
+    const bool keep_pre = a.act && a.pre;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = rbase + 16 * i;
+      const bool rok = row < a.M;
+      uint2 pk[FN], pr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        float4v v = acc[i][j];
+        if (a.biasseg[0]) {
+          const uint2 b4 = bpre[j];
+          v[0] += __uint_as_float(b4.x << 16);
+          v[1] += __uint_as_float(b4.x & 0xffff0000u);
+          v[2] += __uint_as_float(b4.y << 16);
+          v[3] += __uint_as_float(b4.y & 0xffff0000u);
+        }
+        if (a.act_bwd) {           // the producer's activation backward on the data gradient
+          const int col = cbase + 16 * j;
+          const uint2 pq = (rok && col < a.N) ? *reinterpret_cast<const uint2*>(a.act_pre + (long long)row * a.ldc + col)
+                                              : make_uint2(0u, 0u);
+          v[0] *= act_grad(__uint_as_float(pq.x << 16), a.act_bwd);
+          v[1] *= act_grad(__uint_as_float(pq.x & 0xffff0000u), a.act_bwd);
+          v[2] *= act_grad(__uint_as_float(pq.y << 16), a.act_bwd);
+          v[3] *= act_grad(__uint_as_float(pq.y & 0xffff0000u), a.act_bwd);
+        }
+        if (a.act) {
+          pr[j] = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+          // the activation of the ROUNDED pre-activation (what the backward recomputes from)
+          v[0] = act_fwd(__uint_as_float(pr[j].x << 16), a.act);
+          v[1] = act_fwd(__uint_as_float(pr[j].x & 0xffff0000u), a.act);
+          v[2] = act_fwd(__uint_as_float(pr[j].y << 16), a.act);
+          v[3] = act_fwd(__uint_as_float(pr[j].y & 0xffff0000u), a.act);
+        }
+        pk[j] = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+      }
+#pragma unroll
+      for (int j = 0; j + 1 < FN; j += 2) {
+        if (sbase + 16 * j + 32 <= a.N) {              // (wave-uniform)
+          auto sx = __builtin_amdgcn_permlane16_swap(pk[j].x, pk[j + 1].x, false, false);
+          auto sy = __builtin_amdgcn_permlane16_swap(pk[j].y, pk[j + 1].y, false, false);
+          const long long off = (long long)row * a.ldc + sbase + 16 * j + pcol;
+          if (rok) *reinterpret_cast<uint4*>(a.C + off) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+          if (keep_pre) {
+            auto px = __builtin_amdgcn_permlane16_swap(pr[j].x, pr[j + 1].x, false, false);
+            auto py = __builtin_amdgcn_permlane16_swap(pr[j].y, pr[j + 1].y, false, false);
+            if (rok) *reinterpret_cast<uint4*>(a.pre + off) = make_uint4(px[0], py[0], px[1], py[1]);
+          }
+        } else {
+#pragma unroll
+          for (int jj = j; jj < j + 2; ++jj) {
+            const int col = cbase + 16 * jj;
+            if (!rok || col >= a.N) continue;
+            const long long off = (long long)row * a.ldc + col;
+            *reinterpret_cast<uint2*>(a.C + off) = pk[jj];
+            if (keep_pre) *reinterpret_cast<uint2*>(a.pre + off) = pr[jj];
+          }
+        }
+      }
+      if constexpr (FN % 2 == 1) {
+        const int col = cbase + 16 * (FN - 1);
+        if (rok && col < a.N) {
+          const long long off = (long long)row * a.ldc + col;
+          *reinterpret_cast<uint2*>(a.C + off) = pk[FN - 1];
+          if (keep_pre) *reinterpret_cast<uint2*>(a.pre + off) = pr[FN - 1];
+        }
+      }
+    }
   } else {
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
@@ -767,6 +876,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
   }
   it = nxt;
   first = false;
+  prev_st = next_st;
   }
 }
 

@@ -23,6 +23,7 @@ N.register("mdtf_embed_bwd", [N.P, N.P, N.P, N.L, N.I, N.L, N.P])
 N.register("mdtf_attn_fwd", [N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P, N.P])
 N.register("mdtf_attn_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P, N.P])
 N.register("mdtf_set_attn_bwd", [N.I], N.I)     # S = 128 backward kernel: 1 = v1 ([q][k] images), 2 = v2
+N.register("mdtf_set_attn_pp", [N.I], N.I)      # S = 128 persistent kernels: 0 off, 1 on, n >= 2 on, grid <= n
 
 
 def effective_seed(seed, device):

@@ -47,7 +47,7 @@ case "$WHAT" in
     prof_one resnet "$ROOT/bench.py" --steps 5 --warmup 3 --bert 0 "$@"
     prof_one bert "$ROOT/bench/bert_bench.py" --steps 5 --warmup 3
     cd "$ROOT" && python scripts/step_breakdown.py "$OUT/prof_resnet_$TAG" --calls > "$OUT/summary_resnet_$TAG.txt" 2>&1
-    python scripts/step_breakdown.py "$OUT/prof_bert_$TAG" > "$OUT/summary_bert_$TAG.txt" 2>&1
+    python scripts/step_breakdown.py "$OUT/prof_bert_$TAG" --calls > "$OUT/summary_bert_$TAG.txt" 2>&1
     head -30 "$OUT/summary_resnet_$TAG.txt" ;;
   profr)
     prof_one resnet "$ROOT/bench.py" --steps 5 --warmup 3 --bert 0 "$@"

@@ -928,6 +928,39 @@ def test_attention_bwd_v2_matches_v1(p_drop):
         assert _rel(grads[0][:, sl], grads[1][:, sl]) < 1e-2, part
 
 
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+@pytest.mark.parametrize("grid", [7, 1])
+def test_attention_persistent_matches_per_item(p_drop, grid):
+    """S = 128 attention: the persistent kernels (csrc/attention.hip attn_fwd_pp / attn_bwd_pp: one workgroup walks
+    several (batch, head) items with the next item's operands DMA'd into the other half of a double buffer) give the
+    per-item kernels' context, logsumexp-consistent backward and dQ/dK/dV.  grid 7 over 60 items: 8-9 items per
+    workgroup (both buffers, an uneven tail); grid 1 (the value 1 means one workgroup per CU): one item each."""
+    from mdtf.ops import _native as NN
+    from mdtf.ops import transformer as T
+    torch.manual_seed(34)
+    B, S_, nh, dh = 5, 128, 12, 64
+    H = nh * dh
+    qkv = (torch.randn(B * S_, 3 * H, device=DEV) * 0.5).bfloat16()
+    mask = ((torch.rand(B, S_, device=DEV) < 0.2).float() * -10000.0)
+    dout = torch.randn(B * S_, H, device=DEV).bfloat16()
+    res = []
+    prev = NN.fn("mdtf_set_attn_pp")(0)
+    try:
+        for pp in (0, grid):
+            NN.fn("mdtf_set_attn_pp")(pp)
+            x = qkv.clone().requires_grad_(True)
+            out = T._FusedAttention.apply(x, mask, B, S_, nh, p_drop, 4242)
+            out.backward(dout)
+            torch.cuda.synchronize()
+            res.append((out.float(), x.grad.float()))
+    finally:
+        NN.fn("mdtf_set_attn_pp")(prev)
+    assert torch.equal(res[0][0], res[1][0])          # same arithmetic per element in both forward forms
+    for part in range(3):
+        sl = slice(part * H, (part + 1) * H)
+        assert _rel(res[1][1][:, sl], res[0][1][:, sl]) < 1e-2, part
+
+
 def test_bert_fused_vs_unfused_attention_path(monkeypatch):
     """BERT step: fused-attention kernel path == unfused matmul/softmax path (same weights, no dropout)."""
     from mdtf.models import SyntheticBertLoader
