@@ -274,7 +274,9 @@ __global__ void __launch_bounds__(256, PF ? 2 : 3) stem_conv_rows(const bf16_t* 
         *reinterpret_cast<const uint4*>(wt + (long long)ch * (KHP * 32) + (f >> 2) * 32 + 8 * (l >> 4));
   }
 
-  const int rp = lane >> 2, rc = lane & 3;
+  // row layout as conv_ws_kernel's epilogue: pixel rp = (lane & 31) >> 1, chunk rc = (lane & 1) | (lane >> 5) << 1,
+  // so the ds_bpermute sources of each 32-lane half are distinct mod 32 (conflict-free)
+  const int rp = (lane & 31) >> 1, rc = (lane & 1) | ((lane >> 5) << 1);
   const int xsrc = (16 * rc + rp) * 4;
   auto xpose = [&](const uint4& v) {
     return make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute(xsrc, (int)v.x),

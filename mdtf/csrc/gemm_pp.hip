@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
   // (conv forward with BN statistics: + 2 atomics per column fragment)
   // (GEMM: the 16-B paired stores, FN / 2 + FN % 2 per row fragment; conv: 8-B stores)
   constexpr int NSTG = FM * (FN / 2 + FN % 2);
-  constexpr int NST1 = CONV == 0 ? NSTG : FM * FN, NST2 = 2 * NSTG, NST3 = FM * FN + 2 * FN;
+  constexpr int NST1 = NSTG, NST2 = 2 * NSTG, NST3 = NSTG + 2 * FN;
   int prev_st = 0;          // 0: the previous epilogue issued an unknown store count (or none after the prologue)
   while (true) {
     if (first && T > 1) {
@@ -659,6 +659,63 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) s0[j][e] = s1[j][e] = 0.f;
+    if (!(CONV == 2 && a.accumulate)) {
+      // no accumulate source: 16-B paired stores as in the GEMM epilogue (v_permlane16_swap of fragments j, j+1)
+      const int sbase = en0 + wc * CW;
+      const int pcol = 16 * (fq & 1) + 8 * (fq >> 1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = rbase + 16 * i;
+        const bool rok = row < a.M;
+        uint2 pk[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int col = cbase + 16 * j;
+          const float4v v = acc[i][j];
+          pk[j] = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+          if (!rok || col >= a.N) continue;
+          if (CONV == 1 && st) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              s0[j][e] += v[e];
+              s1[j][e] += v[e] * v[e];
+            }
+          } else if (CONV == 2 && st) {
+            const long long off = (long long)row * a.ldc + col;
+            const uint2 xq = *reinterpret_cast<const uint2*>(g.bx + off);
+            const unsigned nb = g.bmask ? (g.bmask[off >> 3] >> (off & 7)) & 15u : 15u;
+            const float gv[4] = {__uint_as_float(pk[j].x << 16), __uint_as_float(pk[j].x & 0xffff0000u),
+                                 __uint_as_float(pk[j].y << 16), __uint_as_float(pk[j].y & 0xffff0000u)};
+            const float xv[4] = {__uint_as_float(xq.x << 16), __uint_as_float(xq.x & 0xffff0000u),
+                                 __uint_as_float(xq.y << 16), __uint_as_float(xq.y & 0xffff0000u)};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float gm = ((nb >> e) & 1u) ? gv[e] : 0.f;
+              s0[j][e] += gm;
+              s1[j][e] += gm * xv[e];
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j + 1 < FN; j += 2) {
+          if (sbase + 16 * j + 32 <= a.N) {
+            auto sx = __builtin_amdgcn_permlane16_swap(pk[j].x, pk[j + 1].x, false, false);
+            auto sy = __builtin_amdgcn_permlane16_swap(pk[j].y, pk[j + 1].y, false, false);
+            if (rok)
+              *reinterpret_cast<uint4*>(a.C + (long long)row * a.ldc + sbase + 16 * j + pcol) =
+                  make_uint4(sx[0], sy[0], sx[1], sy[1]);
+          } else {
+#pragma unroll
+            for (int jj = j; jj < j + 2; ++jj)
+              if (rok && cbase + 16 * jj < a.N) *reinterpret_cast<uint2*>(a.C + (long long)row * a.ldc + cbase + 16 * jj) = pk[jj];
+          }
+        }
+        if constexpr (FN % 2 == 1) {
+          if (rok && cbase + 16 * (FN - 1) < a.N)
+            *reinterpret_cast<uint2*>(a.C + (long long)row * a.ldc + cbase + 16 * (FN - 1)) = pk[FN - 1];
+        }
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int row = rbase + 16 * i;
@@ -704,6 +761,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs a) {
           }
         }
       }
+    }
     }
     if (st) {
       // the 16 lanes of a 4-column group hold 16 rows each: butterfly over lane bits 0..3, then lanes fr = e

@@ -46,9 +46,11 @@ def wgrad_splits(M, R, Cout, bm, bn, ver, splits):
     return -(-kt_total // ks)
 
 
-def wgrad_slab(M, R, Cout, bm, bn, ver, splits, device, dense=False):
-    """(slab tensor or None, capacity) for one v2 weight-gradient launch."""
-    if not (DENSE_WGRAD_SLAB if dense else WGRAD_SLAB) or N.deterministic():
+def wgrad_slab(M, R, Cout, bm, bn, ver, splits, device, dense=False, force=None):
+    """(slab tensor or None, capacity) for one v2 weight-gradient launch.  ``force``: a per-shape choice of the
+    conv table (``"slab"`` field) over the global MDTF_WGRAD_SLAB default."""
+    on = (DENSE_WGRAD_SLAB if dense else WGRAD_SLAB) if force is None else force
+    if not on or N.deterministic():
         return None, 0
     sp = wgrad_splits(M, R, Cout, bm, bn, ver, splits)
     if sp < 2:
@@ -471,6 +473,18 @@ def ws_depth_ok(k_total, d):
     return ks > 4 and d in (3, 4, 6) and ks % d == 0
 
 
+N.register("mdtf_conv3_rows", [N.P, N.P, N.P] + [N.I] * 4 + [N.P, N.P, N.I, N.P, N.P, N.P])
+# row-staged 3x3 kernel (csrc/conv_rows.hip) for the 64 -> 64 channel, 56-wide stride-1 convolutions the
+# weight-stationary table entries name; MDTF_CONV_ROWS=0 keeps the streamed kernel
+CONV_ROWS = os.environ.get("MDTF_CONV_ROWS", "1") != "0"
+
+
+def rows_ok(h_w, c, co, kh, kw, stride, pads, dil):
+    """Shapes csrc/conv_rows.hip takes: 3x3, stride 1, pad 1, 64 -> 64 channels, 56 wide."""
+    return (CONV_ROWS and c == 64 and co == 64 and kh == 3 and kw == 3 and tuple(stride) == (1, 1)
+            and tuple(pads) == (1, 1, 1, 1) and tuple(dil) == (1, 1) and h_w[1] == 56)
+
+
 def _ws_code(tp, nw, cg, d=4):
     """C-ABI tile code of csrc/conv_ws.hip: pixel subtiles, waves, channel groups, load-ring depth."""
     return tp + 10 * nw + 100 * cg + 1000 * d
@@ -484,6 +498,10 @@ def ws_fwd(x, wt, kh, kw, out_hw, stride, pads, dil, tile, stats=None, grid_cap=
     y = out if out is not None else torch.empty((n, out_hw[0], out_hw[1], co), dtype=x.dtype, device=x.device)
     s_sum, s_sq = stats if stats is not None else (None, None)
     slots = s_sum.shape[0] if s_sum is not None else 0
+    if rows_ok((h, wd), c, co, kh, kw, stride, pads, dil) and tuple(out_hw) == (h, wd):
+        N.check(N.fn("mdtf_conv3_rows")(N.ptr(x), N.ptr(wt), N.ptr(y), n, h, wd, 0, N.ptr(s_sum), N.ptr(s_sq), slots,
+                                        N.ptr(None), N.ptr(None), N.stream_ptr()), "conv3_rows_fwd")
+        return y
     N.check(N.fn("mdtf_conv_ws")(N.ptr(x), N.ptr(wt), N.ptr(y), n, h, wd, c, out_hw[0], out_hw[1], co, kh, kw,
                                  stride[0], stride[1], pads[0], pads[2], dil[0], dil[1], 0, _ws_code(*tile),
                                  int(grid_cap), N.ptr(s_sum), N.ptr(s_sq), slots, N.ptr(None), N.ptr(None),
@@ -501,6 +519,11 @@ def ws_dgrad(dy, w, x_shape, pads, dil, tile, out=None, accumulate=False, bn_sta
     ph = (kh - 1) * dil[0] - pads[0]
     pw = (kw - 1) * dil[1] - pads[2]
     bx, bmask, bsum, bsq, bslots = bn_stats if bn_stats is not None else (None, None, None, None, 0)
+    if (not accumulate and acc_src is None and rows_ok((h, wd), co, ci, kh, kw, (1, 1), pads, dil)
+            and tuple(dy.shape[1:3]) == (h, wd)):
+        N.check(N.fn("mdtf_conv3_rows")(N.ptr(dy), N.ptr(w), N.ptr(dx), n, h, wd, 1, N.ptr(bsum), N.ptr(bsq),
+                                        int(bslots), N.ptr(bx), N.ptr(bmask), N.stream_ptr()), "conv3_rows_dgrad")
+        return dx
     N.check(N.fn("mdtf_conv_ws")(N.ptr(dy), N.ptr(w), N.ptr(dx), n, dy.shape[1], dy.shape[2], co, h, wd, ci, kh, kw,
                                  1, 1, ph, pw, dil[0], dil[1], 1, _ws_code(*tile), int(grid_cap), N.ptr(None),
                                  N.ptr(None), 0, N.ptr(bx), N.ptr(bmask), N.ptr(bsum), N.ptr(bsq), int(bslots),
@@ -558,7 +581,13 @@ def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=
     n, h, wd, c = x.shape
     kh, kw, ci, co = w_shape
     if ver in (2, 3):
-        slab, cap = wgrad_slab(n * dy.shape[1] * dy.shape[2], kh * kw * ci, co, bm, bn, ver, int(splits), x.device)
+        force = None
+        if _SLAB_MODE not in ("0", "1"):          # MDTF_WGRAD_SLAB=0/1 pin it; else the table's per-shape choice
+            ent = table().get(shape_key("wgrad", tuple(x.shape), tuple(w_shape), stride, pads, dil))
+            if ent is not None and "slab" in ent:
+                force = bool(ent["slab"])
+        slab, cap = wgrad_slab(n * dy.shape[1] * dy.shape[2], kh * kw * ci, co, bm, bn, ver, int(splits), x.device,
+                               force=force)
         N.check(N.fn("mdtf_conv_wgrad_v2")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co,
                                            kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
                                            _v2_code(bm, stages, ver), bn, int(splits), N.ptr(slab), cap,

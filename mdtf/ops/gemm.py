@@ -124,6 +124,9 @@ FFN_FUSE = os.environ.get("MDTF_FFN_FUSE", "1") != "0"
 # (K, N) of the second layer's W [K][N] -> (bm, bn, stages, ver) of the fused data gradient (output K columns)
 # (bench/dgrad_act_probe.py, graph-timed at M 8192: 128 x 256 8-wave, 3 stages)
 DGRAD_ACT_TILES = {(3072, 768): (128, 256, 3, 3)}
+# MDTF_ACT_DGRAD=core: that data gradient on the GEMM core (csrc/gemm_pp.hip, act-backward epilogue with 16-B
+# stores) instead of the conv-kernel MODE 4 (A/B switch)
+ACT_DGRAD_CORE = os.environ.get("MDTF_ACT_DGRAD", "conv") == "core"
 
 # MDTF_DENSE_FWD: "auto" (default) = the shapes of FWD_TILES, where the kernel beats hipBLASLt inside the
 # captured BERT-base step; "mdtf" = every shape it takes; "hipblaslt" = none (torch.addmm + activation kernel).
@@ -514,7 +517,10 @@ class _Dense(torch.autograd.Function):
             hand = not ctx.trans
             li = ctx.link_in
             if xs is None and li is not None and li.pre is not None and hand and ctx.nw == 1:
-                dx = hand_dgrad_act(dpre, w, li.pre, li.act)      # ffn(): dx already carries act'(pre)
+                if ACT_DGRAD_CORE:                     # the GEMM core's dgrad with the act-backward epilogue
+                    dx = mm.dgrad(dpre, w, act_pre=li.pre, act_bwd=li.act)
+                else:
+                    dx = hand_dgrad_act(dpre, w, li.pre, li.act)      # ffn(): dx already carries act'(pre)
                 li.fused = dx is not None
             if dx is None and xs is None:
                 dx = _hand_dgrad(dpre, w) if hand else None

@@ -1599,6 +1599,49 @@ def test_conv_weight_stationary(tile, geo):
     assert _rel(bsum[1].sum(0), (gm * bx.float().reshape(-1, c)).sum(0)) < 5e-3
 
 
+@pytest.mark.parametrize("n,h", [(2, 56), (3, 13)])
+def test_conv3_rows(n, h):
+    """csrc/conv_rows.hip (64 -> 64 channel 3x3 / stride 1 / pad 1, 56 wide): forward with the BN-statistics
+    epilogue and the data gradient plain / with the BN-backward statistics (with and without a ReLU mask) vs fp32
+    references; row groups past the image's last row (h = 13), persistent loops (n * 7 groups > 1 per block
+    only at large n: here the tails)."""
+    from mdtf.ops import conv as C
+    w, c = 56, 64
+    torch.manual_seed(n * h)
+    pads = (1, 1, 1, 1)
+    assert C.rows_ok((h, w), c, c, 3, 3, (1, 1), pads, (1, 1))
+    x = torch.randn(n, h, w, c).bfloat16()
+    wt = (torch.randn(3, 3, c, c) / (9 * c) ** 0.5).bfloat16()
+    wr = wt.float().permute(3, 2, 0, 1)
+    yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wr, padding=1).permute(0, 2, 3, 1)
+    sbuf = torch.zeros(2, 8, c, device=DEV)
+    y = C.ws_fwd(x.to(DEV), C.transpose_filter(wt.to(DEV)), 3, 3, (h, w), (1, 1), pads, (1, 1), (4, 8, 1, 3),
+                 (sbuf[0], sbuf[1]))
+    assert _rel(y, yr) < 1e-2
+    yf = yr.reshape(-1, c)
+    assert _rel(sbuf[0].sum(0), yf.sum(0)) < 5e-3
+    assert _rel(sbuf[1].sum(0), (yf * yf).sum(0)) < 5e-3
+    dy = torch.randn(n, h, w, c).bfloat16()
+    xg = torch.zeros(n, c, h, w, requires_grad=True)
+    torch.nn.functional.conv2d(xg, wr, padding=1).backward(dy.float().permute(0, 3, 1, 2))
+    ref = xg.grad.permute(0, 2, 3, 1)
+    dx = C.ws_dgrad(dy.to(DEV), wt.to(DEV), (n, h, w, c), pads, (1, 1), (2, 8, 1, 3))
+    assert _rel(dx, ref) < 1e-2
+    bx = torch.randn(n, h, w, c).bfloat16()
+    mbits = torch.rand(n * h * w * c) > 0.4
+    packed = (mbits.view(-1, 8).to(torch.int32) << torch.arange(8)).sum(1).to(torch.uint8)
+    for mask in (packed, None):
+        bsum = torch.zeros(2, 4, c, device=DEV)
+        gd = C.ws_dgrad(dy.to(DEV), wt.to(DEV), (n, h, w, c), pads, (1, 1), (2, 8, 1, 3),
+                        bn_stats=(bx.to(DEV), None if mask is None else mask.to(DEV), bsum[0], bsum[1], 4))
+        assert _rel(gd, ref) < 1e-2
+        gm = gd.float().cpu().reshape(-1, c)
+        if mask is not None:
+            gm = gm * mbits.view(-1, c).float()
+        assert _rel(bsum[0].sum(0), gm.sum(0)) < 5e-3
+        assert _rel(bsum[1].sum(0), (gm * bx.float().reshape(-1, c)).sum(0)) < 5e-3
+
+
 @pytest.mark.parametrize("geo", [(2, 30, 31, 3, 7, 64, 2, 3), (3, 17, 16, 1, 5, 128, 1, 2), (2, 24, 24, 4, 3, 64, 2, 1),
                                  (1, 224, 224, 3, 7, 64, 2, 3)])
 @pytest.mark.parametrize("kernel", ["rows", "ws"])
