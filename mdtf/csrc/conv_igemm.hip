@@ -1366,7 +1366,9 @@ __global__ void __launch_bounds__(64 * NW, (wgrad_min_waves<BM, BN, STAGES, NW>(
     }
 }
 
-// DW[r][c] (row stride ld) += sum_s slab[s][r][c]  (slab rows dense, C % 4 == 0); 4 splits in flight
+// DW[r][c] (row stride ld) += sum_s slab[s][r][c]  (slab rows dense, C % 4 == 0); 4 splits in flight.
+// (Spreading the splits of a small filter over more blocks with fp32 atomics measured 1.7 % slower in the ResNet
+// step: profiles/ab_r5.md.)
 __global__ void __launch_bounds__(256) wgrad_slab_reduce(const float* __restrict__ slab, int splits, long long RC,
                                                          int C, long long ld, float* __restrict__ dw) {
   const long long q = blockIdx.x * 256LL + threadIdx.x;     // float4 index

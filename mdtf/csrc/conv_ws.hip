@@ -40,6 +40,8 @@ extern template int dispatch_ws<1>(WsArgs&, int, int, int, int, int, hipStream_t
 extern template int dispatch_ws<2>(WsArgs&, int, int, int, int, int, hipStream_t);
 extern template int dispatch_ws<3>(WsArgs&, int, int, int, int, int, hipStream_t);
 extern template int dispatch_ws<4>(WsArgs&, int, int, int, int, int, hipStream_t);
+template int dispatch_ws_dual<0>(WsArgs&, int, int, int, hipStream_t);
+template int dispatch_ws_dual<3>(WsArgs&, int, int, int, hipStream_t);
 }  // namespace ws
 }  // namespace mdtf
 
@@ -119,6 +121,60 @@ MDTF_EXPORT int mdtf_conv_ws(const void* src, const void* wgt, void* out, int N,
                              const void* acc_src, const void* acc_mask, hipStream_t st) {
   return conv_ws_impl(src, wgt, out, N, H, W, C, C, OH, OW, Ncol, KH, KW, SH, SW, PH, PW, DH, DW, wmode, tile,
                       grid_cap, ssum, ssq, sslots, bx, bmask, bsum, bsq, bslots, accumulate, acc_src, acc_mask, st);
+}
+
+// Fused fan-out data gradient of a block input x that feeds a 1x1 / stride-1 convolution (gradient dy1
+// [N][H][W][C1], HWIO filter w1 [1][1][Ncol][C1]) and a 1x1 / stride-S2 projection (dy2 [N][H2][W2][C2], w2
+// [1][1][Ncol][C2]): out = dgrad1 + dgrad2 in ONE pass over out, as a single GEMM with K = C1 + C2 whose second
+// k-range runs only over the output pixels the projection sampled (the kernel's pixel order puts them first).
+// C1, C2 multiples of 128 (the 4-deep load ring), stride 2.  Replaces the projection's
+// strided dgrad (GEMM + zero classes, writing out) followed by the 1x1 dgrad accumulating into it.
+// bsum non-null: BN-backward statistics of out against bx / bmask (as mdtf_conv_ws).
+MDTF_EXPORT int mdtf_conv_ws_dual(const void* dy1, const void* w1, const void* dy2, const void* w2, void* out, int N,
+                                  int H, int W, int Ncol, int C1, int H2, int W2, int C2, int S2, int tile,
+                                  const void* bx, const void* bmask, float* bsum, float* bsq, int bslots,
+                                  hipStream_t st) {
+  if (C1 % 128 || C2 % 128 || Ncol % 64 || S2 != 2 || H2 != (H + 1) / 2 || W2 != (W + 1) / 2) return MDTF_EINVAL;
+  if (64LL * (C1 + C2) * 2 > 160 * 1024) return MDTF_EUNSUPPORTED;
+  if ((long long)N * H * W * C1 * 2 >= 0x80000000LL || (long long)N * H2 * W2 * C2 * 2 >= 0x80000000LL)
+    return MDTF_EUNSUPPORTED;
+  WsArgs a{};
+  a.src = (const bf16_t*)dy1;
+  a.wgt = (const bf16_t*)w1;
+  a.out = (bf16_t*)out;
+  a.N = N; a.H = H; a.W = W; a.C = C1; a.cs = C1;
+  a.OH = H; a.OW = W; a.Ncol = Ncol;
+  a.KH = a.KW = a.SH = a.SW = a.DH = a.DW = 1;
+  a.PH = a.PW = 0;
+  a.wmode = 1;
+  a.Cw = C1;
+  a.K = C1 + C2;
+  a.M = (long long)N * H * W;
+  if (a.M + 16LL * 8 * 64 >= 0x7fffffffLL) return MDTF_EUNSUPPORTED;
+  a.sslots = 1;
+  a.bx = (const bf16_t*)bx; a.bmask = (const uint8_t*)bmask; a.bsum = bsum; a.bsq = bsq;
+  a.bslots = bslots > 0 ? bslots : 1;
+  a.direct = 1;
+  a.src2 = (const bf16_t*)dy2;
+  a.wgt2 = (const bf16_t*)w2;
+  a.K1 = C1; a.C2 = C2; a.H2 = H2; a.W2 = W2; a.S2 = S2;
+  a.Mee = N * H2 * W2;
+  a.Cimg = H * W - H2 * W2;
+  a.G = 2 * W - W2;
+  a.wodd = W - W2;
+  magic_div((unsigned)W2, a.mw2, a.sw2);
+  magic_div((unsigned)H2, a.mh2, a.sh2);
+  magic_div((unsigned)a.Cimg, a.mci, a.sci);
+  magic_div((unsigned)a.G, a.mpr, a.spr);
+  magic_div((unsigned)W, a.mow, a.sow);
+  magic_div((unsigned)H, a.mohh, a.sohh);
+  a.dbg = ws_debug;
+  const int tp = tile % 10, nw = (tile / 10) % 10, cg = (tile / 100) % 10;
+  if (bsum) {
+    if (!bx) return MDTF_EINVAL;
+    return dispatch_ws_dual<3>(a, tp, nw, cg, st);
+  }
+  return dispatch_ws_dual<0>(a, tp, nw, cg, st);
 }
 
 // ---------------------------------------------------------------------------------------------

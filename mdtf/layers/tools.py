@@ -181,12 +181,28 @@ def conv_bn(layer_name, x, out_channels, kernel_size=3, stride=1, relu=True, res
     returned unapplied (``ops.bn.DeferredBN``) for the residual BN that adds it to apply (GPU training).
     ``pool = (ksize, stride, padding)``: a max pool after the ReLU (fused with the BN on the GPU).
     """
-    cin = x.shape[-1]
+    variables = conv_bn_variables(layer_name, x, out_channels, kernel_size, zero_gamma=zero_gamma)
+    return conv_bn_apply(x, variables, kernel_size, stride, relu, residual, training, bn_decay, bn_epsilon, padding,
+                         defer, pool)
+
+
+def conv_bn_apply(x, variables, kernel_size=3, stride=1, relu=True, residual=None, training=True, bn_decay=0.9,
+                  bn_epsilon=1e-5, padding=None, defer=False, pool=None):
+    """:func:`conv_bn` on variables already made by :func:`conv_bn_variables`."""
     k = kernel_size
     if padding is None:
         padding = "SAME" if stride == 1 else ((k - 1) // 2, (k - 1) // 2)
+    w, gamma, beta, mm, mv = variables
+    return ops.conv_bn(x, w, gamma, beta, mm, mv, stride, padding, training, bn_decay, bn_epsilon, relu, residual,
+                       defer=defer, pool=pool)
+
+
+def conv_bn_variables(layer_name, x, out_channels, kernel_size=3, zero_gamma=False, **unused):
+    """The variables of :func:`conv_bn` (created on first use, reused after): weights, gamma, beta, moving
+    mean / variance."""
+    k = kernel_size
     with V.variable_scope(layer_name):
-        w = V.get_variable('weights', [k, k, cin, out_channels], initializer=V.variance_scaling_initializer())
+        w = V.get_variable('weights', [k, k, x.shape[-1], out_channels], initializer=V.variance_scaling_initializer())
         c = out_channels
         gamma = V.get_variable('BatchNorm/gamma', [c], initializer=V.constant_initializer(0.0 if zero_gamma else 1.0),
                                keep_fp32=True)
@@ -194,8 +210,7 @@ def conv_bn(layer_name, x, out_channels, kernel_size=3, stride=1, relu=True, res
         mm = V.get_variable('BatchNorm/moving_mean', [c], initializer=V.constant_initializer(0.0), trainable=False)
         mv = V.get_variable('BatchNorm/moving_variance', [c], initializer=V.constant_initializer(1.0),
                             trainable=False)
-        return ops.conv_bn(x, w, gamma, beta, mm, mv, stride, padding, training, bn_decay, bn_epsilon, relu, residual,
-                           defer=defer, pool=pool)
+    return w, gamma, beta, mm, mv
 
 
 def dense(layer_name, x, out_features, act=None, initializer=None):

@@ -10,6 +10,8 @@ Every conv is followed by a fused BatchNorm(+residual)(+ReLU) kernel
 ReLU, so a bottleneck block is 3-4 conv launches + 3 BN launches.  Variable
 names follow TF-slim style scopes (``resnet_v1_50/block1/unit_1/conv1/weights``).
 """
+import os
+
 import torch
 
 from ..layers import tools
@@ -19,6 +21,13 @@ from ..train import variables as V
 
 DEPTHS = {18: None, 50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3], 200: [3, 24, 36, 3]}
 
+
+
+# MDTF_PROJ_LATE=1: run the projection shortcut's conv after conv2, so its backward runs before conv1's and its data
+# gradient can be fused into conv1's (ops.actsink deferral + mdtf_conv_ws_dual).  Off by default: measured neutral
+# in the step (+0.1 %, profiles/ab_r5.md) -- the split order (conv1 writes, the projection accumulates with the
+# statistics, the zero classes only read) already moves little more than the fused pass would.
+PROJ_LATE = os.environ.get("MDTF_PROJ_LATE", "0") == "1"
 
 class ResNet(Model):
     def __init__(self, depth=50, num_classes=1000, zero_init_residual=True, bn_decay=0.9, bn_epsilon=1e-5,
@@ -37,13 +46,22 @@ class ResNet(Model):
     def _bottleneck(self, x, filters, stride, name, training):
         kw = dict(training=training, bn_decay=self.bn_decay, bn_epsilon=self.bn_epsilon)
         with V.variable_scope(name):
-            if stride != 1 or x.shape[-1] != 4 * filters:
-                # GPU training: its BN is applied inside conv3's residual BN pass (ops.bn.DeferredBN)
+            proj = stride != 1 or x.shape[-1] != 4 * filters
+            if proj and not PROJ_LATE:
                 shortcut = tools.conv_bn("shortcut", x, 4 * filters, 1, stride, relu=False, defer=True, **kw)
-            else:
-                shortcut = x
+            elif proj:
+                # GPU training: its BN is applied inside conv3's residual BN pass (ops.bn.DeferredBN).  The
+                # variables are created first (the checkpoint / initialisation order); the conv itself runs
+                # after conv2, so autograd runs its backward BEFORE conv1's: the strided projection's data
+                # gradient is the first contribution to x's gradient and can be deferred into conv1's
+                # (ops.actsink, one fused pass over the block input's gradient)
+                sc_vars = tools.conv_bn_variables("shortcut", x, 4 * filters, 1, **kw)
             y = tools.conv_bn("conv1", x, filters, 1, 1, relu=True, **kw)
             y = tools.conv_bn("conv2", y, filters, 3, stride, relu=True, **kw)
+            if proj and PROJ_LATE:
+                shortcut = tools.conv_bn_apply(x, sc_vars, 1, stride, relu=False, defer=True, **kw)
+            elif not proj:
+                shortcut = x
             y = tools.conv_bn("conv3", y, 4 * filters, 1, 1, relu=True, residual=shortcut,
                               zero_gamma=self.zero_init_residual, **kw)
         return y

@@ -14,6 +14,11 @@ The producer's backward (called with ``None`` once all consumers are done)
 takes the summed gradient from the sink. It also adds whatever ordinary autograd
 gradient arrived, so consumers that are not sink-aware stay correct.
 
+A strided 1x1 projection conv may leave its data gradient *deferred* (``pconv``: the gradient, filter, stride and
+a closure that runs it): when the contributor that completes the sum is the block's 1x1 / stride-1 conv on the
+weight-stationary kernel, both data gradients run as one GEMM (``mdtf_conv_ws_dual``) and the block input's
+gradient is written once; anything else runs the closure first.
+
 A ReLU'd residual BatchNorm's backward may leave its contribution *pending* instead of writing it:
 ``(g, mask)`` meaning ``g * mask`` (the identity shortcut's gradient).  A conv dgrad that supports a
 masked accumulate source (:meth:`target_ex`) folds it into its own epilogue, so that tensor is never
@@ -30,7 +35,7 @@ class ActGradSink(object):
     producing BatchNorm needs for its backward statistics, ``(x, relu_mask)``.  The contributor that
     completes the sum (the ``consumers``-th) may emit the statistics in its epilogue into ``stats``
     (the v2 conv dgrad does)."""
-    __slots__ = ("buf", "count", "consumers", "stat_req", "stats", "pend")
+    __slots__ = ("buf", "count", "consumers", "stat_req", "stats", "pend", "pconv")
 
     def __init__(self):
         self.buf = None
@@ -39,6 +44,26 @@ class ActGradSink(object):
         self.stat_req = None
         self.stats = None
         self.pend = None
+        self.pconv = None
+
+    def idle(self):
+        """Nothing contributed yet (neither written nor left pending / deferred)."""
+        return self.buf is None and self.pend is None and self.pconv is None
+
+    def defer_conv(self, dy, w, stride, run):
+        """Contribute a strided 1x1 conv's data gradient without running it (only as the first contribution);
+        ``run(out, accumulate)`` computes it the ordinary way and returns the tensor written."""
+        assert self.idle()
+        self.pconv = (dy, w, stride, run)
+        self.count += 1
+
+    def take_conv(self):
+        """The deferred conv contribution ``(dy, w, stride)`` for a kernel that fuses it (cleared), or None."""
+        if self.pconv is None or self.buf is not None or self.pend is not None:
+            return None
+        dy, w, stride, _ = self.pconv
+        self.pconv = None
+        return dy, w, stride
 
     def defer_masked(self, g, mask):
         """Contribute ``g * mask`` without materialising it (only as the first contribution)."""
@@ -47,6 +72,9 @@ class ActGradSink(object):
         self.count += 1
 
     def _materialize(self):
+        if self.pconv is not None:
+            run, self.pconv = self.pconv[3], None
+            self.buf = run(self.buf, self.buf is not None)
         if self.pend is None:
             return
         from . import _native as N
@@ -61,7 +89,7 @@ class ActGradSink(object):
     def target_ex(self):
         """(buffer, accumulate, pending) for a kernel that can also fold a pending ``(g, mask)`` into its
         epilogue: with ``pending`` not None, write ``result + g * mask`` into ``buffer`` (None: allocate)."""
-        if self.pend is not None and self.buf is None:
+        if self.pend is not None and self.buf is None and self.pconv is None:
             p, self.pend = self.pend, None
             FOLDED[0] += 1
             return None, False, p

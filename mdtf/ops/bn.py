@@ -123,7 +123,7 @@ class _BNTrain(torch.autograd.Function):
         pending = False
         if ctx.has_res:
             from . import actsink
-            if (rs is not None and ctx.relu and actsink.MASKED_RESIDUAL and rs.buf is None and rs.pend is None
+            if (rs is not None and ctx.relu and actsink.MASKED_RESIDUAL and rs.idle()
                     and not rs.completing()):
                 # identity shortcut: its gradient dy * mask is left pending in the sink; the conv dgrad that
                 # completes the sum folds it into its epilogue (never written / re-read here)

@@ -477,6 +477,7 @@ N.register("mdtf_conv3_rows", [N.P, N.P, N.P] + [N.I] * 4 + [N.P, N.P, N.I, N.P,
 # row-staged 3x3 kernel (csrc/conv_rows.hip) for the 64 -> 64 channel, 56-wide stride-1 convolutions the
 # weight-stationary table entries name; MDTF_CONV_ROWS=0 keeps the streamed kernel
 CONV_ROWS = os.environ.get("MDTF_CONV_ROWS", "1") != "0"
+DUAL_FUSED = [0]            # fused fan-out data gradients launched (tests)
 
 
 def rows_ok(h_w, c, co, kh, kw, stride, pads, dil):
@@ -530,6 +531,48 @@ def ws_dgrad(dy, w, x_shape, pads, dil, tile, out=None, accumulate=False, bn_sta
                                  int(bool(accumulate) or acc_src is not None),
                                  N.ptr(acc_src[0] if acc_src is not None else None),
                                  N.ptr(acc_src[1] if acc_src is not None else None), N.stream_ptr()), "conv_ws_dgrad")
+    return dx
+
+
+N.register("mdtf_conv_ws_dual", [N.P] * 5 + [N.I] * 10 + [N.P, N.P, N.P, N.P, N.I, N.P])
+# fused fan-out data gradient (csrc/conv_ws.hip mdtf_conv_ws_dual) for a block input feeding a 1x1 / stride-1 conv
+# and a strided 1x1 projection; MDTF_DUAL_DGRAD=0 runs the two data gradients one after the other
+DUAL_DGRAD = os.environ.get("MDTF_DUAL_DGRAD", "1") != "0"
+DUAL_TILE = tuple(int(v) for v in os.environ.get("MDTF_DUAL_TILE", "2,8,1").split(","))
+
+
+def proj_deferrable(w_shape, stride, pads, dil):
+    """A strided 1x1 projection whose data gradient may be deferred into the fused fan-out kernel."""
+    return (DUAL_DGRAD and w_shape[0] == 1 and w_shape[1] == 1 and tuple(stride)[0] == tuple(stride)[1] > 1
+            and tuple(pads) == (0, 0, 0, 0) and tuple(dil) == (1, 1) and w_shape[3] % 32 == 0)
+
+
+def dual_ok(x_shape, w_shape, stride, pads, dil, pconv):
+    """The completing 1x1 / stride-1 conv can run the deferred projection gradient ``pconv`` with its own."""
+    if pconv is None or not (w_shape[0] == 1 and w_shape[1] == 1 and tuple(stride) == (1, 1)
+                             and tuple(pads) == (0, 0, 0, 0) and tuple(dil) == (1, 1)):
+        return False
+    dy2, w2, s2 = pconv[:3]
+    n, h, wd, c = x_shape
+    c1, c2 = w_shape[3], w2.shape[3]
+    return (c % 64 == 0 and c1 % 128 == 0 and c2 % 128 == 0 and 128 * (c1 + c2) <= 160 * 1024 and h > 1 and wd > 1
+            and w2.shape[2] == c and tuple(s2) == (2, 2) and tuple(dy2.shape) == (n, -(-h // 2), -(-wd // 2), c2))
+
+
+def ws_dual(dy, w, pconv, x_shape, tile=None, bn_stats=None):
+    """DX = dgrad(dy, w) [1x1 / stride 1] + dgrad(dy2, w2) [1x1 / stride s2] in one pass (``pconv`` =
+    (dy2, w2, stride)); ``bn_stats`` as in :func:`ws_dgrad`."""
+    n, h, wd, c = x_shape
+    dy2, w2, s2 = pconv[:3]
+    dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
+    bx, bmask, bsum, bsq, bslots = bn_stats if bn_stats is not None else (None, None, None, None, 0)
+    tp, nw, cg = tile or DUAL_TILE
+    if bn_stats is not None and tp > 2:
+        tp = 2                                   # the BN-statistics epilogue's register budget
+    N.check(N.fn("mdtf_conv_ws_dual")(N.ptr(dy), N.ptr(w), N.ptr(dy2), N.ptr(w2), N.ptr(dx), n, h, wd, c,
+                                      w.shape[3], dy2.shape[1], dy2.shape[2], dy2.shape[3], s2[0],
+                                      _ws_code(tp, nw, cg), N.ptr(bx), N.ptr(bmask), N.ptr(bsum), N.ptr(bsq),
+                                      int(bslots), N.stream_ptr()), "conv_ws_dual")
     return dx
 
 
@@ -772,6 +815,30 @@ class _Conv(torch.autograd.Function):
                 else:
                     dw = ldw
         xs = ctx.x_sink if need_dx else None
+        if (xs is not None and not lib_dx and xs.idle() and not xs.completing()
+                and proj_deferrable(w.shape, stride, pads, dil) and cd[0] in ("mdtf", "pp")
+                and (cd[0] == "pp" or cd[4] in (2, 3))):
+            # strided 1x1 projection, first contributor: leave its data gradient to the block's 1x1 conv
+            def _run(out, acc, dy=dy, w=w, xshape=tuple(x.shape), stride=stride, pads=pads, dil=dil, cd=cd):
+                if cd[0] == "pp":
+                    return pp_dgrad(dy, w, xshape, pads, dil, cd[1], out=out, accumulate=acc)
+                return mdtf_dgrad(dy, w, xshape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5], out=out,
+                                  accumulate=acc)
+            xs.defer_conv(dy, w, tuple(stride), _run)
+            need_dx = False
+        elif xs is not None and not lib_dx and dual_ok(x.shape, w.shape, stride, pads, dil, xs.pconv) \
+                and xs.buf is None and xs.pend is None:
+            pc = xs.take_conv()
+            bst = None
+            if xs.stat_req is not None and xs.completing() and BWD_STATS and not N.deterministic():
+                bx, bmask = xs.stat_req
+                sbuf = bwd_stats_acquire(x.device, x.shape[3], STAT_SLOTS)
+                bst = (bx, bmask, sbuf[0], sbuf[1], sbuf.shape[1])
+            xs.written(ws_dual(dy, w, pc, x.shape, bn_stats=bst))
+            if bst is not None:
+                xs.stats = sbuf
+            DUAL_FUSED[0] += 1
+            need_dx = False
         if need_dx and cd[0] == "winograd":
             dx = winograd.winograd_dgrad(dy, w, x.shape, pads)
         elif need_dx and cd[0] == "ws":

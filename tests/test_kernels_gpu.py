@@ -423,6 +423,29 @@ def test_resnet_stage1_every_gradient_matches_cpu_fp32(monkeypatch):
     _check_grads(errs)
 
 
+def test_resnet_projection_dgrad_fused_into_conv1(monkeypatch):
+    """The strided projection's data gradient deferred in the block input's sink and fused with conv1's
+    (mdtf_conv_ws_dual, one pass) == the two data gradients run one after the other (MDTF_DUAL_DGRAD=0): same
+    loss, every gradient as close to the fp32 CPU step; the fused path must actually run (stage-2 unit 1)."""
+    from mdtf.models import resnet
+    from mdtf.ops import conv as C
+    monkeypatch.setattr(resnet, "PROJ_LATE", True)
+    torch.manual_seed(7)
+    x = torch.randn(8, 64, 64, 3)
+    y = torch.randint(0, 16, (8,))
+    n0 = C.DUAL_FUSED[0]
+    lf, gf = _one_step(DEV, torch.bfloat16, x, y, blocks=[1, 1], grads=True)
+    assert C.DUAL_FUSED[0] > n0
+    monkeypatch.setattr(C, "DUAL_DGRAD", False)
+    lo, go = _one_step(DEV, torch.bfloat16, x, y, blocks=[1, 1], grads=True)
+    assert lf == lo
+    # the fused pass rounds the summed gradient once (the unfused one rounds the first contribution to bf16
+    # before accumulating): compare both against fp32; BN parameters whose gradients nearly cancel over the
+    # batch amplify either rounding, so the bound is relative to the unfused error there
+    lc, gc = _one_step("cpu", None, x, y, blocks=[1, 1], grads=True)
+    _check_grads({k: (_rel(gf[k], gc[k]), _rel(go[k], gc[k])) for k in gc})
+
+
 class _Tiny(object):
     """conv-BN-ReLU, max-pool, bottleneck-style residual pair, GAP, dense."""
 
@@ -1532,6 +1555,64 @@ def test_conv_wgrad_8wave_tiles(bm, bn, stages, geo, slab, monkeypatch):
         dw = C.mdtf_wgrad(x.to(DEV), dy.permute(0, 2, 3, 1).contiguous().to(DEV), wt.shape, (s, s), pads, (1, 1),
                           bm, bn, sp, ver=3, stages=stages)
         assert _rel(dw, ref) < 1e-2, sp
+
+
+@pytest.mark.parametrize("geo", [(2, 56, 56, 256, 128, 512, 2), (3, 28, 28, 512, 256, 1024, 2), (2, 15, 13, 64, 128, 128, 2),
+                                 (2, 9, 10, 128, 128, 256, 2)])
+@pytest.mark.parametrize("tile", [(2, 8, 1), (2, 4, 1), (4, 8, 1)])
+def test_conv_ws_dual_fanout_dgrad(geo, tile):
+    """csrc/conv_ws.hip mdtf_conv_ws_dual: the gradient of a block input feeding a 1x1 / stride-1 conv and a
+    1x1 / stride-2 projection, both data gradients in one GEMM (the sampled pixels first in the kernel's pixel order,
+    the others skip the second k-range), plain and with the BN-backward statistics, vs the fp32 autograd sum; odd
+    sizes (the projection's last row / column, unpaired last row)."""
+    from mdtf.ops import conv as C
+    n, h, w, c, c1, c2, s = geo
+    torch.manual_seed(sum(geo) + tile[0] * tile[1])
+    x = torch.zeros(n, c, h, w, requires_grad=True)
+    w1 = (torch.randn(1, 1, c, c1) / c ** 0.5).bfloat16()
+    w2 = (torch.randn(1, 1, c, c2) / c ** 0.5).bfloat16()
+    y1 = torch.nn.functional.conv2d(x, w1.float().permute(3, 2, 0, 1))
+    y2 = torch.nn.functional.conv2d(x, w2.float().permute(3, 2, 0, 1), stride=s)
+    dy1 = torch.randn(y1.shape).bfloat16()
+    dy2 = torch.randn(y2.shape).bfloat16()
+    (y1 * dy1.float()).sum().add((y2 * dy2.float()).sum()).backward()
+    ref = x.grad.permute(0, 2, 3, 1)
+    d1 = dy1.permute(0, 2, 3, 1).contiguous().to(DEV)
+    d2 = dy2.permute(0, 2, 3, 1).contiguous().to(DEV)
+    pc = (d2, w2.to(DEV), (s, s))
+    assert C.dual_ok((n, h, w, c), tuple(w1.shape), (1, 1), (0, 0, 0, 0), (1, 1), pc)
+    dx = C.ws_dual(d1, w1.to(DEV), pc, (n, h, w, c), tile=tile)
+    assert _rel(dx, ref) < 1e-2
+    bx = torch.randn(n, h, w, c).bfloat16()
+    mbits = torch.rand(n * h * w * c) > 0.4
+    packed = (mbits.view(-1, 8).to(torch.int32) << torch.arange(8)).sum(1).to(torch.uint8)
+    bsum = torch.zeros(2, 4, c, device=DEV)
+    gd = C.ws_dual(d1, w1.to(DEV), pc, (n, h, w, c), tile=tile,
+                   bn_stats=(bx.to(DEV), packed.to(DEV), bsum[0], bsum[1], 4))
+    assert _rel(gd, ref) < 1e-2
+    gm = gd.float().cpu().reshape(-1, c) * mbits.view(-1, c).float()
+    assert _rel(bsum[0].sum(0), gm.sum(0)) < 5e-3
+    assert _rel(bsum[1].sum(0), (gm * bx.float().reshape(-1, c)).sum(0)) < 5e-3
+
+
+@pytest.mark.parametrize("splits", [64, 24, 9])
+def test_conv_wgrad_slab_split_groups(splits, monkeypatch):
+    """Slab reduction of many split-K partials for a small filter (1x1 64 -> 64: 16 float4 blocks, up to 64
+    splits, uneven last split), vs the fp32 autograd reference."""
+    from mdtf.ops import conv as C
+    monkeypatch.setattr(C, "WGRAD_SLAB", True)
+    n, h, w, c, co = 2, 56, 56, 64, 64
+    torch.manual_seed(splits)
+    x = torch.randn(n, h, w, c).bfloat16()
+    wt = (torch.randn(1, 1, c, co) / c ** 0.5).bfloat16()
+    wr = wt.float().permute(3, 2, 0, 1).requires_grad_(True)
+    yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wr)
+    dy = torch.randn(yr.shape).bfloat16()
+    yr.backward(dy.float())
+    ref = wr.grad.permute(2, 3, 1, 0)
+    dw = C.mdtf_wgrad(x.to(DEV), dy.permute(0, 2, 3, 1).contiguous().to(DEV), wt.shape, (1, 1), (0, 0, 0, 0),
+                      (1, 1), 128, 128, splits, ver=3, stages=3)
+    assert _rel(dw, ref) < 1e-2
 
 
 WS_TILES = [(4, 8, 1, 4), (4, 8, 2, 6), (4, 4, 1, 4), (2, 8, 1, 8), (2, 4, 2, 4), (4, 8, 4, 4)]
