@@ -297,8 +297,35 @@ __device__ __forceinline__ void load_coef8(const float* __restrict__ p, int c, f
   f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
+// Streaming loads / stores of the elementwise passes.  NT: the nontemporal forms (a read-once / write-once stream
+// should not displace the caches): 198 vs 224 us for the stage-1 BN backward shape, 6.3 vs 5.6 TB/s
+// (bench/bn_bw_probe.hip, profiles/bn_bw_probe_r5q.jsonl).  MDTF_BN_NT=0 restores the cached forms.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const bf16_t* p) {
+  if constexpr (NT) return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p)));
+  return *reinterpret_cast<const uint4*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st_bf8(bf16_t* p, const float (&f)[8]) {
+  u32x4_t w;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = pack_bf2(f[2 * i], f[2 * i + 1]);
+  if constexpr (NT)
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
+  else
+    *reinterpret_cast<u32x4_t*>(p) = w;
+}
+bool bn_nt() {
+  static const bool on = [] {
+    const char* e = getenv("MDTF_BN_NT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // One 8-channel vector of the apply: y = x*scale + shift (+ res) (ReLU) and its ReLU mask byte.
-template <bool HAS_RES, bool RELU>
+template <bool HAS_RES, bool RELU, bool NT = false>
 __device__ __forceinline__ void apply8(const uint4& xr, const uint4& rr, const float (&sc)[8], const float (&sh)[8],
                                        bf16_t* __restrict__ y, uint8_t* __restrict__ mask, long long i) {
   float v[8], r[8];
@@ -315,7 +342,7 @@ __device__ __forceinline__ void apply8(const uint4& xr, const uint4& rr, const f
     }
     v[k] = o;
   }
-  store_bf8(y + i * 8, v);
+  st_bf8<NT>(y + i * 8, v);
   if (RELU && mask) mask[i] = static_cast<uint8_t>(bits);   // 1 bit per element: the backward's ReLU mask
 }
 
@@ -326,7 +353,7 @@ __device__ __forceinline__ void apply8(const uint4& xr, const uint4& rr, const f
 // their 8 channels, so the coefficients are loaded once.
 constexpr int kVpt = 4;
 
-template <bool HAS_RES, bool RELU>
+template <bool HAS_RES, bool RELU, bool NT = false>
 __global__ void __launch_bounds__(kThreads)
     bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
                     uint8_t* __restrict__ mask, long long n8, int C, const float* __restrict__ scale,
@@ -337,8 +364,8 @@ __global__ void __launch_bounds__(kThreads)
 #pragma unroll
   for (int u = 0; u < kVpt; ++u) {
     const long long i = base + u * kThreads;
-    xr[u] = i < n8 ? *reinterpret_cast<const uint4*>(x + i * 8) : z4;
-    rr[u] = (HAS_RES && i < n8) ? *reinterpret_cast<const uint4*>(res + i * 8) : z4;
+    xr[u] = i < n8 ? ld16<NT>(x + i * 8) : z4;
+    rr[u] = (HAS_RES && i < n8) ? ld16<NT>(res + i * 8) : z4;
   }
   const bool fixed = (kThreads * 8) % C == 0;
   float sc[8], sh[8];
@@ -352,12 +379,13 @@ __global__ void __launch_bounds__(kThreads)
       load_coef8(scale, static_cast<int>((i * 8) % C), sc);
       load_coef8(shift, static_cast<int>((i * 8) % C), sh);
     }
-    apply8<HAS_RES, RELU>(xr[u], rr[u], sc, sh, y, mask, i);
+    apply8<HAS_RES, RELU, NT>(xr[u], rr[u], sc, sh, y, mask, i);
   }
 }
 
 // Residual block whose shortcut is a projection conv + BN (no ReLU): y = relu(x*scale + shift + r*scale2 + shift2),
 // the shortcut BN applied on the fly from its conv output r, so its normalised tensor is never written / re-read.
+template <bool NT>
 __global__ void __launch_bounds__(kThreads)
     bn_apply_dual_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r, bf16_t* __restrict__ y,
                          uint8_t* __restrict__ mask, long long n8, int C, const float* __restrict__ scale,
@@ -369,8 +397,8 @@ __global__ void __launch_bounds__(kThreads)
 #pragma unroll
   for (int u = 0; u < kVpt; ++u) {
     const long long i = base + u * kThreads;
-    xr[u] = i < n8 ? *reinterpret_cast<const uint4*>(x + i * 8) : z4;
-    rr[u] = i < n8 ? *reinterpret_cast<const uint4*>(r + i * 8) : z4;
+    xr[u] = i < n8 ? ld16<NT>(x + i * 8) : z4;
+    rr[u] = i < n8 ? ld16<NT>(r + i * 8) : z4;
   }
   const bool fixed = (kThreads * 8) % C == 0;
   float sc[8], sh[8], sc2[8], sh2[8];
@@ -400,7 +428,7 @@ __global__ void __launch_bounds__(kThreads)
       bits |= (o > 0.f ? 1u : 0u) << k;
       v[k] = o;
     }
-    store_bf8(y + i * 8, v);
+    st_bf8<NT>(y + i * 8, v);
     mask[i] = static_cast<uint8_t>(bits);
   }
 }
@@ -456,7 +484,7 @@ __global__ void __launch_bounds__(1024) bn_finalize_bwd2(FinBwd a0, FinBwd a1, l
 }
 
 // One 8-channel vector of the BN backward: dz = dy (ReLU-masked), d(res) = dz, dx = k1*dz + k2*x + k3.
-template <bool RELU, bool WRITE_DRES>
+template <bool RELU, bool WRITE_DRES, bool NT = false>
 __device__ __forceinline__ void dx8(const uint4& gr, const uint4& xr, uint32_t m8, const uint4& orr,
                                     const float (&A)[8], const float (&B)[8], const float (&E)[8],
                                     bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long i, int accum_dres) {
@@ -473,19 +501,19 @@ __device__ __forceinline__ void dx8(const uint4& gr, const uint4& xr, uint32_t m
       unpack8(orr, o);
 #pragma unroll
       for (int k = 0; k < 8; ++k) o[k] += g[k];
-      store_bf8(dres + i * 8, o);
+      st_bf8<NT>(dres + i * 8, o);
     } else {
-      store_bf8(dres + i * 8, g);
+      st_bf8<NT>(dres + i * 8, g);
     }
   }
   float o[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) o[k] = A[k] * g[k] + B[k] * xv[k] + E[k];
-  store_bf8(dx + i * 8, o);
+  st_bf8<NT>(dx + i * 8, o);
 }
 
 // Same chunked structure as bn_apply_kernel (k1..k3 loaded once when C | 2048).
-template <bool RELU, bool WRITE_DRES>
+template <bool RELU, bool WRITE_DRES, bool NT = false>
 __global__ void __launch_bounds__(kThreads)
     bn_dx_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const uint8_t* __restrict__ mk,
                  bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long n8, int C, const float* __restrict__ k1,
@@ -499,10 +527,10 @@ __global__ void __launch_bounds__(kThreads)
   for (int u = 0; u < kVpt; ++u) {
     const long long i = base + u * kThreads;
     const bool ok = i < n8;
-    gr[u] = ok ? *reinterpret_cast<const uint4*>(dy + i * 8) : z4;
-    xr[u] = ok ? *reinterpret_cast<const uint4*>(x + i * 8) : z4;
+    gr[u] = ok ? ld16<NT>(dy + i * 8) : z4;
+    xr[u] = ok ? ld16<NT>(x + i * 8) : z4;
     m8[u] = (RELU && ok) ? mk[i] : 0xffu;
-    orr[u] = (acc && ok) ? *reinterpret_cast<const uint4*>(dres + i * 8) : z4;
+    orr[u] = (acc && ok) ? ld16<NT>(dres + i * 8) : z4;
   }
   const bool fixed = (kThreads * 8) % C == 0;
   float A[8], B[8], E[8];
@@ -520,7 +548,7 @@ __global__ void __launch_bounds__(kThreads)
       load_coef8(k2, c, B);
       load_coef8(k3, c, E);
     }
-    dx8<RELU, WRITE_DRES>(gr[u], xr[u], m8[u], orr[u], A, B, E, dx, dres, i, accum_dres);
+    dx8<RELU, WRITE_DRES, NT>(gr[u], xr[u], m8[u], orr[u], A, B, E, dx, dres, i, accum_dres);
   }
 }
 
@@ -533,18 +561,19 @@ void launch_apply(const void* x, const void* res, void* y, uint8_t* mask, long l
   const bf16_t* r = (const bf16_t*)res;
   const bf16_t* xx = (const bf16_t*)x;
   bf16_t* yy = (bf16_t*)y;
+  const bool nt = bn_nt();
+#define APPLY(R_, L_)                                                                                               \
+  hipLaunchKernelGGL((nt ? bn_apply_kernel<R_, L_, true> : bn_apply_kernel<R_, L_, false>), dim3(ew_grid(n8)),     \
+                     dim3(kThreads), 0, st, xx, R_ ? r : nullptr, yy, L_ ? mask : nullptr, n8, C, scale, shift)
   if (r && relu)
-    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, xx, r, yy, mask, n8, C,
-                       scale, shift);
+    APPLY(true, true);
   else if (r)
-    hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, xx, r, yy, nullptr,
-                       n8, C, scale, shift);
+    APPLY(true, false);
   else if (relu)
-    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, xx, nullptr, yy, mask,
-                       n8, C, scale, shift);
+    APPLY(false, true);
   else
-    hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, xx, nullptr, yy,
-                       nullptr, n8, C, scale, shift);
+    APPLY(false, false);
+#undef APPLY
 }
 
 // one block per contiguous chunk of kVpt * kThreads vectors
@@ -618,7 +647,8 @@ MDTF_EXPORT int mdtf_bn_fwd_dual(const void* x, const void* r, void* y, uint8_t*
                      FinFwd{psum2, psq2, P2, gamma2, beta2, mmean2, mvar2, mean2, invstd2, scale2, shift2, 1}, M, C,
                      decay, eps);
   const long long n8 = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_dual_kernel, dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)x,
+  hipLaunchKernelGGL((bn_nt() ? bn_apply_dual_kernel<true> : bn_apply_dual_kernel<false>), dim3(ew_grid(n8)),
+                     dim3(kThreads), 0, st, (const bf16_t*)x,
                      (const bf16_t*)r, (bf16_t*)y, mask, n8, C, scale, shift, scale2, shift2);
   MDTF_LAUNCH_CHECK();
   return 0;
@@ -686,18 +716,20 @@ namespace {
 void launch_dx(const void* dy, const void* x, const void* mask, void* dx, void* dres, long long M, int C,
                const float* k1, const float* k2, const float* k3, int relu, int accum_dres, hipStream_t st) {
   long long n8 = M * C / 8;
+  const bool nt = bn_nt();
+#define DX(L_, W_)                                                                                                  \
+  hipLaunchKernelGGL((nt ? bn_dx_kernel<L_, W_, true> : bn_dx_kernel<L_, W_, false>), dim3(ew_grid(n8)),          \
+                     dim3(kThreads), 0, st, (const bf16_t*)dy, (const bf16_t*)x, L_ ? (const uint8_t*)mask : nullptr,\
+                     (bf16_t*)dx, W_ ? (bf16_t*)dres : nullptr, n8, C, k1, k2, k3, W_ ? accum_dres : 0)
   if (relu && dres)
-    hipLaunchKernelGGL((bn_dx_kernel<true, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, (const uint8_t*)mask, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3, accum_dres);
+    DX(true, true);
   else if (relu)
-    hipLaunchKernelGGL((bn_dx_kernel<true, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, (const uint8_t*)mask, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3, 0);
+    DX(true, false);
   else if (dres)
-    hipLaunchKernelGGL((bn_dx_kernel<false, true>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, nullptr, (bf16_t*)dx, (bf16_t*)dres, n8, C, k1, k2, k3, accum_dres);
+    DX(false, true);
   else
-    hipLaunchKernelGGL((bn_dx_kernel<false, false>), dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)x, nullptr, (bf16_t*)dx, nullptr, n8, C, k1, k2, k3, 0);
+    DX(false, false);
+#undef DX
 }
 }  // namespace
 
@@ -1344,6 +1376,7 @@ MDTF_EXPORT int mdtf_maxpool_bn_bwd(const void* dy, const uint8_t* arg, const vo
 // reduction; the shortcut's from one reduction over (dy, mask, r).  Then ONE pass reads dy, mask, x, r and
 // writes both input gradients (the unfused path reads dy and the mask twice).
 namespace {
+template <bool NT>
 __global__ void __launch_bounds__(kThreads)
     bn_dx_dual_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
                       const uint8_t* __restrict__ mk, bf16_t* __restrict__ dx, bf16_t* __restrict__ dr, long long n8,
@@ -1356,9 +1389,9 @@ __global__ void __launch_bounds__(kThreads)
   for (int u = 0; u < kVpt; ++u) {
     const long long i = base + u * kThreads;
     const bool ok = i < n8;
-    gr[u] = ok ? *reinterpret_cast<const uint4*>(dy + i * 8) : z4;
-    xr[u] = ok ? *reinterpret_cast<const uint4*>(x + i * 8) : z4;
-    rr[u] = ok ? *reinterpret_cast<const uint4*>(r + i * 8) : z4;
+    gr[u] = ok ? ld16<NT>(dy + i * 8) : z4;
+    xr[u] = ok ? ld16<NT>(x + i * 8) : z4;
+    rr[u] = ok ? ld16<NT>(r + i * 8) : z4;
     m8[u] = ok ? mk[i] : 0u;
   }
   const bool fixed = (kThreads * 8) % C == 0;
@@ -1393,8 +1426,8 @@ __global__ void __launch_bounds__(kThreads)
       o[e] = A[e] * gm + B[e] * xv[e] + E[e];
       o2[e] = A2[e] * gm + B2[e] * rv[e] + E2[e];
     }
-    store_bf8(dx + i * 8, o);
-    store_bf8(dr + i * 8, o2);
+    st_bf8<NT>(dx + i * 8, o);
+    st_bf8<NT>(dr + i * 8, o2);
   }
 }
 }  // namespace
@@ -1432,7 +1465,8 @@ MDTF_EXPORT int mdtf_bn_bwd_dual(const void* dy, const void* x, const void* r, c
     hipLaunchKernelGGL(bn_finalize_bwd2, dim3(ceil_div(C, kFinCh), 1), dim3(kFinCh * kFinGroups), 0, st, sc, sc, M,
                        C);
   const long long n8 = M * C / 8;
-  hipLaunchKernelGGL(bn_dx_dual_kernel, dim3(ew_grid(n8)), dim3(kThreads), 0, st, (const bf16_t*)dy,
+  hipLaunchKernelGGL((bn_nt() ? bn_dx_dual_kernel<true> : bn_dx_dual_kernel<false>), dim3(ew_grid(n8)),
+                     dim3(kThreads), 0, st, (const bf16_t*)dy,
                      (const bf16_t*)x, (const bf16_t*)r, mask, (bf16_t*)dx, (bf16_t*)dr, n8, C, kk, kk2);
   MDTF_LAUNCH_CHECK();
   return 0;
