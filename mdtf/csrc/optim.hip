@@ -56,6 +56,30 @@ __global__ void __launch_bounds__(kThreads) sgd_kernel(long long n, float* __res
   }
 }
 
+// optimizer state streams (master, gradient, moments: read and written once per step) with nontemporal loads /
+// stores; the bf16 shadow the next forward reads stays cached.  MDTF_NT_OPT=0: cached forms.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ float4 ldf4(const float* p, long long i) {
+  if constexpr (NT) return __builtin_bit_cast(float4, __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(p) + i));
+  return reinterpret_cast<const float4*>(p)[i];
+}
+template <bool NT>
+__device__ __forceinline__ void stf4(float* p, long long i, const float4& v) {
+  if constexpr (NT)
+    __builtin_nontemporal_store(__builtin_bit_cast(f32x4_t, v), reinterpret_cast<f32x4_t*>(p) + i);
+  else
+    reinterpret_cast<float4*>(p)[i] = v;
+}
+inline bool nt_opt() {
+  static const bool on = [] {
+    const char* e = getenv("MDTF_NT_OPT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <bool NT>
 __global__ void __launch_bounds__(kThreads) momentum_kernel(long long n, float* __restrict__ w,
                                                            const float* __restrict__ g, float* __restrict__ acc,
                                                            bf16_t* __restrict__ shadow, float lr, float mom, float gs,
@@ -64,9 +88,9 @@ __global__ void __launch_bounds__(kThreads) momentum_kernel(long long n, float* 
   load_dyn(dyn, lr, lr_t, gs);
   long long n4 = n >> 2;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
-    float4 wv = reinterpret_cast<float4*>(w)[i];
-    float4 gv = reinterpret_cast<const float4*>(g)[i];
-    float4 av = reinterpret_cast<float4*>(acc)[i];
+    float4 wv = ldf4<NT>(w, i);
+    float4 gv = ldf4<NT>(g, i);
+    float4 av = ldf4<NT>(acc, i);
     float gx = gv.x * gs + wd * wv.x, gy = gv.y * gs + wd * wv.y;
     float gz = gv.z * gs + wd * wv.z, gw = gv.w * gs + wd * wv.w;
     av.x = mom * av.x + gx;
@@ -84,8 +108,8 @@ __global__ void __launch_bounds__(kThreads) momentum_kernel(long long n, float* 
       wv.z -= lr * av.z;
       wv.w -= lr * av.w;
     }
-    reinterpret_cast<float4*>(acc)[i] = av;
-    reinterpret_cast<float4*>(w)[i] = wv;
+    stf4<NT>(acc, i, av);
+    stf4<NT>(w, i, wv);
     if (shadow) store_shadow4(shadow, i * 4, wv);
   }
 }
@@ -102,6 +126,7 @@ __device__ __forceinline__ float adam1(float& w, float g, float& m, float& v, fl
   return w;
 }
 
+template <bool NT>
 __global__ void __launch_bounds__(kThreads) adam_kernel(long long n, float* __restrict__ w, const float* __restrict__ g,
                                                        float* __restrict__ m, float* __restrict__ v,
                                                        bf16_t* __restrict__ shadow, float lr, float lr_t, float b1,
@@ -110,17 +135,17 @@ __global__ void __launch_bounds__(kThreads) adam_kernel(long long n, float* __re
   load_dyn(dyn, lr, lr_t, gs);
   long long n4 = n >> 2;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
-    float4 wv = reinterpret_cast<float4*>(w)[i];
-    float4 gv = reinterpret_cast<const float4*>(g)[i];
-    float4 mv = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float4 wv = ldf4<NT>(w, i);
+    float4 gv = ldf4<NT>(g, i);
+    float4 mv = ldf4<NT>(m, i);
+    float4 vv = ldf4<NT>(v, i);
     adam1(wv.x, gv.x, mv.x, vv.x, lr, lr_t, b1, b2, eps, gs, wd, decoupled);
     adam1(wv.y, gv.y, mv.y, vv.y, lr, lr_t, b1, b2, eps, gs, wd, decoupled);
     adam1(wv.z, gv.z, mv.z, vv.z, lr, lr_t, b1, b2, eps, gs, wd, decoupled);
     adam1(wv.w, gv.w, mv.w, vv.w, lr, lr_t, b1, b2, eps, gs, wd, decoupled);
-    reinterpret_cast<float4*>(m)[i] = mv;
-    reinterpret_cast<float4*>(v)[i] = vv;
-    reinterpret_cast<float4*>(w)[i] = wv;
+    stf4<NT>(m, i, mv);
+    stf4<NT>(v, i, vv);
+    stf4<NT>(w, i, wv);
     if (shadow) store_shadow4(shadow, i * 4, wv);
   }
 }
@@ -219,7 +244,7 @@ MDTF_EXPORT int mdtf_fused_sgd(long long n, void* w, const void* g, void* shadow
 MDTF_EXPORT int mdtf_fused_momentum(long long n, void* w, const void* g, void* acc, void* shadow, float lr, float mom,
                                     float gs, float wd, int nesterov, const void* dyn, hipStream_t st) {
   if (n % 4) return MDTF_EINVAL;
-  hipLaunchKernelGGL(momentum_kernel, dim3(grid_for(n / 4)), dim3(kThreads), 0, st, n, (float*)w, (const float*)g,
+  hipLaunchKernelGGL((nt_opt() ? momentum_kernel<true> : momentum_kernel<false>), dim3(grid_for(n / 4)), dim3(kThreads), 0, st, n, (float*)w, (const float*)g,
                      (float*)acc, (bf16_t*)shadow, lr, mom, gs, wd, nesterov, (const float*)dyn);
   MDTF_LAUNCH_CHECK();
   return 0;
@@ -229,7 +254,7 @@ MDTF_EXPORT int mdtf_fused_adam(long long n, void* w, const void* g, void* m, vo
                                 float lr_t, float b1, float b2, float eps, float gs, float wd, int decoupled,
                                 const void* dyn, hipStream_t st) {
   if (n % 4) return MDTF_EINVAL;
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4)), dim3(kThreads), 0, st, n, (float*)w, (const float*)g,
+  hipLaunchKernelGGL((nt_opt() ? adam_kernel<true> : adam_kernel<false>), dim3(grid_for(n / 4)), dim3(kThreads), 0, st, n, (float*)w, (const float*)g,
                      (float*)m, (float*)v, (bf16_t*)shadow, lr, lr_t, b1, b2, eps, gs, wd, decoupled,
                      (const float*)dyn);
   MDTF_LAUNCH_CHECK();
