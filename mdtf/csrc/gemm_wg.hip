@@ -44,8 +44,12 @@ struct WgArgs {
   float* cf[4];
   long long ldc;
   float* db[4];              // column sums of B added here (null: none)
-  float* slab;               // splits > 1: [tiles][splits][BM * 128] partial tiles
+  float* slab;               // splits > 1: [tiles][splits][BM * 128] partial tiles (stream-K: [tiles][maxp][..])
   int* cnt;                  // splits > 1: per-tile arrival tickets, 0 on entry, reset by the last arriver
+  // stream-K (sk_q > 0): worker w of the grid runs K-tile iterations [w sk_q, (w + 1) sk_q) of the tile-major
+  // sequence (tile t owns [t KT, (t + 1) KT)), so every worker does the same work whatever tiles x splits is;
+  // the pieces of a tile (at most maxp) are summed by its last arriver as the splits are
+  int sk_q, kt_total, maxp;
 };
 
 __device__ __forceinline__ void dma16(i32x4_t rsrc, unsigned lds_addr, unsigned voff, int soff) {
@@ -69,7 +73,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // of a transposed read touches ({0-3} + 8 fq and +4) land in 8 distinct 32-B bank slots.
 __device__ __forceinline__ int trg(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 
-template <int BM, int STAGES, bool PIPE>
+template <int BM, int STAGES, bool PIPE, bool SK = false>
 __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
   constexpr int BN = 128;
   constexpr int NT = 2 * BM, NW = NT / 64;          // waves: (BM / 64) rows x 2 columns of 64x64 blocks
@@ -86,10 +90,15 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
   const int ntiles = a.tiles_m * a.tiles_n;
-  const int lid = xcd_remap(blockIdx.x, ntiles * a.splits);
-  const int split = lid / ntiles, tile = lid - split * ntiles;
-  // tile order inside a split: gm x gn blocks (row-major over the block grid, edge blocks partial), so the
-  // contiguous range of logical ids one XCD gets shares few operand panels in its L2
+  const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<unsigned long long>(
+      (__attribute__((address_space(3))) char*)smem));
+  const i32x4_t ra = buffer_rsrc(a.A, a.bytes_a);
+  const i32x4_t rb = buffer_rsrc(a.B, a.bytes_b);
+
+  // one piece: K-tiles [kt0, kt0 + T) of tile `tile`, piece `pidx` of the tile's `np` (np == 1: the whole tile)
+  auto run_piece = [&](int tile, int kt0, int T, int pidx, int np) {
+  // tile order: gm x gn blocks (row-major over the block grid, edge blocks partial), so the contiguous range of
+  // logical ids one XCD gets shares few operand panels in its L2
   int tm, tn;
   {
     const int gi = tile / (a.gm * a.tiles_n);
@@ -102,14 +111,7 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
     tn = gj * a.gn + r3 - (r3 / wn) * wn;
   }
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kt0 = split * a.kt_split;
-  const int T = min(a.kt_split, a.K / 64 - kt0);
   const int seg = n0 / a.seg_cols;
-
-  const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<unsigned long long>(
-      (__attribute__((address_space(3))) char*)smem));
-  const i32x4_t ra = buffer_rsrc(a.A, a.bytes_a);
-  const i32x4_t rb = buffer_rsrc(a.B, a.bytes_b);
 
   // per-lane DMA source offset of this wave's first instruction into an image of pitch P; the wave's later
   // instructions are RJ k rows further (a multiple of 16: same swizzle), a wave-uniform soffset
@@ -239,8 +241,8 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) unsafeAtomicAdd(db + 16 * j + e, accb[j][e]);
   }
-  if (a.splits > 1) {
-    float4v* sl = reinterpret_cast<float4v*>(a.slab) + ((long long)tile * a.splits + split) * (BM * BN / 4);
+  if (np > 1) {
+    float4v* sl = reinterpret_cast<float4v*>(a.slab) + ((long long)tile * a.maxp + pidx) * (BM * BN / 4);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -253,7 +255,7 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int prev = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = prev == a.splits - 1;
+      const int last = prev == np - 1;
       if (last) {
         __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -264,14 +266,14 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
     __syncthreads();
     if (!*flag) return;
     // the last arriver: sum the slabs in split order (deterministic), own partial from registers
-    const float4v* s0 = reinterpret_cast<const float4v*>(a.slab) + (long long)tile * a.splits * (BM * BN / 4);
+    const float4v* s0 = reinterpret_cast<const float4v*>(a.slab) + (long long)tile * a.maxp * (BM * BN / 4);
     float4v sum[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) sum[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < a.splits; ++s) {     // wave-uniform branch: all 16 loads of a slab issue together
-      if (s == split) {
+    for (int s = 0; s < np; ++s) {           // wave-uniform branch: all 16 loads of a slab issue together
+      if (s == pidx) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -308,18 +310,48 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
       *dst = o;
     }
   }
+  };
+
+  if constexpr (!SK) {
+    const int lid = xcd_remap(blockIdx.x, ntiles * a.splits);
+    const int split = lid / ntiles, tile = lid - split * ntiles;
+    const int kt0 = split * a.kt_split;
+    run_piece(tile, kt0, min(a.kt_split, a.K / 64 - kt0), split, a.splits);
+  } else {
+    // stream-K: this worker's iteration range, cut at tile boundaries; pieces of one tile are consecutive workers
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int KT = a.kt_total;
+    const long long total = (long long)ntiles * KT;
+    long long it = (long long)w * a.sk_q;
+    const long long end = min(total, it + a.sk_q);
+    bool first = true;
+    while (it < end) {
+      const int tile = (int)(it / KT), k0 = (int)(it - (long long)tile * KT);
+      const int T = (int)min((long long)KT - k0, end - it);
+      const int wf = (int)(((long long)tile * KT) / a.sk_q), wl = (int)(((long long)tile * KT + KT - 1) / a.sk_q);
+      if (!first) __syncthreads();           // every wave is done with the previous piece's LDS slots
+      first = false;
+      run_piece(tile, k0, T, w - wf, wl - wf + 1);
+      it += T;
+    }
+  }
 }
 
 template <int BM, int STAGES, bool PIPE>
 int launch_wg(const WgArgs& a, hipStream_t st) {
   constexpr int lds = STAGES * (BM + 128) * 128;
-  auto k = gemm_wg_kernel<BM, STAGES, PIPE>;
+  auto k = a.sk_q > 0 ? gemm_wg_kernel<BM, STAGES, PIPE, true> : gemm_wg_kernel<BM, STAGES, PIPE, false>;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_wg_kernel<BM, STAGES, PIPE, true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_wg_kernel<BM, STAGES, PIPE, false>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(a.tiles_m * a.tiles_n * a.splits), dim3(2 * BM), lds, st, a);
+  const long long grid = a.sk_q > 0 ? ceil_div((long long)a.tiles_m * a.tiles_n * a.kt_total, (long long)a.sk_q)
+                                     : (long long)a.tiles_m * a.tiles_n * a.splits;
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(2 * BM), lds, st, a);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
@@ -334,9 +366,17 @@ MDTF_EXPORT long long mdtf_gemm_wg_slab_floats(int M, int N, int bm, int splits)
   return (long long)(M / bm) * (N / 128) * splits * bm * 128;
 }
 
+// The same with K known: splits < 0 is stream-K over -splits workers (tiles * maxp partial tiles).
+MDTF_EXPORT long long mdtf_gemm_wg_slab_floats_k(int M, int N, int K, int bm, int splits) {
+  if (splits >= 0) return mdtf_gemm_wg_slab_floats(M, N, bm, splits);
+  const long long tiles = (long long)(M / bm) * (N / 128), KT = K / 64;
+  const long long q = ceil_div(tiles * KT, (long long)-splits);
+  return tiles * (ceil_div(KT, q) + 1) * bm * 128;
+}
+
 // C_s[M][seg_cols] (fp32, ldc) += A^T B over the segment's columns; A [K][lda], B [K][ldb] bf16 (k-major), M % bm,
 // N % 128, K % 64 and seg_cols % 128 == 0.  bm: 128 or 256; stages 2..4 (negative: the pipelined loop); splits: K-split count (clamped so every
-// split has at least one 64-deep tile).  dbias (per segment, may be null): += column sums of B.  slab / cnt:
+// split has at least one 64-deep tile), or -G: stream-K over G workers (every worker the same number of K-tiles).  dbias (per segment, may be null): += column sums of B.  slab / cnt:
 // workspace of mdtf_gemm_wg_slab_floats() floats and tiles zeroed ints (splits > 1).  Returns the splits used
 // (> 0) or a negative MDTF status.
 MDTF_EXPORT int mdtf_gemm_wg(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
@@ -357,11 +397,24 @@ MDTF_EXPORT int mdtf_gemm_wg(const bf16_t* A, long long lda, const bf16_t* B, lo
   a.tiles_m = M / bm;
   a.tiles_n = N / 128;
   const int KT = K / 64;
-  if (splits < 1) splits = 1;
-  if (splits > KT) splits = KT;
-  a.kt_split = (KT + splits - 1) / splits;
-  a.splits = (KT + a.kt_split - 1) / a.kt_split;
-  if (a.splits > 1 && (slab == nullptr || cnt == nullptr)) return MDTF_EINVAL;
+  a.kt_total = KT;
+  if (splits < 0) {
+    // stream-K over -splits workers
+    const long long total = (long long)a.tiles_m * a.tiles_n * KT;
+    const long long q = ceil_div(total, (long long)-splits);
+    a.sk_q = (int)q;
+    a.maxp = (int)ceil_div((long long)KT, q) + 1;
+    a.splits = 1;
+    a.kt_split = KT;
+    if (slab == nullptr || cnt == nullptr) return MDTF_EINVAL;
+  } else {
+    if (splits < 1) splits = 1;
+    if (splits > KT) splits = KT;
+    a.kt_split = (KT + splits - 1) / splits;
+    a.splits = (KT + a.kt_split - 1) / a.kt_split;
+    a.maxp = a.splits;
+    if (a.splits > 1 && (slab == nullptr || cnt == nullptr)) return MDTF_EINVAL;
+  }
   a.bytes_a = (int)(K * lda * 2);
   a.bytes_b = (int)(K * ldb * 2);
   a.nseg = nseg;
@@ -377,7 +430,7 @@ MDTF_EXPORT int mdtf_gemm_wg(const bf16_t* A, long long lda, const bf16_t* B, lo
   // (gm * bm + gn * 128) -- a speed choice only, any gm / gn is correct
   {
     const int tiles = a.tiles_m * a.tiles_n;
-    const int per_xcd = (tiles * a.splits + 7) / 8;
+    const int per_xcd = a.sk_q > 0 ? (tiles + 7) / 8 : (tiles * a.splits + 7) / 8;
     const int want = per_xcd < tiles ? per_xcd : tiles;
     int best = 1 << 30;
     a.gm = a.tiles_m;

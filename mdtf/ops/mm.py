@@ -156,6 +156,13 @@ def wgrad_into(gws, x, dy, dbs=None, tile=None, splits=None):
 N.register("mdtf_gemm_wg", [N.P, N.L, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.P, N.L, N.P, N.I, N.I, N.I, N.P, N.P,
                             N.P])
 N.register("mdtf_gemm_wg_slab_floats", [N.I, N.I, N.I, N.I], N.L)
+N.register("mdtf_gemm_wg_slab_floats_k", [N.I, N.I, N.I, N.I, N.I], N.L)
+# stream-K weight gradients (MDTF_WG_SK=1): every CU runs the same number of K-tiles, cut at tile boundaries,
+# instead of tiles x splits workgroups that leave CUs idle (BERT-base: 72 tiles x 3 = 216 of 256 CUs).  Off: a
+# worker whose range crosses a tile boundary pays a second pipeline fill + slab epilogue (+ the last arriver's
+# sum) on the critical path -- 256 workers 72-86 us vs 55-64 us for the split grid (profiles/wg_sk_probe_r5w.jsonl),
+# BERT step 6045 vs 6509 seq/s
+WG_SK = os.environ.get("MDTF_WG_SK", "0") == "1"
 
 # (M, N, K) -> (bm, stages, splits): graph-timed on an MI355X (bench/gemm_wg_probe.py, profiles/gemm_wg_probe_r3b.jsonl;
 # the 3/4-stage rings and the mid-tile-barrier loop (stages < 0) measured slower than the 2-stage ring on every shape)
@@ -210,9 +217,11 @@ def wg_into(gws, x, dy, dbs=None, bm=None, stages=None, splits=None):
         return False
     pb, ps, psp = wg_pick(Kin, Nn, T)
     bm, stages, splits = bm or pb, stages or ps, splits or psp
+    if WG_SK and splits > 1 and not N.deterministic():
+        splits = -(CUS * (1 if bm == 256 else 2))      # stream-K over one (256-row) / two workgroups per CU
     if N.deterministic():
         dbs = None
-    slab_n = N.fn("mdtf_gemm_wg_slab_floats")(Kin, Nn, bm, splits)
+    slab_n = N.fn("mdtf_gemm_wg_slab_floats_k")(Kin, Nn, T, bm, splits)
     slab = torch.empty(max(slab_n, 1), dtype=torch.float32, device=x.device) if slab_n > 0 else None
     cnt = _tickets(x.device, (Kin // bm) * (Nn // 128)) if slab_n > 0 else None
     rc = N.fn("mdtf_gemm_wg")(N.ptr(x), x.stride(0), N.ptr(dy), dy.stride(0), Kin, Nn, T, len(gws), ns,

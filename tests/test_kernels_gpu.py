@@ -2021,11 +2021,17 @@ def test_gemm_core_segments_and_fused_epilogues():
 @pytest.mark.parametrize("bm,stages", [(128, 2), (128, 3), (128, -3), (128, -4), (256, 2), (256, 3), (256, -3)])
 @pytest.mark.parametrize("T,K,N,nseg", [(8192, 768, 2304, 3), (4096, 3072, 768, 1), (704, 256, 384, 1),
                                         (64, 256, 128, 1)])
-@pytest.mark.parametrize("splits", [1, 3, 7])
-def test_gemm_wg_vs_fp32(bm, stages, T, K, N, nseg, splits):
+@pytest.mark.parametrize("splits", [1, 3, 7, -5, -37, -256])
+@pytest.mark.parametrize("sk", [True, False])
+def test_gemm_wg_vs_fp32(bm, stages, T, K, N, nseg, splits, sk, monkeypatch):
     """C_s (fp32) += x^T dy[:, seg s] with the fused bias column sums, every ring depth / loop variant and split
-    count (slabs summed by the last arriving workgroup), vs fp32; repeated launches are bitwise equal."""
+    count (slabs summed by the last arriving workgroup; splits > 1 run stream-K when sk, negative splits are
+    stream-K worker counts: pieces cut at tile boundaries, uneven last worker), vs fp32; repeated launches are
+    bitwise equal."""
     from mdtf.ops import mm
+    if splits < 0 and not sk:
+        pytest.skip("explicit stream-K worker count")
+    monkeypatch.setattr(mm, "WG_SK", sk)
     if K % bm:
         pytest.skip("tile does not divide K")
     torch.manual_seed(T + K + splits)
