@@ -133,15 +133,17 @@ __global__ void __launch_bounds__(kThreads)
   const int W = tpr * 8;
   float* L0 = smem;
   float* L1 = smem + rg * W;
-  // each thread's 8 partials as two 16-B stores: the 8 lanes of a store group cover 256 contiguous bytes (all 64
-  // banks once); eight scalar stores at an 8-float stride put 32 lanes on 4 banks
+  // each thread's 8 partials as two 16-B stores into lane-contiguous halves (element 4h + e of channel vector
+  // lane_c at h * 4 tpr + 4 lane_c + e): the 8 lanes of a ds_write_b128 group write 128 contiguous bytes, all 32
+  // banks once (the thread-contiguous form, 32 B per lane, put lanes l and l + 4 on the same banks: 25 % conflicts
+  // in pmc_resnet50_r4p)
   {
-    float4* d0 = reinterpret_cast<float4*>(L0 + rgi * W + lane_c * 8);
-    float4* d1 = reinterpret_cast<float4*>(L1 + rgi * W + lane_c * 8);
-    d0[0] = make_float4(s0[0], s0[1], s0[2], s0[3]);
-    d0[1] = make_float4(s0[4], s0[5], s0[6], s0[7]);
-    d1[0] = make_float4(s1[0], s1[1], s1[2], s1[3]);
-    d1[1] = make_float4(s1[4], s1[5], s1[6], s1[7]);
+    float4* d0 = reinterpret_cast<float4*>(L0 + rgi * W);
+    float4* d1 = reinterpret_cast<float4*>(L1 + rgi * W);
+    d0[lane_c] = make_float4(s0[0], s0[1], s0[2], s0[3]);
+    d0[tpr + lane_c] = make_float4(s0[4], s0[5], s0[6], s0[7]);
+    d1[lane_c] = make_float4(s1[0], s1[1], s1[2], s1[3]);
+    d1[tpr + lane_c] = make_float4(s1[4], s1[5], s1[6], s1[7]);
   }
   __syncthreads();
   // tree over row groups (consecutive threads on consecutive floats)
@@ -154,7 +156,8 @@ __global__ void __launch_bounds__(kThreads)
     __syncthreads();
   }
   for (int k = t; k < W; k += kThreads) {
-    int c = blockIdx.y * W + k;
+    const int h = k / (4 * tpr), r = k - h * 4 * tpr;
+    const int c = blockIdx.y * W + (r >> 2) * 8 + 4 * h + (r & 3);
     if (c < C) {
       p0[(long long)blockIdx.x * C + c] = L0[k];
       p1[(long long)blockIdx.x * C + c] = L1[k];
@@ -908,12 +911,13 @@ __global__ void __launch_bounds__(kThreads)
   float* L0 = smem;
   float* L1 = smem + rg * W;
   {
-    float4* d0 = reinterpret_cast<float4*>(L0 + rgi * W + lane_c * 8);
-    float4* d1 = reinterpret_cast<float4*>(L1 + rgi * W + lane_c * 8);
-    d0[0] = make_float4(s0[0], s0[1], s0[2], s0[3]);
-    d0[1] = make_float4(s0[4], s0[5], s0[6], s0[7]);
-    d1[0] = make_float4(s1[0], s1[1], s1[2], s1[3]);
-    d1[1] = make_float4(s1[4], s1[5], s1[6], s1[7]);
+    // lane-contiguous halves (as bn_reduce_kernel): conflict-free 16-B LDS stores
+    float4* d0 = reinterpret_cast<float4*>(L0 + rgi * W);
+    float4* d1 = reinterpret_cast<float4*>(L1 + rgi * W);
+    d0[lane_c] = make_float4(s0[0], s0[1], s0[2], s0[3]);
+    d0[tpr + lane_c] = make_float4(s0[4], s0[5], s0[6], s0[7]);
+    d1[lane_c] = make_float4(s1[0], s1[1], s1[2], s1[3]);
+    d1[tpr + lane_c] = make_float4(s1[4], s1[5], s1[6], s1[7]);
   }
   __syncthreads();
   for (int step = rg / 2; step > 0; step >>= 1) {
@@ -925,7 +929,8 @@ __global__ void __launch_bounds__(kThreads)
     __syncthreads();
   }
   for (int k = t; k < W; k += kThreads) {
-    const int c = blockIdx.y * W + k;
+    const int h = k / (4 * tpr), r = k - h * 4 * tpr;
+    const int c = blockIdx.y * W + (r >> 2) * 8 + 4 * h + (r & 3);
     if (c < g.C) {
       p0[(long long)blockIdx.x * g.C + c] = L0[k];
       p1[(long long)blockIdx.x * g.C + c] = L1[k];
@@ -1243,12 +1248,13 @@ __global__ void __launch_bounds__(kThreads)
   float* L0 = smem;
   float* L1 = smem + rg * W;
   {
-    float4* d0 = reinterpret_cast<float4*>(L0 + rgi * W + lane_c * 8);
-    float4* d1 = reinterpret_cast<float4*>(L1 + rgi * W + lane_c * 8);
-    d0[0] = make_float4(s0[0], s0[1], s0[2], s0[3]);
-    d0[1] = make_float4(s0[4], s0[5], s0[6], s0[7]);
-    d1[0] = make_float4(s1[0], s1[1], s1[2], s1[3]);
-    d1[1] = make_float4(s1[4], s1[5], s1[6], s1[7]);
+    // lane-contiguous halves (as bn_reduce_kernel): conflict-free 16-B LDS stores
+    float4* d0 = reinterpret_cast<float4*>(L0 + rgi * W);
+    float4* d1 = reinterpret_cast<float4*>(L1 + rgi * W);
+    d0[lane_c] = make_float4(s0[0], s0[1], s0[2], s0[3]);
+    d0[tpr + lane_c] = make_float4(s0[4], s0[5], s0[6], s0[7]);
+    d1[lane_c] = make_float4(s1[0], s1[1], s1[2], s1[3]);
+    d1[tpr + lane_c] = make_float4(s1[4], s1[5], s1[6], s1[7]);
   }
   __syncthreads();
   for (int step = rg / 2; step > 0; step >>= 1) {
@@ -1260,7 +1266,8 @@ __global__ void __launch_bounds__(kThreads)
     __syncthreads();
   }
   for (int k = t; k < W; k += kThreads) {
-    const int c = blockIdx.y * W + k;
+    const int h = k / (4 * tpr), r = k - h * 4 * tpr;
+    const int c = blockIdx.y * W + (r >> 2) * 8 + 4 * h + (r & 3);
     if (c < g.C) {
       p0[(long long)blockIdx.x * g.C + c] = L0[k];
       p1[(long long)blockIdx.x * g.C + c] = L1[k];
