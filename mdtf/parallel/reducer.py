@@ -57,6 +57,29 @@ import torch
 import torch.distributed as dist
 
 
+
+class _DoneThen(object):
+    """An async collective's work handle whose ``wait`` also runs a follow-up (the shard copy of an emulated
+    reduce-scatter)."""
+    __slots__ = ("work", "then")
+
+    def __init__(self, work, then):
+        self.work, self.then = work, then
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+            self.then()
+        return True
+
+
+# gloo's reduce_scatter / all_gather move the same bytes as its all_reduce but cost 1.7-1.9x / 1.7x as much
+# (2 ranks, 64 MiB: 122 / 114 ms vs 66 ms, profiles/sharded_vs_allreduce_r5.md); on gloo the sharded mode runs
+# them as all_reduces (reduce-scatter: all_reduce + own shard; all-gather: all_reduce of the zero-padded
+# shard).  RCCL keeps the native collectives (its all_reduce IS reduce-scatter + all-gather).
+GLOO_VIA_ALLREDUCE = os.environ.get("MDTF_GLOO_RS_AR", "1") != "0"
+
 class UpdateTarget(object):
     """Tensors one fused optimizer launch operates on."""
     __slots__ = ("group", "master", "grad", "shadow", "numel", "key", "decay")
@@ -285,8 +308,40 @@ class GradReducer(object):
             # backward nodes that have not run yet (the values they read are unchanged: this bucket's layers'
             # backward is complete), so the gather must not trip autograd's in-place check
             dst = (g.shadow if g.shadow is not None else g.master).data[b.start:b.end]
-            b.gather = dist.all_gather_into_tensor(dst, src, group=self.pg, async_op=True)
+            b.gather = self._all_gather(dst, src)
         b.updated = True
+
+    def _gloo_emulate(self):
+        if not GLOO_VIA_ALLREDUCE or self.world == 1:
+            return False
+        if getattr(self, "_is_gloo", None) is None:
+            self._is_gloo = dist.get_backend(self.pg) == "gloo"
+        return self._is_gloo
+
+    def _reduce_scatter(self, out, inp, async_op=True):
+        """out (this rank's 1/world of inp) = sum over ranks of inp's shard."""
+        if not self._gloo_emulate():
+            return dist.reduce_scatter_tensor(out, inp, group=self.pg, async_op=async_op)
+        n = out.numel()
+        r = dist.get_rank(self.pg)
+        w = dist.all_reduce(inp, group=self.pg, async_op=True)
+        done = _DoneThen(w, lambda: out.copy_(inp[r * n:(r + 1) * n]))
+        if not async_op:
+            done.wait()
+        return done
+
+    def _all_gather(self, dst, src, async_op=True):
+        """dst (world x src) = every rank's src, in rank order."""
+        if not self._gloo_emulate():
+            return dist.all_gather_into_tensor(dst, src, group=self.pg, async_op=async_op)
+        n = src.numel()
+        r = dist.get_rank(self.pg)
+        own = src.clone() if src.data_ptr() >= dst.data_ptr() and src.data_ptr() < dst.data_ptr() + dst.numel() * \
+            dst.element_size() else src
+        dst.zero_()
+        dst[r * n:(r + 1) * n].copy_(own)
+        w = dist.all_reduce(dst, group=self.pg, async_op=async_op)
+        return w
 
     def _launch(self, b):
         if b.launched:
@@ -303,12 +358,12 @@ class GradReducer(object):
             if self.mode == "allreduce":
                 b.work = dist.all_reduce(wire, group=self.pg, async_op=True)
             else:
-                b.work = dist.reduce_scatter_tensor(wshard, wire, group=self.pg, async_op=True)
+                b.work = self._reduce_scatter(wshard, wire)
         elif self.mode == "allreduce":
             b.work = dist.all_reduce(g.grad[b.start:b.end], group=self.pg, async_op=True)
         else:
             out = self._shards[id(g)]["grad"][b.shard_offset:b.shard_offset + b.shard_len]
-            b.work = dist.reduce_scatter_tensor(out, g.grad[b.start:b.end], group=self.pg, async_op=True)
+            b.work = self._reduce_scatter(out, g.grad[b.start:b.end])
         if self.eager_update is not None:
             self._update_bucket(b)
 
@@ -490,7 +545,7 @@ class GradReducer(object):
                 if not self.collective:
                     dst.copy_(part)
                 else:
-                    works.append(dist.all_gather_into_tensor(dst, part, group=self.pg, async_op=True))
+                    works.append(self._all_gather(dst, part))
         for w in works:
             w.wait()
 
@@ -509,7 +564,7 @@ class GradReducer(object):
                 if self.world == 1:
                     dst.copy_(part)
                 else:
-                    dist.all_gather_into_tensor(dst, part, group=self.pg)
+                    self._all_gather(dst, part, async_op=False)
 
     def gather_full_state(self, target_key, name):
         """Full-size optimizer state buffer for checkpointing (sharded → gathered)."""
@@ -525,7 +580,7 @@ class GradReducer(object):
                 if self.world == 1:
                     full[b.start:b.end].copy_(part)
                 else:
-                    dist.all_gather_into_tensor(full[b.start:b.end], part, group=self.pg)
+                    self._all_gather(full[b.start:b.end], part, async_op=False)
             out.append(full)
         return out
 
