@@ -150,6 +150,10 @@ def main():
     p.add_argument("--merge", action="store_true", help="update the existing table at --out instead of replacing it")
     p.add_argument("--graph", action="store_true",
                    help="time the mdtf and Winograd candidates inside captured graphs (no host launch cost)")
+    p.add_argument("--step_epilogues", action="store_true",
+                   help="dgrad: time every candidate with the epilogue the training step runs -- the BN-backward "
+                        "statistics of the gradient it completes, plus (block inputs: 1x1 stride-1 convs narrowing "
+                        "the channels) the masked identity-shortcut gradient folded in; adds the ping-pong core")
     args = p.parse_args()
     GRAPH[0] = args.graph
     dev = torch.device("cuda")
@@ -182,8 +186,14 @@ def main():
                 cands += [(t, 0, 0, 4) for t in ws_tiles("fwd", c, co, kh, kw, s)]
                 wtt = C.transpose_filter(wt)
 
+                if args.step_epilogues:
+                    cands += [(t, 0, 0, 5) for t in C.PP_TILES if C.pp_ok("fwd", c, co, (s, s), kh, kw, t)]
+
                 # training always runs conv -> BN: time the forward with its fused statistics epilogue
                 def mk(bm, bn, sp, v):
+                    if v == 5:
+                        st = _stats(co, C.PP_TILES[bm][0], n * oh * ow)
+                        return lambda: C.pp_fwd(x, wt, (oh, ow), (s, s), pads4, (1, 1), bm, st)
                     if v == 4:
                         st = _stats(co, 128, n * oh * ow)
                         return lambda: C.ws_fwd(x, wtt, kh, kw, (oh, ow), (s, s), pads4, (1, 1), bm, st)
@@ -197,10 +207,31 @@ def main():
                     cands += [(bm, bn, st, 3) for bm, bn, st in V3_TILES]
                 cands += [(t, 0, 0, 4) for t in ws_tiles("dgrad", c, co, kh, kw, s)]
 
-                def mk(bm, bn, sp, v):
-                    if v == 4:
-                        return lambda: C.ws_dgrad(dy, wt, x.shape, pads4, (1, 1), bm)
-                    return lambda: C.mdtf_dgrad(dy, wt, x.shape, (s, s), pads4, (1, 1), bm, bn, v, sp)
+                if args.step_epilogues:
+                    cands = [cd for cd in cands if cd[3] != 1]          # v1: no statistics epilogue
+                    cands += [(t, 0, 0, 5) for t in C.PP_TILES if C.pp_ok("dgrad", c, co, (s, s), kh, kw, t)]
+                    bx = torch.randn(n, h, w, c, device=dev).bfloat16()
+                    mbits = torch.randint(0, 256, (n * h * w * c // 8,), device=dev, dtype=torch.uint8)
+                    sb = torch.zeros(2, C.STAT_SLOTS, c, device=dev)
+                    bst = (bx, mbits, sb[0], sb[1], C.STAT_SLOTS)
+                    block_in = kh == 1 and s == 1 and c > co
+                    pend = (torch.randn(n, h, w, c, device=dev).bfloat16(), mbits) if block_in else None
+                    dxb = torch.empty(n, h, w, c, device=dev, dtype=torch.bfloat16)
+
+                    def mk(bm, bn, sp, v):
+                        if v == 4:
+                            return lambda: C.ws_dgrad(dy, wt, x.shape, pads4, (1, 1), (2,) + tuple(bm[1:]), out=dxb,
+                                                      bn_stats=bst, acc_src=pend)
+                        if v == 5:
+                            return lambda: C.pp_dgrad(dy, wt, x.shape, pads4, (1, 1), bm, out=dxb, bn_stats=bst,
+                                                      acc_src=pend)
+                        return lambda: C.mdtf_dgrad(dy, wt, x.shape, (s, s), pads4, (1, 1), bm, bn, v, sp, out=dxb,
+                                                    bn_stats=bst, acc_src=pend)
+                else:
+                    def mk(bm, bn, sp, v):
+                        if v == 4:
+                            return lambda: C.ws_dgrad(dy, wt, x.shape, pads4, (1, 1), bm)
+                        return lambda: C.mdtf_dgrad(dy, wt, x.shape, (s, s), pads4, (1, 1), bm, bn, v, sp)
             else:
                 lib = lambda: C.miopen_bwd(x, wt, dy, (s, s), pads4, (1, 1), False, True)  # noqa: E731
                 cands = [(bm, bn, sp, 1) for bm, bn in ((128, 128), (64, 64), (128, 64), (64, 128))
@@ -223,6 +254,8 @@ def main():
                 except RuntimeError:
                     t_wino = timeit(wfn, args.reps)
             best = None
+            best_np = None                                   # best candidate outside the ping-pong core
+            second = {}
             if native_ok:
                 for bm, bn, sp, v in cands:
                     try:
@@ -232,6 +265,15 @@ def main():
                         continue
                     if best is None or t < best[0]:
                         best = (t, bm, bn, sp, v)
+                    if v != 5 and (best_np is None or t < best_np[0]):
+                        best_np = (t, bm, bn, sp, v)
+            if best_np is not None:
+                t0, bm0, bn0, sp0, v0 = best_np
+                if v0 == 4:
+                    second[pass_] = {"backend": "mdtf", "ver": 4, "ws": list(bm0), "ms": round(t0, 4)}
+                else:
+                    second[pass_] = {"backend": "mdtf", "bm": bm0, "bn": bn0, "splits": 0, "ver": v0,
+                                     "stages": sp0, "ms": round(t0, 4)}
             if t_wino is not None and t_wino < t_lib and (best is None or t_wino < best[0]):
                 table[key] = {"backend": "winograd", "ms": round(t_wino, 4), "miopen_ms": round(t_lib, 4),
                               "mdtf_ms": round(best[0], 4) if best else None}
@@ -246,6 +288,12 @@ def main():
                 if best[4] == 4:                          # weight-stationary kernel: tile in "ws"
                     ent = {"backend": "mdtf", "ver": 4, "ws": list(best[1]), "ms": round(best[0], 4),
                            "miopen_ms": round(t_lib, 4)}
+                elif best[4] == 5:                        # ping-pong core: tile index, "prev" = best of the rest
+                    ent = {"backend": "mdtf", "ver": 5, "tile": best[1], "ms": round(best[0], 4),
+                           "miopen_ms": round(t_lib, 4)}
+                    rest = second[pass_] if second.get(pass_) else None
+                    if rest is not None:
+                        ent["prev"] = rest
                 elif best[4] >= 2 and pass_ == "wgrad":   # v2 wgrad: bm field carries (rows, stages)
                     ent["bm"], ent["stages"] = best[1]
                 elif best[4] in (2, 3):                   # v2 fwd/dgrad: the third field is the pipeline depth

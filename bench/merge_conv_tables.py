@@ -35,11 +35,14 @@ def main():
     changed = 0
     for k, e in sorted(best.items()):
         old = base.get(k)
-        same = old is not None and all(old.get(f) == e.get(f) for f in ("bm", "bn", "splits", "ver", "stages", "ws"))
+        same = old is not None and all(old.get(f) == e.get(f)
+                                       for f in ("bm", "bn", "splits", "ver", "stages", "ws", "tile"))
         if not same or old.get("slab", 0) != e.get("slab", 0):
             changed += 1
-            print("%-45s %s -> %s" % (k, {f: (old or {}).get(f) for f in ("bm", "bn", "splits", "stages", "ver")},
-                                      {f: e.get(f) for f in ("bm", "bn", "splits", "stages", "ver", "slab", "ms")}))
+            print("%-45s %s -> %s" % (k, {f: (old or {}).get(f) for f in ("bm", "bn", "splits", "stages", "ver", "ws",
+                                                                        "tile", "ms")},
+                                      {f: e.get(f) for f in ("bm", "bn", "splits", "stages", "ver", "ws", "tile", "slab",
+                                                             "ms")}))
         base[k] = e
     json.dump(base, open(a.out, "w"), indent=1, sort_keys=True)
     print("changed %d of %d measured keys -> %s" % (changed, len(best), a.out))
