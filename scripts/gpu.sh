@@ -4,7 +4,8 @@
 #   bench   : bench.py (ResNet-50 + BERT-base line), three times
 #   prof    : rocprofv3 --kernel-trace --stats of the captured ResNet-50 and BERT-base steps
 #   profr   : the same, ResNet-50 only
-#   pmc     : SQ / FETCH / WRITE+L2 counter passes over both steps (eager), each its own run
+#   pmc     : SQ / FETCH / WRITE+L2 counter passes over both steps (captured steps; PMC_GRAPH=0: eager), each its
+#             own run; summarise one step with scripts/pmc_summary.py <dir prefix> 40 --last-step
 #   envab   : alternating A/B of bench.py under two env settings: gpu.sh envab TAG "A=1" "A=0" [steps]
 #   py      : run a python script under a time limit: gpu.sh py TAG path/to/script.py [args]
 #   bertab  : alternating A/B of bench/bert_bench.py under two env settings: gpu.sh bertab TAG "A=1" "A=0" [steps]
@@ -61,10 +62,10 @@ case "$WHAT" in
     for P in "$P1" "$P2" "$P3"; do
       i=$((i+1))
       (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $P --kernel-trace -d "$OUT/pmcr_${TAG}_p$i" -o run \
-          --output-format csv -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --hip_graph 0 --bert 0) \
+          --output-format csv -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --hip_graph ${PMC_GRAPH:-1} --bert 0) \
           > "$OUT/pmcr_${TAG}_p$i.log" 2>&1 || fail "resnet pmc $i" "$OUT/pmcr_${TAG}_p$i.log"
       (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $P --kernel-trace -d "$OUT/pmcb_${TAG}_p$i" -o run \
-          --output-format csv -- python3 "$ROOT/bench/bert_bench.py" --steps 2 --warmup 1 --hip_graph 0) \
+          --output-format csv -- python3 "$ROOT/bench/bert_bench.py" --steps 2 --warmup 1 --hip_graph ${PMC_GRAPH:-1}) \
           > "$OUT/pmcb_${TAG}_p$i.log" 2>&1 || fail "bert pmc $i" "$OUT/pmcb_${TAG}_p$i.log"
       echo "pmc pass $i ok"
     done ;;

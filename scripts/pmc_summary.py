@@ -1,7 +1,10 @@
 #!/usr/bin/env python
 """Summarise the rocprofv3 --pmc passes of scripts/gpu_pmc.sh per kernel.
 
-usage: pmc_summary.py <dir prefix, e.g. gpurun_out/pmc1> [top N]
+usage: pmc_summary.py <dir prefix, e.g. gpurun_out/pmc1> [top N] [--last-step]
+
+--last-step: only the dispatches of the last training step (from the end of the second-to-last optimizer
+launch group to the end of the last one), so model setup, warmup and graph capture do not count.
 
 Per kernel (aggregated over its dispatches in the profiled steps):
   time      summed dispatch time (serialised by the counter collection)
@@ -21,13 +24,31 @@ CLOCK = 2.4e9
 SIMDS = 1024
 
 
-def load(path):
+OPT = ("adam_kernel", "momentum_kernel", "sgd_kernel", "apply_multi_kernel")
+
+
+def last_step(ds):
+    """Dispatches of the last step: after the second-to-last optimizer group, through the last one."""
+    idx = [i for i, d in enumerate(ds) if any(o in d["name"] for o in OPT)]
+    groups = []
+    for i in idx:
+        if groups and i - groups[-1][-1] <= 16:
+            groups[-1].append(i)
+        else:
+            groups.append([i])
+    if len(groups) < 2:
+        return ds
+    return ds[groups[-2][-1] + 1:groups[-1][-1] + 1]
+
+
+def load(path, step_only=False):
     per = collections.OrderedDict()
     for r in csv.DictReader(open(path)):
         d = per.setdefault(int(r["Dispatch_Id"]), {"name": r["Kernel_Name"],
                                                    "dur": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    return list(per.values())
+    ds = [per[k] for k in sorted(per)]
+    return last_step(ds) if step_only else ds
 
 
 def short(name):
@@ -37,7 +58,7 @@ def short(name):
     return n[:70]
 
 
-def main(prefix, top):
+def main(prefix, top, step_only=False):
     # each pass is its own run: aggregate per kernel name within a pass, then join the passes by name
     aggs = []
     for i in (1, 2, 3):
@@ -46,7 +67,7 @@ def main(prefix, top):
         if i > 1 and not os.path.exists(path):      # SQ-only runs: one pass
             aggs.append(agg)
             continue
-        for d in load(path):
+        for d in load(path, step_only):
             a = agg[short(d["name"])]
             a["calls"] += 1
             a["dur"] += d["dur"]
@@ -71,9 +92,10 @@ def main(prefix, top):
         hit = 100.0 * c.get("TCC_HIT_sum", 0) / hit if hit else 0
         print("| `%s` | %d | %.3f | %.0f | %.1f | %.1f | %.0f + %.0f | %.0f |" % (
             name, a["calls"], dur * 1e3, tf, mf, lds, rd, wr, hit))
-    print("\nprofiled dispatches (pass 1): %d, total serialized kernel time %.2f ms" % (
-        sum(a["calls"] for _, a in rows), tot * 1e3))
+    print("\nprofiled dispatches (pass 1%s): %d, total serialized kernel time %.2f ms" % (
+        ", last step only" if step_only else "", sum(a["calls"] for _, a in rows), tot * 1e3))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 40)
+    pos = [v for v in sys.argv[1:] if not v.startswith("--")]
+    main(pos[0], int(pos[1]) if len(pos) > 1 else 40, "--last-step" in sys.argv)
