@@ -80,6 +80,7 @@ struct ConvArgs {
   // into DW by one reduction pass, instead of fp32 atomics into DW (null: atomics)
   float* slab;
   int slab_cap;          // splits the slab has room for
+  int slab_nt;           // partials with nontemporal stores, summed with nontemporal loads (MDTF_SLAB_NT=0: cached)
   int wg_xcd;            // wgrad v2: XCD-aware block order (the row/col tiles of one pixel split share an L2)
   // dense forward (fd v2 MODE 3): Y[M][Ncol] = act(X[M][K] W + bias), W N-contiguous [K][ld_b] read as
   // [64 k][64 col] half-images by transposed fragment reads (no transposed weight copy).  The columns are
@@ -1359,7 +1360,10 @@ __global__ void __launch_bounds__(64 * NW, (wgrad_min_waves<BM, BN, STAGES, NW>(
         const int r = r0 + wm * (TM * 16) + i * 16 + 4 * g + rr;
         if (r >= R) continue;
         if (slab)
-          slab[(long long)r * a.Cout + co] = acc[i][j][rr];
+          if (a.slab_nt)
+            __builtin_nontemporal_store(acc[i][j][rr], slab + (long long)r * a.Cout + co);
+          else
+            slab[(long long)r * a.Cout + co] = acc[i][j][rr];
         else
           atomicAdd(a.dw + (long long)r * a.ld_dw + co, acc[i][j][rr]);
       }
@@ -1369,23 +1373,29 @@ __global__ void __launch_bounds__(64 * NW, (wgrad_min_waves<BM, BN, STAGES, NW>(
 // DW[r][c] (row stride ld) += sum_s slab[s][r][c]  (slab rows dense, C % 4 == 0); 4 splits in flight.
 // (Spreading the splits of a small filter over more blocks with fp32 atomics measured 1.7 % slower in the ResNet
 // step: profiles/ab_r5.md.)
+template <bool NT>
 __global__ void __launch_bounds__(256) wgrad_slab_reduce(const float* __restrict__ slab, int splits, long long RC,
                                                          int C, long long ld, float* __restrict__ dw) {
   const long long q = blockIdx.x * 256LL + threadIdx.x;     // float4 index
   if (q * 4 >= RC) return;
+  typedef float f4v __attribute__((ext_vector_type(4)));
   const float4* s4 = reinterpret_cast<const float4*>(slab);
+  auto ldq = [&](long long i) -> float4 {
+    if constexpr (NT) return __builtin_bit_cast(float4, __builtin_nontemporal_load(reinterpret_cast<const f4v*>(s4) + i));
+    return s4[i];
+  };
   const long long st = RC / 4;
   float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
   int sp = 0;
   for (; sp + 3 < splits; sp += 4) {
-    const float4 a = s4[q + sp * st], b = s4[q + (sp + 1) * st], c = s4[q + (sp + 2) * st], d = s4[q + (sp + 3) * st];
+    const float4 a = ldq(q + sp * st), b = ldq(q + (sp + 1) * st), c = ldq(q + (sp + 2) * st), d = ldq(q + (sp + 3) * st);
     t.x += (a.x + b.x) + (c.x + d.x);
     t.y += (a.y + b.y) + (c.y + d.y);
     t.z += (a.z + b.z) + (c.z + d.z);
     t.w += (a.w + b.w) + (c.w + d.w);
   }
   for (; sp < splits; ++sp) {
-    const float4 a = s4[q + sp * st];
+    const float4 a = ldq(q + sp * st);
     t.x += a.x;
     t.y += a.y;
     t.z += a.z;
@@ -1419,13 +1429,21 @@ int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
   if (lds > 160 * 1024) return MDTF_EUNSUPPORTED;
   ConvArgs b = a;
   if (a.slab && (splits < 2 || splits > a.slab_cap || (a.ld_dw % 4) || (a.Cout % 4))) b.slab = nullptr;
+  {
+    static const int nt = [] {
+      const char* e = getenv("MDTF_SLAB_NT");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
+    b.slab_nt = nt;
+  }
   hipLaunchKernelGGL((conv_wgrad_v2<BM, BN, STAGES, NW, PIPE>), dim3(a.mtiles * a.ntiles * splits), dim3(64 * NW), lds,
                      st, b);
   MDTF_LAUNCH_CHECK();
   if (b.slab) {
     const long long RC = (long long)R * a.Cout;
-    hipLaunchKernelGGL(wgrad_slab_reduce, dim3((unsigned)ceil_div(RC / 4, 256)), dim3(256), 0, st, b.slab, splits, RC,
-                       a.Cout, (long long)a.ld_dw, a.dw);
+    hipLaunchKernelGGL((b.slab_nt ? wgrad_slab_reduce<true> : wgrad_slab_reduce<false>),
+                       dim3((unsigned)ceil_div(RC / 4, 256)), dim3(256), 0, st, b.slab, splits, RC, a.Cout,
+                       (long long)a.ld_dw, a.dw);
     MDTF_LAUNCH_CHECK();
   }
   return 0;
@@ -1549,9 +1567,10 @@ __global__ void __launch_bounds__(256) dgrad_zero_classes(ConvArgs a, int C8) {
     }
   }
   if constexpr (BSTAT) {
-    // rows padded to 257 floats: the reads below take 8 channels k x 8 thread chunks t per wave; with 256-float
-    // rows the 8 k of one t shared a bank (8-way, 78 % LDS bank conflicts in pmc_resnet50_r4p)
-    __shared__ float red[2][8][257];
+    // rows padded to 260 floats (4 mod 32 banks): a 32-lane half of the reads below takes channels k = 0..7 x
+    // thread chunks cc = 0..3, at bank 4 k + cc -- 32 distinct.  (256: the 8 k of one cc shared a bank, 78 %
+    // conflicts in pmc_resnet50_r4p; 257: bank k + cc, 11 banks for 32 lanes, 60 % in pmc_resnet50_r5f)
+    __shared__ float red[2][8][260];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       red[0][k][tid] = s0[k];
