@@ -135,7 +135,8 @@ def iso_fn(pass_, xs, ws, stride, pads, dil, fam, cand, bufs):
 
 def dgrad_variants(xs, ws, stride, pads, dil, fam, cand, bufs):
     """The data gradient as the step runs it when it completes a BN output's gradient: BN-statistics epilogue
-    plus a masked pending accumulate source (raises like the step would)."""
+    plus a masked pending accumulate source (raises like the step would).  Returns the launch as a closure over
+    its buffers, so it can also be timed."""
     x, wt, dy, oh, ow = bufs
     M = xs[0] * xs[1] * xs[2]
     mask = torch.full((M * xs[3] // 8,), 0x55, dtype=torch.uint8, device=x.device)
@@ -143,13 +144,15 @@ def dgrad_variants(xs, ws, stride, pads, dil, fam, cand, bufs):
     out = torch.empty_like(x)
     if fam == "ws":
         st = T._stats(xs[3], 128, M)
-        C.ws_dgrad(dy, wt, x.shape, pads, dil, (2,) + tuple(cand[1:]), out=out,
-                   bn_stats=(x, mask, st[0], st[1], st[0].shape[0]), acc_src=(g, mask))
+        fn = lambda: C.ws_dgrad(dy, wt, x.shape, pads, dil, (2,) + tuple(cand[1:]), out=out,  # noqa: E731
+                                bn_stats=(x, mask, st[0], st[1], st[0].shape[0]), acc_src=(g, mask))
     else:
         bm, bn, sp, ver, stg = cand
         st = T._stats(xs[3], bm, M)
-        C.mdtf_dgrad(dy, wt, x.shape, stride, pads, dil, bm, bn, ver, stg, out=out,
-                     bn_stats=(x, mask, st[0], st[1], st[0].shape[0]), acc_src=(g, mask))
+        fn = lambda: C.mdtf_dgrad(dy, wt, x.shape, stride, pads, dil, bm, bn, ver, stg, out=out,  # noqa: E731
+                                  bn_stats=(x, mask, st[0], st[1], st[0].shape[0]), acc_src=(g, mask))
+    fn()
+    return fn
 
 
 def main():
@@ -163,6 +166,11 @@ def main():
     p.add_argument("--budget_s", type=float, default=900.0, help="stop trying new keys after this long")
     p.add_argument("--reverse", action="store_true", help="tune the keys last-seen first (continues a budget-capped "
                    "earlier run from the other end of the step)")
+    p.add_argument("--rank_epilogue", action="store_true", help="short-list data-gradient tiles by their isolated "
+                   "time WITH the BN-statistics + pending-accumulate epilogue (the plain launch ranks the small "
+                   "tiles first, whose epilogue then costs the most in the step)")
+    p.add_argument("--keys", default="", help="comma-free substrings: only tune keys containing one of them "
+                   "(';'-separated)")
     p.add_argument("--out", default="gpurun_out/conv_table_step.json")
     p.add_argument("--report", default="gpurun_out/conv_step_tune.md")
     args = p.parse_args()
@@ -185,6 +193,8 @@ def main():
     table = C.table()
     keys = [k for k in seen if k in table and k.split(":")[0] in args.passes.split(",")
             and table[k].get("backend") == "mdtf"]
+    if args.keys:
+        keys = [k for k in keys if any(sub in k for sub in args.keys.split(";"))]
     if args.reverse:
         keys = keys[::-1]
     base = [step_ms(sess, op, args.steps, args.warm) for _ in range(6)]
@@ -212,7 +222,9 @@ def main():
                 fn = iso_fn(pass_, xs, ws, stride, pads, dil, fam, cand, bufs)
                 fn()
                 if pass_ == "dgrad":          # the step's epilogue variants must take this tile too
-                    dgrad_variants(xs, ws, stride, pads, dil, fam, cand, bufs)
+                    fe = dgrad_variants(xs, ws, stride, pads, dil, fam, cand, bufs)
+                    if args.rank_epilogue:    # short-list by the epilogue-carrying launch the step mostly runs
+                        fn = fe
                 torch.cuda.synchronize()
                 t = T.timeit(fn, 3, warm=1)
             except RuntimeError:

@@ -411,11 +411,11 @@ __device__ __forceinline__ float ld<float>(const float* p, long long i) {
 
 template <typename T>
 __global__ void xent_fwd(const T* __restrict__ logits, const long long* __restrict__ labels, int N, int K,
-                         float* __restrict__ loss, float* __restrict__ lse) {
+                         long long ldr, float* __restrict__ loss, float* __restrict__ lse) {
   int row = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   int lane = threadIdx.x % 64;
   if (row >= N) return;
-  const T* p = logits + (long long)row * K;
+  const T* p = logits + (long long)row * ldr;
   float m = -INFINITY;
   for (int k = lane; k < K; k += 64) m = fmaxf(m, ld(p, k));
   m = wave_max(m);
@@ -441,10 +441,10 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2
 }
 
 __global__ void __launch_bounds__(256) xent_fwd_row_bf16(const bf16_t* __restrict__ logits,
-                                                         const long long* __restrict__ labels, int K,
+                                                         const long long* __restrict__ labels, int K, long long ld,
                                                          float* __restrict__ loss, float* __restrict__ lse) {
   const int row = blockIdx.x, tid = threadIdx.x;
-  const bf16_t* p = logits + (long long)row * K;
+  const bf16_t* p = logits + (long long)row * ld;
   const uint32_t* p2 = reinterpret_cast<const uint32_t*>(p);
   const int K2 = K >> 1;
   float m = -INFINITY, s = 0.f;
@@ -481,17 +481,52 @@ __global__ void __launch_bounds__(256) xent_fwd_row_bf16(const bf16_t* __restric
 template <typename T>
 __global__ void xent_bwd(const T* __restrict__ logits, const long long* __restrict__ labels,
                          const float* __restrict__ lse, const float* __restrict__ dloss, T* __restrict__ dlogits,
-                         int N, int K) {
+                         int N, int K, long long ldi, long long ldo) {
   long long total = (long long)N * K;
   GRID_STRIDE(i, total) {
     int row = static_cast<int>(i / K);
     int k = static_cast<int>(i % K);
-    float pr = __expf(ld(logits, i) - lse[row]);
+    float pr = __expf(ld(logits, row * ldi + k) - lse[row]);
     float g = (pr - (labels[row] == k ? 1.f : 0.f)) * dloss[row];
     if constexpr (sizeof(T) == 2)
-      dlogits[i] = f2bf(g);
+      dlogits[row * ldo + k] = f2bf(g);
     else
-      dlogits[i] = g;
+      dlogits[row * ldo + k] = g;
+  }
+}
+
+// bf16 rows whose strides are multiples of 8 (the padded MLM decoder's [rows][30720] logits): one 256-thread block
+// per row, 16-B vectors, no per-element division; columns K .. ldo of the output row are written as zeros (the
+// decoder's split-K data gradient and weight gradient read the whole padded row)
+__global__ void __launch_bounds__(256) xent_bwd_row_bf16(const bf16_t* __restrict__ logits,
+                                                         const long long* __restrict__ labels,
+                                                         const float* __restrict__ lse,
+                                                         const float* __restrict__ dloss, bf16_t* __restrict__ dlogits,
+                                                         int K, long long ldi, long long ldo) {
+  const int row = blockIdx.x;
+  const float l = lse[row], dl = dloss[row];
+  const long long lab = labels[row];
+  const bf16_t* p = logits + row * ldi;
+  bf16_t* q = dlogits + row * ldo;
+  const int nv = static_cast<int>(ldo >> 3), kv = (K + 7) >> 3;
+  for (int v = threadIdx.x; v < nv; v += 256) {
+    uint4 o = {0u, 0u, 0u, 0u};
+    if (v < kv) {
+      const uint4 w = *reinterpret_cast<const uint4*>(p + v * 8);
+      const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
+      uint32_t ov[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int k0 = v * 8 + 2 * h;
+        float g0 = __expf(__uint_as_float(wv[h] << 16) - l) - (lab == k0 ? 1.f : 0.f);
+        float g1 = __expf(__uint_as_float(wv[h] & 0xffff0000u) - l) - (lab == k0 + 1 ? 1.f : 0.f);
+        g0 = k0 < K ? g0 * dl : 0.f;
+        g1 = k0 + 1 < K ? g1 * dl : 0.f;
+        ov[h] = f2bf(g0) | (f2bf(g1) << 16);
+      }
+      o = {ov[0], ov[1], ov[2], ov[3]};
+    }
+    *reinterpret_cast<uint4*>(q + v * 8) = o;
   }
 }
 
@@ -753,28 +788,39 @@ MDTF_EXPORT int mdtf_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hip
   return 0;
 }
 
-MDTF_EXPORT int mdtf_xent_fwd(const void* logits, int is_bf16, const long long* labels, int N, int K, float* loss,
-                              float* lse, hipStream_t st) {
+// logits rows ld elements apart (ld >= K)
+MDTF_EXPORT int mdtf_xent_fwd(const void* logits, int is_bf16, const long long* labels, int N, int K, long long ld,
+                              float* loss, float* lse, hipStream_t st) {
+  if (ld < K) return MDTF_EINVAL;
   dim3 grid(ceil_div(N, 4));
-  if (is_bf16 && K >= 2048 && (reinterpret_cast<uintptr_t>(logits) & 3) == 0 && (K & 1) == 0)
-    hipLaunchKernelGGL(xent_fwd_row_bf16, dim3(N), dim3(256), 0, st, (const bf16_t*)logits, labels, K, loss, lse);
+  if (is_bf16 && K >= 2048 && (reinterpret_cast<uintptr_t>(logits) & 3) == 0 && (K & 1) == 0 && (ld & 1) == 0)
+    hipLaunchKernelGGL(xent_fwd_row_bf16, dim3(N), dim3(256), 0, st, (const bf16_t*)logits, labels, K, ld, loss, lse);
   else if (is_bf16)
-    hipLaunchKernelGGL(xent_fwd<bf16_t>, grid, dim3(kT), 0, st, (const bf16_t*)logits, labels, N, K, loss, lse);
+    hipLaunchKernelGGL(xent_fwd<bf16_t>, grid, dim3(kT), 0, st, (const bf16_t*)logits, labels, N, K, ld, loss, lse);
   else
-    hipLaunchKernelGGL(xent_fwd<float>, grid, dim3(kT), 0, st, (const float*)logits, labels, N, K, loss, lse);
+    hipLaunchKernelGGL(xent_fwd<float>, grid, dim3(kT), 0, st, (const float*)logits, labels, N, K, ld, loss, lse);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
 
+// dlogits rows ldo elements apart; with the vector kernel (bf16, strides multiples of 8, 16-B aligned rows) the
+// columns K .. ldo are zero-filled, otherwise left untouched
 MDTF_EXPORT int mdtf_xent_bwd(const void* logits, int is_bf16, const long long* labels, const float* lse,
-                              const float* dloss, void* dlogits, int N, int K, hipStream_t st) {
+                              const float* dloss, void* dlogits, int N, int K, long long ldi, long long ldo,
+                              hipStream_t st) {
+  if (ldi < K || ldo < K) return MDTF_EINVAL;
+  const bool vec = is_bf16 && (ldi % 8) == 0 && (ldo % 8) == 0 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(dlogits) & 15) == 0;
   long long total = (long long)N * K;
-  if (is_bf16)
+  if (vec)
+    hipLaunchKernelGGL(xent_bwd_row_bf16, dim3(N), dim3(256), 0, st, (const bf16_t*)logits, labels, lse, dloss,
+                       (bf16_t*)dlogits, K, ldi, ldo);
+  else if (is_bf16)
     hipLaunchKernelGGL(xent_bwd<bf16_t>, dim3(grid_cap(total)), dim3(kT), 0, st, (const bf16_t*)logits, labels, lse,
-                       dloss, (bf16_t*)dlogits, N, K);
+                       dloss, (bf16_t*)dlogits, N, K, ldi, ldo);
   else
     hipLaunchKernelGGL(xent_bwd<float>, dim3(grid_cap(total)), dim3(kT), 0, st, (const float*)logits, labels, lse,
-                       dloss, (float*)dlogits, N, K);
+                       dloss, (float*)dlogits, N, K, ldi, ldo);
   MDTF_LAUNCH_CHECK();
   return 0;
 }

@@ -97,6 +97,7 @@ class Bert(Model):
         with V.variable_scope("bert"):
             with V.variable_scope("embeddings"):
                 word = V.get_variable("word_embeddings", [self.vocab, H], initializer=_init())
+                word_obj = V.find_variable("word_embeddings")
                 pos = V.get_variable("position_embeddings", [self.max_position, H], initializer=_init())
                 typ = V.get_variable("token_type_embeddings", [self.type_vocab, H], initializer=_init())
                 e = T.bert_embeddings(word, pos, typ, ids, types)      # one fused kernel each way on the GPU
@@ -125,8 +126,14 @@ class Bert(Model):
                 # into the fp32 gradient slot (one shared read made autograd add their two zero-stride markers into
                 # a materialised [vocab, H] tensor and add that into the slot: two extra passes per step)
                 wvar = getattr(word, "_mdtf_var", None)
+                bias_obj = V.find_variable("output_bias")
+                if word_obj is not None and bias_obj is not None:
+                    # zero rows after the embedding and the bias in the flat buffers: the decoder's products run
+                    # over a 30720-wide vocabulary (ops.tied_decoder); checkpoints keep the [30522, H] shapes.
+                    # Set on the build pass, before the flat parameter space exists.
+                    word_obj.pad_rows = bias_obj.pad_rows = ops.decoder_pad_rows(self.vocab)
                 word_dec = wvar.read(store.compute_dtype) if wvar is not None else word
-                mlm = ops.dense_transposed(h, word_dec, out_bias)
+                mlm = ops.tied_decoder(h, word_dec, out_bias)
             with V.variable_scope("seq_relationship"):
                 w = V.get_variable("output_weights", [2, H], initializer=_init())
                 b = V.get_variable("output_bias", [2], initializer=V.constant_initializer(0.0))

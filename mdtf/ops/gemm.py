@@ -739,6 +739,85 @@ def dense_multi(x, ws, bs, act=None):
     return y.reshape(*shp[:-1], y.shape[-1])
 
 
+# MDTF_DEC_SPLIT: split-K chunks of the padded tied decoder's data gradient (0: the plain dense_transposed path)
+DEC_SPLIT = int(os.environ.get("MDTF_DEC_SPLIT", "8"))
+_PADDED_GRADS = {}     # data_ptr -> row stride of zero-padded logit gradients made by kernels._Xent
+
+
+def decoder_pad_rows(vocab, split=None):
+    """Zero rows to reserve after a tied [vocab, H] embedding so the decoder's vocabulary splits into ``split``
+    chunks of whole 256-row blocks (BERT: 30522 -> 30720 = 8 x 3840)."""
+    split = DEC_SPLIT if split is None else split
+    q = 256 * max(split, 1)
+    return (-vocab) % q
+
+
+class _TiedDecoder(torch.autograd.Function):
+    """``logits = h W^T + b`` of a tied MLM decoder over the vocabulary padded to the variables' ``pad_rows``
+    (parallel/flat.py keeps the pad rows of master, gradient and bf16 shadow at zero), reference
+    ``distribute_tools.py:204-206`` (tf.matmul + bias_add of FC_layer; BERT's decoder is that product against the
+    transposed embedding).  Padded, the three products leave the library's odd-width tiles:
+
+      forward   logits_p = b_p + h W_p^T       [rows, VP]; the model sees the [rows, V] view
+      dgrad     dh = sum_s dlogits_p[:, s] W_p[s]   split-K over DEC_SPLIT vocabulary chunks as one batched
+                product with fp32 partials (80 output tiles unsplit: profiles/mlm_decoder_r5.md)
+      wgrad     gW_p += dlogits_p^T h  and  gb_p += colsum(dlogits_p), straight into the padded fp32 slots
+
+    The logit gradient arrives as the [rows, V] view of the zero-padded [rows, VP] buffer kernels._Xent writes for
+    strided logits; any other producer's gradient is copied into a zero-padded buffer first."""
+
+    @staticmethod
+    def forward(ctx, h, w, b):
+        wv, bv = w._mdtf_var, b._mdtf_var
+        Wp = wv.shadow_padded
+        bp = bv.shadow_padded if bv.shadow_padded is not None else bv.master_padded.to(h.dtype)
+        Vn = wv.shape[0]
+        logits = torch.addmm(bp, h, Wp.t())
+        ctx.save_for_backward(h)
+        ctx.wv, ctx.bv, ctx.V = wv, bv, Vn
+        ctx.like = (w, b)
+        return logits[:, :Vn]
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, = ctx.saved_tensors
+        wv, bv, Vn = ctx.wv, ctx.bv, ctx.V
+        Wp = wv.shadow_padded
+        VP, H = Wp.shape
+        M = h.shape[0]
+        if dy.stride(1) == 1 and dy.stride(0) == VP and _PADDED_GRADS.pop(dy.data_ptr(), None) == VP:
+            dp = dy.as_strided((M, VP), (VP, 1))
+        else:
+            dp = torch.zeros((M, VP), dtype=h.dtype, device=h.device)
+            dp[:, :Vn].copy_(dy)
+        S = DEC_SPLIT
+        try:
+            part = torch.bmm(dp.view(M, S, VP // S).transpose(0, 1), Wp.view(S, VP // S, H), out_dtype=torch.float32)
+            dh = part.sum(0).to(h.dtype)
+        except (RuntimeError, TypeError):
+            dh = torch.mm(dp, Wp)
+        _accum_mm(wv.grad_padded, dp.t(), h)
+        kernels.colsum_into(dp, bv.grad_padded)
+        w, b = ctx.like
+        return dh, V.grad_marker(w), V.grad_marker(b)
+
+
+def tied_decoder(x, w, b):
+    """``x @ w^T + b`` for a tied decoder: the padded path when both variables carry padded flat views (set
+    ``pad_rows`` from :func:`decoder_pad_rows` before the flat space is built), else :func:`dense_transposed`."""
+    wv, bv = getattr(w, "_mdtf_var", None), getattr(b, "_mdtf_var", None)
+    ok = (DEC_SPLIT > 0 and wv is not None and bv is not None and x.dim() == 2 and x.is_cuda
+          and x.dtype == torch.bfloat16 and wv.shadow_padded is not None and wv.grad_padded is not None
+          and bv.grad_padded is not None and (bv.shadow_padded is not None or bv.master_padded is not None)
+          and wv.shadow_padded.shape[0] == bv.grad_padded.shape[0]
+          and wv.shadow_padded.shape[0] % (256 * DEC_SPLIT) == 0 and torch.is_grad_enabled()
+          and V.grad_sink(w) is wv and V.grad_sink(b) is bv)
+    if not ok:
+        return dense_transposed(x, w, b)
+    _check(x, "dense")
+    return _TiedDecoder.apply(x.contiguous(), w, b)
+
+
 def dense_transposed(x, w, b=None):
     """``x @ w^T + b`` with w [N, K] (tied embedding decoders)."""
     _check(x, "dense")

@@ -13,8 +13,8 @@ N.register("mdtf_pool_fwd", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.P])
 N.register("mdtf_pool_bwd", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.P])
 N.register("mdtf_gap_fwd", [N.P, N.P, N.I, N.I, N.I, N.P])
 N.register("mdtf_gap_bwd", [N.P, N.P, N.I, N.I, N.I, N.P])
-N.register("mdtf_xent_fwd", [N.P, N.I, N.P, N.I, N.I, N.P, N.P, N.P])
-N.register("mdtf_xent_bwd", [N.P, N.I, N.P, N.P, N.P, N.P, N.I, N.I, N.P])
+N.register("mdtf_xent_fwd", [N.P, N.I, N.P, N.I, N.I, N.L, N.P, N.P, N.P])
+N.register("mdtf_xent_bwd", [N.P, N.I, N.P, N.P, N.P, N.P, N.I, N.I, N.L, N.L, N.P])
 N.register("mdtf_transpose_brs", [N.P, N.P, N.I, N.I, N.I, N.I, N.P])
 N.register("mdtf_lrn_fwd", [N.P, N.P, N.P, N.L, N.I, N.I, N.F, N.F, N.F, N.P])
 N.register("mdtf_lrn_bwd", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.I, N.F, N.F, N.P])
@@ -161,18 +161,23 @@ def global_avg_pool(x):
 
 # ---------------------------------------------------------------- softmax xent
 class _Xent(torch.autograd.Function):
+    """Rows may be strided (``logits.stride(0) >= K``, unit column stride): the padded MLM decoder hands over a
+    [rows, 30522] view of its [rows, 30720] logits.  The gradient then comes back as the same view of a zero-padded
+    [rows, 30720] buffer, which the decoder's backward reads whole (``gemm.tied_decoder``)."""
+
     @staticmethod
     def forward(ctx, logits, labels):
-        logits = logits.contiguous()
         if logits.dtype not in (torch.bfloat16, torch.float32):
             logits = logits.float()
+        if logits.stride(1) != 1 or logits.stride(0) < logits.shape[1]:
+            logits = logits.contiguous()
         labels = labels.to(torch.int64).contiguous()
         n, k = logits.shape
         loss = torch.empty(n, dtype=torch.float32, device=logits.device)
         lse = torch.empty_like(loss)
         is_bf = int(logits.dtype == torch.bfloat16)
-        N.check(N.fn("mdtf_xent_fwd")(N.ptr(logits), is_bf, N.ptr(labels), n, k, N.ptr(loss), N.ptr(lse),
-                                      N.stream_ptr()), "xent_fwd")
+        N.check(N.fn("mdtf_xent_fwd")(N.ptr(logits), is_bf, N.ptr(labels), n, k, logits.stride(0), N.ptr(loss),
+                                      N.ptr(lse), N.stream_ptr()), "xent_fwd")
         ctx.save_for_backward(logits, labels, lse)
         return loss
 
@@ -180,11 +185,19 @@ class _Xent(torch.autograd.Function):
     def backward(ctx, dloss):
         logits, labels, lse = ctx.saved_tensors
         n, k = logits.shape
-        dl = torch.empty_like(logits)
+        ldi = logits.stride(0)
+        ldo = ldi if (ldi != k and ldi % 8 == 0 and logits.dtype == torch.bfloat16) else k
+        dl = torch.empty((n, ldo), dtype=logits.dtype, device=logits.device)
         dloss = dloss.float().contiguous()
         N.check(N.fn("mdtf_xent_bwd")(N.ptr(logits), int(logits.dtype == torch.bfloat16), N.ptr(labels), N.ptr(lse),
-                                      N.ptr(dloss), N.ptr(dl), n, k, N.stream_ptr()), "xent_bwd")
-        return dl, None
+                                      N.ptr(dloss), N.ptr(dl), n, k, ldi, ldo, N.stream_ptr()), "xent_bwd")
+        if ldo == k:
+            return dl, None
+        from . import gemm
+        if len(gemm._PADDED_GRADS) > 16:
+            gemm._PADDED_GRADS.clear()
+        gemm._PADDED_GRADS[dl.data_ptr()] = ldo     # zero-padded: the tied decoder may read the whole rows
+        return dl[:, :k], None
 
 
 def softmax_xent(logits, labels):

@@ -348,6 +348,21 @@ def dense_transposed(x, w, b=None):
     return y + b.to(y.dtype) if b is not None else y
 
 
+def tied_decoder(x, w, b):
+    """``x @ w^T + b`` of a decoder tied to an embedding variable: on the GPU over the vocabulary padded to the
+    variables' ``pad_rows`` (``gemm.tied_decoder``), else :func:`dense_transposed`."""
+    if _native.use_native(x):
+        from . import gemm
+        return gemm.tied_decoder(x, w, b)
+    return dense_transposed(x, w, b)
+
+
+def decoder_pad_rows(vocab):
+    """Zero rows a tied embedding reserves for :func:`tied_decoder` (0 when the padded path is off)."""
+    from . import gemm
+    return gemm.decoder_pad_rows(vocab) if gemm.DEC_SPLIT > 0 else 0
+
+
 def gelu(x):
     return F.gelu(x.float(), approximate="tanh").to(x.dtype)
 

@@ -15,6 +15,14 @@ layout is *reverse creation order*, so the tail of the forward pass (the first
 gradients of backward) fills the first bucket.  Each bucket is padded to a
 multiple of ``pad_to`` (= world size in PS-shard mode) so that
 reduce-scatter/all-gather shards are equal and contiguous.
+
+A variable with ``pad_rows > 0`` gets that many zero rows reserved after it in
+every buffer (master, gradient, shadow), exposed as ``master_padded`` /
+``grad_padded`` / ``shadow_padded`` views of ``rows + pad_rows`` rows: the tied
+BERT decoder reads the vocabulary as 30720 rows (a multiple of its split-K
+chunks) without a per-step copy.  The pad rows stay exactly zero: their master
+starts at zero, their gradient is only ever a sum of zero products, and every
+fused update maps (w, g) = (0, 0) to 0.
 """
 import collections
 
@@ -25,6 +33,14 @@ _ALIGN = 64  # elements; 256-B aligned fp32 / 128-B aligned bf16 slices
 
 def _round_up(x, m):
     return -(-x // m) * m
+
+
+def _extent(v):
+    """Elements a variable occupies in the flat buffers, trailing zero rows included."""
+    pad = int(getattr(v, "pad_rows", 0) or 0)
+    if pad <= 0 or len(v.shape) == 0:
+        return v.numel()
+    return v.numel() + pad * (v.numel() // max(v.shape[0], 1))
 
 
 class Bucket(object):
@@ -65,7 +81,7 @@ class FlatGroup(object):
         for v in self.variables:
             self.offsets.append(off)
             bvars.append(v)
-            off += _round_up(v.numel(), _ALIGN)
+            off += _round_up(_extent(v), _ALIGN)
             if off - bstart >= bucket_elems:
                 off = bstart + _round_up(off - bstart, _ALIGN * self.pad_to)
                 self.buckets.append(Bucket(self, len(self.buckets), bstart, off, bvars))
@@ -91,6 +107,12 @@ class FlatGroup(object):
                 sview = self.shadow[o:o + n].view(v.shape)
                 sview.copy_(mview)
                 v.shadow = sview
+            e = _extent(v)
+            if e > n:
+                pshape = (v.shape[0] + int(v.pad_rows),) + tuple(v.shape[1:])
+                v.master_padded = self.master[o:o + e].view(pshape)
+                v.grad_padded = self.grad[o:o + e].view(pshape)
+                v.shadow_padded = self.shadow[o:o + e].view(pshape) if self.shadow is not None else None
             v.flat_group = self
             v.flat_offset = o
 

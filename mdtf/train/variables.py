@@ -142,6 +142,8 @@ class Variable(object):
         self.collections = list(collections_ or [])
         self.initial_value = None
         self.apply_weight_decay = tensor.dim() > 1   # optimizer-fused decay: weights yes, biases/BN no
+        self.pad_rows = 0                   # zero rows reserved after the variable in the flat buffers
+        self.master_padded = self.grad_padded = self.shadow_padded = None   # their views (parallel/flat.py)
 
     @property
     def shape(self):
@@ -446,6 +448,13 @@ def variable_scope(name_or_scope, reuse=None, default_name=None):
 
 def get_variable_scope():
     return _STORE.current_scope()
+
+
+def find_variable(name):
+    """The :class:`Variable` object ``name`` names in the current scope (None if absent), whatever the grad mode
+    (``get_variable`` returns its read, which carries the object only under grad mode)."""
+    scope = _STORE.current_scope()
+    return _STORE.vars.get("%s/%s" % (scope.name, name) if scope.name else name)
 
 
 @contextlib.contextmanager

@@ -287,3 +287,40 @@ def test_conv_table_lookup_is_batch_agnostic():
     a = C.choose("fwd", (256, 56, 56, 64), w, (1, 1), (0, 0, 0, 0), (1, 1))
     b = C.choose("fwd", (64, 56, 56, 64), w, (1, 1), (0, 0, 0, 0), (1, 1))
     assert a == b
+
+
+def test_flat_space_padded_rows_stay_zero():
+    """A variable with ``pad_rows`` gets zero rows after it in master, gradient and shadow (the tied BERT decoder's
+    30720-row vocabulary): the padded views alias the variable, the fused updates keep the pad at zero, and the
+    layout of every other variable is unchanged apart from the offset."""
+    from mdtf.ops import optim
+    from mdtf.parallel.flat import FlatParamSpace
+    torch.manual_seed(0)
+    a = V.Variable("emb", torch.randn(10, 4))
+    b = V.Variable("bias", torch.randn(10))
+    c = V.Variable("other", torch.randn(3, 4))
+    a.pad_rows = b.pad_rows = 6
+    space = FlatParamSpace([a, b, c], "cpu", torch.bfloat16)
+    for v, rows in ((a, 16), (b, 16)):
+        assert v.master_padded.shape[0] == rows and v.grad_padded.shape[0] == rows
+        assert v.shadow_padded.shape[0] == rows
+        assert v.master_padded.data_ptr() == v.master.data_ptr()
+        assert v.grad_padded.data_ptr() == v.grad.data_ptr()
+        assert v.shadow_padded.data_ptr() == v.shadow.data_ptr()
+        assert not v.master_padded[v.shape[0]:].any() and not v.shadow_padded[v.shape[0]:].any()
+    assert c.master_padded is None
+    a0, c0 = a.master.clone(), c.master.clone()
+    for kind in ("momentum", "adam"):
+        for g in space.groups:
+            g.grad.normal_()
+            a.grad_padded[10:].zero_()          # a sum of zero products, as the decoder writes it
+            b.grad_padded[10:].zero_()
+            if kind == "momentum":
+                optim.momentum_(g.master, g.grad, g.state_buffer("m"), g.shadow, 0.1, 0.9, weight_decay=1e-2)
+            else:
+                optim.adam_(g.master, g.grad, g.state_buffer("m1"), g.state_buffer("v1"), g.shadow, 0.01, 0.9, 0.999,
+                            1e-8, 1, weight_decay=1e-2)
+        for v in (a, b):
+            assert not v.master_padded[v.shape[0]:].any() and not v.shadow_padded[v.shape[0]:].any()
+    assert not torch.equal(a.master, a0) and not torch.equal(c.master, c0)
+    assert torch.equal(c.shadow, c.master.to(torch.bfloat16))

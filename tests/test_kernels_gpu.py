@@ -2129,3 +2129,49 @@ def test_backup_workers_device_mask_two_ranks(tmp_path):
     assert sum(r["contributed"] for r in res) == 5
     for k in res[0]["weights"]:
         assert torch.allclose(torch.tensor(res[0]["weights"][k]), torch.tensor(res[1]["weights"][k]), atol=1e-6)
+
+
+def test_tied_decoder_padded_vocab_matches_fp32():
+    """The tied MLM decoder over the zero-padded 30720-row vocabulary (forward with bias, split-K data gradient,
+    weight + bias gradients into the padded fp32 slots) against fp32 PyTorch on the unpadded [30522, 768]
+    shapes, with the loss on the strided logits view (kernels._Xent hands back the zero-padded gradient)."""
+    from mdtf.ops import gemm, kernels
+    from mdtf.parallel.flat import FlatParamSpace
+    from mdtf.train import variables as V
+    torch.manual_seed(11)
+    Vn, H, M = 30522, 768, 1280
+    wv = V.Variable("word_embeddings", torch.randn(Vn, H) * 0.05)
+    bv = V.Variable("output_bias", torch.randn(Vn) * 0.1)
+    wv.pad_rows = bv.pad_rows = gemm.decoder_pad_rows(Vn)
+    assert Vn + wv.pad_rows == 30720
+    FlatParamSpace([wv, bv], DEV, torch.bfloat16)
+    for v in (wv, bv):
+        v.grad.zero_()
+    h = (torch.randn(M, H, device=DEV) * 0.5).bfloat16().requires_grad_(True)
+    labels = torch.randint(0, Vn, (M,), device=DEV)
+    calls = []
+    orig = gemm._TiedDecoder.backward
+
+    def spy(ctx, dy):
+        calls.append(dy.stride(0))
+        return orig(ctx, dy)
+    gemm._TiedDecoder.backward = staticmethod(spy)
+    try:
+        w, b = wv.read(torch.bfloat16), bv.read(torch.bfloat16)
+        logits = ops.tied_decoder(h, w, b)
+        assert logits.shape == (M, Vn) and logits.stride(0) == 30720
+        loss = kernels.softmax_xent(logits, labels).mean()
+        loss.backward()
+    finally:
+        gemm._TiedDecoder.backward = orig
+    assert calls == [30720], "the padded decoder backward did not run on the zero-padded logit gradient"
+    hf = h.detach().float().requires_grad_(True)
+    wf = wv.shadow.float().requires_grad_(True)
+    bf = bv.shadow.float().requires_grad_(True)
+    lf = hf @ wf.t() + bf
+    assert _rel(logits.float(), lf) < 1e-2
+    torch.nn.functional.cross_entropy(lf, labels).backward()
+    assert _rel(h.grad, hf.grad) < 1e-2
+    assert _rel(wv.grad, wf.grad) < 2e-2
+    assert _rel(bv.grad, bf.grad) < 1e-2
+    assert not wv.grad_padded[Vn:].any() and not bv.grad_padded[Vn:].any()
