@@ -478,6 +478,61 @@ __global__ void __launch_bounds__(256) xent_fwd_row_bf16(const bf16_t* __restric
   }
 }
 
+// rows 16-B aligned with a stride that is a multiple of 8 (the padded decoder's [rows][30720] logits): 16-B loads,
+// four in flight per thread, columns >= K masked out; the same online (max, sum) merge as xent_fwd_row_bf16
+__global__ void __launch_bounds__(256) xent_fwd_row_v8(const bf16_t* __restrict__ logits,
+                                                       const long long* __restrict__ labels, int K, long long ld,
+                                                       float* __restrict__ loss, float* __restrict__ lse) {
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const bf16_t* p = logits + (long long)row * ld;
+  const int kv = (K + 7) >> 3;
+  float m = -INFINITY, s = 0.f;
+  auto eat = [&](const uint4& w, int v) {
+    const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
+    float a[8];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      a[2 * h] = v * 8 + 2 * h < K ? __uint_as_float(wv[h] << 16) : -INFINITY;
+      a[2 * h + 1] = v * 8 + 2 * h + 1 < K ? __uint_as_float(wv[h] & 0xffff0000u) : -INFINITY;
+    }
+    float mx = a[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) mx = fmaxf(mx, a[j]);
+    if (mx > m) {
+      s = (m == -INFINITY ? 0.f : s * __expf(m - mx));
+      m = mx;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += __expf(a[j] - m);
+  };
+  int v = tid;
+  for (; v + 3 * 256 < kv; v += 4 * 256) {
+    uint4 w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) w[u] = *reinterpret_cast<const uint4*>(p + (v + u * 256) * 8);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) eat(w[u], v + u * 256);
+  }
+  for (; v < kv; v += 256) eat(*reinterpret_cast<const uint4*>(p + v * 8), v);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lse_merge(m, s, __shfl_xor(m, o, 64), __shfl_xor(s, o, 64));
+  __shared__ float sm[4], ss[4];
+  if ((tid & 63) == 0) {
+    sm[tid >> 6] = m;
+    ss[tid >> 6] = s;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float M = sm[0], S = ss[0];
+    for (int w = 1; w < 4; ++w) lse_merge(M, S, sm[w], ss[w]);
+    const float l = M + __logf(S);
+    const long long lab = labels[row];
+    const float xl = (lab >= 0 && lab < K) ? bf2f(p[lab]) : 0.f;
+    lse[row] = l;
+    loss[row] = l - xl;
+  }
+}
+
 template <typename T>
 __global__ void xent_bwd(const T* __restrict__ logits, const long long* __restrict__ labels,
                          const float* __restrict__ lse, const float* __restrict__ dloss, T* __restrict__ dlogits,
@@ -793,7 +848,9 @@ MDTF_EXPORT int mdtf_xent_fwd(const void* logits, int is_bf16, const long long* 
                               float* loss, float* lse, hipStream_t st) {
   if (ld < K) return MDTF_EINVAL;
   dim3 grid(ceil_div(N, 4));
-  if (is_bf16 && K >= 2048 && (reinterpret_cast<uintptr_t>(logits) & 3) == 0 && (K & 1) == 0 && (ld & 1) == 0)
+  if (is_bf16 && K >= 2048 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0 && (ld & 7) == 0)
+    hipLaunchKernelGGL(xent_fwd_row_v8, dim3(N), dim3(256), 0, st, (const bf16_t*)logits, labels, K, ld, loss, lse);
+  else if (is_bf16 && K >= 2048 && (reinterpret_cast<uintptr_t>(logits) & 3) == 0 && (K & 1) == 0 && (ld & 1) == 0)
     hipLaunchKernelGGL(xent_fwd_row_bf16, dim3(N), dim3(256), 0, st, (const bf16_t*)logits, labels, K, ld, loss, lse);
   else if (is_bf16)
     hipLaunchKernelGGL(xent_fwd<bf16_t>, grid, dim3(kT), 0, st, (const bf16_t*)logits, labels, N, K, ld, loss, lse);

@@ -152,6 +152,27 @@ def test_softmax_xent(dtype, N, K):
     assert _rel(lg.grad, lc.grad) < 2e-2
 
 
+def test_softmax_xent_strided_rows():
+    """Logits as a [rows, 30522] view of [rows, 30720] rows (the padded MLM decoder): the 16-B vector forward and
+    backward kernels, the gradient handed back as the same view of a zero-padded buffer."""
+    from mdtf.ops import gemm
+    torch.manual_seed(3)
+    N, K, LD = 67, 30522, 30720
+    full = (torch.randn(N, LD) * 3).bfloat16()
+    labels = torch.randint(0, K, (N,))
+    lp = full.to(DEV).requires_grad_(True)
+    lg = lp[:, :K]
+    l = ops.sparse_softmax_cross_entropy_with_logits(labels.to(DEV), lg)
+    lc = full[:, :K].float().requires_grad_(True)
+    lr = torch.nn.functional.cross_entropy(lc, labels, reduction="none")
+    assert _rel(l, lr) < 1e-3
+    l.mean().backward()
+    lr.mean().backward()
+    assert _rel(lp.grad[:, :K], lc.grad) < 2e-2
+    assert not lp.grad[:, K:].any()
+    gemm._PADDED_GRADS.clear()
+
+
 @pytest.mark.parametrize("act", ["relu", "gelu", None])
 @pytest.mark.parametrize("C", [64, 10])
 def test_bias_act(act, C):
