@@ -62,6 +62,18 @@ void magic_div(unsigned d, unsigned& m, int& l) {
 
 MDTF_EXPORT void mdtf_conv_ws_debug(int mode) { ws_debug = mode; }
 
+namespace {
+// MDTF_WS_EPF=1: the epilogue's global reads are issued before the tile's MFMAs (2-subtile tiles); measured
+// neutral in the ResNet-50 step (profiles/ab_r5.md), so off by default
+int ws_epf() {
+  static const int on = [] {
+    const char* e = getenv("MDTF_WS_EPF");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return on;
+}
+}  // namespace
+
 // out = conv(src, filter) on the weight-stationary kernel (see the header comment).
 // wmode 0: wgt = Wt[Ncol][K] (K = KH*KW*C); wmode 1: wgt = W HWIO [KH][KW][Ncol][C] used flipped
 // (the stride-1 data gradient; pass the DX pads (KH-1)*DH-PH, (KW-1)*DW-PW).
@@ -105,6 +117,7 @@ int conv_ws_impl(const void* src, const void* wgt, void* out, int N, int H, int 
   if (a.M + 16LL * 8 * 64 >= 0x7fffffffLL) return MDTF_EUNSUPPORTED;           // 32-bit pixel indices
   if (nw % cg) return MDTF_EINVAL;
   a.dbg = ws_debug;
+  a.epf = ws_epf();
   const bool stats = ssum != nullptr, bstat = bsum != nullptr;
   if (stats && bstat) return MDTF_EINVAL;
   if (stats) return accumulate ? MDTF_EINVAL : dispatch_ws<1>(a, tp, nw, cg, d, grid_cap, st);
@@ -169,6 +182,7 @@ MDTF_EXPORT int mdtf_conv_ws_dual(const void* dy1, const void* w1, const void* d
   magic_div((unsigned)W, a.mow, a.sow);
   magic_div((unsigned)H, a.mohh, a.sohh);
   a.dbg = ws_debug;
+  a.epf = ws_epf();
   const int tp = tile % 10, nw = (tile / 10) % 10, cg = (tile / 100) % 10;
   if (bsum) {
     if (!bx) return MDTF_EINVAL;
