@@ -1,0 +1,151 @@
+#!/usr/bin/env python
+"""In-step selection of the BERT-base weight-gradient kernel's (rows per tile, ring depth, split-K) per shape.
+
+``mm.WG_TILES`` was chosen from graph-timed isolated launches whose operands stay MALL-resident; in the step the
+operands arrive HBM-cold behind the data-gradient GEMM.  This re-times the eager BERT-base training step (batch 64,
+seq 128, the bench config) with every candidate of each (K, N, tokens) entry swapped in, keeps a candidate only
+when it beats the current entry by more than the step noise twice in a row, and writes a markdown report.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def build(batch, seq):
+    import mdtf
+    from mdtf.models import Bert, BertPretrainingLoss, SyntheticBertLoader
+    from mdtf.runtime import Net, Tower
+    from mdtf.train import variables as V
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    store = V.get_store()
+    store.device = dev
+    store.compute_dtype = torch.bfloat16
+    P = 20
+    ld = SyntheticBertLoader(seq, P, seed=0)
+    ld.batch_size = batch
+    raw, gt = ld.load_train_batch()
+    base = mdtf.train.AdamWeightDecayOptimizer(1e-4, weight_decay_rate=0.01)
+    tg = []
+    Tower(Net(Bert("base", seq_len=seq, max_predictions=P)), "tower_0/", tg, raw, gt, BertPretrainingLoss(P), base,
+          batch_size=batch).process()
+    opt = mdtf.train.SyncReplicasOptimizer(base, 1, 1, hip_graph=False)
+    op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
+    sess = mdtf.train.MonitoredTrainingSession(is_chief=True, log_step_count_steps=0)
+    return sess, op
+
+
+def step_ms(sess, op, steps, warm):
+    for _ in range(warm):
+        sess.run(op)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(steps):
+        sess.run(op)
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / steps
+
+
+def candidates(M, Nn, K):
+    out = []
+    for bm, stages in ((256, 3), (256, 2), (128, 2)):
+        if M % bm:
+            continue
+        for sp in (1, 2, 3, 4, 5, 6, 8):
+            if (K // 64) // sp >= 8:
+                out.append((bm, stages, sp))
+    return out
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--batch", type=int, default=64)
+    p.add_argument("--seq", type=int, default=128)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warm", type=int, default=2)
+    p.add_argument("--budget_s", type=float, default=600.0)
+    p.add_argument("--report", default="gpurun_out/bert_wg_tune.md")
+    args = p.parse_args()
+    from mdtf.ops import mm
+    t_start = time.time()
+    sess, op = build(args.batch, args.seq)
+    seen = []
+    real = mm.wg_pick
+
+    def rec(M, Nn, K):
+        if (M, Nn, K) not in seen:
+            seen.append((M, Nn, K))
+        return real(M, Nn, K)
+    mm.wg_pick = rec
+    for _ in range(3):
+        sess.run(op)
+    torch.cuda.synchronize()
+    mm.wg_pick = real
+    base = [step_ms(sess, op, args.steps, args.warm) for _ in range(6)]
+    noise = statistics.pstdev(base)
+    thr = max(2.5 * noise, 0.02)
+    t0 = statistics.median(base)
+    print("step %.3f ms (noise %.3f), shapes %s, threshold %.3f" % (t0, noise, seen, thr), flush=True)
+    lines = ["| shape (K, N, tokens) | before | after | step ms before | step ms after | tried |",
+             "|---|---|---|---:|---:|---:|"]
+    changed = {}
+    for key in seen:
+        if time.time() - t_start > args.budget_s:
+            print("budget reached", flush=True)
+            break
+        cur = real(*key)
+        t_cur = step_ms(sess, op, args.steps, args.warm)
+        best = (t_cur, cur)
+        had = key in mm.WG_TILES
+        old = mm.WG_TILES.get(key)
+        tried = 0
+        for cand in candidates(*key):
+            if cand == cur:
+                continue
+            mm.WG_TILES[key] = cand
+            try:
+                t = step_ms(sess, op, args.steps, args.warm)
+            except RuntimeError as ex:
+                print("  %s %s failed: %s" % (key, cand, ex), flush=True)
+                torch.cuda.synchronize()
+                continue
+            tried += 1
+            print("  %s %s %.3f ms" % (key, cand, t), flush=True)
+            if t < best[0]:
+                best = (t, cand)
+        keep = False
+        if best[1] != cur and best[0] < t_cur - thr:
+            mm.WG_TILES[key] = cur
+            a = step_ms(sess, op, args.steps, args.warm)
+            mm.WG_TILES[key] = best[1]
+            b = step_ms(sess, op, args.steps, args.warm)
+            keep = b < a - thr
+            if keep:
+                changed[str(key)] = list(best[1])
+                lines.append("| %s | %s | %s | %.3f | %.3f | %d |" % (key, cur, best[1], a, b, tried))
+        if not keep:
+            if had:
+                mm.WG_TILES[key] = old
+            else:
+                mm.WG_TILES.pop(key, None)
+        print("%s: %d tried, %s" % (key, tried, ("-> %s" % (best[1],)) if keep else "kept %s" % (cur,)), flush=True)
+    t1 = statistics.median([step_ms(sess, op, args.steps, args.warm) for _ in range(6)])
+    with open(args.report, "w") as f:
+        f.write("# In-step weight-gradient tile tuning (BERT-base, batch %d, seq %d, eager step)\n\n" % (
+            args.batch, args.seq))
+        f.write("Step before: %.3f ms (noise %.3f ms); after: %.3f ms.  Changes: %s\n\n" % (
+            t0, noise, t1, json.dumps(changed)))
+        f.write("\n".join(lines) + "\n")
+    print("step %.3f -> %.3f ms, changes %s" % (t0, t1, changed), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -324,3 +324,38 @@ def test_flat_space_padded_rows_stay_zero():
             assert not v.master_padded[v.shape[0]:].any() and not v.shadow_padded[v.shape[0]:].any()
     assert not torch.equal(a.master, a0) and not torch.equal(c.master, c0)
     assert torch.equal(c.shadow, c.master.to(torch.bfloat16))
+
+
+def test_bert_tied_decoder_padding_on_the_build_pass(tmp_path):
+    """BERT reserves the decoder's zero rows on the word embedding and the MLM bias during the build pass, so the
+    flat space has the padded views; training keeps the pad at zero and the checkpoint keeps the [vocab, H] shapes."""
+    from mdtf.models import Bert, BertPretrainingLoss, SyntheticBertLoader
+    from mdtf.ops import nn as ops
+    from mdtf.train.saver import Saver
+    V.reset_default_graph()
+    S.reset()
+    P = 4
+    ld = SyntheticBertLoader(16, P, vocab=1000, seed=0)
+    ld.batch_size = 2
+    raw, gt = ld.load_train_batch()
+    opt = mdtf.train.AdamWeightDecayOptimizer(1e-3, weight_decay_rate=0.01)
+    tg = []
+    Tower(Net(Bert("tiny", vocab_size=1000, seq_len=16, max_predictions=P)), "tower_0/", tg, raw, gt,
+          BertPretrainingLoss(P), opt, batch_size=2).process()
+    op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
+    sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
+    for _ in range(2):
+        sess.run(op)
+    pad = ops.decoder_pad_rows(1000)
+    store = V.get_store()
+    emb = store.vars["bert/embeddings/word_embeddings"]
+    bias = store.vars["cls/predictions/output_bias"]
+    for v in (emb, bias):
+        assert v.pad_rows == pad > 0
+        assert v.master_padded.shape[0] == 1000 + pad
+        assert not v.master_padded[1000:].any() and not v.grad_padded[1000:].any()
+    path = Saver().save(sess, str(tmp_path / "ckpt"))
+    from mdtf.ckpt.tensor_bundle import BundleReader
+    r = BundleReader(path)
+    assert tuple(r.get_tensor("bert/embeddings/word_embeddings").shape) == (1000, 128)
+    assert tuple(r.get_tensor("cls/predictions/output_bias").shape) == (1000,)
