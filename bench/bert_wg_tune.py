@@ -2,8 +2,9 @@
 """In-step selection of the BERT-base weight-gradient kernel's (rows per tile, ring depth, split-K) per shape.
 
 ``mm.WG_TILES`` was chosen from graph-timed isolated launches whose operands stay MALL-resident; in the step the
-operands arrive HBM-cold behind the data-gradient GEMM.  This re-times the eager BERT-base training step (batch 64,
-seq 128, the bench config) with every candidate of each (K, N, tokens) entry swapped in, keeps a candidate only
+operands arrive HBM-cold behind the data-gradient GEMM.  This re-times the captured (hipGraph) BERT-base training
+step (batch 64, seq 128, the bench config; re-captured after every table change -- the eager step is launch-bound
+and too noisy) with every candidate of each (K, N, tokens) entry swapped in, keeps a candidate only
 when it beats the current entry by more than the step noise twice in a row, and writes a markdown report.
 """
 import argparse
@@ -36,13 +37,14 @@ def build(batch, seq):
     tg = []
     Tower(Net(Bert("base", seq_len=seq, max_predictions=P)), "tower_0/", tg, raw, gt, BertPretrainingLoss(P), base,
           batch_size=batch).process()
-    opt = mdtf.train.SyncReplicasOptimizer(base, 1, 1, hip_graph=False)
+    opt = mdtf.train.SyncReplicasOptimizer(base, 1, 1, hip_graph=True)
     op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
     sess = mdtf.train.MonitoredTrainingSession(is_chief=True, log_step_count_steps=0)
     return sess, op
 
 
 def step_ms(sess, op, steps, warm):
+    op.release_graph()                  # the next step re-captures with the current table
     for _ in range(warm):
         sess.run(op)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -69,8 +71,8 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--batch", type=int, default=64)
     p.add_argument("--seq", type=int, default=128)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warm", type=int, default=2)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warm", type=int, default=3)
     p.add_argument("--budget_s", type=float, default=600.0)
     p.add_argument("--report", default="gpurun_out/bert_wg_tune.md")
     args = p.parse_args()
@@ -139,7 +141,7 @@ def main():
         print("%s: %d tried, %s" % (key, tried, ("-> %s" % (best[1],)) if keep else "kept %s" % (cur,)), flush=True)
     t1 = statistics.median([step_ms(sess, op, args.steps, args.warm) for _ in range(6)])
     with open(args.report, "w") as f:
-        f.write("# In-step weight-gradient tile tuning (BERT-base, batch %d, seq %d, eager step)\n\n" % (
+        f.write("# In-step weight-gradient tile tuning (BERT-base, batch %d, seq %d, captured step)\n\n" % (
             args.batch, args.seq))
         f.write("Step before: %.3f ms (noise %.3f ms); after: %.3f ms.  Changes: %s\n\n" % (
             t0, noise, t1, json.dumps(changed)))
