@@ -1,5 +1,7 @@
 #!/usr/bin/env python
-"""In-step selection of the BERT-base weight-gradient kernel's (rows per tile, ring depth, split-K) per shape.
+"""In-step selection of the BERT-base weight-gradient kernel's (rows per tile, ring depth, split-K) per shape, and
+(``--act``) of the FFN data gradient's tile (the v2 dgrad kernel with the GELU-backward epilogue,
+``gemm.DGRAD_ACT_TILES``).
 
 ``mm.WG_TILES`` was chosen from graph-timed isolated launches whose operands stay MALL-resident; in the step the
 operands arrive HBM-cold behind the data-gradient GEMM.  This re-times the captured (hipGraph) BERT-base training
@@ -67,6 +69,52 @@ def candidates(M, Nn, K):
     return out
 
 
+def act_candidates():
+    """(bm, bn, stages, ver) tiles the MODE-4 dispatch instantiates (csrc/conv_igemm.hip dispatch_fd_v2)."""
+    out = [(bm, bn, st, 2) for bm, bn in ((128, 128), (128, 64), (256, 128), (256, 64), (64, 128), (64, 64))
+           for st in (2, 3)]
+    out += [(256, 256, 1, 3), (256, 256, 2, 3), (256, 128, 2, 3), (256, 128, 3, 3), (256, 64, 3, 3),
+            (128, 256, 2, 3), (128, 256, 3, 3)]
+    return out
+
+
+def tune_act(sess, op, args, thr, lines, changed):
+    from mdtf.ops import gemm
+    for key in list(gemm.DGRAD_ACT_TILES):
+        cur = gemm.DGRAD_ACT_TILES[key]
+        t_cur = step_ms(sess, op, args.steps, args.warm)
+        best = (t_cur, cur)
+        tried = 0
+        for cand in act_candidates():
+            if cand == cur:
+                continue
+            gemm.DGRAD_ACT_TILES[key] = cand
+            try:
+                t = step_ms(sess, op, args.steps, args.warm)
+            except RuntimeError as ex:
+                print("  act %s %s failed: %s" % (key, cand, ex), flush=True)
+                torch.cuda.synchronize()
+                continue
+            tried += 1
+            print("  act %s %s %.3f ms" % (key, cand, t), flush=True)
+            if t < best[0]:
+                best = (t, cand)
+        keep = False
+        if best[1] != cur and best[0] < t_cur - thr:
+            gemm.DGRAD_ACT_TILES[key] = cur
+            a = step_ms(sess, op, args.steps, args.warm)
+            gemm.DGRAD_ACT_TILES[key] = best[1]
+            b = step_ms(sess, op, args.steps, args.warm)
+            keep = b < a - thr
+            if keep:
+                changed["act" + str(key)] = list(best[1])
+                lines.append("| act %s | %s | %s | %.3f | %.3f | %d |" % (key, cur, best[1], a, b, tried))
+        if not keep:
+            gemm.DGRAD_ACT_TILES[key] = cur
+        print("act %s: %d tried, %s" % (key, tried, ("-> %s" % (best[1],)) if keep else "kept %s" % (cur,)),
+              flush=True)
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--batch", type=int, default=64)
@@ -75,6 +123,7 @@ def main():
     p.add_argument("--warm", type=int, default=3)
     p.add_argument("--budget_s", type=float, default=600.0)
     p.add_argument("--report", default="gpurun_out/bert_wg_tune.md")
+    p.add_argument("--act", action="store_true", help="tune the FFN activation data-gradient tile only")
     args = p.parse_args()
     from mdtf.ops import mm
     t_start = time.time()
@@ -99,6 +148,9 @@ def main():
     lines = ["| shape (K, N, tokens) | before | after | step ms before | step ms after | tried |",
              "|---|---|---|---:|---:|---:|"]
     changed = {}
+    if args.act:
+        tune_act(sess, op, args, thr, lines, changed)
+        seen = []
     for key in seen:
         if time.time() - t_start > args.budget_s:
             print("budget reached", flush=True)
