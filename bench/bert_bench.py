@@ -107,7 +107,9 @@ def main():
         server, rank, world, pg = None, 0, 1, None
     lr = int(os.environ.get("LOCAL_RANK", "0"))
     gpu = torch.cuda.is_available()
-    dev = torch.device("cuda", lr) if gpu else torch.device("cpu")      # cpu: gloo rehearsal of the launch
+    # the server's device: one per local rank, or shared when an MDTF_DIST_BACKEND=gloo rehearsal runs more ranks
+    # than there are GPUs (as bench.py); cpu: gloo rehearsal of the launch
+    dev = (server.device() if server is not None else torch.device("cuda", lr)) if gpu else torch.device("cpu")
     if gpu:
         torch.cuda.set_device(dev)
     if args.stock and not gpu:
