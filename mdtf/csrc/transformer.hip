@@ -453,9 +453,20 @@ extern "C" int mdtf_reduce_partials(const float* ws, int B, int C, float* out, h
 extern "C" int mdtf_get_deterministic();
 extern "C" int mdtf_reduce_partials_strided(const float* ws, int B, int C, long long ld, float* out, hipStream_t st);
 
+// MDTF_LN_BWD_RPB: minimum rows per LayerNorm-backward block (default 16: 512 blocks at 8192 rows; A/B switch)
+static long long ln_bwd_rpb() {
+  static const long long v = [] {
+    const char* e = getenv("MDTF_LN_BWD_RPB");
+    const long long r = e ? atoll(e) : 0;
+    return r > 0 ? r : 16LL;
+  }();
+  return v;
+}
+
 static void ln_bwd_geometry(long long rows, int* blocks, int* rpb) {
-  long long b = ceil_div(rows, 16);         // >= 4 rows per wave (all in flight together)
-  if (b > 512) b = 512;
+  long long b = ceil_div(rows, ln_bwd_rpb());  // >= 4 rows per wave (all in flight together) by default
+  const long long cap = ln_bwd_rpb() == 16 ? 512 : 2048;
+  if (b > cap) b = cap;
   if (b < 1) b = 1;
   *rpb = static_cast<int>(ceil_div(rows, b));
   *blocks = static_cast<int>(ceil_div(rows, *rpb));
