@@ -24,6 +24,10 @@
 // Σy / Σy² partials for the following BatchNorm (bn.hip consumes them).
 #include "mdtf_common.h"
 
+#ifndef FD_PF16
+#define FD_PF16 1
+#endif
+
 using namespace mdtf;
 
 namespace {
@@ -811,7 +815,10 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   constexpr int ITER = BM * (BN / 8) / NT;
   static_assert(ITER * NT == BM * (BN / 8), "copy-out rows per thread");
   // rows in flight (register budget of the 256-row tiles; the 448-row tile's 14 rows per thread go in pairs)
-  constexpr int PF = ITER < 4 ? ITER : (ITER % 4 == 0 ? 4 : 2);
+  // (data gradients: the accumulators are dead once the C tile is in LDS, so up to 16 rows' reads go out at once
+  // -- one latency per tile instead of ITER / 4; MDTF_FD_PF16=0 builds keep groups of 4)
+  constexpr int PF = (FD_PF16 && (MODE == 1 || MODE == 2) && ITER <= 16) ? ITER
+                                                                        : (ITER < 4 ? ITER : (ITER % 4 == 0 ? 4 : 2));
   static_assert(ITER % PF == 0, "prefetch groups");
 #pragma unroll
   for (int g0 = 0; g0 < ITER; g0 += PF) {
