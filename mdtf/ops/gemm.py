@@ -785,8 +785,10 @@ class _TiedDecoder(torch.autograd.Function):
         Wp = wv.shadow_padded
         VP, H = Wp.shape
         M = h.shape[0]
-        if dy.stride(1) == 1 and dy.stride(0) == VP and _PADDED_GRADS.pop(dy.data_ptr(), None) == VP:
-            dp = dy.as_strided((M, VP), (VP, 1))
+        base = dy._base
+        if (dy.stride(1) == 1 and dy.stride(0) == VP and base is not None and tuple(base.shape) == (M, VP)
+                and base.data_ptr() == dy.data_ptr() and _PADDED_GRADS.pop(dy.data_ptr(), None) == VP):
+            dp = base                      # the zero-padded [rows, VP] buffer kernels._Xent wrote
         else:
             dp = torch.zeros((M, VP), dtype=h.dtype, device=h.device)
             dp[:, :Vn].copy_(dy)
