@@ -457,10 +457,13 @@ __device__ __forceinline__ void finalize_bwd(const FinBwd& a, long long M, int C
   const bool own = threadIdx.x < kFinCh && c < C;
   const float mu = own ? a.mean[c] : 0.f, inv = own ? a.invstd[c] : 0.f;
   const float g = own && a.gamma ? a.gamma[c] : 1.f;
-  const float dg0 = own && a.dgamma ? a.dgamma[c] : 0.f;
-  const float db0 = own && a.dbeta ? a.dbeta[c] : 0.f;
+  // zero_after bit 0: re-zero the partial rows; bit 1: write dgamma / dbeta instead of accumulating (the early
+  // finalize's workspace, added into the slots by the input-gradient pass)
+  const bool ow = (a.zero_after & 2) != 0;
+  const float dg0 = own && a.dgamma && !ow ? a.dgamma[c] : 0.f;
+  const float db0 = own && a.dbeta && !ow ? a.dbeta[c] : 0.f;
   double sdz, sdzx;
-  if (!sum_partials(a.p0, a.p1, a.gx, C, sdz, sdzx, a.zero_after != 0)) return;
+  if (!sum_partials(a.p0, a.p1, a.gx, C, sdz, sdzx, (a.zero_after & 1) != 0)) return;
   float db = (float)sdz;
   float dg = (float)((sdzx - (double)mu * sdz) * inv);
   if (a.dgamma) a.dgamma[c] = dg0 + dg;   // accumulate: zeroed buffer or the variable's fp32 grad slot
@@ -520,7 +523,14 @@ template <bool RELU, bool WRITE_DRES, bool NT = false>
 __global__ void __launch_bounds__(kThreads)
     bn_dx_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const uint8_t* __restrict__ mk,
                  bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long n8, int C, const float* __restrict__ k1,
-                 const float* __restrict__ k2, const float* __restrict__ k3, int accum_dres) {
+                 const float* __restrict__ k2, const float* __restrict__ k3, int accum_dres,
+                 const float* __restrict__ fin_dgdb, float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  if (fin_dgdb && blockIdx.x == 0) {        // an early finalize left dgamma | dbeta in its workspace
+    for (int c = threadIdx.x; c < C; c += kThreads) {
+      if (dgamma) dgamma[c] += fin_dgdb[c];
+      if (dbeta) dbeta[c] += fin_dgdb[C + c];
+    }
+  }
   const long long base = (long long)blockIdx.x * (kThreads * kVpt) + threadIdx.x;
   const uint4 z4 = make_uint4(0, 0, 0, 0);
   const bool acc = WRITE_DRES && accum_dres;
@@ -557,7 +567,8 @@ __global__ void __launch_bounds__(kThreads)
 
 inline int ew_grid(long long n8);
 void launch_dx(const void* dy, const void* x, const void* mask, void* dx, void* dres, long long M, int C,
-               const float* k1, const float* k2, const float* k3, int relu, int accum_dres, hipStream_t st);
+               const float* k1, const float* k2, const float* k3, int relu, int accum_dres, hipStream_t st,
+               const float* fin_dgdb = nullptr, float* dgamma = nullptr, float* dbeta = nullptr);
 
 void launch_apply(const void* x, const void* res, void* y, uint8_t* mask, long long n8, int C, const float* scale,
                   const float* shift, int relu, hipStream_t st) {
@@ -715,15 +726,40 @@ MDTF_EXPORT int mdtf_bn_bwd_stats(const void* dy, const void* x, const void* mas
   return 0;
 }
 
+// The backward finalize of mdtf_bn_bwd_stats alone, issued early (on a side stream beside the conv weight
+// gradient that follows the data gradient completing the statistics): ws[5C] = k1 | k2 | k3 | dgamma | dbeta,
+// dgamma / dbeta written, not accumulated; the partial rows are re-zeroed.
+MDTF_EXPORT int mdtf_bn_bwd_finalize_ws(long long M, int C, const float* gamma, const float* mean,
+                                        const float* invstd, const float* psum, const float* psq, int P, float* ws,
+                                        hipStream_t st) {
+  if (C % 8) return MDTF_EINVAL;
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M, C,
+                     gamma, mean, invstd, ws + 3 * C, ws + 4 * C, ws, ws + C, ws + 2 * C, 3);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// ... and its input-gradient pass: dx from ws's coefficients; dgamma / dbeta += ws's (block 0)
+MDTF_EXPORT int mdtf_bn_dx_ws(const void* dy, const void* x, const void* mask, void* dx, void* dres, long long M,
+                              int C, const float* ws, float* dgamma, float* dbeta, int relu, int accum_dres,
+                              hipStream_t st) {
+  if (C % 8) return MDTF_EINVAL;
+  launch_dx(dy, x, mask, dx, dres, M, C, ws, ws + C, ws + 2 * C, relu, accum_dres, st, ws + 3 * C, dgamma, dbeta);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
 namespace {
 void launch_dx(const void* dy, const void* x, const void* mask, void* dx, void* dres, long long M, int C,
-               const float* k1, const float* k2, const float* k3, int relu, int accum_dres, hipStream_t st) {
+               const float* k1, const float* k2, const float* k3, int relu, int accum_dres, hipStream_t st,
+               const float* fin_dgdb, float* dgamma, float* dbeta) {
   long long n8 = M * C / 8;
   const bool nt = bn_nt();
 #define DX(L_, W_)                                                                                                  \
   hipLaunchKernelGGL((nt ? bn_dx_kernel<L_, W_, true> : bn_dx_kernel<L_, W_, false>), dim3(ew_grid(n8)),          \
                      dim3(kThreads), 0, st, (const bf16_t*)dy, (const bf16_t*)x, L_ ? (const uint8_t*)mask : nullptr,\
-                     (bf16_t*)dx, W_ ? (bf16_t*)dres : nullptr, n8, C, k1, k2, k3, W_ ? accum_dres : 0)
+                     (bf16_t*)dx, W_ ? (bf16_t*)dres : nullptr, n8, C, k1, k2, k3, W_ ? accum_dres : 0, fin_dgdb,   \
+                     dgamma, dbeta)
   if (relu && dres)
     DX(true, true);
   else if (relu)

@@ -32,10 +32,10 @@ import torch
 
 class ActGradSink(object):
     """``consumers``: sink-aware consumers registered in the forward.  ``stat_req``: what the
-    producing BatchNorm needs for its backward statistics, ``(x, relu_mask)``.  The contributor that
+    producing BatchNorm needs for its backward statistics, ``(x, relu_mask[, early_finalize])``.  The contributor that
     completes the sum (the ``consumers``-th) may emit the statistics in its epilogue into ``stats``
     (the v2 conv dgrad does)."""
-    __slots__ = ("buf", "count", "consumers", "stat_req", "stats", "pend", "pconv")
+    __slots__ = ("buf", "count", "consumers", "stat_req", "stats", "pend", "pconv", "early")
 
     def __init__(self):
         self.buf = None
@@ -45,6 +45,7 @@ class ActGradSink(object):
         self.stats = None
         self.pend = None
         self.pconv = None
+        self.early = None       # (workspace, done event) of a backward finalize issued early (ops.bn)
 
     def idle(self):
         """Nothing contributed yet (neither written nor left pending / deferred)."""
@@ -138,6 +139,11 @@ class ActGradSink(object):
         """The emitted BN statistics ``(psum, psq, slots)`` or None (cleared)."""
         st, self.stats = self.stats, None
         return st
+
+    def take_early(self):
+        """The early backward finalize ``(ws, event)`` or None (cleared)."""
+        e, self.early = self.early, None
+        return e
 
 
 ENABLED = os.environ.get("MDTF_ACT_SINKS", "1") != "0"      # switch for A/B tests and benches

@@ -20,9 +20,42 @@ N.register("mdtf_bn_relu_maxpool_fwd", [N.P, N.P, N.P] + [N.I] * 12 + [N.P] * 4 
            + [N.P, N.P])
 N.register("mdtf_maxpool_bn_bwd", [N.P] * 4 + [N.I] * 12 + [N.P] * 8 + [N.P])
 N.register("mdtf_bn_bwd_dual", [N.P] * 6 + [N.L, N.I] + [N.P] * 7 + [N.I] + [N.P] * 6 + [N.P])
+N.register("mdtf_bn_bwd_finalize_ws", [N.L, N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P, N.P])
+N.register("mdtf_bn_dx_ws", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.I, N.I, N.P])
 
 
 FUSED_BWD = [0]      # backward passes that took their statistics from the dgrad epilogue (tests)
+# MDTF_BN_EARLY_FIN=1: the backward finalize runs on a side stream right after the data gradient that completes its
+# statistics instead of in the BN's backward (after the conv's weight gradient).  Measured -3 % in the captured
+# ResNet-50 step (the 45 fork / join pairs cost more than the finalize latency they hide, profiles/ab_r5.md): off.
+EARLY_FIN = os.environ.get("MDTF_BN_EARLY_FIN", "0") == "1"
+EARLY_USED = [0]     # backward passes that used an early finalize (tests)
+_FIN_SIDE = {}
+
+
+def _early_finalize(sbuf, g, mean, invstd, M, C):
+    """Issue the backward finalize of statistics ``sbuf`` ([2, slots, C], complete) on a side stream forked from
+    the current one: k1..k3 | dgamma | dbeta into a fresh workspace, the partial rows re-zeroed.  The conv's
+    weight gradient that follows on the main stream hides its latency; the BN backward waits for the returned
+    event before its input-gradient pass (csrc/bn.hip mdtf_bn_bwd_finalize_ws / mdtf_bn_dx_ws)."""
+    dev = sbuf.device
+    main = torch.cuda.current_stream(dev)
+    side = _FIN_SIDE.get(dev)
+    if side is None:
+        side = _FIN_SIDE[dev] = torch.cuda.Stream(device=dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        ws = torch.empty(5 * C, dtype=torch.float32, device=dev)
+        N.check(N.fn("mdtf_bn_bwd_finalize_ws")(M, C, N.ptr(g), N.ptr(mean), N.ptr(invstd), N.ptr(sbuf[0]),
+                                                N.ptr(sbuf[1]), int(sbuf.shape[1]), N.ptr(ws), N.stream_ptr()),
+                "bn_bwd_finalize_ws")
+        ev = torch.cuda.Event()
+        ev.record(side)
+    ws.record_stream(main)
+    for t in (sbuf, g, mean, invstd):
+        if t is not None:
+            t.record_stream(side)
+    return ws, ev
 # projection-shortcut BNs applied inside the residual BN's pass (MDTF_DEFER_SHORTCUT_BN=0: separate apply)
 DEFER_SHORTCUT = os.environ.get("MDTF_DEFER_SHORTCUT_BN", "1") != "0"
 
@@ -90,18 +123,30 @@ class _BNTrain(torch.autograd.Function):
         ctx.like = (gamma, beta)
         ctx.out_sink = actsink.attach(y)             # this output's consumers may accumulate here
         if ctx.out_sink is not None:
-            # the consumer that completes dy may emit Σ dy·mask, Σ dy·mask·x for this backward
-            ctx.out_sink.stat_req = (x, mask)
+            # the consumer that completes dy may emit Σ dy·mask, Σ dy·mask·x for this backward, and start its
+            # finalize right away
+            fin = None
+            if EARLY_FIN and x.is_cuda and not N.deterministic():
+                def fin(sbuf, g=g, mean=mean, invstd=invstd, M=M, C=C):
+                    return _early_finalize(sbuf, g, mean, invstd, M, C)
+            ctx.out_sink.stat_req = (x, mask, fin)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mask, g, mean, invstd = ctx.saved_tensors
         pstats = None
+        early = None
         why = "no_sink"
         if ctx.out_sink is not None:
             pstats = ctx.out_sink.take_stats()
+            early = ctx.out_sink.take_early()
             why = "no_epilogue_stats" if pstats is None else "fused"
+            if early is not None and (pstats is None or dy is not None):
+                # finalized early from statistics that turned out incomplete: wait for it (it re-zeroed the
+                # partial rows) and drop its workspace -- nothing reached the slots
+                torch.cuda.current_stream(x.device).wait_event(early[1])
+                early = None
             if pstats is not None and dy is not None:
                 # part of dy came through plain autograd: the epilogue statistics are incomplete
                 from . import conv as _conv
@@ -113,6 +158,8 @@ class _BNTrain(torch.autograd.Function):
         if BWD_TRACE is not None:
             BWD_TRACE.append((tuple(x.shape), ctx.has_res, why))
         if dy is None:
+            if early is not None:                        # join the side stream (captures must not end forked)
+                torch.cuda.current_stream(x.device).wait_event(early[1])
             return (None,) * 10
         dy = dy.contiguous()
         C = x.shape[-1]
@@ -138,7 +185,17 @@ class _BNTrain(torch.autograd.Function):
         # dgamma/dbeta accumulate straight into the fp32 grad slots when available
         dgamma = sg.grad if sg is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
         dbeta = sb.grad if sb is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
-        if pstats is not None:
+        if pstats is not None and early is not None:
+            from . import conv as _conv
+            ws, ev = early
+            torch.cuda.current_stream(x.device).wait_event(ev)
+            N.check(N.fn("mdtf_bn_dx_ws")(N.ptr(dy), N.ptr(x), N.ptr(mask if ctx.relu else None), N.ptr(dx),
+                                          N.ptr(dres), M, C, N.ptr(ws), N.ptr(dgamma), N.ptr(dbeta), int(ctx.relu),
+                                          accum, N.stream_ptr()), "bn_dx_ws")
+            _conv.bwd_stats_release(pstats, True)        # the early finalize re-zeroed it
+            FUSED_BWD[0] += 1
+            EARLY_USED[0] += 1
+        elif pstats is not None:
             from . import conv as _conv
             ws = torch.empty(3 * C, dtype=torch.float32, device=x.device)
             N.check(N.fn("mdtf_bn_bwd_stats")(N.ptr(dy), N.ptr(x), N.ptr(mask if ctx.relu else None), N.ptr(dx),

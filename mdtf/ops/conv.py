@@ -722,6 +722,14 @@ def bwd_stats_acquire(device, C, slots):
     return pool.pop() if pool else torch.zeros((2, slots, C), dtype=torch.float32, device=device)
 
 
+def _early_finalize(xs, sbuf):
+    """The BN whose output gradient this data gradient just completed may finalize its backward statistics now, on
+    a side stream beside this conv's weight gradient (``ops.bn`` EARLY_FIN), instead of after it."""
+    req = xs.stat_req
+    if req is not None and len(req) > 2 and req[2] is not None:
+        xs.early = req[2](sbuf)
+
+
 def bwd_stats_release(buf, zeroed):
     """Return a buffer to the pool; ``zeroed``: the BN finalize already re-zeroed it."""
     if not zeroed:
@@ -831,12 +839,13 @@ class _Conv(torch.autograd.Function):
             pc = xs.take_conv()
             bst = None
             if xs.stat_req is not None and xs.completing() and BWD_STATS and not N.deterministic():
-                bx, bmask = xs.stat_req
+                bx, bmask = xs.stat_req[:2]
                 sbuf = bwd_stats_acquire(x.device, x.shape[3], STAT_SLOTS)
                 bst = (bx, bmask, sbuf[0], sbuf[1], sbuf.shape[1])
             xs.written(ws_dual(dy, w, pc, x.shape, bn_stats=bst))
             if bst is not None:
                 xs.stats = sbuf
+                _early_finalize(xs, sbuf)
             DUAL_FUSED[0] += 1
             need_dx = False
         if need_dx and cd[0] == "winograd":
@@ -847,7 +856,7 @@ class _Conv(torch.autograd.Function):
                 buf, acc, pend = xs.target_ex()
                 bst = None
                 if xs.stat_req is not None and xs.completing() and BWD_STATS:
-                    bx, bmask = xs.stat_req
+                    bx, bmask = xs.stat_req[:2]
                     sbuf = bwd_stats_acquire(x.device, x.shape[3], STAT_SLOTS)
                     bst = (bx, bmask, sbuf[0], sbuf[1], sbuf.shape[1])
                     tile = (2,) + tuple(tile[1:])      # the statistics epilogue's register budget
@@ -855,6 +864,7 @@ class _Conv(torch.autograd.Function):
                                     acc_src=pend))
                 if bst is not None:
                     xs.stats = sbuf
+                    _early_finalize(xs, sbuf)
             else:
                 dx = ws_dgrad(dy, w, x.shape, pads, dil, tile)
         elif need_dx and cd[0] == "pp":
@@ -862,7 +872,7 @@ class _Conv(torch.autograd.Function):
                 buf, acc, pend = xs.target_ex()
                 bst = None
                 if xs.stat_req is not None and xs.completing() and BWD_STATS and not N.deterministic():
-                    bx, bmask = xs.stat_req
+                    bx, bmask = xs.stat_req[:2]
                     sbuf = bwd_stats_acquire(x.device, x.shape[3],
                                              stat_slots(-(-x.numel() // x.shape[3] // PP_TILES[cd[1]][0])))
                     bst = (bx, bmask, sbuf[0], sbuf[1], sbuf.shape[1])
@@ -870,6 +880,7 @@ class _Conv(torch.autograd.Function):
                                     acc_src=pend))
                 if bst is not None:
                     xs.stats = sbuf
+                    _early_finalize(xs, sbuf)
             else:
                 dx = pp_dgrad(dy, w, x.shape, pads, dil, cd[1])
         elif need_dx and not lib_dx:
@@ -878,13 +889,14 @@ class _Conv(torch.autograd.Function):
                 bst = None
                 if xs.stat_req is not None and xs.completing() and BWD_STATS and not N.deterministic():
                     # this dgrad completes the BN output's gradient: emit the BN backward statistics
-                    bx, bmask = xs.stat_req
+                    bx, bmask = xs.stat_req[:2]
                     sbuf = bwd_stats_acquire(x.device, x.shape[3], stat_slots(-(-x.numel() // x.shape[3] // cd[1])))
                     bst = (bx, bmask, sbuf[0], sbuf[1], sbuf.shape[1])
                 xs.written(mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5], out=buf,
                                       accumulate=acc, bn_stats=bst, acc_src=pend))
                 if bst is not None:
                     xs.stats = sbuf
+                    _early_finalize(xs, sbuf)
                 dx = None
             else:
                 dx = mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5])

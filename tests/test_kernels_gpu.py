@@ -2196,3 +2196,25 @@ def test_tied_decoder_padded_vocab_matches_fp32():
     assert _rel(wv.grad, wf.grad) < 2e-2
     assert _rel(bv.grad, bf.grad) < 1e-2
     assert not wv.grad_padded[Vn:].any() and not bv.grad_padded[Vn:].any()
+
+
+def test_bn_backward_early_finalize_matches_inline(monkeypatch):
+    """The BN backward finalize issued early on a side stream (MDTF_BN_EARLY_FIN=1: right after the data gradient
+    that completes its statistics, beside the conv weight gradient) == the finalize inside the BN backward:
+    same loss and the same gradients on a two-stage ResNet (up to the order of the fp32 weight-gradient atomics,
+    which differs run to run); the early path must actually run."""
+    from mdtf.ops import bn
+    torch.manual_seed(9)
+    x = torch.randn(8, 64, 64, 3)
+    y = torch.randint(0, 16, (8,))
+    monkeypatch.setattr(bn, "EARLY_FIN", True)
+    n0 = bn.EARLY_USED[0]
+    le, ge = _one_step(DEV, torch.bfloat16, x, y, blocks=[1, 1], grads=True)
+    assert bn.EARLY_USED[0] > n0
+    monkeypatch.setattr(bn, "EARLY_FIN", False)
+    n1 = bn.EARLY_USED[0]
+    li, gi = _one_step(DEV, torch.bfloat16, x, y, blocks=[1, 1], grads=True)
+    assert bn.EARLY_USED[0] == n1
+    assert le == li
+    for k in gi:
+        assert _rel(ge[k], gi[k]) < 1e-4, (k, _rel(ge[k], gi[k]))
