@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const bf16_t* __restrict__ x
                                                    bf16_t* __restrict__ y, bf16_t* __restrict__ s_out,
                                                    float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                    long long rows, int H, float eps, uint32_t thr, float inv_keep,
-                                                   uint32_t seed, const long long* __restrict__ seed_off) {
+                                                   uint32_t seed, const long long* __restrict__ seed_off, int nt_s) {
   seed = step_seed(seed, seed_off);
   const int lane = threadIdx.x & (LPR - 1);
   const long long row = (long long)blockIdx.x * (kT / LPR) + (threadIdx.x / LPR);
@@ -99,7 +99,17 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const bf16_t* __restrict__ x
   for (int i = 0; i < NV; ++i) {
     const int c = (lane + i * LPR);
     if (c < nvec) {
-      if (s_out) store_bf8(s_out + row * H + c * 8, v[i]);
+      if (s_out) {             // the residual sum is read again only by the backward: nt_s streams it out
+        if (nt_s) {
+          typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+          u32x4_t w;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) w[k] = pack_bf2(v[i][2 * k], v[i][2 * k + 1]);
+          __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(s_out + row * H + c * 8));
+        } else {
+          store_bf8(s_out + row * H + c * 8, v[i]);
+        }
+      }
       const float4 g0 = *reinterpret_cast<const float4*>(gamma + c * 8);
       const float4 g1 = *reinterpret_cast<const float4*>(gamma + c * 8 + 4);
       const float4 b0 = *reinterpret_cast<const float4*>(beta + c * 8);
@@ -442,9 +452,14 @@ MDTF_EXPORT int mdtf_ln_fwd(const void* x, const void* res, const float* gamma, 
   if (rows * H > 0xffffffffLL && p_drop > 0.f) return MDTF_EUNSUPPORTED;
   const uint32_t thr = drop_thr(p_drop);
   const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  // MDTF_LN_NT=1: nontemporal stores of the saved residual sum (A/B switch)
+  static const int nt_s = [] {
+    const char* e = getenv("MDTF_LN_NT");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
   LN_DISPATCH(H, ln_fwd_kernel, dim3(ceil_div(rows, kT / 32)), dim3(ceil_div(rows, kT / 64)), (const bf16_t*)x,
               (const bf16_t*)res, gamma, beta, (bf16_t*)y, (bf16_t*)s, mean, rstd, rows, H, eps, thr, inv_keep,
-              (uint32_t)seed, seed_off);
+              (uint32_t)seed, seed_off, nt_s);
   MDTF_LAUNCH_CHECK();
   return 0;
 }
