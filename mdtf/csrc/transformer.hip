@@ -401,6 +401,47 @@ __global__ void embed_bwd_small_kernel(const bf16_t* __restrict__ dy, const long
       if (acc[r][k] != 0.f) atomicAdd(dtable + (long long)r * H + v8 * 8 + k, acc[r][k]);
 }
 
+// Small tables, deterministic two-pass form: block b sums tokens [16 b, 16 b + 16) per (row, 8-column vector) in
+// registers (four tokens' loads in flight) and writes its partial rows ws[b][vocab][H]; the shared partial-row
+// reduction then adds them into the table gradient.  512 blocks at 8192 tokens instead of 128 blocks whose
+// atomics all hit the same vocab x H addresses (the type embedding: 2 x 768).
+constexpr int kSmallTok2 = 16;
+__global__ void embed_bwd_small_part(const bf16_t* __restrict__ dy, const long long* __restrict__ ids,
+                                     float* __restrict__ ws, long long n, int H, int vocab) {
+  const int v8 = threadIdx.x;
+  if (v8 * 8 >= H) return;
+  const long long t0 = (long long)blockIdx.x * kSmallTok2;
+  const long long t1 = t0 + kSmallTok2 < n ? t0 + kSmallTok2 : n;
+  float acc[kSmallVocab][8];
+#pragma unroll
+  for (int r = 0; r < kSmallVocab; ++r)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[r][k] = 0.f;
+  for (long long t = t0; t < t1; t += 4) {
+    long long id[4];
+    float g[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = t + u < t1;
+      id[u] = ok ? ids[t + u] : -1;
+      if (ok) load_bf8(dy + (t + u) * H + v8 * 8, g[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < kSmallVocab; ++r)
+        if (id[u] == r) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[r][k] += g[u][k];
+        }
+  }
+  for (int r = 0; r < vocab; ++r) {
+    float* dst = ws + ((long long)blockIdx.x * vocab + r) * H + v8 * 8;
+    *reinterpret_cast<float4*>(dst) = make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(acc[r][4], acc[r][5], acc[r][6], acc[r][7]);
+  }
+}
+
 inline int gcap(long long work) {
   long long b = ceil_div(work, kT);
   return static_cast<int>(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -660,6 +701,26 @@ MDTF_EXPORT int mdtf_embed_fwd(const void* table, const long long* ids, void* ou
                      (bf16_t*)out, n, H, vocab);
   MDTF_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int mdtf_reduce_partials(const float* ws, int B, int C, float* out, hipStream_t st);
+
+// fp32 workspace floats mdtf_embed_bwd_ws needs (0: the table is not small)
+MDTF_EXPORT long long mdtf_embed_bwd_ws_floats(long long n, int H, long long vocab) {
+  if (vocab > kSmallVocab || H % 8 || H / 8 > 1024 || n <= 0) return 0;
+  return ceil_div(n, kSmallTok2) * vocab * H;
+}
+
+// dtable += scatter of dy by ids for a small table (vocab <= 4), deterministic: partial rows + one reduction
+MDTF_EXPORT int mdtf_embed_bwd_ws(const void* dy, const long long* ids, float* dtable, long long n, int H,
+                                  long long vocab, float* ws, hipStream_t st) {
+  if (mdtf_embed_bwd_ws_floats(n, H, vocab) == 0) return MDTF_EINVAL;
+  const int nb = static_cast<int>(ceil_div(n, kSmallTok2));
+  const int threads = static_cast<int>(ceil_div(H / 8, 64) * 64);
+  hipLaunchKernelGGL(embed_bwd_small_part, dim3((unsigned)nb), dim3(threads), 0, st, (const bf16_t*)dy, ids, ws, n,
+                     H, static_cast<int>(vocab));
+  MDTF_LAUNCH_CHECK();
+  return mdtf_reduce_partials(ws, nb, static_cast<int>(vocab) * H, dtable, st);
 }
 
 MDTF_EXPORT int mdtf_embed_bwd(const void* dy, const long long* ids, float* dtable, long long n, int H,

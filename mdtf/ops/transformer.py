@@ -20,6 +20,11 @@ N.register("mdtf_softmax_fwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.L, N.P])
 N.register("mdtf_softmax_bwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.P])
 N.register("mdtf_embed_fwd", [N.P, N.P, N.P, N.L, N.I, N.L, N.P])
 N.register("mdtf_embed_bwd", [N.P, N.P, N.P, N.L, N.I, N.L, N.P])
+N.register("mdtf_embed_bwd_ws_floats", [N.L, N.I, N.L], N.L)
+N.register("mdtf_embed_bwd_ws", [N.P, N.P, N.P, N.L, N.I, N.L, N.P, N.P])
+# MDTF_EMBED_SMALL_2PASS=0: small tables (token types) by the one-pass atomic kernel instead of partial rows + one
+# reduction
+EMBED_SMALL_2PASS = os.environ.get("MDTF_EMBED_SMALL_2PASS", "1") != "0"
 N.register("mdtf_attn_fwd", [N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P, N.P])
 N.register("mdtf_attn_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P, N.P])
 N.register("mdtf_set_attn_bwd", [N.I], N.I)     # S = 128 backward kernel: 1 = v1 ([q][k] images), 2 = v2
@@ -200,8 +205,14 @@ class _Embed(torch.autograd.Function):
             finally:
                 torch.use_deterministic_algorithms(prev)
         else:
-            N.check(N.fn("mdtf_embed_bwd")(N.ptr(dy), N.ptr(ids), N.ptr(dt), ids.numel(), H, vocab,
-                                           N.stream_ptr()), "embed_bwd")
+            nws = int(N.fn("mdtf_embed_bwd_ws_floats")(ids.numel(), H, vocab)) if EMBED_SMALL_2PASS else 0
+            if nws > 0:
+                ws = torch.empty(nws, dtype=torch.float32, device=dy.device)
+                N.check(N.fn("mdtf_embed_bwd_ws")(N.ptr(dy), N.ptr(ids), N.ptr(dt), ids.numel(), H, vocab, N.ptr(ws),
+                                                  N.stream_ptr()), "embed_bwd_ws")
+            else:
+                N.check(N.fn("mdtf_embed_bwd")(N.ptr(dy), N.ptr(ids), N.ptr(dt), ids.numel(), H, vocab,
+                                               N.stream_ptr()), "embed_bwd")
         if sink is not None:
             return V.grad_marker(ctx.like), None
         return dt.to(ctx.like.dtype), None
