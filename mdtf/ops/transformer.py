@@ -263,8 +263,36 @@ class _BertEmbed(torch.autograd.Function):
         return out[0], out[1], out[2], None, None
 
 
+class _AddPositions(torch.autograd.Function):
+    """``e + pos[0..S)`` broadcast over the batch for ``e`` [B, S, H].  The position table's gradient is the
+    column sum of ``dy`` over the batch (``mdtf_colsum`` of dy viewed [B, S*H] into slot rows 0..S-1), not a
+    scatter of B*S rows onto S rows with atomics; no position-id tensor and no gather either way."""
+
+    @staticmethod
+    def forward(ctx, e, pos):
+        S_ = e.shape[1]
+        ctx.S = S_
+        ctx.like = pos
+        ctx.sink = V.grad_sink(pos)
+        return e + pos[:S_]
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import kernels as K
+        B, S_, H = dy.shape
+        dy = dy.contiguous()
+        sink = ctx.sink
+        dt = sink.grad if sink is not None else torch.zeros(ctx.like.shape, dtype=torch.float32, device=dy.device)
+        K.colsum_into(dy.view(B, S_ * H), dt[:S_].view(S_ * H))
+        if sink is not None:
+            return dy, V.grad_marker(ctx.like)
+        return dy, dt.to(ctx.like.dtype)
+
+
 # MDTF_BERT_EMBED=1: the one-kernel embedding (bert_embeddings)
 BERT_EMBED_FUSED = os.environ.get("MDTF_BERT_EMBED", "0") == "1"
+# MDTF_POS_BCAST=0: the position embedding as a gather of arange ids (atomic scatter backward), for A/B
+POS_BCAST = os.environ.get("MDTF_POS_BCAST", "1") == "1"
 
 
 def bert_embeddings(word, pos, typ, ids, types):
@@ -274,8 +302,11 @@ def bert_embeddings(word, pos, typ, ids, types):
     if (BERT_EMBED_FUSED and N.use_native(word) and not N.deterministic() and word.dtype == torch.bfloat16 and pos.dtype == word.dtype
             and typ.dtype == word.dtype and word.shape[1] % 8 == 0 and S_ <= pos.shape[0] and typ.shape[0] <= 4):
         return _BertEmbed.apply(word, pos, typ, ids, types)
-    pos_ids = torch.arange(S_, device=ids.device).unsqueeze(0).expand(B, S_)
     e = embedding_lookup(word, ids)
+    if (POS_BCAST and N.use_native(word) and pos.dtype == e.dtype and pos.dim() == 2 and S_ <= pos.shape[0]
+            and (S_ * pos.shape[1]) % 8 == 0 and e.dtype == torch.bfloat16):
+        return _AddPositions.apply(e, pos) + embedding_lookup(typ, types)
+    pos_ids = torch.arange(S_, device=ids.device).unsqueeze(0).expand(B, S_)
     return e + embedding_lookup(pos, pos_ids) + embedding_lookup(typ, types)
 
 

@@ -563,11 +563,14 @@ def test_conv_bn_fused_stats(shape, k, s, co, relu, res, monkeypatch):
         assert _rel(outs[DEV]["dr"], outs["cpu"]["dr"]) < 5e-2
 
 
-def test_bert_embeddings_fused_vs_fp32(monkeypatch):
-    """word[ids] + pos[s] + type[types] (one kernel each way, csrc/transformer.hip) vs fp32 lookups on the CPU:
-    output and the three table gradients (word rows by atomics, position rows summed over the batch)."""
+@pytest.mark.parametrize("path", ["fused", "pos_bcast", "gather"])
+def test_bert_embeddings_fused_vs_fp32(path, monkeypatch):
+    """word[ids] + pos[s] + type[types] vs fp32 lookups on the CPU: output and the three table gradients.  fused:
+    one kernel each way (csrc/transformer.hip); pos_bcast: three-op path with the position rows added by broadcast
+    and their gradient a column sum over the batch (the step's default); gather: position ids looked up."""
     from mdtf.ops import transformer as T
-    monkeypatch.setattr(T, "BERT_EMBED_FUSED", True)
+    monkeypatch.setattr(T, "BERT_EMBED_FUSED", path == "fused")
+    monkeypatch.setattr(T, "POS_BCAST", path == "pos_bcast")
     torch.manual_seed(21)
     B, S_, H, Vv = 12, 24, 64, 50
     word, pos, typ = torch.randn(Vv, H), torch.randn(40, H), torch.randn(2, H)
