@@ -166,6 +166,13 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=pg)
     elapsed = float(t.item())
+    # the communicator's own rank count (a SUM all-reduce of ones over the training group), so a scaling record
+    # shows that RCCL -- not a fallback -- saw every rank
+    comm = {"backend": None, "ranks_in_collective": 1}
+    if distributed and dist.is_initialized():
+        one = torch.ones(1, dtype=torch.float32, device=dev if dev.type == "cuda" else "cpu")
+        dist.all_reduce(one, group=pg)
+        comm = {"backend": str(dist.get_backend(pg)), "ranks_in_collective": int(round(float(one.item())))}
     final_loss = float(sess.run(loss))
     if rank == 0:
         ips = world * args.batch * args.steps / elapsed
@@ -190,7 +197,7 @@ def main():
                        # whether the step really replayed a captured graph (gloo rehearsals and a rejected
                        # capture run eagerly)
                        "hip_graph": bool(getattr(getattr(train_op, "graph", None), "replays", 0))},
-            "loss_first": float(lv), "loss_last": final_loss,
+            "loss_first": float(lv), "loss_last": final_loss, "comm": comm,
         }
         # scaling efficiency = rate(N) / (N x rate(1)) against this config's N=1 rate (--ref_rate, or the rate
         # the last N=1 run cached next to this file)

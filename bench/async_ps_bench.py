@@ -29,6 +29,10 @@ def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--num_ps", type=int, default=2)
     p.add_argument("--num_workers", type=int, default=6)
+    p.add_argument("--model", choices=("resnet", "bert"), default="resnet",
+                   help="bert: BERT pre-training (tied, vocabulary-padded MLM decoder) under the async PS")
+    p.add_argument("--bert_size", default="tiny")
+    p.add_argument("--seq", type=int, default=128)
     p.add_argument("--depth", type=int, default=152)
     p.add_argument("--batch", type=int, default=64)
     p.add_argument("--image", type=int, default=224)
@@ -52,7 +56,8 @@ def parent(a):
         # 1-GPU rehearsal of the async data plane, not a throughput measurement of config 5
         env["MDTF_DIST_BACKEND"] = "gloo"
     argv = [os.path.abspath(__file__), "--depth=%d" % a.depth, "--batch=%d" % a.batch, "--image=%d" % a.image,
-            "--steps=%d" % a.steps, "--warmup=%d" % a.warmup, "--ps_mode=async"]
+            "--steps=%d" % a.steps, "--warmup=%d" % a.warmup, "--ps_mode=async", "--model=%s" % a.model,
+            "--bert_size=%s" % a.bert_size, "--seq=%d" % a.seq]
     t0 = time.time()
     codes = launch_local_cluster(argv, a.num_ps, a.num_workers, extra_env=env, timeout_s=a.timeout_s)
     wall = time.time() - t0
@@ -72,15 +77,16 @@ def parent(a):
             with open(fn) as f:
                 ps_stats.append(json.load(f))
     print(json.dumps({
-        "metric": "images/sec ResNet-%d async parameter-server, %d ps + %d workers, one node" % (
-            a.depth, a.num_ps, a.num_workers),
-        "value": round(value, 2), "unit": "images/sec", "n_gpus": 0 if a.cpu else (1 if a.share_gpu else a.num_ps + a.num_workers),
+        "metric": "%s async parameter-server, %d ps + %d workers, one node" % (
+            ("sequences/sec BERT-%s" % a.bert_size) if a.model == "bert" else ("images/sec ResNet-%d" % a.depth),
+            a.num_ps, a.num_workers),
+        "value": round(value, 2), "unit": "sequences/sec" if a.model == "bert" else "images/sec", "n_gpus": 0 if a.cpu else (1 if a.share_gpu else a.num_ps + a.num_workers),
         "higher_is_better": True, "per_worker": [round(x, 2) for x in rates], "wall_s": round(wall, 1),
         "ps": [{k: r.get(k) for k in ("ps", "updates", "mean_staleness", "max_staleness", "apply_s", "idle_s", "wall_s",
                                       "store_wait_s", "store_calls", "applies", "batched_max", "poll", "wire")}
                for r in ps_stats],
         "dtype": "bf16" if not a.cpu else "fp32", "data": "synthetic", "config": {
-            "model": "resnet%d_v1.5" % a.depth, "per_worker_batch": a.batch, "image": a.image,
+            "model": ("bert-%s seq%d" % (a.bert_size, a.seq)) if a.model == "bert" else "resnet%d_v1.5" % a.depth, "per_worker_batch": a.batch, "image": a.image,
             "parallelism": "async-ps %dps+%dw" % (a.num_ps, a.num_workers)}}), flush=True)
     return 0
 
@@ -93,6 +99,8 @@ def task(a):
     from mdtf.models import ResNet, SoftmaxCrossEntropyLoss
     from mdtf.runtime.entry import run_from_annotations
 
+    from mdtf.models import Bert, BertPretrainingLoss, SyntheticBertLoader
+
     class BenchResNet(ResNet):
         def __init__(self):
             super(BenchResNet, self).__init__(a.depth)
@@ -101,16 +109,29 @@ def task(a):
         def __init__(self):
             super(BenchLoader, self).__init__(shape=(a.image, a.image, 3), num_classes=1000)
 
-    annotations.register_class(BenchResNet)
-    annotations.register_class(BenchLoader)
-    annotations.register_class(SoftmaxCrossEntropyLoss)
-    total = (a.warmup + a.steps) * a.num_workers
+    class BenchBert(Bert):
+        def __init__(self):
+            super(BenchBert, self).__init__(a.bert_size, seq_len=a.seq)
 
-    @annotations.current_model(model="BenchResNet")
-    @annotations.optimizer(optimizer=mdtf.train.MomentumOptimizer(0.1 * a.batch / 256, 0.9))
-    @annotations.loss(loss="SoftmaxCrossEntropyLoss")
+    class BenchBertLoader(SyntheticBertLoader):
+        def __init__(self):
+            super(BenchBertLoader, self).__init__(a.seq, seed=FLAGS.task_index)
+
+    class BenchBertLoss(BertPretrainingLoss):
+        def __init__(self):
+            super(BenchBertLoss, self).__init__()
+
+    for c in (BenchResNet, BenchLoader, SoftmaxCrossEntropyLoss, BenchBert, BenchBertLoader, BenchBertLoss):
+        annotations.register_class(c)
+    total = (a.warmup + a.steps) * a.num_workers
+    bert = a.model == "bert"
+    opt = (mdtf.train.AdamOptimizer(1e-4) if bert else mdtf.train.MomentumOptimizer(0.1 * a.batch / 256, 0.9))
+
+    @annotations.current_model(model="BenchBert" if bert else "BenchResNet")
+    @annotations.optimizer(optimizer=opt)
+    @annotations.loss(loss="BenchBertLoss" if bert else "SoftmaxCrossEntropyLoss")
     @annotations.current_mode(mode="Train")
-    @annotations.current_input(input="BenchLoader")
+    @annotations.current_input(input="BenchBertLoader" if bert else "BenchLoader")
     @annotations.gpu_num(gpu_num=1)
     @annotations.job_name(job_name=FLAGS.job_name)
     @annotations.task_index(task_index=FLAGS.task_index)

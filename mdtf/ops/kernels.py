@@ -193,6 +193,10 @@ class _Xent(torch.autograd.Function):
                                       N.ptr(dloss), N.ptr(dl), n, k, ldi, ldo, N.stream_ptr()), "xent_bwd")
         if ldo == k:
             return dl, None
+        if logits.data_ptr() % 16 or dl.data_ptr() % 16:
+            # mdtf_xent_bwd zero-fills the pad columns only on its 16-B vector path (kernels.hip:863-870); the
+            # generic kernel leaves them as torch.empty made them, and the tied decoder reads whole rows
+            dl[:, k:].zero_()
         from . import gemm
         if len(gemm._PADDED_GRADS) > 16:
             gemm._PADDED_GRADS.clear()

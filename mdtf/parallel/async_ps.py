@@ -81,8 +81,11 @@ class _PSGroupedSpace(FlatParamSpace):
 
 
 def _varspec(variables):
+    # pad_rows travels too: the PS must rebuild the same flat layout (e.g. BERT's tied decoder reserves zero rows
+    # after the word embedding and the MLM bias), or every chief send / push / pull would differ in size
     return [{"name": v.name, "shape": list(v.shape), "keep_fp32": bool(v.keep_fp32),
-             "decay": bool(v.apply_weight_decay), "ps": int(v.ps_task or 0)} for v in variables]
+             "decay": bool(v.apply_weight_decay), "ps": int(v.ps_task or 0),
+             "pad_rows": int(getattr(v, "pad_rows", 0) or 0)} for v in variables]
 
 
 K_PULL, K_PUSH, K_DONE, K_MASTER = 0, 1, 2, 3
@@ -259,6 +262,7 @@ def run_parameter_server(op, server, sync_replicas=None, total_step=None):
         v = V.Variable(s["name"], t, trainable=True, keep_fp32=s["keep_fp32"])
         v.apply_weight_decay = s["decay"]
         v.ps_task = ps
+        v.pad_rows = int(s.get("pad_rows", 0))
         variables.append(v)
     space = _PSGroupedSpace(variables, device, vstore.compute_dtype, num_ps)
     groups = [g for g in space.groups]

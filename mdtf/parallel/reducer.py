@@ -269,31 +269,59 @@ class GradReducer(object):
         # the capture stream captures and replays bitwise equal to eager (tests/test_hip_graph.py).  The collectives
         # still run on RCCL's own stream beside backward; only the small fused update kernels run in line.
         # MDTF_SHARDED_CAPTURE_OVERLAP=0: no in-backward update inside a capture (gathers after the update).
+        # Round 6: issuing the update from the capture stream made every later backward kernel wait for that bucket's
+        # reduce-scatter + update (the compute stream waited on the RS work in _update_bucket).  Inside a capture
+        # the update now runs on a side stream that the MAIN thread forks from the capture stream before backward
+        # (fork_update_stream) and after_update joins; the autograd thread only makes that stream wait for the RS
+        # and launches on it, it never forks.  MDTF_SHARDED_CAPTURE_UPD=lag keeps the capture stream but issues
+        # bucket k's update when bucket k+1 launches (the compute stream then waits for an RS that has had a whole
+        # bucket of backward to finish); =inline is the round-5 behaviour.
         capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         self._capturing = capturing
+        self._forked = False
+        self._lagged = None
         allowed = not capturing or os.environ.get("MDTF_SHARDED_CAPTURE_OVERLAP", "1") != "0"
         self.eager_update = fn if (self.mode == "sharded" and self.overlap and self.collective
                                    and self.R == self.world and allowed) else None
+
+    CAPTURE_UPD = os.environ.get("MDTF_SHARDED_CAPTURE_UPD", "fork")
+
+    def fork_update_stream(self):
+        """Main thread, before backward, inside a capture: fork the update side stream from the capture stream
+        (see set_update_fn).  A no-op outside a capture or when no in-backward update runs."""
+        if self.eager_update is None or not getattr(self, "_capturing", False) or self.CAPTURE_UPD != "fork":
+            return
+        dev = self.space.device
+        if self._upd_stream is None:
+            self._upd_stream = torch.cuda.Stream(dev)
+        self._upd_stream.wait_stream(torch.cuda.current_stream(dev))
+        self._forked = True
 
     def _update_bucket(self, b):
         g = b.group
         sh = self._shards[id(g)]
         cuda = torch.device(g.device).type == "cuda"
         us = None
-        # eager steps: a side stream; inside a capture: the capture stream (see set_update_fn)
-        # (MDTF_SHARDED_UPD_STREAM=1 forces the side stream in capture too: reproduces the EndCapture segfault)
+        # eager steps: a side stream forked here; inside a capture: the side stream the main thread forked before
+        # backward (fork_update_stream), else the capture stream (see set_update_fn).  MDTF_SHARDED_UPD_STREAM=1
+        # forks in this (autograd) thread inside a capture too: reproduces the round-4 EndCapture segfault.
         capt = getattr(self, "_capturing", False)
         env = os.environ.get("MDTF_SHARDED_UPD_STREAM", "")
-        cuda = cuda and (env == "1" if capt else env != "0")
+        forked = capt and getattr(self, "_forked", False)
+        side = cuda and (forked or env == "1" if capt else env != "0")
         self.bucket_updates = getattr(self, "bucket_updates", 0) + 1
         if capt:
             self.captured_bucket_updates = getattr(self, "captured_bucket_updates", 0) + 1
-        if cuda:
+            if not side:
+                # the compute (capture) stream itself waits for this bucket's reduce-scatter
+                self.capture_compute_waits = getattr(self, "capture_compute_waits", 0) + 1
+        if side:
             if self._upd_stream is None:
                 self._upd_stream = torch.cuda.Stream(g.device)
             us = self._upd_stream
-            us.wait_stream(torch.cuda.current_stream(g.device))
-        ctx = torch.cuda.stream(us) if cuda else _NullCtx()
+            if not forked:
+                us.wait_stream(torch.cuda.current_stream(g.device))
+        ctx = torch.cuda.stream(us) if side else _NullCtx()
         with ctx, torch.no_grad():
             b.work.wait()                       # the update stream waits for this bucket's reduce-scatter
             b.work = None
@@ -319,7 +347,12 @@ class GradReducer(object):
         return self._is_gloo
 
     def _reduce_scatter(self, out, inp, async_op=True):
-        """out (this rank's 1/world of inp) = sum over ranks of inp's shard."""
+        """out (this rank's 1/world of inp) = sum over ranks of inp's shard.
+
+        gloo emulation (GLOO_VIA_ALLREDUCE): all-reduces ``inp`` IN PLACE -- after the call the caller's gradient
+        bucket holds the global sum, not the local gradient (the native reduce-scatter leaves it untouched).  Every
+        caller passes the flat gradient bucket (or its bf16 wire copy), which nothing reads after its collective
+        until begin_step zeroes it; a caller that needs the local gradient afterwards must pass a scratch copy."""
         if not self._gloo_emulate():
             return dist.reduce_scatter_tensor(out, inp, group=self.pg, async_op=async_op)
         n = out.numel()
@@ -331,7 +364,12 @@ class GradReducer(object):
         return done
 
     def _all_gather(self, dst, src, async_op=True):
-        """dst (world x src) = every rank's src, in rank order."""
+        """dst (world x src) = every rank's src, in rank order.
+
+        gloo emulation: ``dst`` is zeroed and this rank's shard written before the async all-reduce, so until the
+        returned work is waited on ``dst`` reads as zeros outside this rank's shard (neither old nor new values).
+        Callers wait before any read: after_update / gather_full_* wait every gather, and the in-backward gathers
+        target buckets whose layers' backward has completed."""
         if not self._gloo_emulate():
             return dist.all_gather_into_tensor(dst, src, group=self.pg, async_op=async_op)
         n = src.numel()
@@ -365,7 +403,17 @@ class GradReducer(object):
             out = self._shards[id(g)]["grad"][b.shard_offset:b.shard_offset + b.shard_len]
             b.work = self._reduce_scatter(out, g.grad[b.start:b.end])
         if self.eager_update is not None:
-            self._update_bucket(b)
+            if getattr(self, "_capturing", False) and self.CAPTURE_UPD == "lag":
+                prev, self._lagged = self._lagged, b
+                if prev is not None:
+                    self._update_bucket(prev)
+            else:
+                self._update_bucket(b)
+
+    def _flush_lagged(self):
+        prev, self._lagged = getattr(self, "_lagged", None), None
+        if prev is not None:
+            self._update_bucket(prev)
 
     def _wire_buffers(self, b):
         """Persistent (graph-capture safe) bf16 wire buffers of one bucket."""
@@ -492,6 +540,7 @@ class GradReducer(object):
         for b in self.space.buckets:
             if not b.launched:
                 self._launch(b)
+        self._flush_lagged()
         for b in self.space.buckets:
             if b.work is not None:
                 b.work.wait()

@@ -323,6 +323,7 @@ class TrainOp(Fetchable):
             red.set_update_fn(lambda t: self.optimizer.update(t, lr, pre_scale, self.step_count, dyn=dyn))
         else:
             red.set_update_fn(None)
+        red.fork_update_stream()               # inside a capture: the side stream of the in-backward updates
         _conv._WT.step_begin()                 # conv filters' K-contiguous copies: one batched refresh per step
         _gemm._CATS.step_begin()               # q|k|v weight concatenations: one batched copy per step
         try:

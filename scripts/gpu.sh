@@ -10,6 +10,11 @@
 #   py      : run a python script under a time limit: gpu.sh py TAG path/to/script.py [args]
 #   bertab  : alternating A/B of bench/bert_bench.py under two env settings: gpu.sh bertab TAG "A=1" "A=0" [steps]
 #   rehearse2: 2-rank gloo rehearsal of bench.py on the one GPU (allreduce and sharded/bf16 modes; not a scaling run)
+#   final   : tests + bench (30 steps, three runs) + prof of the tree, stopping at the first failure (the sequence
+#             every round-5 "final" session ran)
+# A session is one gpurun call chaining subcommands with &&, e.g.
+#   gpurun -- 'bash scripts/gpu.sh tests r6a && bash scripts/gpu.sh envab r6a "X=1" "X=0"'
+# (round 5's 58 one-off scripts/r5*_session.sh were exactly such chains; they are in the git history.)
 # (Round 4 replaced the per-experiment scripts/gpu_*.sh launchers that older profiles/ notes name with these modes;
 #  their exact commands are in the git history.)
 # Every GPU step runs under its own time limit and the script stops at the first failure.
@@ -109,6 +114,10 @@ case "$WHAT" in
     S=$1; shift
     timeout -k 10 600 python -u "$S" "$@" > "$OUT/py_$TAG.log" 2>&1 || fail "py $S" "$OUT/py_$TAG.log"
     tail -40 "$OUT/py_$TAG.log" ;;
+  final)
+    bash "$ROOT/scripts/gpu.sh" tests "$TAG" && \
+    bash "$ROOT/scripts/gpu.sh" bench "$TAG" --steps 30 --warmup 5 && \
+    bash "$ROOT/scripts/gpu.sh" prof "$TAG" > /dev/null && echo "prof ok" ;;
   *)
     echo "unknown: $WHAT"; exit 2 ;;
 esac

@@ -15,11 +15,16 @@ def _teardown(server):
     import torch.distributed as dist
     if getattr(server, "heartbeat", None) is not None:
         server.heartbeat.stop(done=True)
+    code = 0
     if dist.is_initialized():
-        dist.barrier()
+        try:
+            dist.barrier()
+        except Exception as e:  # noqa: BLE001 - a peer that crashed or hung in shutdown must fail the test
+            sys.stderr.write("teardown barrier failed: %r\n" % (e,))
+            code = 1
     sys.stdout.flush()
     sys.stderr.flush()
-    os._exit(0)
+    os._exit(code)
 
 
 def _linear_setup(rank, world, batch, seed=0):

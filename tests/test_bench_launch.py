@@ -41,6 +41,7 @@ def test_bench_torchrun_two_ranks(mode):
     assert rec["config"]["grad_sync"] == mode
     assert rec["value"] > 0 and rec["ms_per_step"] > 0
     assert rec["loss_last"] == rec["loss_last"]           # finite
+    assert rec["comm"] == {"backend": "gloo", "ranks_in_collective": 2}
 
 
 def _one_json(out):
@@ -139,3 +140,17 @@ def test_async_ps_single_worker_staleness_counts_the_overlap():
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     ps = rec["ps"][0]
     assert ps["max_staleness"] == 1 and ps["mean_staleness"] >= 0.8, ps
+
+
+@pytest.mark.slow
+def test_async_ps_bert_padded_decoder_cpu():
+    """BERT's tied decoder reserves zero pad rows after the word embedding and the MLM bias in
+    the flat buffers; the PS must rebuild the same flat layout from the variable spec, or the chief's initial
+    send and every push / pull mismatch in size (a gloo size error, an RCCL hang).  2 ps + 2 workers, BERT-tiny."""
+    cmd = [sys.executable, "bench/async_ps_bench.py", "--cpu", "--model", "bert", "--num_ps", "2", "--num_workers", "2",
+           "--seq", "32", "--batch", "2", "--steps", "2", "--warmup", "1", "--timeout_s", "300"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=360)
+    assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-2000:])
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["unit"] == "sequences/sec" and len(rec["per_worker"]) == 2 and all(r > 0 for r in rec["per_worker"])
+    assert all(ps["updates"] >= 6 for ps in rec["ps"])

@@ -44,6 +44,26 @@ def test_sync_dp_equals_single_process(mode, world, tmp_path):
             assert torch.allclose(torch.tensor(r["weights"][name]), torch.tensor(vals), atol=1e-5), (mode, name)
 
 
+def test_sharded_gloo_emulation_matches_native_collectives(tmp_path, monkeypatch):
+    """on gloo the sharded mode runs its reduce-scatter / all-gather as all-reduces
+    (MDTF_GLOO_RS_AR=1, mutating the buckets it is given); the native gloo collectives (=0) must give the same
+    weights, and both the single-process large-batch result."""
+    sys.path.insert(0, os.path.dirname(__file__))
+    import dist_helpers
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MDTF_GLOO_RS_AR", flag)       # read at import by the spawned ranks
+        d = tmp_path / flag
+        d.mkdir()
+        out[flag] = _run(2, "sharded", 4, d)
+    ref = dist_helpers.single_process_reference(2, 4)
+    for a, b in zip(out["0"], out["1"]):
+        for name in ref:
+            ta, tb = torch.tensor(a["weights"][name]), torch.tensor(b["weights"][name])
+            assert torch.allclose(ta, tb, atol=1e-6), name
+            assert torch.allclose(tb, torch.tensor(ref[name]), atol=1e-5), name
+
+
 @pytest.mark.parametrize("mode", ["allreduce", "sharded"])
 def test_bf16_wire_dtype_matches_fp32_within_tolerance(mode, tmp_path):
     """comm_dtype='bf16': gradients cross the wire in bf16 (half the bytes), masters stay fp32.

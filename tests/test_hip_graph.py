@@ -185,11 +185,20 @@ def test_hip_graph_bert_dropout_advances_per_replay():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["allreduce", "sharded"])
+@pytest.mark.parametrize("mode", ["allreduce", "sharded", "sharded-lag"])
 def test_hip_graph_captures_rccl_collectives(mode, monkeypatch):
     """The bucketed RCCL all-reduce (or PS-shard reduce-scatter + all-gather) fired from the gradient hooks
-    is captured into the step graph: a 1-rank nccl group with collectives forced on, eager == replay."""
+    is captured into the step graph: a 1-rank nccl group with collectives forced on, eager == replay.
+
+    Sharded: inside the capture each bucket's update runs on the side stream the main thread
+    forked before backward, so no backward kernel captured after bucket k's hook depends on bucket k's
+    reduce-scatter (the capture stream never waits on an RS work: ``capture_compute_waits == 0``).  ``lag`` issues
+    bucket k's update from the capture stream when bucket k+1 launches."""
     _gpu()
+    from mdtf.parallel import reducer as R
+    lag = mode == "sharded-lag"
+    mode = "sharded" if lag else mode
+    monkeypatch.setattr(R.GradReducer, "CAPTURE_UPD", "lag" if lag else "fork")
     import socket
     import torch.distributed as dist
     from mdtf.ops import _native
@@ -218,6 +227,8 @@ def test_hip_graph_captures_rccl_collectives(mode, monkeypatch):
             # every bucket was updated + all-gathered during backward INSIDE the capture (not after the update)
             assert getattr(op.reducer, "captured_bucket_updates", 0) == len(op.space.buckets), \
                 (getattr(op.reducer, "captured_bucket_updates", 0), len(op.space.buckets))
+            waits = getattr(op.reducer, "capture_compute_waits", 0)
+            assert (waits == len(op.space.buckets)) if lag else (waits == 0), waits
         from mdtf.train import graph as G
         assert G.LAST_DRAIN[0] == "recorder", G.LAST_DRAIN
         assert l_e == l_g, (l_e, l_g)

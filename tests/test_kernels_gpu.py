@@ -173,6 +173,33 @@ def test_softmax_xent_strided_rows():
     gemm._PADDED_GRADS.clear()
 
 
+def test_softmax_xent_unaligned_strided_rows_zero_pad():
+    """a strided logits view that is NOT 16-B aligned runs the generic backward kernel, which does not
+    touch the pad columns; the gradient buffer registered as zero-padded must still be zero there (the tied decoder
+    reads whole rows, 0 * NaN would poison dh)."""
+    import types
+    from mdtf.ops import gemm, kernels
+    torch.manual_seed(4)
+    N, K, LD = 9, 3000, 3008
+    full = (torch.randn(N, LD + 1) * 3).bfloat16().to(DEV)
+    lg = full.as_strided((N, K), (LD, 1), storage_offset=1)        # 2-B offset: the vector path is refused
+    assert lg.data_ptr() % 16 and lg.stride(0) == LD
+    labels = torch.randint(0, K, (N,), device=DEV)
+    loss = kernels.softmax_xent(lg, labels)
+    lse = torch.logsumexp(lg.float(), 1)
+    ctx = types.SimpleNamespace(saved_tensors=(lg, labels, lse))
+    for _ in range(3):                   # the caching allocator hands back dirty blocks: poison one first
+        torch.full((N, LD), float("nan"), dtype=torch.bfloat16, device=DEV)
+    g, _ = kernels._Xent.backward(ctx, torch.ones(N, device=DEV))
+    whole = g.as_strided((N, LD), (LD, 1))
+    assert not whole[:, K:].isnan().any() and not whole[:, K:].any()
+    ref = torch.softmax(lg.float(), 1)
+    ref[torch.arange(N, device=DEV), labels] -= 1
+    assert _rel(g, ref) < 2e-2
+    assert torch.isfinite(loss).all()
+    gemm._PADDED_GRADS.clear()
+
+
 @pytest.mark.parametrize("act", ["relu", "gelu", None])
 @pytest.mark.parametrize("C", [64, 10])
 def test_bias_act(act, C):
