@@ -29,7 +29,24 @@ def main():
     p.add_argument("--tiles", default="448:128:2:3,448:128:1:3", help="bm:bn:stages:ver,...")
     p.add_argument("--table", action="store_true", help="merge winners into mdtf/ops/conv_table.json")
     p.add_argument("--margin", type=float, default=0.98)
+    p.add_argument("--cold", action="store_true",
+                   help="evict L2 / Infinity Cache before every launch (a 384 MiB fill in the graph, its own time "
+                        "subtracted): the step reads most conv operands cold, the back-to-back default reads them "
+                        "from the 256 MiB Infinity Cache")
     args = p.parse_args()
+    timer = gtime
+    if args.cold:
+        scr = torch.empty(384 << 20, dtype=torch.uint8, device="cuda")
+
+        def flush():
+            scr.fill_(1)
+        base = gtime(flush, args.reps)
+
+        def timer(fn, reps):
+            def both():
+                flush()
+                fn()
+            return gtime(both, reps) - base
     cands = [tuple(int(v) for v in t.split(":")) for t in args.tiles.split(",")]
     dev = torch.device("cuda")
     shapes, all_convs = resnet_convs(50, args.batch)
@@ -63,7 +80,7 @@ def main():
             else:
                 ref = current_dgrad(ch, dy, wt, x.shape, s, pads4)
                 cur = (lambda: current_dgrad(ch, dy, wt, x.shape, s, pads4))
-            t_cur = gtime(cur, args.reps)
+            t_cur = timer(cur, args.reps)
             rec = {"pass": pass_, "key": key, "count": counts[(n, h, w, c, kh, kw, co, s, pads)],
                    "current": list(map(str, ch)), "cur_ms": round(t_cur, 4), "cur_tfs": round(flops / t_cur / 1e9),
                    "cands": {}}
@@ -84,7 +101,7 @@ def main():
                         err = _rel(y, ref)
                         fn = (lambda bm=bm, bn=bn, stg=stg, ver=ver: C.mdtf_dgrad(
                             dy, wt, x.shape, (s, s), pads4, (1, 1), bm, bn, ver, stg))
-                    t = gtime(fn, args.reps)
+                    t = timer(fn, args.reps)
                 except RuntimeError as e:
                     rec["cands"][tag] = {"error": str(e)[:100]}
                     torch.cuda.synchronize()

@@ -94,7 +94,25 @@ struct ConvArgs {
   const bf16_t* bias;    // bf16 [Ncol], added to the fp32 accumulators (null: none)
   bf16_t* pre_out;       // act != 0: the bf16 pre-activation is also stored here (null: not kept)
   int act;               // 0 none, 1 relu, 2 gelu (tanh form)
+  // v2 fwd/dgrad: the row index -> pixel decomposition divides by the row grid's width and height (RW, RH);
+  // n / d = (n * mg) >> sh for n < 2^31 (Granlund-Montgomery, set by launch_fd_v2): the 64-bit divisions of
+  // the per-row setup were ~1,000 VALU instructions per wave before the first DMA of every tile
+  unsigned mg_rw, mg_rh;
+  int sh_rw, sh_rh;
 };
+
+// m, sh with floor(n / d) = (n * m) >> sh for every 0 <= n < 2^31: l = ceil(log2 d), m = ceil(2^(31+l) / d)
+// (m * d - 2^(31+l) < d <= 2^l; m < 2^32 for d >= 1)
+inline void magic31(unsigned d, unsigned* m, int* sh) {
+  int l = 0;
+  while ((1ull << l) < d) ++l;
+  *m = static_cast<unsigned>(((1ull << (31 + l)) + d - 1) / d);
+  *sh = 31 + l;
+}
+
+__device__ __forceinline__ unsigned fdiv31(unsigned n, unsigned m, int sh) {
+  return static_cast<unsigned>((static_cast<unsigned long long>(n) * m) >> sh);
+}
 
 // zero the bf16 elements of an 8-element vector whose mask bit (element k: bit k) is clear
 __device__ __forceinline__ uint4 mask_bf8(const uint4& v, uint32_t m8) {
@@ -582,8 +600,16 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int PER_STAGE = RA + RB;               // LDS-DMA wave-instructions per stage
   constexpr unsigned OOB = 0x80000000u;            // buffer offset past num_records -> zero fill
+  // STAGES >= 10: split ring, SA = STAGES / 10 A stages and SB = STAGES % 10 B stages (SA > SB >= 2).  The A
+  // operand (the gathered activation / output gradient) streams from HBM or the Infinity Cache and is read by one
+  // tile only when the N grid is a single column; the B operand (filter) is shared by every tile and L2-resident.
+  // One 64-KiB stage in flight left the 8-wave tiles latency-bound on A (32 KiB in flight per CU vs ~25-33 GB/s
+  // per CU at ~1-2 us loaded latency); the split ring keeps SA - 1 A stages in flight in the same 160 KiB.
+  constexpr bool SPLIT = STAGES >= 10;
+  constexpr int SA = SPLIT ? STAGES / 10 : STAGES, SB = SPLIT ? STAGES % 10 : STAGES;
   static_assert(RA >= 1 && RB >= 1, "tile too small");
-  static_assert(STAGES >= 1 && (STAGES < 2 || (STAGES - 2) * PER_STAGE < 64), "pipeline depth");  // 1: K == 64 only
+  static_assert(STAGES >= 1 && (STAGES < 2 || SPLIT || (STAGES - 2) * PER_STAGE < 64), "pipeline depth");  // 1: K == 64 only
+  static_assert(!SPLIT || (SA > SB && SB >= 2 && (SA - 1) * PER_STAGE < 64), "split ring");
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -624,15 +650,17 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
     const int row = 8 * (wave + NW * i) + lrow;
     const long long m = m0 + row;
     const bool ok = m < a.M;
-    const long long mm = ok ? m : 0;
-    const int ow = static_cast<int>(mm % RW);
-    const long long t = mm / RW;
-    const int oh = static_cast<int>(t % RH);
-    const int n = static_cast<int>(t / RH);
+    // 32-bit index math: every tensor is < 2 GiB (host-checked), so rows and element offsets fit 31 bits
+    const unsigned mm = ok ? static_cast<unsigned>(m) : 0u;
+    const unsigned t = fdiv31(mm, a.mg_rw, a.sh_rw);
+    const int ow = static_cast<int>(mm - t * static_cast<unsigned>(RW));
+    const unsigned nq = fdiv31(t, a.mg_rh, a.sh_rh);
+    const int oh = static_cast<int>(t - nq * static_cast<unsigned>(RH));
+    const int n = static_cast<int>(nq);
     const int y0 = AM == 0 ? oh * a.SH - a.PH : AM == 1 ? oh + a.PH : a.cls_q0h + oh;
     const int x0 = AM == 0 ? ow * a.SW - a.PW : AM == 1 ? ow + a.PW : a.cls_q0w + ow;
     const int ch = 8 * ((lane & 7) ^ ((row >> 1) & 7));
-    a_off[i] = (unsigned)((((long long)n * GH + y0) * GW + x0) * GC + ch);
+    a_off[i] = static_cast<unsigned>(((n * GH + y0) * GW + x0) * GC + ch);
     unsigned mask = 0;
     if (ok) {
       for (int tt = 0; tt < ntaps; ++tt) {
@@ -716,11 +744,115 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   }
 
   const int KT = a.K / 64;
+  const int fr = lane & 15, fq = lane >> 4;
+  if constexpr (SPLIT) {
+    // separate K walks for the A ring (SA - 1 steps ahead) and the B ring (SB - 1 steps ahead)
+    struct Walk { int t, kh, kw, c0, k0; };
+    Walk wa{0, 0, 0, 0, 0}, wb{0, 0, 0, 0, 0};
+    auto advance = [&](Walk& w) {
+      w.k0 += 64;
+      w.c0 += 64;
+      const int wrap = w.c0 == GC ? 1 : 0;
+      w.c0 = wrap ? 0 : w.c0;
+      w.t += wrap;
+      w.kw += wrap;
+      const int wrap2 = w.kw == TKW ? 1 : 0;
+      w.kw = wrap2 ? 0 : w.kw;
+      w.kh += wrap2;
+    };
+    char* const ringB = smem_raw + SA * BM * ROWB;
+    auto stage_a = [&](int buf) {
+      const int tap_e = (AM == 0 ? (wa.kh * DHe * GW + wa.kw * DWe) : -(wa.kh * DHe * GW + wa.kw * DWe)) * GC + wa.c0;
+      char* lds = smem_raw + buf * (BM * ROWB);
+#pragma unroll
+      for (int i = 0; i < RA; ++i) {
+        const bool ok = (a_mask[i] >> wa.t) & 1u;
+        const unsigned voff = ok ? (a_off[i] + (unsigned)tap_e) * 2u : OOB;
+        dma16(a.src, bytes_a, lds + (wave + NW * i) * 1024, voff, 0);
+      }
+      advance(wa);
+    };
+    auto stage_b = [&](int buf) {
+      char* ldsb = ringB + buf * (BN * ROWB);
+      const int wtap = MODE == 2 ? (a.cls_kh0 + a.SH * wb.kh) * a.KW + a.cls_kw0 + a.SW * wb.kw : wb.t;
+      const int sb = MODE == 3 ? wb.k0 * a.ld_b * 2 : MODE == 0 ? wb.k0 * 2 : (wtap * a.Cin * a.Cout + wb.c0) * 2;
+#pragma unroll
+      for (int i = 0; i < RB; ++i)
+        dma16(wbase, bytes_b, ldsb + (wave + NW * i) * 1024, b_off[i], sb);
+      advance(wb);
+    };
+    // issue order: prologue group s = [B(s) if s <= SB-2, A(s)]; loop group j = [B(j+SB-1), A(j+SA-1)]
+    // (each only while < KT).  vmcnt retires in issue order, so "A(kt) and B(kt) landed" = at most `younger`
+    // operations issued after the later of the two are still outstanding.
+    auto nb_of = [&](int j) { return (j + SB - 1 < KT ? RB : 0); };
+    auto na_of = [&](int j) { return (j + SA - 1 < KT ? RA : 0); };
+#pragma unroll
+    for (int s = 0; s < SA - 1; ++s) {
+      if (s <= SB - 2 && s < KT) stage_b(s);
+      if (s < KT) stage_a(s);
+    }
+    int ca = 0, cb = 0;
+    for (int kt = 0; kt < KT; ++kt) {
+      int younger = 0;
+      if (kt <= SB - 2) {                    // A(kt) last, in prologue group kt
+        for (int s = kt + 1; s <= SA - 2; ++s) younger += (s <= SB - 2 && s < KT ? RB : 0) + (s < KT ? RA : 0);
+        for (int j = 0; j < kt; ++j) younger += nb_of(j) + na_of(j);
+      } else {                               // B(kt) last, first of loop group kt - SB + 1
+        const int g0 = kt - SB + 1;
+        younger = na_of(g0);
+        for (int j = g0 + 1; j < kt; ++j) younger += nb_of(j) + na_of(j);
+      }
+      wait_vmcnt_le<(SA - 1) * PER_STAGE>(younger);
+      __builtin_amdgcn_s_barrier();          // every wave's DMA of step kt is in; A(kt-1), B(kt-1) are free
+      if (kt + SB - 1 < KT) stage_b(cb == 0 ? SB - 1 : cb - 1);      // buffer (kt + SB - 1) % SB
+      if (kt + SA - 1 < KT) stage_a(ca == 0 ? SA - 1 : ca - 1);      // buffer (kt + SA - 1) % SA
+      const char* As = smem_raw + ca * (BM * ROWB);
+      const char* Bs = ringB + cb * (BN * ROWB);
+      ca = ca + 1 == SA ? 0 : ca + 1;
+      cb = cb + 1 == SB ? 0 : cb + 1;
+      bf16x8_t fa[2][TM], fb[2][TN];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * (TM * 16) + i * 16 + fr;
+          const int pc = (h * 4 + fq) ^ ((row >> 1) & 7);
+          fa[h][i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(As + row * ROWB + pc * 16));
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if (MODE == 3) {
+            const int col = wn * (TN * 16) + j * 16;
+            fb[h][j] = frag_tr(Bs + (col >> 6) * 8192, col & 63, 32 * h, lane);
+            continue;
+          }
+          const int row = wn * (TN * 16) + j * 16 + fr;
+          const int pc = (h * 4 + fq) ^ ((row >> 1) & 7);
+          fb[h][j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(Bs + row * ROWB + pc * 16));
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fb[h][j], fa[h][i], acc[i][j]);
+      {
+        constexpr int R = TM + TN, MF = TM * TN, PER = MF / R > 0 ? MF / R : 1;
+        __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * MF, 0);
+      }
+    }
+  } else {
   // prologue: stages 0 .. STAGES-2 in flight
 #pragma unroll
   for (int s = 0; s < (STAGES > 1 ? STAGES - 1 : 1); ++s)
     if (s < KT) stage(s);
-  const int fr = lane & 15, fq = lane >> 4;
   int cur = 0;
   for (int kt = 0; kt < KT; ++kt) {
     // stage kt must have landed: leave the (STAGES-2) younger stages in flight
@@ -775,6 +907,7 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 2 * MF, 0); // the rest
     }
+  }
   }
 
   // ---- epilogue: the C tile goes through LDS ([px][ch], rows padded by 16 B) so the
@@ -835,11 +968,12 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
     if (m < a.M && n < a.Ncol) {
       long long pix = m;
       if (MODE == 2) {          // class pixel (n, i, j) -> DX pixel (n, h0 + SH i, w0 + SW j)
-        const int j = static_cast<int>(m % a.cls_Wc);
-        const long long t = m / a.cls_Wc;
-        const int i = static_cast<int>(t % a.cls_Hc);
-        const long long nb = t / a.cls_Hc;
-        pix = (nb * a.H + a.cls_h0 + a.SH * i) * a.W + a.cls_w0 + a.SW * j;
+        const unsigned mu = static_cast<unsigned>(m);
+        const unsigned t = fdiv31(mu, a.mg_rw, a.sh_rw);          // RW = cls_Wc, RH = cls_Hc in MODE 2
+        const int j = static_cast<int>(mu - t * static_cast<unsigned>(a.cls_Wc));
+        const unsigned nb = fdiv31(t, a.mg_rh, a.sh_rh);
+        const int i = static_cast<int>(t - nb * static_cast<unsigned>(a.cls_Hc));
+        pix = (static_cast<long long>(nb) * a.H + a.cls_h0 + a.SH * i) * a.W + a.cls_w0 + a.SW * j;
       }
       off[it] = pix * a.Ncol + n;
       if (a.accumulate) {
@@ -1010,11 +1144,22 @@ int launch_fd_v2(ConvArgs& a, hipStream_t st) {
   a.ntiles = static_cast<int>(ceil_div(a.Ncol, BN));
   const long long nblk = (long long)a.mtiles * a.ntiles;
   if (nblk > 0x7fffffff) return MDTF_EUNSUPPORTED;
-  const size_t stage_bytes = STAGES * (size_t)(BM + BN) * 128, ctile = (size_t)BM * (BN * 2 + 16);
+  const size_t stage_bytes = STAGES >= 10 ? ((size_t)(STAGES / 10) * BM + (size_t)(STAGES % 10) * BN) * 128
+                                          : STAGES * (size_t)(BM + BN) * 128;
+  const size_t ctile = (size_t)BM * (BN * 2 + 16);
   size_t lds = stage_bytes > ctile ? stage_bytes : ctile;
   if (lds < (size_t)(NT + 8) * 16 * sizeof(float)) lds = (size_t)(NT + 8) * 16 * sizeof(float);   // BN-stat reduction
   if (STAGES == 1 && a.K > 64) return MDTF_EINVAL;      // single buffer: one K step only
   if (lds > 160 * 1024) return MDTF_EUNSUPPORTED;
+  if (a.M >= (1LL << 31)) return MDTF_EUNSUPPORTED;
+  {
+    constexpr int AM = MODE == 3 ? 0 : MODE == 4 ? 1 : MODE;       // as in the kernel
+    const int RH = AM == 0 ? a.OH : AM == 1 ? a.H : a.cls_Hc;
+    const int RW = AM == 0 ? a.OW : AM == 1 ? a.W : a.cls_Wc;
+    if (RH < 1 || RW < 1) return MDTF_EINVAL;
+    magic31(static_cast<unsigned>(RW), &a.mg_rw, &a.sh_rw);
+    magic31(static_cast<unsigned>(RH), &a.mg_rh, &a.sh_rh);
+  }
   hipLaunchKernelGGL((conv_fd_v2<BM, BN, MODE, STATS, STAGES, NW>), dim3((unsigned)nblk), dim3(NT), lds, st, a);
   MDTF_LAUNCH_CHECK();
   return 0;
@@ -1039,6 +1184,8 @@ int dispatch_fd_v2w8(ConvArgs& a, int bm, int bn, int stages, hipStream_t st) {
   if (bm == BM_ && bn == BN_ && stages == S_) return launch_fd_v2<BM_, BN_, MODE, STATS, S_, 8>(a, st);
   FD8(256, 256, 1) FD8(256, 256, 2) FD8(256, 128, 1) FD8(256, 128, 2) FD8(256, 128, 3) FD8(256, 64, 2)
   FD8(256, 64, 3) FD8(256, 64, 4) FD8(128, 256, 2) FD8(128, 256, 3)
+  // split rings (stages = 10 SA + SB): more A stages in flight in the same LDS
+  FD8(256, 256, 32) FD8(256, 128, 32) FD8(256, 128, 42) FD8(128, 256, 32) FD8(128, 256, 42)
   // 448 = 7 x 64 rows: at batch 256 every row count is 49 * 4^k * 256, so 256-row tiles leave 196 * 4^k * (N / BN)
   // tiles = 0.77 of a 256-CU wave; 448-row tiles give 112 * 4^k * (N / 128) = 0.875 of one (4 x 2 waves of 112 x 64)
   // (not the dense act-backward mode: its 14 pre-activation vectors per thread spill)
@@ -1052,6 +1199,15 @@ int dispatch_fd_v2w8(ConvArgs& a, int bm, int bn, int stages, hipStream_t st) {
 template <int MODE, bool STATS>
 int dispatch_fd_v2(ConvArgs& a, int bm, int bn, int stages, hipStream_t st) {
   if (bm >= 10000) return dispatch_fd_v2w8<MODE, STATS>(a, bm % 10000, bn, stages, st);
+  if (stages == 32) {                      // 4-wave split rings
+    if (bm == 128 && bn == 128) return launch_fd_v2<128, 128, MODE, STATS, 32>(a, st);
+    if (bm == 64 && bn == 128) return launch_fd_v2<64, 128, MODE, STATS, 32>(a, st);
+    return MDTF_EUNSUPPORTED;
+  }
+  if (stages == 42) {
+    if (bm == 64 && bn == 128) return launch_fd_v2<64, 128, MODE, STATS, 42>(a, st);
+    return MDTF_EUNSUPPORTED;
+  }
   if (stages == 1) return dispatch_fd_v2s<MODE, STATS, 1>(a, bm, bn, st);
   if (stages == 2) return dispatch_fd_v2s<MODE, STATS, 2>(a, bm, bn, st);
   if (stages == 3) return dispatch_fd_v2s<MODE, STATS, 3>(a, bm, bn, st);
@@ -1607,6 +1763,19 @@ bool zero_class_gemm() {
   return g;
 }
 
+// v2 fwd / dgrad tile code -> (10000 if 8 waves) + rows, and the stage code (2 if unset).  Codes >= 100000 carry a
+// two-digit stage code (split rings): 100000 (1 + w8) + 1000 stages + rows.
+void decode_tile(int* bm, int* stages) {
+  const int c = *bm;
+  if (c >= 100000) {
+    *stages = (c % 100000) / 1000;
+    *bm = (c / 100000 - 1) * 10000 + c % 1000;
+    return;
+  }
+  *stages = (c % 10000) / 1000 ? (c % 10000) / 1000 : 2;
+  *bm = (c / 10000) * 10000 + c % 1000;
+}
+
 ConvArgs make_args(int N, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int SH, int SW, int PH,
                    int PW, int DH, int DW) {
   ConvArgs a{};
@@ -1701,9 +1870,9 @@ MDTF_EXPORT int mdtf_conv_fwd_v2(const void* x, const void* wt, void* y, float* 
   a.M = (long long)N * OH * OW;
   a.Ncol = Cout;
   a.K = KH * KW * Cin;
-  // bm = 10000 (8 waves) + stages * 1000 + tile rows
-  const int w8 = bm / 10000, stages = (bm % 10000) / 1000 ? (bm % 10000) / 1000 : 2;
-  bm = w8 * 10000 + bm % 1000;
+  // bm = 10000 (8 waves) + stages * 1000 + tile rows, or (two-digit stages) 100000 (8 waves) + stages * 1000 + rows
+  int stages;
+  decode_tile(&bm, &stages);
   int rc = stat_sum ? dispatch_fd_v2<0, true>(a, bm, bn, stages, st) : dispatch_fd_v2<0, false>(a, bm, bn, stages, st);
   if (mtiles_out) *mtiles_out = a.mtiles;
   return rc;
@@ -1734,8 +1903,8 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
   a.bsq = bsq;
   a.bslots = bslots > 0 ? bslots : 1;
   a.Ncol = Cin;
-  const int w8 = bm / 10000, stages = (bm % 10000) / 1000 ? (bm % 10000) / 1000 : 2;
-  bm = w8 * 10000 + bm % 1000;
+  int stages;
+  decode_tile(&bm, &stages);
   if (SH == 1 && SW == 1) {
     a.M = (long long)N * H * W;
     a.K = KH * KW * Cout;

@@ -110,4 +110,17 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// s_waitcnt vmcnt(min(n, N)) for a wave-uniform runtime n (a ladder of scalar compares; n <= N expected)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+  if constexpr (N <= 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (n >= N)
+      wait_vmcnt<N>();
+    else
+      wait_vmcnt_le<N - 1>(n);
+  }
+}
+
 }  // namespace mdtf

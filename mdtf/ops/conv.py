@@ -311,7 +311,10 @@ _WT = _FilterTransposes()
 
 def _v2_code(bm, stages, ver):
     """C-ABI tile code of the v2 kernels: [10000 if 8 waves] + 1000 * stages + tile rows.
-    ``ver`` 2 = 4-wave tiles, 3 = 8-wave tiles (one 256-row or 256-column block per CU)."""
+    ``ver`` 2 = 4-wave tiles, 3 = 8-wave tiles (one 256-row or 256-column block per CU).  Two-digit stage codes
+    (split A/B rings: 10 * A stages + B stages) use 100000 * (1 + [8 waves]) + 1000 * stages + rows."""
+    if stages >= 10:
+        return bm + 1000 * stages + 100000 * (2 if ver == 3 else 1)
     return bm + 1000 * stages + (10000 if ver == 3 else 0)
 
 

@@ -1259,6 +1259,51 @@ def test_conv_v2_448_row_tile(stages, k, s, pad, c, co):
     assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("bm,bn,ver,stages", [(256, 256, 3, 32), (256, 128, 3, 32), (256, 128, 3, 42),
+                                              (128, 256, 3, 32), (128, 256, 3, 42), (128, 128, 2, 32),
+                                              (64, 128, 2, 32), (64, 128, 2, 42)])
+@pytest.mark.parametrize("k,s,pad,c,co", [(1, 1, 0, 64, 128), (1, 1, 0, 128, 256), (1, 1, 0, 192, 128),
+                                          (1, 1, 0, 256, 192), (3, 1, 1, 64, 128), (1, 1, 0, 448, 128),
+                                          (3, 2, 1, 128, 128), (1, 2, 0, 64, 256)])
+def test_conv_v2_split_ring(bm, bn, ver, stages, k, s, pad, c, co):
+    """Split A/B LDS rings (stage code 10 SA + SB: SA A stages, SB filter stages): every K-step count from 1 to 9
+    (the counted vmcnt waits of the prologue / steady state / tail), forward with BN statistics, stride-1 and
+    strided data gradients with the accumulate + BN-backward-statistics epilogue, vs fp32."""
+    from mdtf.ops import conv as C
+    torch.manual_seed(k * 7 + c + co + s)
+    n, h, w = 3, 13, 11
+    x = torch.randn(n, h, w, c, device=DEV).bfloat16()
+    wt = (torch.randn(k, k, c, co, device=DEV) / (k * k * c) ** 0.5).bfloat16()
+    oh, ow = (h + 2 * pad - k) // s + 1, (w + 2 * pad - k) // s + 1
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wt.float().permute(3, 2, 0, 1), stride=s,
+                                     padding=pad).permute(0, 2, 3, 1)
+    st = torch.zeros(2, 8, co, device=DEV)
+    y = C.mdtf_fwd(x, wt, (oh, ow), (s, s), (pad,) * 4, (1, 1), bm, bn, (st[0], st[1]), ver, stages)
+    assert _rel(y, ref) < 1e-2
+    assert _rel(st[0].sum(0), ref.sum((0, 1, 2))) < 1e-3
+    assert _rel(st[1].sum(0), (ref.bfloat16().float() ** 2).sum((0, 1, 2))) < 1e-2
+    dy = torch.randn(n, oh, ow, co, device=DEV).bfloat16()
+    xr = torch.zeros(n, c, h, w, device=DEV, requires_grad=True)
+    torch.nn.functional.conv2d(xr, wt.float().permute(3, 2, 0, 1), stride=s, padding=pad).backward(
+        dy.float().permute(0, 3, 1, 2))
+    gref = xr.grad.permute(0, 2, 3, 1)
+    dx = C.mdtf_dgrad(dy, wt, (n, h, w, c), (s, s), (pad,) * 4, (1, 1), bm, bn, ver, stages)
+    assert _rel(dx, gref) < 1e-2
+    # accumulate onto a base + the BN-backward statistics of the completed gradient
+    base = torch.randn(n, h, w, c, device=DEV).bfloat16()
+    out = base.clone()
+    bx = torch.randn(n, h, w, c, device=DEV).bfloat16()
+    ps = torch.zeros(2, 4, c, device=DEV)
+    C.mdtf_dgrad(dy, wt, (n, h, w, c), (s, s), (pad,) * 4, (1, 1), bm, bn, ver, stages, out=out, accumulate=True,
+                 bn_stats=(bx, None, ps[0], ps[1], 4))
+    full = gref + base.float()
+    assert _rel(out, full) < 1e-2
+    g = out.float()
+    assert _rel(ps[0].sum(0), g.sum((0, 1, 2))) < 1e-2
+    assert _rel(ps[1].sum(0), (g * bx.float()).sum((0, 1, 2))) < 1e-2
+
+
 def _bits(b):
     """bool [..., C] -> the kernels' 1-bit-per-element mask bytes (element 8i + k = bit k of byte i)."""
     w = (1 << torch.arange(8, device=b.device)).to(torch.int32)
