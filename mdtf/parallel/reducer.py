@@ -269,22 +269,26 @@ class GradReducer(object):
         # the capture stream captures and replays bitwise equal to eager (tests/test_hip_graph.py).  The collectives
         # still run on RCCL's own stream beside backward; only the small fused update kernels run in line.
         # MDTF_SHARDED_CAPTURE_OVERLAP=0: no in-backward update inside a capture (gathers after the update).
-        # Round 6: issuing the update from the capture stream made every later backward kernel wait for that bucket's
-        # reduce-scatter + update (the compute stream waited on the RS work in _update_bucket).  Inside a capture
-        # the update now runs on a side stream that the MAIN thread forks from the capture stream before backward
-        # (fork_update_stream) and after_update joins; the autograd thread only makes that stream wait for the RS
-        # and launches on it, it never forks.  MDTF_SHARDED_CAPTURE_UPD=lag keeps the capture stream but issues
-        # bucket k's update when bucket k+1 launches (the compute stream then waits for an RS that has had a whole
-        # bucket of backward to finish); =inline is the round-5 behaviour.
+        # Round 6: issuing the update from the capture stream right after the bucket's reduce-scatter made every
+        # later backward kernel wait for that RS + update (the compute stream waited on the RS work in
+        # _update_bucket, inside the bucket's own hook).  Inside a capture the update of bucket k is now issued when
+        # bucket k+1 launches (MDTF_SHARDED_CAPTURE_UPD=lag, the default; the last one in end_backward): in the graph
+        # the update node depends on RS_k and on the backward kernels issued before hook k+1, so RS_k runs beside a
+        # whole bucket of backward and the compute stream only waits for an RS that has had that long to finish.
+        # =fork runs the updates and all-gathers on a side stream the MAIN thread forks from the capture stream
+        # before backward (fork_update_stream): still a hipStreamEndCapture segfault on ROCm 7 (r6,
+        # tests/test_hip_graph.py sharded-fork, not run by default) -- the fork's thread was not the cause.
+        # =inline is the round-5 behaviour.
         capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         self._capturing = capturing
         self._forked = False
         self._lagged = None
+        self.launch_count = 0
         allowed = not capturing or os.environ.get("MDTF_SHARDED_CAPTURE_OVERLAP", "1") != "0"
         self.eager_update = fn if (self.mode == "sharded" and self.overlap and self.collective
                                    and self.R == self.world and allowed) else None
 
-    CAPTURE_UPD = os.environ.get("MDTF_SHARDED_CAPTURE_UPD", "fork")
+    CAPTURE_UPD = os.environ.get("MDTF_SHARDED_CAPTURE_UPD", "lag")
 
     def fork_update_stream(self):
         """Main thread, before backward, inside a capture: fork the update side stream from the capture stream
@@ -312,6 +316,9 @@ class GradReducer(object):
         self.bucket_updates = getattr(self, "bucket_updates", 0) + 1
         if capt:
             self.captured_bucket_updates = getattr(self, "captured_bucket_updates", 0) + 1
+            # (bucket updated, buckets launched so far this step): lag mode updates bucket k after k+1 launched
+            self.capture_update_log = getattr(self, "capture_update_log", []) + [
+                (self.space.buckets.index(b), getattr(self, "launch_count", 0))]
             if not side:
                 # the compute (capture) stream itself waits for this bucket's reduce-scatter
                 self.capture_compute_waits = getattr(self, "capture_compute_waits", 0) + 1
@@ -405,6 +412,7 @@ class GradReducer(object):
         if self.eager_update is not None:
             if getattr(self, "_capturing", False) and self.CAPTURE_UPD == "lag":
                 prev, self._lagged = self._lagged, b
+                self.launch_count = getattr(self, "launch_count", 0) + 1
                 if prev is not None:
                     self._update_bucket(prev)
             else:

@@ -185,20 +185,21 @@ def test_hip_graph_bert_dropout_advances_per_replay():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["allreduce", "sharded", "sharded-lag"])
+@pytest.mark.parametrize("mode", ["allreduce", "sharded", "sharded-inline"])
 def test_hip_graph_captures_rccl_collectives(mode, monkeypatch):
     """The bucketed RCCL all-reduce (or PS-shard reduce-scatter + all-gather) fired from the gradient hooks
     is captured into the step graph: a 1-rank nccl group with collectives forced on, eager == replay.
 
-    Sharded: inside the capture each bucket's update runs on the side stream the main thread
-    forked before backward, so no backward kernel captured after bucket k's hook depends on bucket k's
-    reduce-scatter (the capture stream never waits on an RS work: ``capture_compute_waits == 0``).  ``lag`` issues
-    bucket k's update from the capture stream when bucket k+1 launches."""
+    Sharded: inside the capture bucket k's update (and all-gather) is issued when bucket k+1
+    launches, the last one in end_backward, so the backward kernels captured between hook k and hook k+1 do not
+    depend on bucket k's reduce-scatter (``capture_update_log``: bucket k updated once k+2 buckets had launched).
+    ``sharded-inline`` is the round-5 order (update inside the bucket's own hook).  The side-stream form
+    (MDTF_SHARDED_CAPTURE_UPD=fork) segfaults in hipStreamEndCapture on this ROCm and is not run."""
     _gpu()
     from mdtf.parallel import reducer as R
-    lag = mode == "sharded-lag"
-    mode = "sharded" if lag else mode
-    monkeypatch.setattr(R.GradReducer, "CAPTURE_UPD", "lag" if lag else "fork")
+    inline = mode == "sharded-inline"
+    mode = "sharded" if inline else mode
+    monkeypatch.setattr(R.GradReducer, "CAPTURE_UPD", "inline" if inline else "lag")
     import socket
     import torch.distributed as dist
     from mdtf.ops import _native
@@ -227,8 +228,12 @@ def test_hip_graph_captures_rccl_collectives(mode, monkeypatch):
             # every bucket was updated + all-gathered during backward INSIDE the capture (not after the update)
             assert getattr(op.reducer, "captured_bucket_updates", 0) == len(op.space.buckets), \
                 (getattr(op.reducer, "captured_bucket_updates", 0), len(op.space.buckets))
-            waits = getattr(op.reducer, "capture_compute_waits", 0)
-            assert (waits == len(op.space.buckets)) if lag else (waits == 0), waits
+            nb = len(op.space.buckets)
+            log = op.reducer.capture_update_log[-nb:]          # the capture's step
+            assert [b for b, _ in log] == list(range(nb)) or sorted(b for b, _ in log) == list(range(nb)), log
+            if not inline:
+                # bucket k updated after bucket k+1 launched (the last after every bucket launched)
+                assert all(launched >= min(k + 2, nb) for k, (_, launched) in enumerate(log)), log
         from mdtf.train import graph as G
         assert G.LAST_DRAIN[0] == "recorder", G.LAST_DRAIN
         assert l_e == l_g, (l_e, l_g)
