@@ -59,10 +59,12 @@ WG3_TILES = ((256, 256, 2), (256, 128, 2), (256, 128, 3), (128, 256, 2), (128, 2
 # (bm, bn, stages): LDS = stages * (bm + bn) * 128 B <= 160 KiB
 V2_TILES = ((128, 128, 2), (128, 128, 3), (128, 128, 4), (128, 64, 3), (128, 64, 4), (256, 128, 2), (256, 128, 3),
             (256, 64, 3), (64, 128, 2), (64, 128, 3), (64, 128, 4), (64, 64, 4),
-            (128, 128, 1), (128, 64, 1), (256, 128, 1), (64, 128, 1), (256, 64, 1))   # stages 1: K == 64 only
+            (128, 128, 1), (128, 64, 1), (256, 128, 1), (64, 128, 1), (256, 64, 1),   # stages 1: K == 64 only
+            (128, 128, 32), (64, 128, 32), (64, 128, 42))   # split rings: 10 x A stages + filter stages
 # 8-wave (512-thread) v2 tiles: one block per CU, 2 waves per SIMD
 V3_TILES = ((256, 256, 2), (256, 128, 2), (256, 128, 3), (256, 64, 3), (256, 64, 4), (128, 256, 2), (128, 256, 3),
-            (256, 256, 1), (256, 128, 1), (448, 128, 2), (448, 128, 1))   # 448 = 7 x 64: 0.875-wave tile counts
+            (256, 256, 1), (256, 128, 1), (448, 128, 2), (448, 128, 1),   # 448 = 7 x 64: 0.875-wave tile counts
+            (256, 256, 32), (256, 128, 32), (256, 128, 42), (128, 256, 32), (128, 256, 42))   # split rings
 
 
 def ws_tiles(pass_, c, co, kh, kw, s):

@@ -124,6 +124,18 @@ __device__ __forceinline__ uint4 mask_bf8(const uint4& v, uint32_t m8) {
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// 8 packed bf16 -> floats
+__device__ __forceinline__ void unpack8(const uint4& raw, float (&f)[8]) {
+  const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f[2 * k] = __uint_as_float(w[k] << 16);
+    f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+
 __device__ __forceinline__ uint4 ld16(const bf16_t* p, bool ok) {
   return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
 }
@@ -1137,6 +1149,447 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   }
 }
 
+// ============================================================================
+// Persistent v2 forward / data gradient (MODE 0..2), register epilogue.
+// One workgroup per (CU x occupancy) walks tiles w = blockIdx.x + i * gridDim.x in XCD-contiguous order
+// (tile = xcd_remap(w, tiles): the tiles an XCD runs at once are consecutive, sharing A rows in its L2).
+// The epilogue stores straight from the accumulators: v_permlane16_swap of fragment pairs (j, j+1) gives every
+// lane 8 consecutive channels of one pixel (16-B buffer stores; out-of-range rows / columns get an offset past
+// num_records, so every wave issues the same number of memory instructions), so the C tile never goes through
+// LDS.  With a plain (or forward BN-statistics) epilogue the NEXT tile's row setup and prologue LDS-DMA are issued
+// before the stores: its first operands land while this tile's output drains, and the tiles on different CUs
+// drift out of lockstep, spreading the HBM write bursts over the main loops.  Epilogues that read (accumulate
+// source, BN-backward statistics) issue the next prologue after their loads are consumed (an early DMA would be
+// waited for by every load behind it: vmcnt retires in issue order).
+// ============================================================================
+template <int BM, int BN, int MODE, bool STATS, int STAGES, int NW>
+__global__ void __launch_bounds__(64 * NW) conv_fd_p(ConvArgs a) {
+  constexpr int NT = 64 * NW;
+  constexpr int WM = NW == 4 ? 2 : (BM > BN ? 4 : 2), WN = NW / WM;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int RA = BM / (8 * NW), RB = BN / (8 * NW);
+  constexpr int ROWB = 128;
+  constexpr int PER_STAGE = RA + RB;
+  constexpr unsigned OOB = 0x80000000u;
+  constexpr bool SPLIT = STAGES >= 10;
+  constexpr int SA = SPLIT ? STAGES / 10 : STAGES, SB = SPLIT ? STAGES % 10 : STAGES;
+  constexpr int RING = (SA * BM + SB * BN) * ROWB;
+  static_assert(MODE <= 2 && TN % 2 == 0 && RA >= 1 && RB >= 1, "persistent tile");
+  constexpr int EMAX = TM * (TN / 2);             // epilogue stores per wave (the E of the first waits)
+  static_assert(SA >= SB && SB >= 2 && (SA - 1) * PER_STAGE + EMAX < 64, "persistent ring");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  float* red = reinterpret_cast<float*>(smem_raw + RING);        // STATS: [2][WM][BN] (outside the ring)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int total = a.mtiles * a.ntiles;
+  const int GH = MODE == 0 ? a.H : a.OH;
+  const int GW = MODE == 0 ? a.W : a.OW;
+  const int GC = MODE == 0 ? a.Cin : a.Cout;
+  const int RH = MODE == 0 ? a.OH : MODE == 1 ? a.H : a.cls_Hc;
+  const int RW = MODE == 0 ? a.OW : MODE == 1 ? a.W : a.cls_Wc;
+  const int lrow = lane >> 3;
+  const int TKW = MODE == 2 ? a.cls_tw : a.KW;
+  const int ntaps = MODE == 2 ? a.cls_th * a.cls_tw : a.KH * a.KW;
+  const int DHe = MODE == 2 ? 1 : a.DH, DWe = MODE == 2 ? 1 : a.DW;
+  const int bytes_a = (int)((long long)a.N * GH * GW * GC * 2);
+  const int bytes_b = (int)((long long)(MODE == 2 ? a.KH * a.KW * a.Cout : a.K) * a.Ncol * 2);
+  const int bytes_o = (int)((long long)a.N * (MODE == 0 ? a.OH * a.OW : a.H * a.W) * a.Ncol * 2);
+  const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, bytes_o, 0x00020000);
+  const bool heavy = (MODE == 1 || MODE == 2) && (a.accumulate || a.bsum != nullptr);
+  const bool bstat = (MODE == 1 || MODE == 2) && a.bsum != nullptr;
+  const int KT = a.K / 64;
+
+  // ---- per-tile state
+  int mt = 0, nt = 0;
+  long long m0 = 0;
+  int n0 = 0;
+  unsigned a_off[RA], a_mask[RA], b_off[RB];
+  auto setup = [&](int w) {
+    const int tile = xcd_remap(w, total);
+    mt = tile / a.ntiles;
+    nt = tile - mt * a.ntiles;
+    m0 = (long long)mt * BM;
+    n0 = nt * BN;
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      const int row = 8 * (wave + NW * i) + lrow;
+      const long long m = m0 + row;
+      const bool ok = m < a.M;
+      const unsigned mm = ok ? static_cast<unsigned>(m) : 0u;
+      const unsigned t = fdiv31(mm, a.mg_rw, a.sh_rw);
+      const int ow = static_cast<int>(mm - t * static_cast<unsigned>(RW));
+      const unsigned nq = fdiv31(t, a.mg_rh, a.sh_rh);
+      const int oh = static_cast<int>(t - nq * static_cast<unsigned>(RH));
+      const int n = static_cast<int>(nq);
+      const int y0 = MODE == 0 ? oh * a.SH - a.PH : MODE == 1 ? oh + a.PH : a.cls_q0h + oh;
+      const int x0 = MODE == 0 ? ow * a.SW - a.PW : MODE == 1 ? ow + a.PW : a.cls_q0w + ow;
+      const int ch = 8 * ((lane & 7) ^ ((row >> 1) & 7));
+      a_off[i] = static_cast<unsigned>(((n * GH + y0) * GW + x0) * GC + ch);
+      unsigned mask = 0;
+      if (ok) {
+        for (int tt = 0; tt < ntaps; ++tt) {
+          const int kh = tt / TKW, kw = tt - kh * TKW;
+          const int iy = MODE == 0 ? y0 + kh * DHe : y0 - kh * DHe;
+          const int ix = MODE == 0 ? x0 + kw * DWe : x0 - kw * DWe;
+          if (iy >= 0 && iy < GH && ix >= 0 && ix < GW) mask |= 1u << tt;
+        }
+      }
+      a_mask[i] = mask;
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int row = 8 * (wave + NW * i) + lrow;
+      const int n = n0 + row;
+      const int ch = 8 * ((lane & 7) ^ ((row >> 1) & 7));
+      const int e = MODE == 0 ? n * a.K + ch : n * a.Cout + ch;
+      b_off[i] = n < a.Ncol ? static_cast<unsigned>(e * 2) : OOB;
+    }
+  };
+
+  struct Walk { int t, kh, kw, c0, k0; };
+  Walk wa{0, 0, 0, 0, 0}, wb{0, 0, 0, 0, 0};
+  auto advance = [&](Walk& w) {
+    w.k0 += 64;
+    w.c0 += 64;
+    const int wrap = w.c0 == GC ? 1 : 0;
+    w.c0 = wrap ? 0 : w.c0;
+    w.t += wrap;
+    w.kw += wrap;
+    const int wrap2 = w.kw == TKW ? 1 : 0;
+    w.kw = wrap2 ? 0 : w.kw;
+    w.kh += wrap2;
+  };
+  char* const ringB = smem_raw + SA * BM * ROWB;
+  auto stage_a = [&](int buf) {
+    const int tap_e = (MODE == 0 ? (wa.kh * DHe * GW + wa.kw * DWe) : -(wa.kh * DHe * GW + wa.kw * DWe)) * GC + wa.c0;
+    char* lds = smem_raw + buf * (BM * ROWB);
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      const bool ok = (a_mask[i] >> wa.t) & 1u;
+      const unsigned voff = ok ? (a_off[i] + (unsigned)tap_e) * 2u : OOB;
+      dma16(a.src, bytes_a, lds + (wave + NW * i) * 1024, voff, 0);
+    }
+    advance(wa);
+  };
+  auto stage_b = [&](int buf) {
+    char* ldsb = ringB + buf * (BN * ROWB);
+    const int wtap = MODE == 2 ? (a.cls_kh0 + a.SH * wb.kh) * a.KW + a.cls_kw0 + a.SW * wb.kw : wb.t;
+    const int sb = MODE == 0 ? wb.k0 * 2 : (wtap * a.Cin * a.Cout + wb.c0) * 2;
+#pragma unroll
+    for (int i = 0; i < RB; ++i) dma16(a.wgt, bytes_b, ldsb + (wave + NW * i) * 1024, b_off[i], sb);
+    advance(wb);
+  };
+  auto prologue = [&]() {
+    wa = Walk{0, 0, 0, 0, 0};
+    wb = Walk{0, 0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < SA - 1; ++s) {
+      if (s <= SB - 2 && s < KT) stage_b(s);
+      if (s < KT) stage_a(s);
+    }
+  };
+  auto nb_of = [&](int j) { return (j + SB - 1 < KT ? RB : 0); };
+  auto na_of = [&](int j) { return (j + SA - 1 < KT ? RA : 0); };
+
+  int w = blockIdx.x;
+  setup(w);
+  prologue();
+  int E = 0;            // memory instructions this wave issued after the current tile's prologue (lower bound)
+  const int fr = lane & 15, fq = lane >> 4;
+  const int g = fq, li = fr;
+  for (;;) {
+    float4v acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+    int ca = 0, cb = 0;
+    for (int kt = 0; kt < KT; ++kt) {
+      int younger = 0;
+      if (kt <= SB - 2) {                    // A(kt) last, in prologue group kt (the epilogue ops came after it)
+        for (int s = kt + 1; s <= SA - 2; ++s) younger += (s <= SB - 2 && s < KT ? RB : 0) + (s < KT ? RA : 0);
+        younger += E;
+        for (int j = 0; j < kt; ++j) younger += nb_of(j) + na_of(j);
+      } else {
+        const int g0 = kt - SB + 1;          // B(kt) (or, SA == SB, A(kt)) last, in loop group g0
+        younger = SA > SB ? na_of(g0) : 0;
+        for (int j = g0 + 1; j < kt; ++j) younger += nb_of(j) + na_of(j);
+      }
+      wait_vmcnt_le<(SA - 1) * PER_STAGE + EMAX>(younger);
+      __builtin_amdgcn_s_barrier();
+      if (kt + SB - 1 < KT) stage_b(cb == 0 ? SB - 1 : cb - 1);
+      if (kt + SA - 1 < KT) stage_a(ca == 0 ? SA - 1 : ca - 1);
+      const char* As = smem_raw + ca * (BM * ROWB);
+      const char* Bs = ringB + cb * (BN * ROWB);
+      ca = ca + 1 == SA ? 0 : ca + 1;
+      cb = cb + 1 == SB ? 0 : cb + 1;
+      bf16x8_t fa[2][TM], fb[2][TN];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * (TM * 16) + i * 16 + fr;
+          const int pc = (h * 4 + fq) ^ ((row >> 1) & 7);
+          fa[h][i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(As + row * ROWB + pc * 16));
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int row = wn * (TN * 16) + j * 16 + fr;
+          const int pc = (h * 4 + fq) ^ ((row >> 1) & 7);
+          fb[h][j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(Bs + row * ROWB + pc * 16));
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma(fb[h][j], fa[h][i], acc[i][j]);
+      {
+        constexpr int R = TM + TN, MF = TM * TN, PER = MF / R > 0 ? MF / R : 1;
+        __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * MF, 0);
+      }
+    }
+    // every wave is past its last LDS read of this tile: the ring may be refilled
+    __builtin_amdgcn_s_barrier();
+    const int cur_mt = mt;
+    const long long cur_m0 = m0;
+    const int cur_n0 = n0;
+    const int w_next = w + static_cast<int>(gridDim.x);
+    const bool more = w_next < total;
+    if (more && !heavy) {
+      setup(w_next);
+      prologue();
+    }
+    // ---- register epilogue of tile (cur_m0, cur_n0)
+    int issued = 0;
+    float bs0[TN / 2][8], bs1[TN / 2][8];
+#pragma unroll
+    for (int jp = 0; jp < TN / 2; ++jp)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bs0[jp][k] = bs1[jp][k] = 0.f;
+    const int pcol = 16 * (fq & 1) + 8 * (fq >> 1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const long long m = cur_m0 + wm * (TM * 16) + i * 16 + li;
+      const bool rok = m < a.M;
+      long long pix = m;
+      if (MODE == 2) {
+        const unsigned mu = rok ? static_cast<unsigned>(m) : 0u;
+        const unsigned t = fdiv31(mu, a.mg_rw, a.sh_rw);
+        const int jj = static_cast<int>(mu - t * static_cast<unsigned>(a.cls_Wc));
+        const unsigned nb = fdiv31(t, a.mg_rh, a.sh_rh);
+        const int ii = static_cast<int>(t - nb * static_cast<unsigned>(a.cls_Hc));
+        pix = (static_cast<long long>(nb) * a.H + a.cls_h0 + a.SH * ii) * a.W + a.cls_w0 + a.SW * jj;
+      }
+#pragma unroll
+      for (int jp = 0; jp < TN / 2; ++jp) {
+        const int j = 2 * jp;
+        const float4v v0 = acc[i][j], v1 = acc[i][j + 1];
+        const uint32_t x0 = pack_bf2(v0[0], v0[1]), y0 = pack_bf2(v0[2], v0[3]);
+        const uint32_t x1 = pack_bf2(v1[0], v1[1]), y1 = pack_bf2(v1[2], v1[3]);
+        const auto sx = __builtin_amdgcn_permlane16_swap(x0, x1, false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(y0, y1, false, false);
+        uint4 o = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+        const int ch = cur_n0 + wn * (TN * 16) + 16 * j + pcol;
+        const bool ok = rok && ch < a.Ncol;
+        const long long off = ok ? pix * a.Ncol + ch : 0;
+        const unsigned voff = ok ? static_cast<unsigned>(off * 2) : OOB;
+        if (heavy) {
+          float c[8];
+          unpack8(o, c);
+          if (a.accumulate) {
+            const bf16_t* src = a.acc_src ? a.acc_src : a.out;
+            uint4 old = ok ? *reinterpret_cast<const uint4*>(src + off) : make_uint4(0, 0, 0, 0);
+            if (a.acc_mask && ok) old = mask_bf8(old, a.acc_mask[off >> 3]);
+            float ov[8];
+            unpack8(old, ov);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) c[k] = __uint_as_float((uint32_t)f2bf(c[k] + ov[k]) << 16);   // as stored
+            o = make_uint4(pack_bf2(c[0], c[1]), pack_bf2(c[2], c[3]), pack_bf2(c[4], c[5]), pack_bf2(c[6], c[7]));
+          }
+          if (bstat && ok) {
+            const uint4 xq = *reinterpret_cast<const uint4*>(a.bx + off);
+            const uint32_t mb = a.bmask ? a.bmask[off >> 3] : 0xffu;
+            float xv[8];
+            unpack8(xq, xv);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const float gk = ((mb >> k) & 1u) ? c[k] : 0.f;
+              bs0[jp][k] += gk;
+              bs1[jp][k] += gk * xv[k];
+            }
+          }
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, o), rs_out, voff, 0, 0);
+        ++issued;
+      }
+    }
+    if (bstat) {
+      // channels of (jp, lane group fq) summed over the wave's 16 pixel lanes, then over the WM waves of a
+      // column block in LDS (the ring is free: heavy epilogues issue the next prologue afterwards)
+#pragma unroll
+      for (int jp = 0; jp < TN / 2; ++jp)
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+          for (int o2 = 1; o2 < 16; o2 <<= 1) {
+            bs0[jp][k] += __shfl_xor(bs0[jp][k], o2, 64);
+            bs1[jp][k] += __shfl_xor(bs1[jp][k], o2, 64);
+          }
+      float* rb = reinterpret_cast<float*>(smem_raw);           // [2][WM][BN]
+      if (li == 0) {
+#pragma unroll
+        for (int jp = 0; jp < TN / 2; ++jp)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int nl = wn * (TN * 16) + 32 * jp + pcol + k;
+            rb[wm * BN + nl] = bs0[jp][k];
+            rb[WM * BN + wm * BN + nl] = bs1[jp][k];
+          }
+      }
+      __syncthreads();
+      for (int nl = tid; nl < BN; nl += NT) {
+        const int n = cur_n0 + nl;
+        if (n < a.Ncol) {
+          float sv = 0.f, q = 0.f;
+#pragma unroll
+          for (int w2 = 0; w2 < WM; ++w2) {
+            sv += rb[w2 * BN + nl];
+            q += rb[WM * BN + w2 * BN + nl];
+          }
+          const long long slot = (long long)(cur_mt % a.bslots) * a.Ncol + n;
+          atomicAdd(a.bsum + slot, sv);
+          atomicAdd(a.bsq + slot, q);
+        }
+      }
+    }
+    if (STATS) {
+      float ssum[TN][4], ssq[TN][4];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ssum[j][r] = ssq[j][r] = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const bool mok = cur_m0 + wm * (TM * 16) + i * 16 + li < a.M;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          if (mok) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              ssum[j][r] += acc[i][j][r];
+              ssq[j][r] += acc[i][j][r] * acc[i][j][r];
+            }
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int o2 = 1; o2 < 16; o2 <<= 1) {
+            ssum[j][r] += __shfl_xor(ssum[j][r], o2, 64);
+            ssq[j][r] += __shfl_xor(ssq[j][r], o2, 64);
+          }
+      if (li == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int nl = wn * (TN * 16) + j * 16 + 4 * g + r;
+            red[wm * BN + nl] = ssum[j][r];
+            red[WM * BN + wm * BN + nl] = ssq[j][r];
+          }
+      }
+      __syncthreads();
+      for (int nl = tid; nl < BN; nl += NT) {
+        const int n = cur_n0 + nl;
+        if (n < a.Ncol) {
+          float sv = 0.f, q = 0.f;
+#pragma unroll
+          for (int w2 = 0; w2 < WM; ++w2) {
+            sv += red[w2 * BN + nl];
+            q += red[WM * BN + w2 * BN + nl];
+          }
+          const long long slot = (long long)(cur_mt % a.stat_slots) * a.Ncol + n;
+          atomicAdd(a.stat_sum + slot, sv);
+          atomicAdd(a.stat_sq + slot, q);
+        }
+      }
+    }
+    if (!more) break;
+    if (heavy) {
+      __syncthreads();                       // the statistics reduction is done with the ring
+      setup(w_next);
+      prologue();
+      E = 0;
+    } else {
+      E = issued;                            // stores after the prologue (atomics not counted: lower bound)
+    }
+    w = w_next;
+  }
+}
+
+// MDTF_CONV_PERSIST=1: the v2 forward / data-gradient launches run the persistent register-epilogue kernel
+// (conv_fd_p) where its ring fits; =0 (default until the in-step A/B says otherwise) keeps conv_fd_v2
+int conv_persist_mode() {
+  static const int m = [] {
+    const char* e = getenv("MDTF_CONV_PERSIST");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
+
+int num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      return 256;
+    return v;
+  }();
+  return n;
+}
+
+template <int BM, int BN, int MODE, bool STATS, int STAGES, int NW>
+int launch_fd_p(ConvArgs& a, hipStream_t st) {
+  constexpr int NT = 64 * NW;
+  constexpr int WM = NW == 4 ? 2 : (BM > BN ? 4 : 2), WN = NW / WM;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int SA = STAGES >= 10 ? STAGES / 10 : STAGES, SB = STAGES >= 10 ? STAGES % 10 : STAGES;
+  // (wave tiles of 7-8 row fragments, 256 x 256 / 448 x 128: the persistent state does not fit 2 waves per SIMD
+  // next to their 128 accumulator registers -- the compiler spills inside the main loop; they stay on conv_fd_v2)
+  if constexpr (MODE > 2 || TN % 2 != 0 || SB < 2 || TM > 4) {
+    return MDTF_EUNSUPPORTED;
+  } else {
+    const size_t ring = ((size_t)SA * BM + (size_t)SB * BN) * 128;
+    const size_t lds = ring + (STATS ? (size_t)2 * WM * BN * sizeof(float) : 0);
+    if (lds > 160 * 1024) return MDTF_EUNSUPPORTED;
+    auto kern = conv_fd_p<BM, BN, MODE, STATS, STAGES, NW>;
+    static int occ = 0;
+    if (occ == 0) {
+      int o = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, NT, lds) != hipSuccess || o < 1) o = 1;
+      occ = o;
+    }
+    const long long total = (long long)a.mtiles * a.ntiles;
+    const long long cap = (long long)num_cus() * occ;
+    const unsigned grid = (unsigned)(total < cap ? total : cap);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, st, a);
+    MDTF_LAUNCH_CHECK();
+    return 0;
+  }
+}
+
 template <int BM, int BN, int MODE, bool STATS, int STAGES, int NW = 4>
 int launch_fd_v2(ConvArgs& a, hipStream_t st) {
   constexpr int NT = 64 * NW;
@@ -1159,6 +1612,10 @@ int launch_fd_v2(ConvArgs& a, hipStream_t st) {
     if (RH < 1 || RW < 1) return MDTF_EINVAL;
     magic31(static_cast<unsigned>(RW), &a.mg_rw, &a.sh_rw);
     magic31(static_cast<unsigned>(RH), &a.mg_rh, &a.sh_rh);
+  }
+  if (MODE <= 2 && STAGES >= 2 && conv_persist_mode() && a.K >= 64) {
+    const int rc = launch_fd_p<BM, BN, MODE, STATS, STAGES, NW>(a, st);
+    if (rc != MDTF_EUNSUPPORTED) return rc;
   }
   hipLaunchKernelGGL((conv_fd_v2<BM, BN, MODE, STATS, STAGES, NW>), dim3((unsigned)nblk), dim3(NT), lds, st, a);
   MDTF_LAUNCH_CHECK();
