@@ -55,7 +55,7 @@ def resnet_convs(depth=50, batch=256, image=224, width=64):
 WG2_TILES = ((128, 128, 2), (128, 128, 3), (128, 128, 4), (128, 128, 5), (128, 64, 2), (64, 128, 2), (64, 128, 4),
              (64, 128, 6), (64, 64, 3))
 WG3_TILES = ((256, 256, 2), (256, 128, 2), (256, 128, 3), (128, 256, 2), (128, 256, 3), (128, 128, 3), (128, 128, 4),
-             (128, 128, 5))   # 8 waves
+             (128, 128, 5), (64, 256, 3), (64, 256, 4), (256, 64, 3), (256, 64, 4))   # 8 waves
 # (bm, bn, stages): LDS = stages * (bm + bn) * 128 B <= 160 KiB
 V2_TILES = ((128, 128, 2), (128, 128, 3), (128, 128, 4), (128, 64, 3), (128, 64, 4), (256, 128, 2), (256, 128, 3),
             (256, 64, 3), (64, 128, 2), (64, 128, 3), (64, 128, 4), (64, 64, 4),

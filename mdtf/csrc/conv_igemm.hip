@@ -2141,6 +2141,9 @@ int dispatch_wgrad_v2(ConvArgs& a, int bm, int bn, int stages, int w8, int split
   WG2(128, 128, 2, 8) WG2(128, 128, 3, 8) WG2(128, 128, 4, 8)
   // deeper rings (more LDS-DMA in flight per block): 4-5 stages of 128 x 128, 4-6 of 64 x 128
   WG2(128, 128, 5, 8) WG2(128, 128, 4, 4) WG2(128, 128, 5, 4) WG2(64, 128, 4, 4) WG2(64, 128, 6, 4)
+  // skinny 8-wave tiles for 64-row / 64-column filters (the stage-1 1x1 convs, R or Cout = 64): a 128 x 128 tile
+  // there leaves half its rows (columns) empty and reads the other operand twice; 64 x 256 / 256 x 64 read each once
+  WG2(64, 256, 3, 8) WG2(64, 256, 4, 8) WG2(256, 64, 3, 8) WG2(256, 64, 4, 8)
 #undef WG2
   return MDTF_EUNSUPPORTED;
 }

@@ -359,6 +359,15 @@ __global__ void embed_fwd_kernel(const bf16_t* __restrict__ table, const long lo
 __global__ void embed_bwd_kernel(const bf16_t* __restrict__ dy, const long long* __restrict__ ids,
                                  float* __restrict__ dtable, long long n, int H, long long vocab) {
   const long long total = n * H;
+  if (total < 0x7fffffffLL) {         // 32-bit index math: one 32-bit division per element instead of two 64-bit
+    const unsigned tot = (unsigned)total, h = (unsigned)H;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += gridDim.x * blockDim.x) {
+      const unsigned t = i / h, c = i - t * h;
+      const long long id = ids[t];
+      if (id >= 0 && id < vocab) atomicAdd(dtable + id * H + c, bf2f(dy[i]));
+    }
+    return;
+  }
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const long long t = i / H;

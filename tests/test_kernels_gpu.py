@@ -1628,8 +1628,9 @@ def test_conv_v2_8wave_tiles(bm, bn, stages, geo):
 
 
 @pytest.mark.parametrize("bm,bn,stages", [(256, 256, 2), (256, 128, 2), (256, 128, 3), (128, 256, 2), (128, 256, 3),
-                                          (128, 128, 3)])
-@pytest.mark.parametrize("geo", [(3, 9, 9, 64, 3, 320, 1), (2, 12, 12, 192, 1, 256, 1), (2, 15, 13, 64, 3, 128, 2)])
+                                          (128, 128, 3), (64, 256, 3), (64, 256, 4), (256, 64, 3), (256, 64, 4)])
+@pytest.mark.parametrize("geo", [(3, 9, 9, 64, 3, 320, 1), (2, 12, 12, 192, 1, 256, 1), (2, 15, 13, 64, 3, 128, 2),
+                                 (2, 14, 14, 64, 1, 256, 1), (2, 14, 14, 256, 1, 64, 1)])
 @pytest.mark.parametrize("slab", [True, False])
 def test_conv_wgrad_8wave_tiles(bm, bn, stages, geo, slab, monkeypatch):
     """8-wave v2 weight-gradient tiles (split-K fp32 atomics) vs the fp32 autograd reference: R and Cout
