@@ -1993,6 +1993,66 @@ __global__ void __launch_bounds__(64 * NW, (wgrad_min_waves<BM, BN, STAGES, NW>(
 // DW[r][c] (row stride ld) += sum_s slab[s][r][c]  (slab rows dense, C % 4 == 0); 4 splits in flight.
 // (Spreading the splits of a small filter over more blocks with fp32 atomics measured 1.7 % slower in the ResNet
 // step: profiles/ab_r5.md.)
+// Split-parallel form for small filters with many splits (e.g. 64 x 256 over 128 splits: 16 blocks of the plain
+// form, each thread 128 dependent-ish loads): G thread groups of 256 / G per block, group g sums splits g, g + G, ..
+// of the block's 256 / G float4 outputs, then the G partials are added in LDS (fixed order: deterministic).
+template <bool NT, int G>
+__global__ void __launch_bounds__(256) wgrad_slab_reduce_g(const float* __restrict__ slab, int splits,
+                                                           long long RC, int C, long long ld, float* __restrict__ dw) {
+  constexpr int W = 256 / G;                                // float4 outputs per block
+  __shared__ float4 part[G][W];
+  const int g = threadIdx.x / W, l = threadIdx.x - g * W;
+  const long long q = (long long)blockIdx.x * W + l;       // float4 index
+  const long long st = RC / 4;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const float4* s4 = reinterpret_cast<const float4*>(slab);
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (q < st) {
+    int sp = g;
+    for (; sp + 3 * G < splits; sp += 4 * G) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long i = q + (long long)(sp + u * G) * st;
+        if constexpr (NT)
+          v[u] = __builtin_bit_cast(float4, __builtin_nontemporal_load(reinterpret_cast<const f4v*>(s4) + i));
+        else
+          v[u] = s4[i];
+      }
+      t.x += (v[0].x + v[1].x) + (v[2].x + v[3].x);
+      t.y += (v[0].y + v[1].y) + (v[2].y + v[3].y);
+      t.z += (v[0].z + v[1].z) + (v[2].z + v[3].z);
+      t.w += (v[0].w + v[1].w) + (v[2].w + v[3].w);
+    }
+    for (; sp < splits; sp += G) {
+      const float4 a = s4[q + (long long)sp * st];
+      t.x += a.x;
+      t.y += a.y;
+      t.z += a.z;
+      t.w += a.w;
+    }
+  }
+  part[g][l] = t;
+  __syncthreads();
+  if (g != 0 || q >= st) return;
+#pragma unroll
+  for (int h = 1; h < G; ++h) {
+    const float4 a = part[h][l];
+    t.x += a.x;
+    t.y += a.y;
+    t.z += a.z;
+    t.w += a.w;
+  }
+  const long long e = q * 4, r = e / C, c = e - r * C;
+  float4* o = reinterpret_cast<float4*>(dw + r * ld + c);
+  float4 v = *o;
+  v.x += t.x;
+  v.y += t.y;
+  v.z += t.z;
+  v.w += t.w;
+  *o = v;
+}
+
 template <bool NT>
 __global__ void __launch_bounds__(256) wgrad_slab_reduce(const float* __restrict__ slab, int splits, long long RC,
                                                          int C, long long ld, float* __restrict__ dw) {
@@ -2061,9 +2121,26 @@ int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
   MDTF_LAUNCH_CHECK();
   if (b.slab) {
     const long long RC = (long long)R * a.Cout;
-    hipLaunchKernelGGL((b.slab_nt ? wgrad_slab_reduce<true> : wgrad_slab_reduce<false>),
-                       dim3((unsigned)ceil_div(RC / 4, 256)), dim3(256), 0, st, b.slab, splits, RC, a.Cout,
-                       (long long)a.ld_dw, a.dw);
+    // few outputs, many splits: spread the splits of each output over G thread groups (MDTF_SLAB_G=1: plain form)
+    static const int gmax = [] {
+      const char* e = getenv("MDTF_SLAB_G");
+      return e ? atoi(e) : 16;
+    }();
+    const long long q4 = RC / 4;
+    int G = 1;
+    while (G < gmax && G < 16 && q4 * G < 256LL * 256 && splits >= 8 * G) G *= 4;
+    if (G == 16)
+      hipLaunchKernelGGL((b.slab_nt ? wgrad_slab_reduce_g<true, 16> : wgrad_slab_reduce_g<false, 16>),
+                         dim3((unsigned)ceil_div(q4, 16)), dim3(256), 0, st, b.slab, splits, RC, a.Cout,
+                         (long long)a.ld_dw, a.dw);
+    else if (G == 4)
+      hipLaunchKernelGGL((b.slab_nt ? wgrad_slab_reduce_g<true, 4> : wgrad_slab_reduce_g<false, 4>),
+                         dim3((unsigned)ceil_div(q4, 64)), dim3(256), 0, st, b.slab, splits, RC, a.Cout,
+                         (long long)a.ld_dw, a.dw);
+    else
+      hipLaunchKernelGGL((b.slab_nt ? wgrad_slab_reduce<true> : wgrad_slab_reduce<false>),
+                         dim3((unsigned)ceil_div(RC / 4, 256)), dim3(256), 0, st, b.slab, splits, RC, a.Cout,
+                         (long long)a.ld_dw, a.dw);
     MDTF_LAUNCH_CHECK();
   }
   return 0;
@@ -2159,16 +2236,19 @@ __global__ void __launch_bounds__(256) dgrad_zero_classes(ConvArgs a, int C8) {
   const int tid = threadIdx.x;
   const int ppb = 256 / C8;                          // pixels per block iteration
   const int c8 = tid % C8, pl = tid / C8;
-  const long long P = (long long)a.N * a.H * a.W;
+  // 32-bit pixel index math with the host's magic divisors (mg_rw: W, mg_rh: H; P < 2^31 host-checked): the
+  // 64-bit p % W, (p / W) % H of every iteration were ~250 VALU instructions per 32-48 B moved
+  const unsigned P = (unsigned)a.N * a.H * a.W;
   float s0[8], s1[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) s0[k] = s1[k] = 0.f;
-  for (long long p = (long long)blockIdx.x * ppb + pl; p < P; p += (long long)gridDim.x * ppb) {
-    const int w = static_cast<int>(p % a.W);
-    const int h = static_cast<int>((p / a.W) % a.H);
+  for (unsigned p = blockIdx.x * (unsigned)ppb + pl; p < P; p += gridDim.x * (unsigned)ppb) {
+    const unsigned q = fdiv31(p, a.mg_rw, a.sh_rw);
+    const int w = static_cast<int>(p - q * (unsigned)a.W);
+    const int h = static_cast<int>(q - fdiv31(q, a.mg_rh, a.sh_rh) * (unsigned)a.H);
     const int rh = (h + a.PH) % a.SH, rw = (w + a.PW) % a.SW;
     if (rh < a.KH && rw < a.KW) continue;            // this class has taps: the GEMM launch owns it
-    const long long off = p * a.Ncol + c8 * 8;
+    const long long off = (long long)p * a.Ncol + c8 * 8;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (a.accumulate) {
       v = *reinterpret_cast<const uint4*>((a.acc_src ? a.acc_src : a.out) + off);
@@ -2402,6 +2482,9 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
       if (rc) return rc;
     }
   if (zero_pending) {
+    if ((long long)N * H * W >= (1LL << 31)) return MDTF_EUNSUPPORTED;
+    magic31(static_cast<unsigned>(W), &a.mg_rw, &a.sh_rw);
+    magic31(static_cast<unsigned>(H), &a.mg_rh, &a.sh_rh);
     const long long chunks = (long long)N * H * W * C8;
     const int blocks = static_cast<int>(ceil_div(chunks, 256) < 4096 ? ceil_div(chunks, 256) : 4096);
     if (bsum)
