@@ -99,6 +99,9 @@ struct ConvArgs {
   // the per-row setup were ~1,000 VALU instructions per wave before the first DMA of every tile
   unsigned mg_rw, mg_rh;
   int sh_rw, sh_rh;
+  // v2 fwd / dgrad: first GEMM row of this launch (a tile-count tail split runs the last rows as a second launch
+  // with smaller tiles, launch_fd_v2); rows [m_base, M)
+  long long m_base;
 };
 
 // m, sh with floor(n / d) = (n * m) >> sh for every 0 <= n < 2^31: l = ceil(log2 d), m = ceil(2^(31+l) / d)
@@ -629,7 +632,7 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   const int wm = wave / WN, wn = wave % WN;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = tile / a.ntiles, nt = tile % a.ntiles;
-  const long long m0 = (long long)mt * BM;
+  const long long m0 = a.m_base + (long long)mt * BM;
   const int n0 = nt * BN;
 
   // MODE 3 (dense forward) gathers A like a 1x1 forward convolution; MODE 4 (dense data gradient with the
@@ -1210,7 +1213,7 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_p(ConvArgs a) {
     const int tile = xcd_remap(w, total);
     mt = tile / a.ntiles;
     nt = tile - mt * a.ntiles;
-    m0 = (long long)mt * BM;
+    m0 = a.m_base + (long long)mt * BM;
     n0 = nt * BN;
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
@@ -1590,10 +1593,62 @@ int launch_fd_p(ConvArgs& a, hipStream_t st) {
   }
 }
 
+// MDTF_CONV_TAIL=0: no tile-count tail split; 1 (default): tails under a quarter of a wave; 2: every partial wave
+int conv_tail_mode() {
+  static const int m = [] {
+    const char* e = getenv("MDTF_CONV_TAIL");
+    return e ? atoi(e) : 1;
+  }();
+  return m;
+}
+
+extern "C" int mdtf_get_deterministic();
+
 template <int BM, int BN, int MODE, bool STATS, int STAGES, int NW = 4>
+int launch_fd_v2(ConvArgs& a, hipStream_t st);
+
+// The 8-wave 256-row tiles hold one workgroup per CU, so a tile count just past a multiple of the CU count costs a
+// whole extra round for a few tiles (ResNet-50 at batch 256: 784 = 3 x 256 + 16 tiles, 1568 = 6 x 256 + 32).  The
+// rows of the full rounds run as one launch; the tail rows as a second launch on 4-wave 128 x 128 tiles (two
+// workgroups per CU), which spreads the tail's work over 4x as many workgroups.  Off in deterministic mode (the
+// statistics slot of a tile must stay one per M tile).  Returns 1 if it launched, 0 if not applicable.
+template <int BM, int BN, int MODE, bool STATS, int STAGES, int NW>
+int launch_fd_tail_split(ConvArgs& a, hipStream_t st, int* rc) {
+  if constexpr (NW == 8 && BM == 256 && (MODE == 0 || MODE == 1)) {
+    if (!conv_tail_mode() || a.m_base != 0 || mdtf_get_deterministic()) return 0;
+    const long long mtiles = ceil_div(a.M, BM), ntiles = ceil_div(a.Ncol, BN);
+    const long long cus = num_cus(), total = mtiles * ntiles;
+    const long long rounds = total / cus, rem = total - rounds * cus;
+    // MDTF_CONV_TAIL=1: tails under a quarter of a wave; 2: any partial last wave
+    if (rounds < 1 || rem == 0 || (conv_tail_mode() == 1 && rem * 4 > cus) || (rounds * cus) % ntiles) return 0;
+    const long long m1 = rounds * cus / ntiles * BM;        // rows of the full rounds
+    if (m1 >= a.M) return 0;
+    const long long M = a.M;
+    ConvArgs tail = a;
+    tail.m_base = m1;
+    a.M = m1;
+    *rc = launch_fd_v2<BM, BN, MODE, STATS, STAGES, NW>(a, st);
+    a.M = M;
+    if (*rc == 0) *rc = launch_fd_v2<128, 128, MODE, STATS, 2, 4>(tail, st);
+    a.mtiles = static_cast<int>(mtiles);
+    a.ntiles = static_cast<int>(ntiles);
+    return 1;
+  } else {
+    (void)a;
+    (void)st;
+    (void)rc;
+    return 0;
+  }
+}
+
+template <int BM, int BN, int MODE, bool STATS, int STAGES, int NW>
 int launch_fd_v2(ConvArgs& a, hipStream_t st) {
   constexpr int NT = 64 * NW;
-  a.mtiles = static_cast<int>(ceil_div(a.M, BM));
+  {
+    int rc = 0;
+    if (launch_fd_tail_split<BM, BN, MODE, STATS, STAGES, NW>(a, st, &rc)) return rc;
+  }
+  a.mtiles = static_cast<int>(ceil_div(a.M - a.m_base, BM));
   a.ntiles = static_cast<int>(ceil_div(a.Ncol, BN));
   const long long nblk = (long long)a.mtiles * a.ntiles;
   if (nblk > 0x7fffffff) return MDTF_EUNSUPPORTED;

@@ -1304,6 +1304,52 @@ def test_conv_v2_split_ring(bm, bn, ver, stages, k, s, pad, c, co):
     assert _rel(ps[1].sum(0), (g * bx.float()).sum((0, 1, 2))) < 1e-2
 
 
+@pytest.mark.parametrize("stages", [2, 32])
+@pytest.mark.parametrize("tail", ["1", "0"])
+def test_conv_v2_tail_split(stages, tail, monkeypatch):
+    """The tile-count tail split of the 8-wave 256-row tiles (launch_fd_v2): 272 = 256 + 16 tiles of 256 x 256 run
+    as one launch of 256 tiles + the last 4096 rows on 128 x 128 tiles.  Forward with BN statistics and data
+    gradient with accumulate + BN-backward statistics vs fp32, with the split on (default) and off (MDTF_CONV_TAIL=0
+    is read once per process: the "0" case runs in a child)."""
+    if tail == "0":
+        import subprocess
+        import sys
+        code = ("import torch, tests.test_kernels_gpu as t; t.setup_module(None); "
+                "t._tail_case(%d)" % stages)
+        env = dict(__import__("os").environ, MDTF_CONV_TAIL="0")
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
+                           cwd=__import__("os").path.dirname(__import__("os").path.dirname(__file__)))
+        assert r.returncode == 0, r.stderr[-2000:]
+        return
+    _tail_case(stages)
+
+
+def _tail_case(stages):
+    from mdtf.ops import conv as C
+    torch.manual_seed(stages)
+    n, h, w, c, co = 68, 32, 32, 64, 256                      # M = 69632 rows = 272 tiles of 256
+    x = torch.randn(n, h, w, c, device=DEV).bfloat16()
+    wt = (torch.randn(1, 1, c, co, device=DEV) / c ** 0.5).bfloat16()
+    ref = (x.float().reshape(-1, c) @ wt.float().reshape(c, co)).reshape(n, h, w, co)
+    st = torch.zeros(2, 64, co, device=DEV)
+    y = C.mdtf_fwd(x, wt, (h, w), (1, 1), (0, 0, 0, 0), (1, 1), 256, 256, (st[0], st[1]), 3, stages)
+    assert _rel(y, ref) < 1e-2
+    assert _rel(st[0].sum(0), ref.sum((0, 1, 2))) < 1e-3
+    dy = torch.randn(n, h, w, c, device=DEV).bfloat16()       # dgrad of a 1x1 256 -> 64 conv: DX has 256 channels
+    w2 = (torch.randn(1, 1, co, c, device=DEV) / co ** 0.5).bfloat16()
+    gref = (dy.float().reshape(-1, c) @ w2.float().reshape(co, c).t()).reshape(n, h, w, co)
+    base = torch.randn(n, h, w, co, device=DEV).bfloat16()
+    out = base.clone()
+    bx = torch.randn(n, h, w, co, device=DEV).bfloat16()
+    ps = torch.zeros(2, 4, co, device=DEV)
+    C.mdtf_dgrad(dy, w2, (n, h, w, co), (1, 1), (0, 0, 0, 0), (1, 1), 256, 256, 3, stages, out=out, accumulate=True,
+                 bn_stats=(bx, None, ps[0], ps[1], 4))
+    assert _rel(out, gref + base.float()) < 1e-2
+    g = out.float()
+    assert _rel(ps[0].sum(0), g.sum((0, 1, 2))) < 1e-2
+    assert _rel(ps[1].sum(0), (g * bx.float()).sum((0, 1, 2))) < 1e-2
+
+
 def _bits(b):
     """bool [..., C] -> the kernels' 1-bit-per-element mask bytes (element 8i + k = bit k of byte i)."""
     w = (1 << torch.arange(8, device=b.device)).to(torch.int32)
