@@ -1165,7 +1165,7 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
 // source, BN-backward statistics) issue the next prologue after their loads are consumed (an early DMA would be
 // waited for by every load behind it: vmcnt retires in issue order).
 // ============================================================================
-template <int BM, int BN, int MODE, bool STATS, int STAGES, int NW>
+template <int BM, int BN, int MODE, bool STATS, int STAGES, int NW, bool HEAVY>
 __global__ void __launch_bounds__(64 * NW) conv_fd_p(ConvArgs a) {
   constexpr int NT = 64 * NW;
   constexpr int WM = NW == 4 ? 2 : (BM > BN ? 4 : 2), WN = NW / WM;
@@ -1200,8 +1200,10 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_p(ConvArgs a) {
   const int bytes_b = (int)((long long)(MODE == 2 ? a.KH * a.KW * a.Cout : a.K) * a.Ncol * 2);
   const int bytes_o = (int)((long long)a.N * (MODE == 0 ? a.OH * a.OW : a.H * a.W) * a.Ncol * 2);
   const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, bytes_o, 0x00020000);
-  const bool heavy = (MODE == 1 || MODE == 2) && (a.accumulate || a.bsum != nullptr);
-  const bool bstat = (MODE == 1 || MODE == 2) && a.bsum != nullptr;
+  // HEAVY (template): an epilogue that reads (accumulate source / BN-backward statistics); the plain instantiation
+  // carries none of its registers (the 256 x 256 tile fits 2 waves per SIMD without spilling only then)
+  constexpr bool heavy = HEAVY && (MODE == 1 || MODE == 2);
+  const bool bstat = heavy && a.bsum != nullptr;
   const int KT = a.K / 64;
 
   // ---- per-tile state
@@ -1374,9 +1376,10 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_p(ConvArgs a) {
     }
     // ---- register epilogue of tile (cur_m0, cur_n0)
     int issued = 0;
-    float bs0[TN / 2][8], bs1[TN / 2][8];
+    constexpr int NBS = heavy ? TN / 2 : 1;
+    float bs0[NBS][8], bs1[NBS][8];
 #pragma unroll
-    for (int jp = 0; jp < TN / 2; ++jp)
+    for (int jp = 0; jp < NBS; ++jp)
 #pragma unroll
       for (int k = 0; k < 8; ++k) bs0[jp][k] = bs1[jp][k] = 0.f;
     const int pcol = 16 * (fq & 1) + 8 * (fq >> 1);
@@ -1406,7 +1409,7 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_p(ConvArgs a) {
         const bool ok = rok && ch < a.Ncol;
         const long long off = ok ? pix * a.Ncol + ch : 0;
         const unsigned voff = ok ? static_cast<unsigned>(off * 2) : OOB;
-        if (heavy) {
+        if constexpr (heavy) {
           float c[8];
           unpack8(o, c);
           if (a.accumulate) {
@@ -1436,7 +1439,7 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_p(ConvArgs a) {
         ++issued;
       }
     }
-    if (bstat) {
+    if constexpr (heavy) if (bstat) {
       // channels of (jp, lane group fq) summed over the wave's 16 pixel lanes, then over the WM waves of a
       // column block in LDS (the ring is free: heavy epilogues issue the next prologue afterwards)
 #pragma unroll
@@ -1569,23 +1572,29 @@ int launch_fd_p(ConvArgs& a, hipStream_t st) {
   constexpr int WM = NW == 4 ? 2 : (BM > BN ? 4 : 2), WN = NW / WM;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int SA = STAGES >= 10 ? STAGES / 10 : STAGES, SB = STAGES >= 10 ? STAGES % 10 : STAGES;
-  // (wave tiles of 7-8 row fragments, 256 x 256 / 448 x 128: the persistent state does not fit 2 waves per SIMD
-  // next to their 128 accumulator registers -- the compiler spills inside the main loop; they stay on conv_fd_v2)
-  if constexpr (MODE > 2 || TN % 2 != 0 || SB < 2 || TM > 4) {
+  const bool heavy = (MODE == 1 || MODE == 2) && (a.accumulate || a.bsum != nullptr);
+  // MDTF_CONV_PERSIST=2: only the 8-wave 256 x 256 forward (plain / statistics epilogue)
+  if (conv_persist_mode() == 2 && !(MODE == 0 && NW == 8 && BM == 256 && BN == 256)) return MDTF_EUNSUPPORTED;
+  // (wave tiles of 7-8 row fragments with a reading epilogue, 256 x 256 / 448 x 128 dgrads: the persistent state
+  // does not fit 2 waves per SIMD next to their 128 accumulator registers -- they stay on conv_fd_v2)
+  if constexpr (MODE > 2 || TN % 2 != 0 || SB < 2) {
     return MDTF_EUNSUPPORTED;
   } else {
+    if (heavy && TM > 4) return MDTF_EUNSUPPORTED;
     const size_t ring = ((size_t)SA * BM + (size_t)SB * BN) * 128;
     const size_t lds = ring + (STATS ? (size_t)2 * WM * BN * sizeof(float) : 0);
     if (lds > 160 * 1024) return MDTF_EUNSUPPORTED;
-    auto kern = conv_fd_p<BM, BN, MODE, STATS, STAGES, NW>;
-    static int occ = 0;
-    if (occ == 0) {
+    // the heavy instantiation only where its registers fit (TM <= 4)
+    auto kern = heavy ? conv_fd_p<BM, BN, MODE, STATS, STAGES, NW, (MODE != 0 && TM <= 4)>
+                      : conv_fd_p<BM, BN, MODE, STATS, STAGES, NW, false>;
+    static int occ[2] = {0, 0};
+    if (occ[heavy] == 0) {
       int o = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, NT, lds) != hipSuccess || o < 1) o = 1;
-      occ = o;
+      occ[heavy] = o;
     }
     const long long total = (long long)a.mtiles * a.ntiles;
-    const long long cap = (long long)num_cus() * occ;
+    const long long cap = (long long)num_cus() * occ[heavy];
     const unsigned grid = (unsigned)(total < cap ? total : cap);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, st, a);
     MDTF_LAUNCH_CHECK();
