@@ -1309,14 +1309,14 @@ def test_conv_v2_split_ring(bm, bn, ver, stages, k, s, pad, c, co):
 def test_conv_v2_tail_split(stages, tail, monkeypatch):
     """The tile-count tail split of the 8-wave 256-row tiles (launch_fd_v2): 272 = 256 + 16 tiles of 256 x 256 run
     as one launch of 256 tiles + the last 4096 rows on 128 x 128 tiles.  Forward with BN statistics and data
-    gradient with accumulate + BN-backward statistics vs fp32, with the split on (default) and off (MDTF_CONV_TAIL=0
-    is read once per process: the "0" case runs in a child)."""
-    if tail == "0":
+    gradient with accumulate + BN-backward statistics vs fp32, with the split on (MDTF_CONV_TAIL=1) and off (default
+    is read once per process: the other mode runs in a child)."""
+    if tail == "1":
         import subprocess
         import sys
         code = ("import torch, tests.test_kernels_gpu as t; t.setup_module(None); "
                 "t._tail_case(%d)" % stages)
-        env = dict(__import__("os").environ, MDTF_CONV_TAIL="0")
+        env = dict(__import__("os").environ, MDTF_CONV_TAIL="1")
         r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
                            cwd=__import__("os").path.dirname(__import__("os").path.dirname(__file__)))
         assert r.returncode == 0, r.stderr[-2000:]
