@@ -2156,6 +2156,19 @@ __global__ void __launch_bounds__(256) wgrad_slab_reduce(const float* __restrict
   *o = v;
 }
 
+// Slab reduction on a side stream (mdtf_set_slab_stream): the reduction only feeds the gradient buffer, so it can
+// leave the dgrad -> BN-backward chain.  The side stream waits for the weight-gradient kernel through one event
+// (captured hipGraphs turn it into a fork edge); the caller joins the side stream before the gradients are read.
+hipStream_t g_slab_stream = nullptr;
+hipEvent_t slab_event() {
+  static hipEvent_t ev = [] {
+    hipEvent_t e = nullptr;
+    (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    return e;
+  }();
+  return ev;
+}
+
 template <int BM, int BN, int STAGES, int NW = 4, bool PIPE = false>
 int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
   const int R = a.KH * a.KW * a.Cin;
@@ -2185,6 +2198,12 @@ int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
                      st, b);
   MDTF_LAUNCH_CHECK();
   if (b.slab) {
+    if (g_slab_stream && g_slab_stream != st) {
+      hipEvent_t ev = slab_event();
+      if (!ev || hipEventRecord(ev, st) != hipSuccess || hipStreamWaitEvent(g_slab_stream, ev, 0) != hipSuccess)
+        return MDTF_EUNSUPPORTED;
+      st = g_slab_stream;
+    }
     const long long RC = (long long)R * a.Cout;
     // few outputs, many splits: spread the splits of each output over G thread groups (MDTF_SLAB_G=1: plain form)
     static const int gmax = [] {
@@ -2558,6 +2577,12 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
       hipLaunchKernelGGL(dgrad_zero_classes<false>, dim3(blocks), dim3(256), 0, st, a, C8);
     MDTF_LAUNCH_CHECK();
   }
+  return 0;
+}
+
+// Side stream for the split-K slab reductions of the following weight-gradient launches (null: in line).
+MDTF_EXPORT int mdtf_set_slab_stream(hipStream_t s) {
+  g_slab_stream = s;
   return 0;
 }
 

@@ -537,6 +537,14 @@ static void ln_bwd_geometry(long long rows, int* blocks, int* rpb) {
   *blocks = static_cast<int>(ceil_div(rows, *rpb));
 }
 
+// Side stream for the gamma / beta partial reductions of the following LayerNorm backward launches (null: in line;
+// mdtf.ops.conv SLAB_SIDE): they only feed the gradient buffer, so they leave the backward chain through one event.
+static hipStream_t g_ln_red_stream = nullptr;
+MDTF_EXPORT int mdtf_set_ln_reduce_stream(hipStream_t s) {
+  g_ln_red_stream = s;
+  return 0;
+}
+
 // fp32 workspace elements mdtf_ln_bwd needs
 MDTF_EXPORT long long mdtf_ln_bwd_ws(long long rows, int H) {
   int blocks, rpb;
@@ -572,6 +580,16 @@ MDTF_EXPORT int mdtf_ln_bwd(const void* dy, const void* s, const float* gamma, c
               (uint32_t)seed, seed_off, dgamma, dbeta);
   MDTF_LAUNCH_CHECK();
   if (atomics) return 0;
+  if (g_ln_red_stream && g_ln_red_stream != st) {
+    static hipEvent_t ev = [] {
+      hipEvent_t e = nullptr;
+      (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+      return e;
+    }();
+    if (!ev || hipEventRecord(ev, st) != hipSuccess || hipStreamWaitEvent(g_ln_red_stream, ev, 0) != hipSuccess)
+      return MDTF_EUNSUPPORTED;
+    st = g_ln_red_stream;
+  }
   if (beta_first) return mdtf_reduce_partials(ws, blocks, 2 * H, dbeta, st);
   // ws rows are [dgamma(H) | dbeta(H)]: reduce as a [blocks, 2H] matrix when the
   // two outputs are adjacent, else as two strided passes

@@ -9,6 +9,7 @@ beats MIOpen, with its best tile); ``MDTF_CONV=mdtf|miopen`` forces one
 backend.  Shapes the HIP kernel cannot take (C % 8 != 0, e.g. a 3-channel
 stem) use MIOpen.
 """
+import ctypes
 import json
 import os
 
@@ -25,6 +26,7 @@ N.register("mdtf_conv_wgrad", [N.P, N.P, N.P] + [N.I] * 18 + [N.P])
 N.register("mdtf_conv_fwd_v2", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P])
 N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P, N.P, N.P, N.I, N.P, N.P, N.P])
 N.register("mdtf_conv_wgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.I, N.P])
+N.register("mdtf_set_slab_stream", [N.P])
 
 # split-K weight gradients: per-split partial slabs + one reduction pass (plain stores) instead of fp32
 # atomics into DW.  Measured on MI355X (scripts/gpu.sh envab): +0.4 % BERT-base (dense GEMM weight
@@ -634,10 +636,11 @@ def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=
                 force = bool(ent["slab"])
         slab, cap = wgrad_slab(n * dy.shape[1] * dy.shape[2], kh * kw * ci, co, bm, bn, ver, int(splits), x.device,
                                force=force)
-        N.check(N.fn("mdtf_conv_wgrad_v2")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co,
-                                           kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
-                                           _v2_code(bm, stages, ver), bn, int(splits), N.ptr(slab), cap,
-                                           N.stream_ptr()), "conv_wgrad_v2")
+        with slab_side(slab if out is not None else None):
+            N.check(N.fn("mdtf_conv_wgrad_v2")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2],
+                                               co, kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
+                                               _v2_code(bm, stages, ver), bn, int(splits), N.ptr(slab), cap,
+                                               N.stream_ptr()), "conv_wgrad_v2")
         return dw
     N.check(N.fn("mdtf_conv_wgrad")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co, kh,
                                     kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1], bm, bn, int(splits),
@@ -708,6 +711,34 @@ def _side_stream(device):
         s = torch.cuda.Stream(device=device)
         _SIDE[device] = s
     return s
+
+
+# Split-K slab reductions of weight gradients on the side stream (MDTF_SLAB_SIDE=1): the wgrad kernel stays in
+# line, only its reduction pass (10 us per ResNet-50 conv, 36 per step) forks off the dgrad -> BN-backward chain
+# into the gradient buffer, joined by join_side_streams() like the side-stream weight gradients above.
+SLAB_SIDE = os.environ.get("MDTF_SLAB_SIDE", "0") == "1"
+
+
+class slab_side:
+    """Context for one native launch whose partial-sum reduction (a weight gradient's split-K slab, a LayerNorm's
+    gamma / beta block partials in ``ws``) goes to the side stream; ``setter`` names the native stream hook."""
+
+    def __init__(self, slab, setter="mdtf_set_slab_stream"):
+        self.slab = slab if (SLAB_SIDE and slab is not None and slab.is_cuda) else None
+        self.setter = setter
+
+    def __enter__(self):
+        if self.slab is not None:
+            self.side = _side_stream(self.slab.device)
+            N.fn(self.setter)(ctypes.c_void_p(self.side.cuda_stream))
+        return self
+
+    def __exit__(self, *exc):
+        if self.slab is not None:
+            N.fn(self.setter)(None)
+            self.slab.record_stream(self.side)      # read by the side stream's reduction
+            _PENDING.add(self.slab.device)
+        return False
 
 
 def join_side_streams():

@@ -16,6 +16,7 @@ from ..train import variables as V
 N.register("mdtf_ln_fwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.F, N.F, N.U, N.P, N.P])
 N.register("mdtf_ln_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.F, N.U, N.P, N.P])
 N.register("mdtf_ln_bwd_ws", [N.L, N.I], restype=N.L)
+N.register("mdtf_set_ln_reduce_stream", [N.P])
 N.register("mdtf_softmax_fwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.L, N.P])
 N.register("mdtf_softmax_bwd", [N.P, N.P, N.P, N.L, N.I, N.F, N.P])
 N.register("mdtf_embed_fwd", [N.P, N.P, N.P, N.L, N.I, N.L, N.P])
@@ -105,10 +106,14 @@ class _LayerNorm(torch.autograd.Function):
         dg = sg.grad if sg is not None else torch.zeros(H, dtype=torch.float32, device=s.device)
         db = sb.grad if sb is not None else torch.zeros(H, dtype=torch.float32, device=s.device)
         ws = torch.empty(N.fn("mdtf_ln_bwd_ws")(rows, H), dtype=torch.float32, device=s.device)
-        N.check(N.fn("mdtf_ln_bwd")(N.ptr(dy), N.ptr(s), N.ptr(g), N.ptr(mean), N.ptr(rstd), N.ptr(ds), N.ptr(dxb),
-                                    N.ptr(dg), N.ptr(db), N.ptr(ws), rows, H, p_drop, seed,
-                                    N.ptr(_seed_off(p_drop, s.device)), N.stream_ptr()),
-                "ln_bwd")
+        from . import conv as _conv
+        # gamma / beta in grad slots (read after the join at the end of backward): the partial reduction may leave
+        # the chain on the side stream (MDTF_SLAB_SIDE)
+        with _conv.slab_side(ws if (sg is not None and sb is not None) else None, "mdtf_set_ln_reduce_stream"):
+            N.check(N.fn("mdtf_ln_bwd")(N.ptr(dy), N.ptr(s), N.ptr(g), N.ptr(mean), N.ptr(rstd), N.ptr(ds),
+                                        N.ptr(dxb), N.ptr(dg), N.ptr(db), N.ptr(ws), rows, H, p_drop, seed,
+                                        N.ptr(_seed_off(p_drop, s.device)), N.stream_ptr()),
+                    "ln_bwd")
         gamma, beta = ctx.like
         rg = V.grad_marker(gamma) if sg is not None else dg
         rb = V.grad_marker(beta) if sb is not None else db
