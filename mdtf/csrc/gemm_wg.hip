@@ -50,6 +50,7 @@ struct WgArgs {
   // sequence (tile t owns [t KT, (t + 1) KT)), so every worker does the same work whatever tiles x splits is;
   // the pieces of a tile (at most maxp) are summed by its last arriver as the splits are
   int sk_q, kt_total, maxp;
+  int wt;                    // slab publish form: 1 write-through (sc1) stores / loads, 0 plain + agent fences
 };
 
 __device__ __forceinline__ void dma16(i32x4_t rsrc, unsigned lds_addr, unsigned voff, int soff) {
@@ -242,31 +243,53 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
       for (int e = 0; e < 4; ++e) unsafeAtomicAdd(db + 16 * j + e, accb[j][e]);
   }
   if (np > 1) {
-    float4v* sl = reinterpret_cast<float4v*>(a.slab) + ((long long)tile * a.maxp + pidx) * (BM * BN / 4);
+    // this tile's slabs: [maxp][BM * BN] fp32, addressed through one buffer resource (byte offsets < 2 MiB)
+    float* tslab = a.slab + (long long)tile * a.maxp * (BM * BN);
+    const __amdgpu_buffer_rsrc_t srs =
+        __builtin_amdgcn_make_buffer_rsrc(tslab, (short)0, a.maxp * (BM * BN) * 4, 0x00020000);
+    // Publish form (a.wt): write-through.  Every slab byte is stored sc1 (16-B buffer stores, aux 16), every storing
+    // wave drains its stores, the workgroup barrier orders them before the one ticket add, and the last arriver
+    // reads every slab with sc1 buffer loads (L1 bypassed) -- no L2 write-back (release) or L1 invalidate
+    // (acquire) fence (MI355X_MICROARCH.md, publish-large: 3.0 vs 8.2 us for 64 KiB per workgroup).  a.wt = 0:
+    // plain stores + agent release / acquire fences.
+    const int sl0 = pidx * (BM * BN / 4);
+    if (a.wt) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) sl[(i * 4 + j) * NT + tid] = acc[i][j];
-    // publish: the slab stores complete, then one release + ticket for the workgroup
+        for (int j = 0; j < 4; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, acc[i][j]), srs,
+                                                 (sl0 + (i * 4 + j) * NT + tid) * 16, 0, 16);
+    } else {
+      float4v* sl = reinterpret_cast<float4v*>(tslab) + sl0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sl[(i * 4 + j) * NT + tid] = acc[i][j];
+    }
+    // publish: the slab stores complete, then one ticket for the workgroup
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* flag = reinterpret_cast<int*>(smem);
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!a.wt) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       const int prev = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = prev == np - 1;
       if (last) {
         __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!a.wt) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
       }
       *flag = last;
     }
     __syncthreads();
     if (!*flag) return;
     // the last arriver: sum the slabs in split order (deterministic), own partial from registers
-    const float4v* s0 = reinterpret_cast<const float4v*>(a.slab) + (long long)tile * a.maxp * (BM * BN / 4);
     float4v sum[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -279,12 +302,16 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) sum[i][j] += acc[i][j];
       } else {
-        const float4v* sp = s0 + (long long)s * (BM * BN / 4) + tid;
+        const int so = s * (BM * BN / 4) + tid;
         float4v p[4][4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) p[i][j] = sp[(i * 4 + j) * NT];
+          for (int j = 0; j < 4; ++j) {
+            const int off = (so + (i * 4 + j) * NT) * 16;
+            p[i][j] = __builtin_bit_cast(float4v, a.wt ? __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, 16)
+                                                       : __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, 0));
+          }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -426,6 +453,14 @@ MDTF_EXPORT int mdtf_gemm_wg(const bf16_t* A, long long lda, const bf16_t* B, lo
   a.ldc = ldc;
   a.slab = slab;
   a.cnt = cnt;
+  {   // MDTF_WG_WT=0: plain slab stores + agent release / acquire fences (the round-3..5 publish form)
+    static const int wt = [] {
+      const char* e = getenv("MDTF_WG_WT");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
+    a.wt = wt;
+  }
+  if (a.slab && (long long)a.maxp * bm * 128 * 4 >= (1ll << 31)) return MDTF_EUNSUPPORTED;
   // L2 block per XCD: ~ceil(grid / 8) tiles of one split as the gm x gn block with the fewest operand columns
   // (gm * bm + gn * 128) -- a speed choice only, any gm / gn is correct
   {
