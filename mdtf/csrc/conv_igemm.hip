@@ -85,6 +85,8 @@ struct ConvArgs {
   float* slab;
   int slab_cap;          // splits the slab has room for
   int slab_nt;           // partials with nontemporal stores, summed with nontemporal loads (MDTF_SLAB_NT=0: cached)
+  int* cnt;              // non-null: split-K partials summed in the kernel by each tile's last arriving workgroup
+                         // (slab = [tiles][splits][BM * BN], write-through; cnt = per-tile tickets, left zeroed)
   int wg_xcd;            // wgrad v2: XCD-aware block order (the row/col tiles of one pixel split share an L2)
   // dense forward (fd v2 MODE 3): Y[M][Ncol] = act(X[M][K] W + bias), W N-contiguous [K][ld_b] read as
   // [64 k][64 col] half-images by transposed fragment reads (no transposed weight copy).  The columns are
@@ -2033,6 +2035,75 @@ __global__ void __launch_bounds__(64 * NW, (wgrad_min_waves<BM, BN, STAGES, NW>(
       if (co < a.Cout) atomicAdd(a.dbias + co, accb[j][0]);
     }
   }
+  if (a.slab && a.cnt) {
+    // In-kernel split-K reduction.  Each split stores its partial tile write-through (16-B sc1 buffer stores,
+    // aux 16) into the tile's slab region, drains its stores, and takes one ticket per workgroup after the
+    // barrier; the workgroup whose add comes last (told by the returned value) sums every split in split order
+    // with sc1 loads (deterministic whatever the arrival order) and adds the sum into DW once -- no reduction
+    // launch, no agent fences (MI355X_MICROARCH.md: publish-large, Valid forms row 1; gemm_wg.hip, +2 % BERT).
+    constexpr int NT = 64 * NW;
+    const int nsp = static_cast<int>(gridDim.x) / tiles_mn;   // every split is non-empty (launch_wgrad_v2)
+    float* tslab = a.slab + (long long)tile * nsp * (BM * BN);
+    const __amdgpu_buffer_rsrc_t srs =
+        __builtin_amdgcn_make_buffer_rsrc(tslab, (short)0, nsp * (BM * BN) * 4, 0x00020000);
+    const int sb = split * (TM * TN);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, acc[i][j]), srs,
+                                               ((sb + i * TN + j) * NT + tid) * 16, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem_raw);
+    if (tid == 0) {
+      const int prev = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == nsp - 1;
+      if (last) __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    float4v sum[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) sum[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < nsp; ++s) {              // workgroup-uniform: all TM * TN loads of a split in flight
+      if (s == split) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) sum[i][j] += acc[i][j];
+      } else {
+        float4v p[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            p[i][j] = __builtin_bit_cast(
+                float4v, __builtin_amdgcn_raw_buffer_load_b128(srs, ((s * (TM * TN) + i * TN + j) * NT + tid) * 16,
+                                                               0, 16));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) sum[i][j] += p[i][j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int co = n0 + wn * (TN * 16) + j * 16 + li;
+        if (co >= a.Cout) continue;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int r = r0 + wm * (TM * 16) + i * 16 + 4 * g + rr;
+          if (r < R) a.dw[(long long)r * a.ld_dw + co] += sum[i][j][rr];
+        }
+      }
+    return;
+  }
   float* slab = a.slab ? a.slab + (long long)split * R * a.Cout : nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -2160,6 +2231,10 @@ __global__ void __launch_bounds__(256) wgrad_slab_reduce(const float* __restrict
 // leave the dgrad -> BN-backward chain.  The side stream waits for the weight-gradient kernel through one event
 // (captured hipGraphs turn it into a fork edge); the caller joins the side stream before the gradients are read.
 hipStream_t g_slab_stream = nullptr;
+// Per-tile ticket buffer (zeroed ints, n of them) for in-kernel split-K reductions of the following weight-gradient
+// launches (mdtf_set_wgrad_tickets); null: slab + reduction launch.
+int* g_wg_cnt = nullptr;
+long long g_wg_cnt_n = 0;
 hipEvent_t slab_event() {
   static hipEvent_t ev = [] {
     hipEvent_t e = nullptr;
@@ -2187,6 +2262,13 @@ int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
   if (lds > 160 * 1024) return MDTF_EUNSUPPORTED;
   ConvArgs b = a;
   if (a.slab && (splits < 2 || splits > a.slab_cap || (a.ld_dw % 4) || (a.Cout % 4))) b.slab = nullptr;
+  // in-kernel reduction: the slab (>= splits * R * Cout floats, the caller pads to 256-multiples of R and Cout) holds
+  // tiles * splits * BM * BN floats whenever BM, BN divide 256; tickets for every tile
+  b.cnt = nullptr;
+  if (b.slab && g_wg_cnt && g_wg_cnt_n >= (long long)a.mtiles * a.ntiles && 256 % BM == 0 && 256 % BN == 0 &&
+      (long long)splits * BM * BN * a.mtiles * a.ntiles * 4 < (1ll << 31) &&
+      (long long)a.mtiles * BM <= ceil_div(R, 256) * 256 && (long long)a.ntiles * BN <= ceil_div(a.Cout, 256) * 256)
+    b.cnt = g_wg_cnt;
   {
     static const int nt = [] {
       const char* e = getenv("MDTF_SLAB_NT");
@@ -2197,7 +2279,7 @@ int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
   hipLaunchKernelGGL((conv_wgrad_v2<BM, BN, STAGES, NW, PIPE>), dim3(a.mtiles * a.ntiles * splits), dim3(64 * NW), lds,
                      st, b);
   MDTF_LAUNCH_CHECK();
-  if (b.slab) {
+  if (b.slab && !b.cnt) {
     if (g_slab_stream && g_slab_stream != st) {
       hipEvent_t ev = slab_event();
       if (!ev || hipEventRecord(ev, st) != hipSuccess || hipStreamWaitEvent(g_slab_stream, ev, 0) != hipSuccess)
@@ -2577,6 +2659,13 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
       hipLaunchKernelGGL(dgrad_zero_classes<false>, dim3(blocks), dim3(256), 0, st, a, C8);
     MDTF_LAUNCH_CHECK();
   }
+  return 0;
+}
+
+// Tickets for in-kernel split-K reductions of the following v2 weight-gradient launches (null / n = 0: off).
+MDTF_EXPORT int mdtf_set_wgrad_tickets(int* cnt, long long n) {
+  g_wg_cnt = cnt;
+  g_wg_cnt_n = cnt ? n : 0;
   return 0;
 }
 

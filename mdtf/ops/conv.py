@@ -57,7 +57,40 @@ def wgrad_slab(M, R, Cout, bm, bn, ver, splits, device, dense=False, force=None)
     sp = wgrad_splits(M, R, Cout, bm, bn, ver, splits)
     if sp < 2:
         return None, 0
+    if WGRAD_INK:     # in-kernel reduction: [tiles][splits][BM * BN] partial tiles, tiles padded to 256 multiples
+        return torch.empty(sp * (-(-R // 256) * 256) * (-(-Cout // 256) * 256), dtype=torch.float32,
+                           device=device), sp
     return torch.empty(sp * R * Cout, dtype=torch.float32, device=device), sp
+
+
+# MDTF_WGRAD_INK=1: split-K weight gradients summed inside the kernel by each tile's last arriving workgroup
+# (write-through partial tiles + one ticket per workgroup, csrc/conv_igemm.hip) instead of slab stores + a
+# wgrad_slab_reduce launch.  Correct, but -12.5 % ResNet-50 / -1.3 % BERT in the step (profiles/ab_r6.md): one
+# workgroup per tile reads the other splits' partial tiles at ~100 GB/s (a serial tail of several us per tile, 8-128
+# splits), where the reduction launch spreads the same bytes over every CU.  Off.
+WGRAD_INK = os.environ.get("MDTF_WGRAD_INK", "0") == "1"
+N.register("mdtf_set_wgrad_tickets", [N.P, N.L])
+
+
+class wgrad_tickets:
+    """Context for one native v2 weight-gradient launch with a slab: hands it this stream's zeroed per-tile tickets
+    (``ops.mm._tickets``: one buffer per (device, stream), every launch leaves its tickets at zero)."""
+
+    def __init__(self, slab):
+        self.on = WGRAD_INK and slab is not None and slab.is_cuda
+        self.device = slab.device if self.on else None
+
+    def __enter__(self):
+        if self.on:
+            from . import mm
+            t = mm._tickets(self.device, 4096)
+            N.fn("mdtf_set_wgrad_tickets")(N.ptr(t), t.numel())
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            N.fn("mdtf_set_wgrad_tickets")(None, 0)
+        return False
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 TUNED_BATCH = 256        # the batch bench/conv_autotune.py tuned conv_table.json at
@@ -636,7 +669,7 @@ def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=
                 force = bool(ent["slab"])
         slab, cap = wgrad_slab(n * dy.shape[1] * dy.shape[2], kh * kw * ci, co, bm, bn, ver, int(splits), x.device,
                                force=force)
-        with slab_side(slab if out is not None else None):
+        with slab_side(slab if out is not None else None), wgrad_tickets(slab):
             N.check(N.fn("mdtf_conv_wgrad_v2")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2],
                                                co, kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
                                                _v2_code(bm, stages, ver), bn, int(splits), N.ptr(slab), cap,

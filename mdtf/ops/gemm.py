@@ -177,7 +177,7 @@ def wgrad_into(out, x, d, dbias=None):
         from . import conv as C
         slab, cap = C.wgrad_slab(M, K, Nn, bm, bn, 2, splits, x.device, dense=True) if use_slab else (None, 0)
         fuse = dbias is not None and FUSED_BIAS_GRAD and dbias.is_contiguous() and dbias.dtype == torch.float32
-        with C.slab_side(slab):      # callers pass grad slots: the slab reduction may leave the chain
+        with C.slab_side(slab), C.wgrad_tickets(slab):   # grad slots: the slab reduction may leave the chain
             rc = N.fn("mdtf_gemm_wgrad")(N.ptr(x), N.ptr(d), N.ptr(out), M, K, Nn, d.stride(0), out.stride(0), bm, bn,
                                          2, splits, N.ptr(slab), cap, N.ptr(dbias) if fuse else None, N.stream_ptr())
         if rc == 0:

@@ -1758,6 +1758,41 @@ def test_conv_wgrad_slab_split_groups(splits, monkeypatch):
     assert _rel(dw, ref) < 1e-2
 
 
+@pytest.mark.parametrize("ink", [True, False])
+@pytest.mark.parametrize("geo", [(2, 14, 14, 64, 3, 128, 128, 256, 2, 3, 5),    # R = 576: partial 128-row tiles
+                                 (2, 28, 28, 128, 1, 256, 256, 128, 2, 3, 7),
+                                 (4, 7, 7, 256, 3, 64, 256, 64, 3, 3, 3),        # skinny 8-wave tile, Cout 64
+                                 (2, 16, 16, 64, 1, 192, 128, 128, 2, 3, 4),     # Cout 192: partial column tile
+                                 (2, 20, 20, 128, 3, 64, 128, 64, 2, 2, 6)])     # 4-wave tile
+def test_conv_wgrad_inkernel_split_reduction(ink, geo, monkeypatch):
+    """Split-K weight gradient summed in the kernel by each tile's last arriving workgroup (write-through partial
+    tiles + tickets, MDTF_WGRAD_INK) vs the slab + reduction launch, both vs the fp32 autograd reference; the
+    result accumulates into a non-zero gradient slot, and the tickets are left zeroed (a second launch agrees)."""
+    from mdtf.ops import conv as C
+    from mdtf.ops import mm
+    monkeypatch.setattr(C, "WGRAD_SLAB", True)
+    monkeypatch.setattr(C, "WGRAD_INK", ink)
+    n, h, w, c, k, co, bm, bn, stages, ver, splits = geo
+    torch.manual_seed(sum(geo))
+    p = k // 2
+    x = torch.randn(n, h, w, c).bfloat16()
+    wt = (torch.randn(k, k, c, co) / (k * k * c) ** 0.5).bfloat16()
+    wr = wt.float().permute(3, 2, 0, 1).requires_grad_(True)
+    yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wr, padding=p)
+    dy = torch.randn(yr.shape).bfloat16()
+    yr.backward(dy.float())
+    ref = wr.grad.permute(2, 3, 1, 0)
+    base = torch.randn(k, k, c, co)
+    xd, dyd = x.to(DEV), dy.permute(0, 2, 3, 1).contiguous().to(DEV)
+    for rep in range(2):
+        out = base.to(DEV).clone()
+        C.mdtf_wgrad(xd, dyd, wt.shape, (1, 1), (p, p, p, p), (1, 1), bm, bn, splits, out=out, ver=ver,
+                     stages=stages)
+        assert _rel(out.cpu() - base, ref) < 1e-2, rep
+    t = mm._tickets(torch.device(DEV), 4096)
+    assert int(t.abs().sum()) == 0
+
+
 WS_TILES = [(4, 8, 1, 4), (4, 8, 2, 6), (4, 4, 1, 4), (2, 8, 1, 8), (2, 4, 2, 4), (4, 8, 4, 4)]
 
 
