@@ -51,6 +51,7 @@ struct WgArgs {
   // the pieces of a tile (at most maxp) are summed by its last arriver as the splits are
   int sk_q, kt_total, maxp;
   int wt;                    // slab publish form: 1 write-through (sc1) stores / loads, 0 plain + agent fences
+  int store_mask;            // bit s: segment s's C is overwritten (first writer of an unzeroed slot), else +=
 };
 
 __device__ __forceinline__ void dma16(i32x4_t rsrc, unsigned lds_addr, unsigned voff, int soff) {
@@ -323,6 +324,16 @@ __global__ void __launch_bounds__(2 * BM) gemm_wg_kernel(WgArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = sum[i][j];
   }
+  if ((a.store_mask >> seg) & 1) {      // the step's only write into this slot: store, nothing to read
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float* crow = cf + (long long)(rbase + 16 * i) * a.ldc + cseg;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<float4*>(crow + 16 * j) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float* crow = cf + (long long)(rbase + 16 * i) * a.ldc + cseg;
@@ -404,11 +415,12 @@ MDTF_EXPORT long long mdtf_gemm_wg_slab_floats_k(int M, int N, int K, int bm, in
 // C_s[M][seg_cols] (fp32, ldc) += A^T B over the segment's columns; A [K][lda], B [K][ldb] bf16 (k-major), M % bm,
 // N % 128, K % 64 and seg_cols % 128 == 0.  bm: 128 or 256; stages 2..4 (negative: the pipelined loop); splits: K-split count (clamped so every
 // split has at least one 64-deep tile), or -G: stream-K over G workers (every worker the same number of K-tiles).  dbias (per segment, may be null): += column sums of B.  slab / cnt:
-// workspace of mdtf_gemm_wg_slab_floats() floats and tiles zeroed ints (splits > 1).  Returns the splits used
+// workspace of mdtf_gemm_wg_slab_floats() floats and tiles zeroed ints (splits > 1).  store_mask bit s: segment s's
+// C is overwritten instead of accumulated into (the step's only write of a slot that was not zeroed).  Returns the splits used
 // (> 0) or a negative MDTF status.
 MDTF_EXPORT int mdtf_gemm_wg(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                              int nseg, int seg_cols, float* const* cseg, long long ldc, float* const* dbseg, int bm,
-                             int stages, int splits, float* slab, int* cnt, void* stream) {
+                             int stages, int splits, float* slab, int* cnt, int store_mask, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 128 || (bm != 128 && bm != 256) || M % bm) return MDTF_EUNSUPPORTED;
   if (lda % 8 || ldb % 8 || ldc % 4 || nseg < 1 || nseg > 4 || seg_cols % 128 || nseg * seg_cols != N)
     return MDTF_EUNSUPPORTED;
@@ -453,6 +465,7 @@ MDTF_EXPORT int mdtf_gemm_wg(const bf16_t* A, long long lda, const bf16_t* B, lo
   a.ldc = ldc;
   a.slab = slab;
   a.cnt = cnt;
+  a.store_mask = store_mask;
   {   // MDTF_WG_WT=0: plain slab stores + agent release / acquire fences (the round-3..5 publish form)
     static const int wt = [] {
       const char* e = getenv("MDTF_WG_WT");

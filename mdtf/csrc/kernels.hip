@@ -701,7 +701,58 @@ __global__ void __launch_bounds__(256) mask_mul_kernel(const uint4* __restrict__
   store_bf8(reinterpret_cast<bf16_t*>(out + i), f);
 }
 
+// Zero the nr float ranges of a buffer in one launch (a gradient buffer whose store-written slots are skipped):
+// rg = [nr][2] (start, length) in elements, ascending, disjoint; each block owns 4096 elements of the
+// concatenation of the ranges; rows = {prefix of lengths} staged in LDS, one binary search per 4-element group.
+constexpr int kFillMaxRanges = 1024;
+__global__ void __launch_bounds__(256) fill_ranges_kernel(float* __restrict__ base, const long long* __restrict__ rg,
+                                                          int nr, long long total) {
+  __shared__ long long pre[kFillMaxRanges + 1];
+  __shared__ long long st[kFillMaxRanges];
+  // prefix sums: every thread loads starts / lengths in parallel; thread 0 scans them in LDS (nr is small)
+  for (int r = threadIdx.x; r < nr; r += 256) {
+    st[r] = rg[2 * r];
+    pre[r + 1] = rg[2 * r + 1];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    pre[0] = 0;
+    for (int r = 0; r < nr; ++r) pre[r + 1] += pre[r];
+  }
+  __syncthreads();
+  const long long e0 = (long long)blockIdx.x * 4096;
+  for (int q = threadIdx.x; q < 1024; q += 256) {
+    const long long e = e0 + 4LL * q;
+    if (e >= total) break;
+    int lo = 0, hi = nr - 1;               // largest r with pre[r] <= e
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    long long p = st[lo] + (e - pre[lo]);
+    const long long left = pre[lo + 1] - e;   // elements left in this range
+    if (left >= 4 && (p & 3) == 0) {
+      *reinterpret_cast<float4*>(base + p) = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      int r = lo;
+      for (int k = 0; k < 4 && e + k < total; ++k) {
+        while (e + k >= pre[r + 1]) ++r;
+        base[st[r] + (e + k - pre[r])] = 0.f;
+      }
+    }
+  }
+}
+
 }  // namespace
+
+MDTF_EXPORT int mdtf_fill_ranges_zero(float* base, const long long* ranges, int nr, long long total, hipStream_t st) {
+  if (nr <= 0 || total <= 0) return 0;
+  if (nr > kFillMaxRanges) return MDTF_EUNSUPPORTED;
+  hipLaunchKernelGGL(fill_ranges_kernel, dim3((unsigned)ceil_div(total, 4096)), dim3(256), 0, st, base, ranges, nr,
+                     total);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
 
 // ============================================================== exports
 MDTF_EXPORT int mdtf_bias_act_fwd(const void* x, const float* bias, void* y, void* pre, long long M, int C, int act,

@@ -82,7 +82,13 @@ def _wg_backward(ctx, x, dpre):
     if not (x.dim() == 2 and x.dtype == torch.bfloat16 and dpre.dtype == torch.bfloat16 and _wg_ok(x, dpre)):
         return False
     fuse_b = ctx.has_b and not N.deterministic()
-    if not mm.wg_into([sk.grad for sk in ctx.wsinks], x, dpre, dbs=[sk.grad for sk in ctx.bsinks] if fuse_b else None):
+    # a slot this launch is the step's only writer of is overwritten (V.claim_store: no zero fill, no C read)
+    store = [V.claim_store(sk) for sk in ctx.wsinks]
+    if not mm.wg_into([sk.grad for sk in ctx.wsinks], x, dpre, dbs=[sk.grad for sk in ctx.bsinks] if fuse_b else None,
+                      store=store):
+        for sk, st in zip(ctx.wsinks, store):
+            if st:                         # not launched: the fallback accumulates into a zeroed slot
+                V.unclaim_store(sk)
         return False
     if ctx.has_b and not fuse_b:
         col = 0

@@ -154,7 +154,7 @@ def wgrad_into(gws, x, dy, dbs=None, tile=None, splits=None):
 # Weight-gradient kernel (csrc/gemm_wg.hip): C_s (fp32) += x^T dy[:, seg s], both operands k-major, split-K
 # partials reduced by the last arriving workgroup of each tile (no fp32 atomics on C, deterministic order).
 N.register("mdtf_gemm_wg", [N.P, N.L, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.P, N.L, N.P, N.I, N.I, N.I, N.P, N.P,
-                            N.P])
+                            N.I, N.P])
 N.register("mdtf_gemm_wg_slab_floats", [N.I, N.I, N.I, N.I], N.L)
 N.register("mdtf_gemm_wg_slab_floats_k", [N.I, N.I, N.I, N.I, N.I], N.L)
 # stream-K weight gradients (MDTF_WG_SK=1): every CU runs the same number of K-tiles, cut at tile boundaries,
@@ -204,10 +204,11 @@ def wg_pick(M, Nn, K):
     return bm, (3 if bm == 256 else 2), max(1, min(kt // 16, CUS // tiles))
 
 
-def wg_into(gws, x, dy, dbs=None, bm=None, stages=None, splits=None):
+def wg_into(gws, x, dy, dbs=None, bm=None, stages=None, splits=None, store=None):
     """gws[s] [K, Ns] fp32 += x^T @ dy[:, segment s] on the weight-gradient kernel.  x [T, K], dy [T, sum Ns]
     bf16 with unit column stride (dy may be a column slice); dbs: fp32 [Ns] slots that also receive the column
-    sums of dy (the bias gradients).  Returns False when the kernel does not take the shape."""
+    sums of dy (the bias gradients); store[s] true: gws[s] = instead of += (the step's only write of that slot).
+    Returns False when the kernel does not take the shape."""
     gws = gws if isinstance(gws, (list, tuple)) else [gws]
     T, Kin = x.shape
     Nn = dy.shape[1]
@@ -227,7 +228,8 @@ def wg_into(gws, x, dy, dbs=None, bm=None, stages=None, splits=None):
     rc = N.fn("mdtf_gemm_wg")(N.ptr(x), x.stride(0), N.ptr(dy), dy.stride(0), Kin, Nn, T, len(gws), ns,
                               ctypes.cast(_arr(gws), ctypes.c_void_p), gws[0].stride(0),
                               ctypes.cast(_arr(dbs), ctypes.c_void_p) if dbs else None, bm, stages, splits,
-                              N.ptr(slab), N.ptr(cnt), N.stream_ptr())
+                              N.ptr(slab), N.ptr(cnt), sum(1 << i for i, st in enumerate(store or ()) if st),
+                              N.stream_ptr())
     if rc == -2:
         return False
     N.check(min(rc, 0), "gemm_wg")

@@ -122,8 +122,41 @@ class FlatGroup(object):
             self.state[key] = torch.zeros(numel or self.numel, dtype=torch.float32, device=self.device)
         return self.state[key]
 
-    def zero_grad(self):
-        self.grad.zero_()
+    def zero_grad(self, skip_stored=False):
+        """Zero the gradient buffer.  ``skip_stored``: leave out the slots whose first write of the previous step
+        was a store (``variables.claim_store``; this step's writer overwrites them again) -- one fill launch over
+        the remaining ranges."""
+        skips = []
+        for v in self.variables:
+            v.skip_zero = bool(skip_stored and getattr(v, "store_first", False))
+            if v.skip_zero:
+                skips.append((v.flat_offset, v.numel()))
+        if not skips:
+            self.grad.zero_()
+            return
+        key = tuple(skips)
+        cached = getattr(self, "_fill_ranges", None)
+        if cached is None or cached[0] != key:
+            ranges, pos = [], 0
+            for o, n in sorted(skips):
+                if o > pos:
+                    ranges.append((pos, o - pos))
+                pos = max(pos, o + n)
+            if pos < self.numel:
+                ranges.append((pos, self.numel - pos))
+            total = sum(n for _, n in ranges)
+            rt = torch.tensor([x for r in ranges for x in r], dtype=torch.int64).to(self.grad.device)
+            cached = self._fill_ranges = (key, ranges, rt, total)
+        _, ranges, rt, total = cached
+        if self.grad.is_cuda and ranges:
+            from ..ops import _native as N
+            if "mdtf_fill_ranges_zero" not in N.SIGNATURES:
+                N.register("mdtf_fill_ranges_zero", [N.P, N.P, N.I, N.L, N.P])
+            N.check(N.fn("mdtf_fill_ranges_zero")(N.ptr(self.grad), N.ptr(rt), len(ranges), total,
+                                                   N.stream_ptr(self.grad.device)), "fill_ranges_zero")
+        else:
+            for o, n in ranges:
+                self.grad[o:o + n].zero_()
 
     def refresh_shadow(self):
         if self.shadow is not None:
@@ -149,9 +182,9 @@ class FlatParamSpace(object):
     def buckets(self):
         return [b for g in self.groups for b in g.buckets]
 
-    def zero_grad(self):
+    def zero_grad(self, skip_stored=False):
         for g in self.groups:
-            g.zero_grad()
+            g.zero_grad(skip_stored)
 
     def refresh_shadows(self):
         for g in self.groups:

@@ -55,6 +55,7 @@ import os
 
 import torch
 import torch.distributed as dist
+from ..train import variables as V
 
 
 
@@ -225,16 +226,17 @@ class GradReducer(object):
 
     def begin_step(self):
         dev = self.space.device
+        V.begin_grad_epoch()               # store-first slots: a new step's first writes (train/variables.py)
         if self.ZERO_SIDE and dev is not None and torch.device(dev).type == "cuda":
             if getattr(self, "_zero_stream", None) is None:
                 self._zero_stream = torch.cuda.Stream(dev)
             zs = self._zero_stream
             zs.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(zs):
-                self.space.zero_grad()
+                self.space.zero_grad(skip_stored=True)
             self._zero_pending = zs
         else:
-            self.space.zero_grad()
+            self.space.zero_grad(skip_stored=True)
         for v in self.space.variables:
             v.uses = 0
         for b in self.space.buckets:
@@ -525,6 +527,7 @@ class GradReducer(object):
         from ..ops import conv as _conv
         self.join_zero()
         _conv.join_side_streams()          # every weight gradient is in the flat buffer
+        V.unclaimed_skips(self.space.variables)   # skipped slots no kernel wrote this step hold stale sums
         if self.backup_device:
             self.contributed = self._backup_mask_device(step)  # device 0/1 (read only when someone asks)
             self.num_contributors = self.R

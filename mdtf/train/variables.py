@@ -21,6 +21,7 @@ gradient reducer, so bucketed RCCL all-reduces start while backward is still
 running (see ``mdtf/parallel/reducer.py``).
 """
 import collections
+import os
 import contextlib
 import math
 import re
@@ -225,6 +226,7 @@ class _VarRead(torch.autograd.Function):
         if var.grad is None:
             var.grad = torch.zeros_like(var.master)
         if not _is_marker(g):             # a sink-only gradient was already accumulated in place
+            note_accumulate(var)
             var.grad.add_(g)              # one kernel, dtype promotion included
         grad_done(var)
         return None, None, None
@@ -264,6 +266,58 @@ def grad_sink(t):
     if var is None or var.grad is None or var.grad.dtype != torch.float32 or not var.grad.is_contiguous():
         return None
     return var
+
+
+# Store-first gradient slots (MDTF_GRAD_STORE_FIRST, on by default): a weight-gradient kernel that is the step's
+# ONLY writer of a slot (first write of the step, the variable's only use in flight) overwrites it instead of
+# accumulating.  A variable whose first write of a step was such a store is not zeroed at the start of the next
+# step (parallel/flat.py skips its range in the one zero-fill launch), which removes its share of the gradient
+# buffer fill and the read of C in the kernel's epilogue.  Safety nets: any other first write into a skipped slot
+# zeroes it first (note_accumulate, _VarRead.backward), and a skipped slot nobody wrote in a step is zeroed at the
+# end of backward (unclaimed_skips).
+GRAD_EPOCH = [0]
+STORE_FIRST = os.environ.get("MDTF_GRAD_STORE_FIRST", "1") != "0"
+
+
+def begin_grad_epoch():
+    GRAD_EPOCH[0] += 1
+
+
+def claim_store(var):
+    """True when the caller's kernel may overwrite ``var.grad`` (it is the step's only write); records it."""
+    if var is None or getattr(var, "written_epoch", -1) == GRAD_EPOCH[0]:
+        return False
+    if not STORE_FIRST or var.uses != 1:
+        note_accumulate(var)
+        return False
+    var.written_epoch = GRAD_EPOCH[0]
+    var.store_first = True
+    return True
+
+
+def unclaim_store(var):
+    """Undo claim_store() when the kernel did not run: the fallback's accumulation needs a zeroed slot."""
+    var.written_epoch = -1
+    var.store_first = False
+    note_accumulate(var)
+
+
+def note_accumulate(var):
+    """An accumulating write into ``var.grad``: the first one of the step zeroes a slot the fill skipped."""
+    if var is None or getattr(var, "written_epoch", -1) == GRAD_EPOCH[0]:
+        return
+    var.written_epoch = GRAD_EPOCH[0]
+    var.store_first = False
+    if getattr(var, "skip_zero", False) and var.grad is not None:
+        var.grad.zero_()
+
+
+def unclaimed_skips(variables):
+    """Skipped (not zeroed) slots nobody wrote this step: zero them (their gradient is 0) and stop skipping."""
+    for v in variables:
+        if getattr(v, "skip_zero", False) and getattr(v, "written_epoch", -1) != GRAD_EPOCH[0]:
+            v.grad.zero_()
+            v.store_first = False
 
 
 def grad_done(var):

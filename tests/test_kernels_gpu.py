@@ -801,6 +801,67 @@ def test_bert_tiny_train_step_gpu():
     assert ls[-1] < 0.5 * ls[0], ls
 
 
+def test_grad_store_first_matches_zero_and_accumulate(monkeypatch):
+    """Store-first gradient slots (train/variables.py claim_store, parallel/flat.py zero_grad(skip_stored)): the
+    weight-gradient kernel overwrites the slots it is the only writer of, and those slots are left out of the next
+    step's zero fill (one multi-range fill launch).  Tiny BERT over 4096 tokens so the dense weight gradients run on
+    csrc/gemm_wg.hip: losses and final gradients equal the zero-then-accumulate path."""
+    import mdtf
+    from mdtf.models import Bert, BertPretrainingLoss, SyntheticBertLoader
+    from mdtf.runtime import Net, Tower
+    from mdtf.train import step as S
+    from mdtf.train import variables as V
+    monkeypatch.setenv("MDTF_WG_SQUARE", "1")          # the tiny widths on the weight-gradient kernel
+    runs = {}
+    for on in (True, False):
+        monkeypatch.setattr(V, "STORE_FIRST", on)
+        V.reset_default_graph()
+        S.reset()
+        store = V.get_store()
+        store.device = torch.device(DEV)
+        store.compute_dtype = torch.bfloat16
+        store.generator.manual_seed(7)
+        ld = SyntheticBertLoader(seq_len=32, max_predictions=5, vocab=512, seed=3)
+        ld.batch_size = 128
+        raw, gt = ld.load_train_batch()
+        opt = mdtf.train.GradientDescentOptimizer(0.05)
+        tg = []
+        t = Tower(Net(Bert("tiny", vocab_size=512, seq_len=32, max_predictions=5, dropout=0.0)), "tower_0/", tg, raw,
+                  gt, BertPretrainingLoss(5), opt, batch_size=128)
+        _, loss, _ = t.process()
+        op = opt.apply_gradients(Tower.average_gradients(tg), global_step=mdtf.train.get_or_create_global_step())
+        sess = mdtf.train.MonitoredTrainingSession(log_step_count_steps=0)
+        ls = [float(sess.run([op, loss])[1]) for _ in range(4)]
+        vs = store.trainable_variables()
+        runs[on] = (ls, {v.name: v.grad.detach().float().cpu().clone() for v in vs},
+                    {v.name for v in vs if getattr(v, "skip_zero", False)})
+    assert runs[True][2], "no gradient slot was store-written and skipped by the zero fill"
+    assert not runs[False][2]
+    assert runs[True][0] == runs[False][0], (runs[True][0], runs[False][0])
+    for k, g in runs[False][1].items():
+        if k in runs[True][2]:          # the store-written slots: bitwise (0 + x == x)
+            assert torch.equal(runs[True][1][k], g), k
+        else:                           # fp32 atomics elsewhere (embedding scatter, bias sums): order-dependent
+            assert torch.allclose(runs[True][1][k], g, rtol=1e-4, atol=1e-6), k
+
+
+def test_fill_ranges_zero():
+    """csrc/kernels.hip fill_ranges_kernel: zeroes exactly the given ranges (odd starts / lengths, float4 and
+    scalar paths, ranges across 4096-element block boundaries)."""
+    from mdtf.ops import _native as N
+    if "mdtf_fill_ranges_zero" not in N.SIGNATURES:
+        N.register("mdtf_fill_ranges_zero", [N.P, N.P, N.I, N.L, N.P])
+    buf = torch.arange(1, 20001, dtype=torch.float32, device=DEV)
+    ranges = [(0, 3), (5, 4100), (4105, 1), (5000, 7), (9001, 6000), (19999, 1)]
+    rt = torch.tensor([x for r in ranges for x in r], dtype=torch.int64, device=DEV)
+    N.check(N.fn("mdtf_fill_ranges_zero")(N.ptr(buf), N.ptr(rt), len(ranges), sum(n for _, n in ranges),
+                                           N.stream_ptr()), "fill")
+    ref = torch.arange(1, 20001, dtype=torch.float32)
+    for o, n in ranges:
+        ref[o:o + n] = 0
+    assert torch.equal(buf.cpu(), ref)
+
+
 def test_weight_cat_cache_matches_torch_cat(monkeypatch):
     """q|k|v weight concatenations refreshed by one batched copy per step (ops.gemm._WeightCats) train exactly like
     a torch.cat per layer: same losses over several steps (the weights change every step)."""
