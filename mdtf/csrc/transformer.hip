@@ -215,17 +215,39 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
       }
     }
   };
-  // RIF rows per slice per iteration, all their loads in flight before the first is reduced
+  // RIF rows per slice per iteration, all their loads in flight before the first is reduced; with more than one
+  // iteration per block the next iteration's rows are loaded before this one's are reduced and stored
   constexpr int RIF = NV <= 2 ? 4 : (NV == 3 ? 2 : 1);
-  for (long long row = r0 + slice; row < r1; row += RIF * W) {
-    uint4 gr[RIF][NV], sr[RIF][NV];
-    float mu[RIF], rs[RIF];
+  uint4 gr[RIF][NV], sr[RIF][NV];
+  float mu[RIF], rs[RIF];
+  long long row = r0 + slice;
 #pragma unroll
-    for (int j = 0; j < RIF; ++j)
-      if (row + j * W < r1) load_row(row + j * W, gr[j], sr[j], mu[j], rs[j]);
+  for (int j = 0; j < RIF; ++j)
+    if (row + j * W < r1) load_row(row + j * W, gr[j], sr[j], mu[j], rs[j]);
+  for (; row < r1; row += RIF * W) {
+    const long long nrow = row + RIF * W;
+    uint4 gn[RIF][NV], sn[RIF][NV];
+    float mn[RIF], rn[RIF];
+    if (nrow < r1) {
+#pragma unroll
+      for (int j = 0; j < RIF; ++j)
+        if (nrow + j * W < r1) load_row(nrow + j * W, gn[j], sn[j], mn[j], rn[j]);
+    }
 #pragma unroll
     for (int j = 0; j < RIF; ++j)
       if (row + j * W < r1) do_row(row + j * W, gr[j], sr[j], mu[j], rs[j]);
+    if (nrow < r1) {
+#pragma unroll
+      for (int j = 0; j < RIF; ++j) {
+        mu[j] = mn[j];
+        rs[j] = rn[j];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          gr[j][i] = gn[j][i];
+          sr[j][i] = sn[j][i];
+        }
+      }
+    }
   }
   // combine the W slices through LDS; block partials -> ws[block][2][H] (plain stores, summed by a reduction pass:
   // deterministic) or, ws == null, one fp32 atomic per column per block straight into the grad slots

@@ -169,7 +169,9 @@ WG_SK = os.environ.get("MDTF_WG_SK", "0") == "1"
 # In the BERT-base step the 256-row kernels gain from the third ring stage (HBM-cold saved activations; graph-timed
 # with MALL-resident operands 2 and 3 stages tie): MDTF_WG_STAGES=3 vs 2, alternating: 6485 / 6530 vs 6378 / 6420 seq/s
 # (FFN-out 3072 x 768: 256-row 3-stage 6368 / 6362 vs 128-row 2-stage 6356 / 6336 seq/s)
-WG_TILES = {(768, 2304, 8192): (256, 3, 4), (768, 3072, 8192): (256, 3, 3), (3072, 768, 8192): (256, 3, 3),
+# Round 6 (write-through slab publish + store-first slots): in-step re-tune moved the q|k|v and FFN-out shapes to
+# two 128-row workgroups per CU (bench/bert_wg_tune.py, profiles/bert_wg_tune_r6f.md: step 9.511 -> 9.402 ms)
+WG_TILES = {(768, 2304, 8192): (128, 2, 4), (768, 3072, 8192): (256, 3, 3), (3072, 768, 8192): (128, 2, 3),
             (768, 768, 8192): (128, 2, 6), (1024, 3072, 8192): (256, 3, 2), (1024, 4096, 8192): (256, 3, 2),
             (4096, 1024, 8192): (256, 3, 2)}
 _TICKETS = {}
