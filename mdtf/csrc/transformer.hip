@@ -215,39 +215,17 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
       }
     }
   };
-  // RIF rows per slice per iteration, all their loads in flight before the first is reduced; with more than one
-  // iteration per block the next iteration's rows are loaded before this one's are reduced and stored
+  // RIF rows per slice per iteration, all their loads in flight before the first is reduced
   constexpr int RIF = NV <= 2 ? 4 : (NV == 3 ? 2 : 1);
-  uint4 gr[RIF][NV], sr[RIF][NV];
-  float mu[RIF], rs[RIF];
-  long long row = r0 + slice;
+  for (long long row = r0 + slice; row < r1; row += RIF * W) {
+    uint4 gr[RIF][NV], sr[RIF][NV];
+    float mu[RIF], rs[RIF];
 #pragma unroll
-  for (int j = 0; j < RIF; ++j)
-    if (row + j * W < r1) load_row(row + j * W, gr[j], sr[j], mu[j], rs[j]);
-  for (; row < r1; row += RIF * W) {
-    const long long nrow = row + RIF * W;
-    uint4 gn[RIF][NV], sn[RIF][NV];
-    float mn[RIF], rn[RIF];
-    if (nrow < r1) {
-#pragma unroll
-      for (int j = 0; j < RIF; ++j)
-        if (nrow + j * W < r1) load_row(nrow + j * W, gn[j], sn[j], mn[j], rn[j]);
-    }
+    for (int j = 0; j < RIF; ++j)
+      if (row + j * W < r1) load_row(row + j * W, gr[j], sr[j], mu[j], rs[j]);
 #pragma unroll
     for (int j = 0; j < RIF; ++j)
       if (row + j * W < r1) do_row(row + j * W, gr[j], sr[j], mu[j], rs[j]);
-    if (nrow < r1) {
-#pragma unroll
-      for (int j = 0; j < RIF; ++j) {
-        mu[j] = mn[j];
-        rs[j] = rn[j];
-#pragma unroll
-        for (int i = 0; i < NV; ++i) {
-          gr[j][i] = gn[j][i];
-          sr[j][i] = sn[j][i];
-        }
-      }
-    }
   }
   // combine the W slices through LDS; block partials -> ws[block][2][H] (plain stores, summed by a reduction pass:
   // deterministic) or, ws == null, one fp32 atomic per column per block straight into the grad slots
@@ -275,6 +253,151 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const bf16_t* __restrict__ d
 #pragma unroll
         for (int w = 0; w < W; ++w) t += L[which][w][cc];
         if (wg) wg[(which ^ beta_first) * H + col] = t;      // partial rows follow the grad slots' order
+        else unsafeAtomicAdd((which ? db_out : dg_out) + col, t);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// LayerNorm backward, lean form (MDTF_LN_BWD=2 / 3; default ln_bwd_kernel above).  ln_bwd_kernel keeps two rows'
+// fp32 intermediates, gamma and the dgamma / dbeta partials in registers: 232 VGPRs at H = 768, two waves per SIMD,
+// ~2 TB/s.  Here a slice reduces ONE row at a time in two passes over its raw bf16 vectors (pass 1: the row sums
+// and the dgamma / dbeta partials; pass 2 recomputes g and xhat from the raw registers and stores dx), gamma is read
+// from LDS, and PF = true loads the slice's next row before the current one is reduced.  Same outputs and the same
+// block-partial epilogue as ln_bwd_kernel.
+template <int NV, int LPR, bool PF>
+__global__ void __launch_bounds__(kT, 3) ln_bwd_lean(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
+                                                 const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                 const float* __restrict__ rstd, bf16_t* __restrict__ dx,
+                                                 bf16_t* __restrict__ dx_branch, float* __restrict__ ws,
+                                                 long long rows, int H, int rows_per_block, int beta_first,
+                                                 uint32_t thr, float inv_keep, uint32_t seed,
+                                                 const long long* __restrict__ seed_off, float* __restrict__ dg_out,
+                                                 float* __restrict__ db_out) {
+  seed = step_seed(seed, seed_off);
+  constexpr int W = kT / LPR;
+  constexpr int SPAN = LPR * 8;
+  const int lane = threadIdx.x & (LPR - 1), slice = threadIdx.x / LPR;
+  const int nvec = H / 8;
+  __shared__ __attribute__((aligned(16))) float Lg[NV * SPAN];
+  __shared__ __attribute__((aligned(16))) float L[2][W][SPAN];
+  for (int c = threadIdx.x; c < NV * SPAN; c += kT) Lg[c] = c < H ? gamma[c] : 0.f;
+  __syncthreads();
+  float dg[NV][8], db[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dg[i][k] = db[i][k] = 0.f;
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+  auto load_row = [&](long long row, uint4 (&gr)[NV], uint4 (&sr)[NV], float& mu, float& rs) {
+    mu = mean[row];
+    rs = rstd[row];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + i * LPR;
+      if (c < nvec) {
+        gr[i] = *reinterpret_cast<const uint4*>(dy + row * H + c * 8);
+        sr[i] = *reinterpret_cast<const uint4*>(s + row * H + c * 8);
+      }
+    }
+  };
+  auto bf = [](const uint4& v, int k) {
+    const uint32_t w = k < 2 ? v.x : (k < 4 ? v.y : (k < 6 ? v.z : v.w));
+    return __uint_as_float(k & 1 ? w & 0xffff0000u : w << 16);
+  };
+  uint4 gr[NV], sr[NV];
+  float mu = 0.f, rs = 0.f;
+  long long row = r0 + slice;
+  if (row < r1) load_row(row, gr, sr, mu, rs);
+  for (; row < r1; row += W) {
+    const long long nrow = row + W;
+    uint4 gn[NV], sn[NV];
+    float mn = 0.f, rn = 0.f;
+    if (PF && nrow < r1) load_row(nrow, gn, sn, mn, rn);
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + i * LPR;
+      if (c < nvec) {
+        const float4 q0 = *reinterpret_cast<const float4*>(&Lg[c * 8]);
+        const float4 q1 = *reinterpret_cast<const float4*>(&Lg[c * 8 + 4]);
+        const float gmk[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float g = bf(gr[i], k), xh = (bf(sr[i], k) - mu) * rs;
+          dg[i][k] += g * xh;
+          db[i][k] += g;
+          const float gg = g * gmk[k];
+          a += gg;
+          b += gg * xh;
+        }
+      }
+    }
+    a = row_sum<LPR>(a) / (float)H;
+    b = row_sum<LPR>(b) / (float)H;
+    // pass 2 re-derives g and xhat from the raw registers: an empty asm "modifies" them, so the compiler cannot keep
+    // pass 1's 2 x 8 NV unpacked floats alive across the row sums (that CSE costs ~50 VGPRs)
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      asm volatile("" : "+v"(gr[i].x), "+v"(gr[i].y), "+v"(gr[i].z), "+v"(gr[i].w), "+v"(sr[i].x), "+v"(sr[i].y),
+                   "+v"(sr[i].z), "+v"(sr[i].w));
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + i * LPR;
+      if (c < nvec) {
+        const float4 q0 = *reinterpret_cast<const float4*>(&Lg[c * 8]);
+        const float4 q1 = *reinterpret_cast<const float4*>(&Lg[c * 8 + 4]);
+        const float gmk[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float g = bf(gr[i], k), xh = (bf(sr[i], k) - mu) * rs;
+          o[k] = rs * (g * gmk[k] - a - xh * b);
+        }
+        store_bf8(dx + row * H + c * 8, o);
+        if (dx_branch) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            o[k] = (!thr || drop_keep((uint32_t)(row * H + c * 8 + k), seed, thr)) ? o[k] * inv_keep : 0.f;
+          store_bf8(dx_branch + row * H + c * 8, o);
+        }
+      }
+    }
+    if (nrow < r1) {
+      if (PF) {
+        mu = mn;
+        rs = rn;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          gr[i] = gn[i];
+          sr[i] = sn[i];
+        }
+      } else {
+        load_row(nrow, gr, sr, mu, rs);
+      }
+    }
+  }
+  float* wg = ws ? ws + (long long)blockIdx.x * 2 * H : nullptr;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float4* l0 = reinterpret_cast<float4*>(&L[0][slice][0]);
+    float4* l1 = reinterpret_cast<float4*>(&L[1][slice][0]);
+    l0[lane] = make_float4(dg[i][0], dg[i][1], dg[i][2], dg[i][3]);
+    l0[LPR + lane] = make_float4(dg[i][4], dg[i][5], dg[i][6], dg[i][7]);
+    l1[lane] = make_float4(db[i][0], db[i][1], db[i][2], db[i][3]);
+    l1[LPR + lane] = make_float4(db[i][4], db[i][5], db[i][6], db[i][7]);
+    __syncthreads();
+    for (int j = threadIdx.x; j < 2 * SPAN; j += kT) {
+      const int which = j / SPAN, cc = j % SPAN;
+      const int h = cc / (4 * LPR), ln = (cc / 4) % LPR, e = cc % 4;
+      const int col = i * SPAN + ln * 8 + h * 4 + e;
+      if (col < H) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < W; ++w) t += L[which][w][cc];
+        if (wg) wg[(which ^ beta_first) * H + col] = t;
         else unsafeAtomicAdd((which ? db_out : dg_out) + col, t);
       }
     }
@@ -499,6 +622,24 @@ inline int gcap(long long work) {
     else return MDTF_EUNSUPPORTED;                                                                         \
   } while (0)
 
+// LN_DISPATCH with a third template argument X (the lean backward's prefetch switch)
+#define LN_DISPATCH3(H, KERNEL, X, GRID32, GRID64, ...)                                                   \
+  do {                                                                                                     \
+    const int nvec_ = (H) / 8;                                                                             \
+    if (nvec_ % 64 != 0 && nvec_ % 32 == 0 && nvec_ / 32 <= 3) {                                           \
+      if (nvec_ == 32) hipLaunchKernelGGL((KERNEL<1, 32, X>), GRID32, dim3(kT), 0, st, __VA_ARGS__);      \
+      else hipLaunchKernelGGL((KERNEL<3, 32, X>), GRID32, dim3(kT), 0, st, __VA_ARGS__);                  \
+      break;                                                                                               \
+    }                                                                                                      \
+    const int nv_ = static_cast<int>(ceil_div(nvec_, 64));                                                 \
+    if (nv_ <= 1) hipLaunchKernelGGL((KERNEL<1, 64, X>), GRID64, dim3(kT), 0, st, __VA_ARGS__);            \
+    else if (nv_ <= 2) hipLaunchKernelGGL((KERNEL<2, 64, X>), GRID64, dim3(kT), 0, st, __VA_ARGS__);       \
+    else if (nv_ <= 4) hipLaunchKernelGGL((KERNEL<4, 64, X>), GRID64, dim3(kT), 0, st, __VA_ARGS__);       \
+    else if (nv_ <= 8) hipLaunchKernelGGL((KERNEL<8, 64, X>), GRID64, dim3(kT), 0, st, __VA_ARGS__);       \
+    else if (nv_ <= 16) hipLaunchKernelGGL((KERNEL<16, 64, X>), GRID64, dim3(kT), 0, st, __VA_ARGS__);     \
+    else return MDTF_EUNSUPPORTED;                                                                         \
+  } while (0)
+
 #define NV_DISPATCH(H, KERNEL, GRID, ...)                                                                  \
   do {                                                                                                     \
     const int nv_ = static_cast<int>(ceil_div((H) / 8, 64));                                               \
@@ -540,12 +681,25 @@ extern "C" int mdtf_reduce_partials(const float* ws, int B, int C, float* out, h
 extern "C" int mdtf_get_deterministic();
 extern "C" int mdtf_reduce_partials_strided(const float* ws, int B, int C, long long ld, float* out, hipStream_t st);
 
-// MDTF_LN_BWD_RPB: minimum rows per LayerNorm-backward block (default 16: 512 blocks at 8192 rows; A/B switch)
+// MDTF_LN_BWD: 1 ln_bwd_kernel (default), 2 ln_bwd_lean, 3 ln_bwd_lean with the next row prefetched.  Graph-timed at
+// BERT-base's 8192 x 768 (bench/ln_probe.py, profiles/ln_probe_r6h.jsonl) the lean form's extra occupancy (138 vs
+// 232 VGPRs) does not pay: 19.2 us (form 1, 16 rows per block) vs 20.4 (2) / 19.5 (3) incl. the partial reduction.
+static int ln_bwd_form() {
+  static const int v = [] {
+    const char* e = getenv("MDTF_LN_BWD");
+    const int f = e ? atoi(e) : 1;
+    return (f >= 1 && f <= 3) ? f : 1;
+  }();
+  return v;
+}
+
+// MDTF_LN_BWD_RPB: minimum rows per LayerNorm-backward block (default 16 for ln_bwd_kernel: 512 blocks at 8192 rows;
+// 8 for the lean form: 1024 blocks, one row per 32-lane slice; A/B switch)
 static long long ln_bwd_rpb() {
   static const long long v = [] {
     const char* e = getenv("MDTF_LN_BWD_RPB");
     const long long r = e ? atoll(e) : 0;
-    return r > 0 ? r : 16LL;
+    return r > 0 ? r : (ln_bwd_form() == 1 ? 16LL : 8LL);
   }();
   return v;
 }
@@ -597,9 +751,18 @@ MDTF_EXPORT int mdtf_ln_bwd(const void* dy, const void* s, const float* gamma, c
     return e && e[0] == '1';
   }();
   const bool atomics = atomics_env && !mdtf_get_deterministic();
-  LN_DISPATCH(H, ln_bwd_kernel, dim3(blocks), dim3(blocks), (const bf16_t*)dy, (const bf16_t*)s, gamma, mean, rstd,
-              (bf16_t*)dx, (bf16_t*)dx_branch, atomics ? nullptr : ws, rows, H, rpb, beta_first, thr, inv_keep,
-              (uint32_t)seed, seed_off, dgamma, dbeta);
+  if (ln_bwd_form() == 1 || H > 2048)       // (the lean form spills past 4 vectors per lane)
+    LN_DISPATCH(H, ln_bwd_kernel, dim3(blocks), dim3(blocks), (const bf16_t*)dy, (const bf16_t*)s, gamma, mean, rstd,
+                (bf16_t*)dx, (bf16_t*)dx_branch, atomics ? nullptr : ws, rows, H, rpb, beta_first, thr, inv_keep,
+                (uint32_t)seed, seed_off, dgamma, dbeta);
+  else if (ln_bwd_form() == 2)
+    LN_DISPATCH3(H, ln_bwd_lean, false, dim3(blocks), dim3(blocks), (const bf16_t*)dy, (const bf16_t*)s, gamma, mean,
+                 rstd, (bf16_t*)dx, (bf16_t*)dx_branch, atomics ? nullptr : ws, rows, H, rpb, beta_first, thr,
+                 inv_keep, (uint32_t)seed, seed_off, dgamma, dbeta);
+  else
+    LN_DISPATCH3(H, ln_bwd_lean, true, dim3(blocks), dim3(blocks), (const bf16_t*)dy, (const bf16_t*)s, gamma, mean,
+                 rstd, (bf16_t*)dx, (bf16_t*)dx_branch, atomics ? nullptr : ws, rows, H, rpb, beta_first, thr,
+                 inv_keep, (uint32_t)seed, seed_off, dgamma, dbeta);
   MDTF_LAUNCH_CHECK();
   if (atomics) return 0;
   if (g_ln_red_stream && g_ln_red_stream != st) {
