@@ -99,12 +99,14 @@ def _wg_backward(ctx, x, dpre):
 
 
 def _wg_ok(x, d):
-    """Shapes the weight-gradient kernel (csrc/gemm_wg.hip) takes and wins on (profiles/gemm_wg_probe_r3a.jsonl):
-    K x N weights of 128-multiples over >= 4096 tokens except the square 768 x 768 (the split conv-kernel
-    weight gradient is 10 % faster there)."""
+    """Shapes the weight-gradient kernel (csrc/gemm_wg.hip) takes and wins on: K x N weights of 128-multiples over
+    >= 4096 tokens.  Until round 5 the square 768 x 768 stayed on the split conv-kernel weight gradient (10 % faster,
+    profiles/gemm_wg_probe_r3a.jsonl); with round 6's write-through slabs and store-first slots the weight-gradient
+    kernel wins it in the BERT-base step too (+0.4 %, 9.54 vs 9.58 ms, profiles/ab_r6.md).  MDTF_WG_SQUARE=0: the
+    conv-kernel path for K * N <= 768 * 768."""
     T, K = x.shape
     Nn = d.shape[1]
-    small_ok = os.environ.get("MDTF_WG_SQUARE", "0") == "1"        # (A/B switch: the 768 x 768 product too)
+    small_ok = os.environ.get("MDTF_WG_SQUARE", "1") == "1"
     return T >= 4096 and K % 128 == 0 and Nn % 128 == 0 and (K * Nn > 768 * 768 or small_ok) and T % 64 == 0
 
 
