@@ -667,6 +667,205 @@ __global__ void __launch_bounds__(512, 2) attn_bwd_v2(const bf16_t* __restrict__
   }
 }
 
+// ============================================================================ backward v2, split phases (round 6)
+// attn_bwd_v2's two phases as separate workgroups: block 2 bh runs phase A (dK, dV: Q and dO images in LDS, this
+// wave's K / V rows in registers), block 2 bh + 1 phase B (dQ: K and V images, this wave's Q / dO rows).  Each
+// phase needs only two of the four 16 KiB images, so a workgroup does half the work on half the LDS.  Why: 768
+// (batch, head) items on 512 slots of the one-workgroup-per-item kernel run as 1.5 rounds of whole items; 1536
+// half items on 512 slots are 3 full rounds of half items.  The per-lane D = rowsum(dO * O) of the lane's row is
+// computed by both phases (phase A needs it for every query, phase B for its own).  Numerics, dropout bits and
+// outputs are those of attn_bwd_v2.  Measured in the BERT-base step: -0.8 % (two workgroups per CU), -3.5 % with
+// the 80-register build (three per CU, spills): the backward is bound by its operand loads, which the split
+// repeats (both halves load their rows' Q / dO / O), not by the half-empty last round.  MDTF_ATTN_BWD=v2s: opt-in.
+constexpr int kBwd2sLds = 2 * S * D * 2 + 3 * S * 4;
+
+// MINB: 512-thread workgroups per CU the register allocation must allow (launch bound 2 MINB waves per SIMD; 2:
+// <= 128 VGPRs; 3: <= 80, 1536 half items in 2 rounds of 768 slots)
+template <int MINB>
+__global__ void __launch_bounds__(512, 2 * MINB) attn_bwd_v2s(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+                                                     const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
+                                                     const float* __restrict__ lse, bf16_t* __restrict__ dqkv, int B,
+                                                     int nh, float scale, float p_drop, uint32_t seed,
+                                                     const long long* __restrict__ seed_off) {
+  seed = step_seed(seed, seed_off);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* I0 = smem;                            // phase A: Q    phase B: K
+  char* I1 = I0 + S * D * 2;                  // phase A: dO   phase B: V
+  float* LS = reinterpret_cast<float*>(I1 + S * D * 2);
+  float* DV = LS + S;                         // D = rowsum(dO * O)
+  float* MK = DV + S;                         // additive key mask
+  const int bh = blockIdx.x >> 1, phase = blockIdx.x & 1;
+  const int b = bh / nh, h = bh - b * nh;
+  const int H = nh * D, ld = 3 * H;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const long long row0 = (long long)b * S * ld;
+  const long long orow0 = (long long)b * S * H;
+  const int tbytes = (int)((long long)B * S * ld * 2);
+  const int obytes = (int)((long long)B * S * H * 2);
+
+  if (phase == 0) {
+    load_head<SwzV, 8>(qkv, tbytes, row0 + h * D, ld, I0, wave, lane);
+    load_head<SwzV, 8>(dout, obytes, orow0 + h * D, H, I1, wave, lane);
+  } else {
+    load_head<SwzV, 8>(qkv, tbytes, row0 + H + h * D, ld, I0, wave, lane);
+    load_head<SwzV, 8>(qkv, tbytes, row0 + 2 * H + h * D, ld, I1, wave, lane);
+  }
+  // register operands of row 16*wave + li: phase A its key (K, V rows), phase B its query (Q, dO rows)
+  const int r = 16 * wave + li;
+  bf16x8_t f0[2], f1[2];
+  float part = 0.f;
+#pragma unroll
+  for (int ds = 0; ds < 2; ++ds) {
+    const int d = 32 * ds + 8 * g;
+    if (phase == 0) {
+      f0[ds] = load_frag_global(qkv + row0 + (long long)r * ld + H + h * D + d);
+      f1[ds] = load_frag_global(qkv + row0 + (long long)r * ld + 2 * H + h * D + d);
+    } else {
+      f0[ds] = load_frag_global(qkv + row0 + (long long)r * ld + h * D + d);
+      f1[ds] = load_frag_global(dout + orow0 + (long long)r * H + h * D + d);
+    }
+    float o8[8], do8[8];
+    load_bf8(out + orow0 + (long long)r * H + h * D + d, o8);
+    load_bf8(dout + orow0 + (long long)r * H + h * D + d, do8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part += o8[e] * do8[e];
+  }
+  part += __shfl_xor(part, 16, 64);
+  part += __shfl_xor(part, 32, 64);
+  const float lq = lse[(long long)bh * S + r];
+  const float mr = mask ? mask[(long long)b * S + r] : 0.f;
+  if (g == 0) {
+    LS[r] = lq;
+    DV[r] = part;
+    MK[r] = mr;
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  const uint32_t thr = p_drop > 0.f ? (uint32_t)fminf(p_drop * 4294967296.f, 4294967295.f) : 0u;
+  const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const int q4 = li >> 2, p4 = li & 3;
+
+  if (phase == 0) {
+    // ---- phase A: keys r (lane column) -- dV^T[d][k] = dO^T P, dK^T[d][k] = Q^T dS over all queries
+    const char* QI = I0;
+    const char* OI = I1;
+    float4v dvacc[4], dkacc[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dvacc[dt] = dkacc[dt] = float4v{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < 4; ++s) {                       // queries 32s .. 32s+31
+      float4v sc[2], dp[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) sc[t] = dp[t] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8_t qa = row_frag<SwzV>(QI, 32 * s + 16 * t, 4 * ds, lane);
+          const bf16x8_t oa = row_frag<SwzV>(OI, 32 * s + 16 * t, 4 * ds, lane);
+          sc[t] = mfma(qa, f0[ds], sc[t]);
+          dp[t] = mfma(oa, f1[ds], dp[t]);
+        }
+      float pv[8], sv[8];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int q0 = 32 * s + 16 * t + 4 * g;       // this lane's 4 queries of the tile
+        const float4 l4 = *reinterpret_cast<const float4*>(LS + q0);
+        const float4 d4 = *reinterpret_cast<const float4*>(DV + q0);
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = __expf(sc[t][i] * scale + mr - lv[i]);
+          float dpv = dp[t][i], pk = p;
+          if (thr) {
+            const bool keep = keep_elem(seed, bh, q0 + i, r, thr);
+            pk = keep ? p * inv_keep : 0.f;
+            dpv = keep ? dpv * inv_keep : 0.f;
+          }
+          pv[4 * t + i] = pk;
+          sv[4 * t + i] = p * (dpv - dv[i]);
+        }
+      }
+      const bf16x8_t pf = __builtin_bit_cast(bf16x8_t, make_uint4(pack2(pv[0], pv[1]), pack2(pv[2], pv[3]),
+                                                                  pack2(pv[4], pv[5]), pack2(pv[6], pv[7])));
+      const bf16x8_t sf = __builtin_bit_cast(bf16x8_t, make_uint4(pack2(sv[0], sv[1]), pack2(sv[2], sv[3]),
+                                                                  pack2(sv[4], sv[5]), pack2(sv[6], sv[7])));
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        v4s lo = tr4<SwzV, 128>(OI, 32 * s + 4 * g + q4, dt * 16 + 4 * p4);
+        v4s hi = tr4<SwzV, 128>(OI, 32 * s + 16 + 4 * g + q4, dt * 16 + 4 * p4);
+        short8 fo = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        dvacc[dt] = mfma(__builtin_bit_cast(bf16x8_t, fo), pf, dvacc[dt]);
+        lo = tr4<SwzV, 128>(QI, 32 * s + 4 * g + q4, dt * 16 + 4 * p4);
+        hi = tr4<SwzV, 128>(QI, 32 * s + 16 + 4 * g + q4, dt * 16 + 4 * p4);
+        short8 fq = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        dkacc[dt] = mfma(__builtin_bit_cast(bf16x8_t, fq), sf, dkacc[dt]);
+      }
+    }
+    bf16_t* rowp = dqkv + row0 + (long long)r * ld + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const float4v kv = dkacc[dt], vv = dvacc[dt];
+      *reinterpret_cast<uint2*>(rowp + H + dt * 16 + 4 * g) =
+          make_uint2(pack2(kv[0] * scale, kv[1] * scale), pack2(kv[2] * scale, kv[3] * scale));
+      *reinterpret_cast<uint2*>(rowp + 2 * H + dt * 16 + 4 * g) = make_uint2(pack2(vv[0], vv[1]), pack2(vv[2], vv[3]));
+    }
+  } else {
+    // ---- phase B: query r (lane column) -- dQ^T[d][q] = K^T dS^T over all keys
+    const char* KI = I0;
+    const char* VI = I1;
+    float4v qacc[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) qacc[dt] = float4v{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < 4; ++ks) {                    // keys 32ks .. 32ks+31
+      float4v sc[2], dp[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) sc[t] = dp[t] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8_t ka = row_frag<SwzV>(KI, 32 * ks + 16 * t, 4 * ds, lane);
+          const bf16x8_t va = row_frag<SwzV>(VI, 32 * ks + 16 * t, 4 * ds, lane);
+          sc[t] = mfma(ka, f0[ds], sc[t]);
+          dp[t] = mfma(va, f1[ds], dp[t]);
+        }
+      float sv[8];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int k0 = 32 * ks + 16 * t + 4 * g;       // this lane's 4 keys of the tile
+        const float4 m4 = *reinterpret_cast<const float4*>(MK + k0);
+        const float mv[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = __expf(sc[t][i] * scale + mv[i] - lq);
+          float dpv = dp[t][i];
+          if (thr) dpv = keep_elem(seed, bh, r, k0 + i, thr) ? dpv * inv_keep : 0.f;
+          sv[4 * t + i] = p * (dpv - part);
+        }
+      }
+      const bf16x8_t sf = __builtin_bit_cast(bf16x8_t, make_uint4(pack2(sv[0], sv[1]), pack2(sv[2], sv[3]),
+                                                                  pack2(sv[4], sv[5]), pack2(sv[6], sv[7])));
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        v4s lo = tr4<SwzV, 128>(KI, 32 * ks + 4 * g + q4, dt * 16 + 4 * p4);
+        v4s hi = tr4<SwzV, 128>(KI, 32 * ks + 16 + 4 * g + q4, dt * 16 + 4 * p4);
+        short8 fk = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        qacc[dt] = mfma(__builtin_bit_cast(bf16x8_t, fk), sf, qacc[dt]);
+      }
+    }
+    bf16_t* rowp = dqkv + row0 + (long long)r * ld + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const float4v v = qacc[dt];
+      *reinterpret_cast<uint2*>(rowp + dt * 16 + 4 * g) =
+          make_uint2(pack2(v[0] * scale, v[1] * scale), pack2(v[2] * scale, v[3] * scale));
+    }
+  }
+}
+
 // ============================================================================ persistent forms (round 5)
 // The kernels above give each (batch, head) item its own workgroup: every workgroup pays one HBM load latency,
 // computes for ~1 us, then stores, so the chip streams at about half the HBM rate (attn_fwd 20 us for 50 MB,
@@ -1090,7 +1289,7 @@ MDTF_EXPORT int mdtf_attn_fwd(const void* qkv, const float* mask, void* out, flo
   return 0;
 }
 
-static int g_attn_bwd = -1;    // backward kernel version: 1 = v1, 2 = v2; -1: from MDTF_ATTN_BWD at the first call
+static int g_attn_bwd = -1;    // backward kernel version: 1 = v1, 2 = v2, 3 = v2s; -1: from MDTF_ATTN_BWD at the first call
 
 // select the S = 128 backward kernel (tests / A/B); returns the previous choice
 MDTF_EXPORT int mdtf_set_attn_bwd(int version) {
@@ -1107,9 +1306,9 @@ MDTF_EXPORT int mdtf_attn_bwd(const void* qkv, const float* mask, const void* ou
   if ((long long)B * S * 3 * nh * D * 2 > 0x7fffffffLL) return MDTF_EUNSUPPORTED;
   // v2 (default; in the BERT-base step 39 vs 45 us per call, profiles/attention_bwd_v2_r3.md); MDTF_ATTN_BWD=v1:
   // the r1 kernel with [q][k] images (MDTF_ATTN_BWD_WAVES=4: its 4-wave form) -- A/B switches
-  if (g_attn_bwd < 0) {
+  if (g_attn_bwd < 0) {     // MDTF_ATTN_BWD=v1 | v2 (default) | v2s (split phases: -0.8 % BERT-base, profiles/ab_r6.md)
     const char* e = getenv("MDTF_ATTN_BWD");
-    g_attn_bwd = (e && e[0] == 'v' && e[1] == '1') ? 1 : 2;
+    g_attn_bwd = (e && e[0] == 'v' && e[1] == '1') ? 1 : (e && e[0] == 'v' && e[1] == '2' && e[2] == 's') ? 3 : 2;
   }
   const bool v1 = g_attn_bwd == 1;
   static const bool w4 = [] {
@@ -1120,6 +1319,18 @@ MDTF_EXPORT int mdtf_attn_bwd(const void* qkv, const float* mask, const void* ou
     hipLaunchKernelGGL(attn_bwd_pp, dim3(pp_grid(B * nh)), dim3(1024), kBwdPpLds, st, (const bf16_t*)qkv, mask,
                        (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv, B, nh, scale, p_drop,
                        (uint32_t)seed, seed_off);
+    MDTF_LAUNCH_CHECK();
+    return 0;
+  }
+  if (g_attn_bwd == 3 && !w4) {
+    // MDTF_ATTN_BWD_OCC=3: the 80-register build (three workgroups per CU)
+    static const int occ = [] {
+      const char* e = getenv("MDTF_ATTN_BWD_OCC");
+      return (e && e[0] == '3') ? 3 : 2;
+    }();
+    hipLaunchKernelGGL((occ == 3 ? attn_bwd_v2s<3> : attn_bwd_v2s<2>), dim3(2 * B * nh), dim3(512), kBwd2sLds, st,
+                       (const bf16_t*)qkv, mask, (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv, B, nh,
+                       scale, p_drop, (uint32_t)seed, seed_off);
     MDTF_LAUNCH_CHECK();
     return 0;
   }

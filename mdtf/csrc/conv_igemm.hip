@@ -2134,7 +2134,8 @@ __global__ void __launch_bounds__(64 * NW, (wgrad_min_waves<BM, BN, STAGES, NW>(
 // of the block's 256 / G float4 outputs, then the G partials are added in LDS (fixed order: deterministic).
 template <bool NT, int G>
 __global__ void __launch_bounds__(256) wgrad_slab_reduce_g(const float* __restrict__ slab, int splits,
-                                                           long long RC, int C, long long ld, float* __restrict__ dw) {
+                                                           long long RC, int C, long long ld, float* __restrict__ dw,
+                                                           int store) {
   constexpr int W = 256 / G;                                // float4 outputs per block
   __shared__ float4 part[G][W];
   const int g = threadIdx.x / W, l = threadIdx.x - g * W;
@@ -2181,6 +2182,10 @@ __global__ void __launch_bounds__(256) wgrad_slab_reduce_g(const float* __restri
   }
   const long long e = q * 4, r = e / C, c = e - r * C;
   float4* o = reinterpret_cast<float4*>(dw + r * ld + c);
+  if (store) {                 // the step's first writer of the gradient slot: DW is not read
+    *o = t;
+    return;
+  }
   float4 v = *o;
   v.x += t.x;
   v.y += t.y;
@@ -2191,7 +2196,7 @@ __global__ void __launch_bounds__(256) wgrad_slab_reduce_g(const float* __restri
 
 template <bool NT>
 __global__ void __launch_bounds__(256) wgrad_slab_reduce(const float* __restrict__ slab, int splits, long long RC,
-                                                         int C, long long ld, float* __restrict__ dw) {
+                                                         int C, long long ld, float* __restrict__ dw, int store) {
   const long long q = blockIdx.x * 256LL + threadIdx.x;     // float4 index
   if (q * 4 >= RC) return;
   typedef float f4v __attribute__((ext_vector_type(4)));
@@ -2219,6 +2224,10 @@ __global__ void __launch_bounds__(256) wgrad_slab_reduce(const float* __restrict
   }
   const long long e = q * 4, r = e / C, c = e - r * C;
   float4* o = reinterpret_cast<float4*>(dw + r * ld + c);
+  if (store) {
+    *o = t;
+    return;
+  }
   float4 v = *o;
   v.x += t.x;
   v.y += t.y;
@@ -2235,6 +2244,10 @@ hipStream_t g_slab_stream = nullptr;
 // launches (mdtf_set_wgrad_tickets); null: slab + reduction launch.
 int* g_wg_cnt = nullptr;
 long long g_wg_cnt_n = 0;
+// The following weight-gradient launch overwrites DW instead of accumulating (mdtf_set_wgrad_store: the step's
+// first writer of that gradient slot, ops.conv / train.variables claim_store): the slab reduction stores its sum;
+// without one (fp32 atomics, in-kernel split reduction) DW is zeroed before the kernel.
+int g_wg_store = 0;
 hipEvent_t slab_event() {
   static hipEvent_t ev = [] {
     hipEvent_t e = nullptr;
@@ -2276,6 +2289,11 @@ int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
     }();
     b.slab_nt = nt;
   }
+  const int store = g_wg_store;
+  if (store && !(b.slab && !b.cnt)) {     // accumulating epilogues: the slot must start at zero
+    if (hipMemset2DAsync(a.dw, (size_t)a.ld_dw * 4, 0, (size_t)a.Cout * 4, (size_t)R, st) != hipSuccess)
+      return MDTF_EUNSUPPORTED;
+  }
   hipLaunchKernelGGL((conv_wgrad_v2<BM, BN, STAGES, NW, PIPE>), dim3(a.mtiles * a.ntiles * splits), dim3(64 * NW), lds,
                      st, b);
   MDTF_LAUNCH_CHECK();
@@ -2298,15 +2316,15 @@ int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
     if (G == 16)
       hipLaunchKernelGGL((b.slab_nt ? wgrad_slab_reduce_g<true, 16> : wgrad_slab_reduce_g<false, 16>),
                          dim3((unsigned)ceil_div(q4, 16)), dim3(256), 0, st, b.slab, splits, RC, a.Cout,
-                         (long long)a.ld_dw, a.dw);
+                         (long long)a.ld_dw, a.dw, store);
     else if (G == 4)
       hipLaunchKernelGGL((b.slab_nt ? wgrad_slab_reduce_g<true, 4> : wgrad_slab_reduce_g<false, 4>),
                          dim3((unsigned)ceil_div(q4, 64)), dim3(256), 0, st, b.slab, splits, RC, a.Cout,
-                         (long long)a.ld_dw, a.dw);
+                         (long long)a.ld_dw, a.dw, store);
     else
       hipLaunchKernelGGL((b.slab_nt ? wgrad_slab_reduce<true> : wgrad_slab_reduce<false>),
                          dim3((unsigned)ceil_div(RC / 4, 256)), dim3(256), 0, st, b.slab, splits, RC, a.Cout,
-                         (long long)a.ld_dw, a.dw);
+                         (long long)a.ld_dw, a.dw, store);
     MDTF_LAUNCH_CHECK();
   }
   return 0;
@@ -2659,6 +2677,12 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
       hipLaunchKernelGGL(dgrad_zero_classes<false>, dim3(blocks), dim3(256), 0, st, a, C8);
     MDTF_LAUNCH_CHECK();
   }
+  return 0;
+}
+
+// The following v2 weight-gradient launches overwrite DW instead of accumulating into it (1) or accumulate (0).
+MDTF_EXPORT int mdtf_set_wgrad_store(int on) {
+  g_wg_store = on ? 1 : 0;
   return 0;
 }
 

@@ -27,6 +27,7 @@ N.register("mdtf_conv_fwd_v2", [N.P, N.P, N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.
 N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P, N.P, N.P, N.I, N.P, N.P, N.P])
 N.register("mdtf_conv_wgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.I, N.P])
 N.register("mdtf_set_slab_stream", [N.P])
+N.register("mdtf_set_wgrad_store", [N.I])
 
 # split-K weight gradients: per-split partial slabs + one reduction pass (plain stores) instead of fp32
 # atomics into DW.  Measured on MI355X (scripts/gpu.sh envab): +0.4 % BERT-base (dense GEMM weight
@@ -656,8 +657,9 @@ def pp_dgrad(dy, w, x_shape, pads, dil, tile, out=None, accumulate=False, bn_sta
     return dx
 
 
-def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=1, stages=2):
-    """fp32 HWIO weight gradient; accumulates into ``out`` when given (must be zeroed or a grad slot)."""
+def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=1, stages=2, store=False):
+    """fp32 HWIO weight gradient; accumulates into ``out`` when given (must be zeroed or a grad slot), or with
+    ``store`` (v2 kernels) overwrites it -- the step's first writer of that gradient slot (V.claim_store)."""
     dw = torch.zeros(w_shape, dtype=torch.float32, device=x.device) if out is None else out
     n, h, wd, c = x.shape
     kh, kw, ci, co = w_shape
@@ -669,11 +671,17 @@ def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=
                 force = bool(ent["slab"])
         slab, cap = wgrad_slab(n * dy.shape[1] * dy.shape[2], kh * kw * ci, co, bm, bn, ver, int(splits), x.device,
                                force=force)
-        with slab_side(slab if out is not None else None), wgrad_tickets(slab):
-            N.check(N.fn("mdtf_conv_wgrad_v2")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2],
-                                               co, kh, kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
-                                               _v2_code(bm, stages, ver), bn, int(splits), N.ptr(slab), cap,
-                                               N.stream_ptr()), "conv_wgrad_v2")
+        if store:
+            N.fn("mdtf_set_wgrad_store")(1)
+        try:
+            with slab_side(slab if out is not None else None), wgrad_tickets(slab):
+                N.check(N.fn("mdtf_conv_wgrad_v2")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1],
+                                                   dy.shape[2], co, kh, kw, stride[0], stride[1], pads[0], pads[2],
+                                                   dil[0], dil[1], _v2_code(bm, stages, ver), bn, int(splits),
+                                                   N.ptr(slab), cap, N.stream_ptr()), "conv_wgrad_v2")
+        finally:
+            if store:
+                N.fn("mdtf_set_wgrad_store")(0)
         return dw
     N.check(N.fn("mdtf_conv_wgrad")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co, kh,
                                     kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1], bm, bn, int(splits),
@@ -983,6 +991,7 @@ class _Conv(torch.autograd.Function):
             if sink is not None:
                 # fp32 atomics of the wgrad kernel accumulate into the flat gradient buffer
                 if WGRAD_STREAM and x.is_cuda:
+                    V.note_accumulate(sink)           # (zeroes a store-first slot the fill skipped)
                     side = _side_stream(x.device)
                     side.wait_stream(torch.cuda.current_stream(x.device))
                     with torch.cuda.stream(side):
@@ -992,8 +1001,13 @@ class _Conv(torch.autograd.Function):
                     dy.record_stream(side)
                     _PENDING.add(x.device)
                 else:
+                    # v2 kernels overwrite the slot as the step's first writer of it (V.claim_store): no zero fill,
+                    # no read of the slot in the slab reduction
+                    st = cw[4] in (2, 3) and V.claim_store(sink)
+                    if not st and cw[4] not in (2, 3):
+                        V.note_accumulate(sink)
                     mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], out=sink.grad, ver=cw[4],
-                               stages=cw[5])
+                               stages=cw[5], store=st)
                 dw = V.grad_marker(w)
             else:
                 dw = mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], ver=cw[4], stages=cw[5])

@@ -287,17 +287,20 @@ class _ActLink(object):
         self.pre, self.act, self.fused = None, 0, False
 
 
-def _accum_mm(out, a, b):
-    """``out += a @ b`` with bf16 a/b and fp32 out."""
+def _accum_mm(out, a, b, store=False):
+    """``out += a @ b`` (``store``: ``out = a @ b``, out not read) with bf16 a/b and fp32 out."""
     global _fp32_out_ok
     if _fp32_out_ok is None or _fp32_out_ok:
         try:
-            torch.addmm(out, a, b, out_dtype=torch.float32, out=out)
+            torch.addmm(out, a, b, beta=0 if store else 1, out_dtype=torch.float32, out=out)
             _fp32_out_ok = True
             return
         except (RuntimeError, TypeError):
             _fp32_out_ok = False
-    out.add_(torch.mm(a, b))
+    if store:
+        out.copy_(torch.mm(a, b))
+    else:
+        out.add_(torch.mm(a, b))
 
 
 def _act_fwd(pre, act):
@@ -807,7 +810,9 @@ class _TiedDecoder(torch.autograd.Function):
             dh = part.sum(0).to(h.dtype)
         except (RuntimeError, TypeError):
             dh = torch.mm(dp, Wp)
-        _accum_mm(wv.grad_padded, dp.t(), h)
+        # the decoder's weight gradient writes the whole (padded) slot: as the step's first writer it overwrites it
+        # (V.claim_store; the word embedding's scatter-add accumulates onto it later)
+        _accum_mm(wv.grad_padded, dp.t(), h, store=V.claim_store(wv))
         kernels.colsum_into(dp, bv.grad_padded)
         w, b = ctx.like
         return dh, V.grad_marker(w), V.grad_marker(b)

@@ -28,7 +28,7 @@ N.register("mdtf_embed_bwd_ws", [N.P, N.P, N.P, N.L, N.I, N.L, N.P, N.P])
 EMBED_SMALL_2PASS = os.environ.get("MDTF_EMBED_SMALL_2PASS", "1") != "0"
 N.register("mdtf_attn_fwd", [N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P, N.P])
 N.register("mdtf_attn_bwd", [N.P, N.P, N.P, N.P, N.P, N.P, N.I, N.I, N.I, N.I, N.F, N.F, N.U, N.P, N.P])
-N.register("mdtf_set_attn_bwd", [N.I], N.I)     # S = 128 backward kernel: 1 = v1 ([q][k] images), 2 = v2
+N.register("mdtf_set_attn_bwd", [N.I], N.I)     # S = 128 backward kernel: 1 = v1 ([q][k] images), 2 = v2, 3 = v2s
 N.register("mdtf_set_attn_pp", [N.I], N.I)      # S = 128 persistent kernels: 0 off, 1 on, n >= 2 on, grid <= n
 
 

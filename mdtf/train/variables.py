@@ -268,9 +268,9 @@ def grad_sink(t):
     return var
 
 
-# Store-first gradient slots (MDTF_GRAD_STORE_FIRST, on by default): a weight-gradient kernel that is the step's
-# ONLY writer of a slot (first write of the step, the variable's only use in flight) overwrites it instead of
-# accumulating.  A variable whose first write of a step was such a store is not zeroed at the start of the next
+# Store-first gradient slots (MDTF_GRAD_STORE_FIRST, on by default): a weight-gradient kernel that writes every
+# element of a slot and is the step's FIRST writer of it overwrites it instead of accumulating (the other writers
+# of the step -- a shared weight's other consumers -- accumulate onto it).  A variable whose first write of a step was such a store is not zeroed at the start of the next
 # step (parallel/flat.py skips its range in the one zero-fill launch), which removes its share of the gradient
 # buffer fill and the read of C in the kernel's epilogue.  Safety nets: any other first write into a skipped slot
 # zeroes it first (note_accumulate, _VarRead.backward), and a skipped slot nobody wrote in a step is zeroed at the
@@ -284,10 +284,12 @@ def begin_grad_epoch():
 
 
 def claim_store(var):
-    """True when the caller's kernel may overwrite ``var.grad`` (it is the step's only write); records it."""
+    """True when the caller's kernel -- which writes EVERY element of ``var.grad`` -- may overwrite the slot: it is
+    the step's first write into it (later writers of the step, e.g. the other consumers of a shared weight,
+    accumulate onto it as usual); records the claim."""
     if var is None or getattr(var, "written_epoch", -1) == GRAD_EPOCH[0]:
         return False
-    if not STORE_FIRST or var.uses != 1:
+    if not STORE_FIRST:
         note_accumulate(var)
         return False
     var.written_epoch = GRAD_EPOCH[0]

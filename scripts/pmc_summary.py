@@ -13,6 +13,10 @@ Per kernel (aggregated over its dispatches in the profiled steps):
   LDS conf  SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra cycles per LDS-array cycle)
   HBM GB/s  (FETCH_SIZE + WRITE_SIZE) KiB / time
   L2 hit    TCC_HIT / (TCC_HIT + TCC_MISS)
+--roofline: two more columns per kernel -- the roofline time max(FLOP / 2.5 PF dense bf16, HBM bytes / 6.3 TB/s
+  measured copy rate) and that floor as a % of the measured time.  HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE
+  (MI355X_MICROARCH.md: FETCH_SIZE reports half the bytes of wide coalesced streaming reads; narrower or L2-resident
+  re-reads make this an over-estimate of the floor, i.e. the % an upper bound).
 """
 import collections
 import csv
@@ -58,7 +62,11 @@ def short(name):
     return n[:70]
 
 
-def main(prefix, top, step_only=False):
+PEAK_FLOPS = 2.5e15
+HBM_BPS = 6.3e12
+
+
+def main(prefix, top, step_only=False, roofline=False):
     # each pass is its own run: aggregate per kernel name within a pass, then join the passes by name
     aggs = []
     for i in (1, 2, 3):
@@ -78,8 +86,14 @@ def main(prefix, top, step_only=False):
     a1, a2, a3 = aggs
     rows = sorted(a1.items(), key=lambda t: -t[1]["dur"])
     tot = sum(a["dur"] for _, a in rows)
-    print("| kernel | calls | ms | TF/s | MFMA busy % | LDS bank-conflict % | HBM GB/s (rd+wr) | L2 hit % |")
-    print("|---|---|---|---|---|---|---|---|")
+    if roofline:
+        print("| kernel | calls | ms | TF/s | MFMA busy % | LDS bank-conflict % | HBM GB/s (rd+wr) | L2 hit % "
+              "| roofline ms (bound) | % of roofline |")
+        print("|---|---|---|---|---|---|---|---|---|---|")
+    else:
+        print("| kernel | calls | ms | TF/s | MFMA busy % | LDS bank-conflict % | HBM GB/s (rd+wr) | L2 hit % |")
+        print("|---|---|---|---|---|---|---|---|")
+    floor_tot = 0.0
     for name, a in rows[:top]:
         b, c = a2.get(name, {}), a3.get(name, {})
         dur = a["dur"]
@@ -90,12 +104,25 @@ def main(prefix, top, step_only=False):
         wr = c.get("WRITE_SIZE", 0) * 1024 / c["dur"] / 1e9 if c.get("dur") else 0
         hit = c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0)
         hit = 100.0 * c.get("TCC_HIT_sum", 0) / hit if hit else 0
-        print("| `%s` | %d | %.3f | %.0f | %.1f | %.1f | %.0f + %.0f | %.0f |" % (
-            name, a["calls"], dur * 1e3, tf, mf, lds, rd, wr, hit))
+        line = "| `%s` | %d | %.3f | %.0f | %.1f | %.1f | %.0f + %.0f | %.0f |" % (
+            name, a["calls"], dur * 1e3, tf, mf, lds, rd, wr, hit)
+        if roofline:
+            flops = a["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512
+            hbm = 2 * b.get("FETCH_SIZE", 0) * 1024 + c.get("WRITE_SIZE", 0) * 1024
+            t_mf, t_hbm = flops / PEAK_FLOPS, hbm / HBM_BPS
+            floor = max(t_mf, t_hbm)
+            floor_tot += floor
+            line += " %.3f (%s) | %.0f |" % (floor * 1e3, "MFMA" if t_mf > t_hbm else "HBM",
+                                             100.0 * floor / dur if dur else 0)
+        print(line)
     print("\nprofiled dispatches (pass 1%s): %d, total serialized kernel time %.2f ms" % (
         ", last step only" if step_only else "", sum(a["calls"] for _, a in rows), tot * 1e3))
+    if roofline:
+        shown = sum(a["dur"] for _, a in rows[:top])
+        print("roofline floor of the %d kernels shown: %.2f ms of their %.2f ms (%.0f %%)" % (
+            min(top, len(rows)), floor_tot * 1e3, shown * 1e3, 100.0 * floor_tot / shown if shown else 0))
 
 
 if __name__ == "__main__":
     pos = [v for v in sys.argv[1:] if not v.startswith("--")]
-    main(pos[0], int(pos[1]) if len(pos) > 1 else 40, "--last-step" in sys.argv)
+    main(pos[0], int(pos[1]) if len(pos) > 1 else 40, "--last-step" in sys.argv, "--roofline" in sys.argv)

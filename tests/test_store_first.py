@@ -25,14 +25,14 @@ def test_zero_grad_skips_only_store_written_slots():
     assert g.grad.abs().sum() == 0 and not b.skip_zero
 
 
-def test_claim_store_first_write_single_use_only(monkeypatch):
+def test_claim_store_first_write_only(monkeypatch):
     monkeypatch.setattr(V, "STORE_FIRST", True)
     g, (a, b, c) = _group()
     V.begin_grad_epoch()
-    a.uses, b.uses = 1, 2
-    assert V.claim_store(a)                       # first write, only use: overwrite
+    assert V.claim_store(a)                       # the step's first (full-slot) write: overwrite
     assert not V.claim_store(a)                   # a second write the same step accumulates
-    assert not V.claim_store(b)                   # two uses in flight: accumulate
+    V.note_accumulate(b)                          # b's first write accumulates ...
+    assert not V.claim_store(b)                   # ... so a later full-slot writer must too
     assert a.store_first and not b.store_first
     # next step: a's slot is skipped by the fill; an accumulating first write zeroes it before adding
     g.grad.fill_(3.0)
