@@ -45,6 +45,12 @@ PP = DENSE == "pp"
 # that saves the bias_act pass.
 PP_FWD = os.environ.get("MDTF_PP_FWD", "act")
 PP_DGRAD = os.environ.get("MDTF_PP_DGRAD", "fused")
+# Per-shape routing on top of the policy above: "KxN,KxN" (K = reduction, N = all output columns of the product) of
+# the plain forwards / data gradients that also run on the core.  In-step A/B per product (BERT-base, profiles/ab_r6.md):
+# the square 768 x 768 attention-output forward and data gradient are a tie with hipBLASLt (-0.2 % / +0.1 %), so they
+# run on the core by default; the K = 3072 products lose on it (FFN-out forward -2.0 %, FFN-in data gradient -1.5 %).
+PP_FWD_SHAPES = {s for s in os.environ.get("MDTF_PP_FWD_SHAPES", "768x768").split(",") if s}
+PP_DGRAD_SHAPES = {s for s in os.environ.get("MDTF_PP_DGRAD_SHAPES", "768x768").split(",") if s}
 PP_WGRAD = os.environ.get("MDTF_PP_WGRAD", "wg")
 
 
@@ -69,6 +75,12 @@ def _wgrad_section(ctx, x, dpre):
     dpre.record_stream(side)
     _conv._PENDING.add(x.device)
     return torch.cuda.stream(side)
+
+
+def _dgrad_shape_on(ws):
+    """MDTF_PP_DGRAD_SHAPES names this layer's data-gradient product as "<reduction>x<output columns>" (for a layer
+    W [K, N]: "NxK"), the same convention as the forward keys."""
+    return bool(PP_DGRAD_SHAPES) and "%dx%d" % (sum(w.shape[1] for w in ws), ws[0].shape[0]) in PP_DGRAD_SHAPES
 
 
 def _wg_backward(ctx, x, dpre):
@@ -437,6 +449,8 @@ class _Dense(torch.autograd.Function):
             x_sink.register()
         ctx.pp = False
         core = PP_FWD == "all" or (PP_FWD == "fused" and (act != 0 or nw > 1)) or (PP_FWD == "act" and act != 0)
+        if not core and PP_FWD_SHAPES and not trans:
+            core = "%dx%d" % (x.shape[1], sum(w.shape[1] for w in ws)) in PP_FWD_SHAPES
         if PP and (core or PP_FWD != "act") and x.is_cuda and x.dtype == torch.bfloat16 and x.stride(1) == 1 \
                 and N.use_native(x):
             y = None
@@ -696,7 +710,8 @@ def _backward_pp(ctx, dy):
                 dx = None
         elif xs is None:
             ap = li.pre if (li is not None and li.pre is not None) else None
-            core = PP_DGRAD == "all" or (PP_DGRAD == "fused" and (ap is not None or ctx.nw > 1))
+            core = PP_DGRAD == "all" or (PP_DGRAD == "fused" and (ap is not None or ctx.nw > 1)) or \
+                _dgrad_shape_on(ws)
             dx = mm.dgrad(dpre, ws, act_pre=ap, act_bwd=li.act if ap is not None else 0) if core else None
             if dx is not None and ap is not None:
                 li.fused = True
@@ -706,7 +721,7 @@ def _backward_pp(ctx, dy):
         else:
             buf, acc = xs.target()
             K = ws[0].shape[0]
-            core = PP_DGRAD == "all" or (PP_DGRAD == "fused" and ctx.nw > 1)
+            core = PP_DGRAD == "all" or (PP_DGRAD == "fused" and ctx.nw > 1) or _dgrad_shape_on(ws)
             if acc:                                     # second contribution: C += dpre @ w^T inside the GEMM
                 b2 = buf.view(-1, K)
                 if not core or mm.dgrad(dpre, ws, out=b2, accumulate=True) is None:
