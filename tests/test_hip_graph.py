@@ -272,8 +272,10 @@ def test_drain_waits_for_watchdog_retirement(monkeypatch):
         got = G._drain_comm_watchdog(timeout_s=30.0)
         assert got == wm and G.LAST_DRAIN[0] == "recorder"
         assert G._unretired(G._recorder_entries(), wm) == []
-        # the watchdog loop sleeps between polls, so right after synchronize() it normally still held the works
-        # and the drain had to poll; when it had already retired them the drain returns at once
-        assert held_before == 0 or G.LAST_DRAIN_POLLS[0] > 0
+        # the watchdog loop sleeps between polls, so right after synchronize() it normally still holds the works
+        # (held_before > 0) and the drain polls until they are retired; the watchdog may also retire them between
+        # that sample and the drain's first look (a round-6 suite run saw held_before = 3 and no poll), so the
+        # poll count is reported, not asserted -- the invariant is the line above: nothing unretired at return
+        assert held_before >= 0 and G.LAST_DRAIN_POLLS[0] >= 0
     finally:
         dist.destroy_process_group()
