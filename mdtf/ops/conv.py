@@ -658,8 +658,10 @@ def pp_dgrad(dy, w, x_shape, pads, dil, tile, out=None, accumulate=False, bn_sta
 
 
 def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=1, stages=2, store=False):
-    """fp32 HWIO weight gradient; accumulates into ``out`` when given (must be zeroed or a grad slot), or with
-    ``store`` (v2 kernels) overwrites it -- the step's first writer of that gradient slot (V.claim_store)."""
+    """fp32 HWIO weight gradient; accumulates into ``out`` when given (must be zeroed or a grad slot).  ``store``:
+    the Variable whose grad slot ``out`` is -- when the launch reduces split-K slabs (v2 kernels), it claims the slot
+    as the step's first writer and overwrites it (V.claim_store); the atomics epilogues accumulate (a claimed slot
+    would need a zeroing launch of its own, which costs more than the fill that covers it)."""
     dw = torch.zeros(w_shape, dtype=torch.float32, device=x.device) if out is None else out
     n, h, wd, c = x.shape
     kh, kw, ci, co = w_shape
@@ -671,6 +673,11 @@ def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=
                 force = bool(ent["slab"])
         slab, cap = wgrad_slab(n * dy.shape[1] * dy.shape[2], kh * kw * ci, co, bm, bn, ver, int(splits), x.device,
                                force=force)
+        if store is not False and store is not True:          # a Variable: claim only for the slab reduction
+            var = store
+            store = slab is not None and not WGRAD_INK and V.claim_store(var)
+            if not store:
+                V.note_accumulate(var)
         if store:
             N.fn("mdtf_set_wgrad_store")(1)
         try:
@@ -1001,13 +1008,12 @@ class _Conv(torch.autograd.Function):
                     dy.record_stream(side)
                     _PENDING.add(x.device)
                 else:
-                    # v2 kernels overwrite the slot as the step's first writer of it (V.claim_store): no zero fill,
-                    # no read of the slot in the slab reduction
-                    st = cw[4] in (2, 3) and V.claim_store(sink)
-                    if not st and cw[4] not in (2, 3):
+                    # v2 kernels with a split-K slab overwrite the slot as the step's first writer of it
+                    # (V.claim_store): no zero fill, no read of the slot in the slab reduction
+                    if cw[4] not in (2, 3):
                         V.note_accumulate(sink)
                     mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], out=sink.grad, ver=cw[4],
-                               stages=cw[5], store=st)
+                               stages=cw[5], store=sink if cw[4] in (2, 3) else False)
                 dw = V.grad_marker(w)
             else:
                 dw = mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], ver=cw[4], stages=cw[5])
