@@ -29,8 +29,12 @@ _TILE_DIMS = {0: (256, 256), 1: (256, 128), 2: (128, 256), 3: (128, 128), 4: (25
 _TILE_COST = {0: 1.0, 1: 1.14, 2: 1.10, 3: 1.35, 4: 1.05, 5: 1.16}
 CUS = 256
 
-# (layout, M, N, K) -> (tile, splits): measured choices (graph-timed on MI355X, bench/gemm_pp_probe.py)
+# (layout, M, N, K) -> (tile, splits): measured choices (graph-timed on MI355X, bench/gemm_pp_probe.py); MDTF_PP_TILES
+# "layout,M,N,K:tile,splits;..." pins more (in-step A/B)
 TILES = {}
+for _ent in filter(None, os.environ.get("MDTF_PP_TILES", "").split(";")):
+    _k, _v = _ent.split(":")
+    TILES[tuple(int(t) for t in _k.split(","))] = tuple(int(t) for t in _v.split(","))
 
 ACT = {None: 0, "relu": 1, "gelu": 2}
 
