@@ -131,6 +131,10 @@ class FlatGroup(object):
             v.skip_zero = bool(skip_stored and getattr(v, "store_first", False))
             if v.skip_zero:
                 skips.append((v.flat_offset, v.numel()))
+        if len(skips) > 1000:       # more holes than the one-launch fill takes (kFillMaxRanges): zero everything
+            for v in self.variables:
+                v.skip_zero = False
+            skips = []
         if not skips:
             self.grad.zero_()
             return
