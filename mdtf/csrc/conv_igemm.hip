@@ -104,7 +104,76 @@ struct ConvArgs {
   // v2 fwd / dgrad: first GEMM row of this launch (a tile-count tail split runs the last rows as a second launch
   // with smaller tiles, launch_fd_v2); rows [m_base, M)
   long long m_base;
+  // wgrad v2: fin_blocks extra workgroups (the last blocks of the grid) run the backward finalize of the BatchNorm
+  // whose output gradient the conv's data gradient just completed (fin_*; see fin_bwd_block)
+  int fin_blocks;
+  const float* fin_psum;
+  const float* fin_psq;
+  int fin_P, fin_C;
+  long long fin_M;
+  const float* fin_gamma;
+  const float* fin_mean;
+  const float* fin_invstd;
+  float* fin_ws;
 };
+
+// BatchNorm backward finalize of one 32-channel group, run by an extra workgroup of a weight-gradient launch: the
+// conv's data gradient (the previous launch) completed the BN's statistics Σ g·mask, Σ g·mask·x in fin_P partial
+// rows; this sums them (fp64 across the thread groups), writes k1 | k2 | k3 | dgamma | dbeta into fin_ws[5][C]
+// (dgamma / dbeta written, not accumulated: csrc/bn.hip mdtf_bn_dx_ws adds them into the slots) and re-zeroes the
+// partial rows -- the math of bn.hip finalize_bwd with zero_after = 3.  The finalize then costs no launch of its
+// own: it runs beside the weight gradient, which does not depend on it (ops.conv MDTF_BN_WG_FIN).
+// (the fields are passed by value: a reference to the kernel's ConvArgs would take its address and turn the GEMM
+// path's uniform buffer descriptors into per-lane values)
+__device__ __noinline__ void fin_bwd_block(float* psum, float* psq, int P, int C, long long M, const float* gamma,
+                                           const float* meanp, const float* invstdp, float* ws, int blk, char* smem) {
+  const int G = blockDim.x / 32;
+  const int lc = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int c = blk * 32 + lc;
+  const bool own = grp == 0 && c < C;
+  const float mu = own ? meanp[c] : 0.f, inv = own ? invstdp[c] : 0.f;
+  const float gm = own && gamma ? gamma[c] : 1.f;
+  float s[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    int r = grp;
+    for (; r + 3 * G < P; r += 4 * G) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s[u] += psum[(long long)(r + u * G) * C + c];
+        q[u] += psq[(long long)(r + u * G) * C + c];
+      }
+    }
+    for (; r < P; r += G) {
+      s[0] += psum[(long long)r * C + c];
+      q[0] += psq[(long long)r * C + c];
+    }
+    // re-zero the rows this thread read (no other thread reads them): the persistent statistics pool's next user
+    // accumulates into zeros
+    for (r = grp; r < P; r += G) {
+      psum[(long long)r * C + c] = 0.f;
+      psq[(long long)r * C + c] = 0.f;
+    }
+  }
+  double* L0 = reinterpret_cast<double*>(smem);
+  double* L1 = L0 + G * 32;
+  L0[grp * 32 + lc] = (double)s[0] + (double)s[1] + (double)s[2] + (double)s[3];
+  L1[grp * 32 + lc] = (double)q[0] + (double)q[1] + (double)q[2] + (double)q[3];
+  __syncthreads();
+  if (!own) return;
+  double sdz = 0.0, sdzx = 0.0;
+  for (int g = 0; g < G; ++g) {
+    sdz += L0[g * 32 + lc];
+    sdzx += L1[g * 32 + lc];
+  }
+  const float db = (float)sdz;
+  const float dg = (float)((sdzx - (double)mu * sdz) * inv);
+  ws[3 * C + c] = dg;
+  ws[4 * C + c] = db;
+  const float ak = gm * inv, invM = 1.f / (float)M;
+  ws[c] = ak;
+  ws[C + c] = -ak * inv * dg * invM;
+  ws[2 * C + c] = ak * (-db * invM + mu * inv * dg * invM);
+}
 
 // m, sh with floor(n / d) = (n * m) >> sh for every 0 <= n < 2^31: l = ceil(log2 d), m = ceil(2^(31+l) / d)
 // (m * d - 2^(31+l) < d <= 2^l; m < 2^32 for d >= 1)
@@ -1780,9 +1849,15 @@ __global__ void __launch_bounds__(64 * NW, (wgrad_min_waves<BM, BN, STAGES, NW>(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int tiles_mn = a.mtiles * a.ntiles;
+  const int nwg = static_cast<int>(gridDim.x) - a.fin_blocks;     // the GEMM's workgroups (then the finalize's)
+  if (static_cast<int>(blockIdx.x) >= nwg) {
+    fin_bwd_block(const_cast<float*>(a.fin_psum), const_cast<float*>(a.fin_psq), a.fin_P, a.fin_C, a.fin_M,
+                  a.fin_gamma, a.fin_mean, a.fin_invstd, a.fin_ws, static_cast<int>(blockIdx.x) - nwg, smem_raw);
+    return;
+  }
   // consecutive blocks run on different XCDs (round robin); with wg_xcd the tiles of one pixel split
   // (which read the same DY rows / X pixels) are consecutive in the remapped order, i.e. on one XCD's L2
-  const int lb = a.wg_xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int lb = a.wg_xcd ? xcd_remap(blockIdx.x, nwg) : blockIdx.x;
   const int tile = lb % tiles_mn;
   const int split = lb / tiles_mn;
   const int mt = tile / a.ntiles, nt = tile % a.ntiles;
@@ -2042,7 +2117,7 @@ __global__ void __launch_bounds__(64 * NW, (wgrad_min_waves<BM, BN, STAGES, NW>(
     // with sc1 loads (deterministic whatever the arrival order) and adds the sum into DW once -- no reduction
     // launch, no agent fences (MI355X_MICROARCH.md: publish-large, Valid forms row 1; gemm_wg.hip, +2 % BERT).
     constexpr int NT = 64 * NW;
-    const int nsp = static_cast<int>(gridDim.x) / tiles_mn;   // every split is non-empty (launch_wgrad_v2)
+    const int nsp = nwg / tiles_mn;                          // every split is non-empty (launch_wgrad_v2)
     float* tslab = a.slab + (long long)tile * nsp * (BM * BN);
     const __amdgpu_buffer_rsrc_t srs =
         __builtin_amdgcn_make_buffer_rsrc(tslab, (short)0, nsp * (BM * BN) * 4, 0x00020000);
@@ -2248,6 +2323,14 @@ long long g_wg_cnt_n = 0;
 // first writer of that gradient slot, ops.conv / train.variables claim_store): the slab reduction stores its sum;
 // without one (fp32 atomics, in-kernel split reduction) DW is zeroed before the kernel.
 int g_wg_store = 0;
+// BN backward finalize job for the next weight-gradient launch (mdtf_set_wgrad_fin; C = 0: none)
+struct FinReq {
+  const float *psum, *psq, *gamma, *mean, *invstd;
+  float* ws;
+  int P, C;
+  long long M;
+};
+FinReq g_wg_fin = {};
 hipEvent_t slab_event() {
   static hipEvent_t ev = [] {
     hipEvent_t e = nullptr;
@@ -2290,12 +2373,28 @@ int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
     b.slab_nt = nt;
   }
   const int store = g_wg_store;
+  if (g_wg_fin.C > 0) {
+    // finalize blocks beside the GEMM's (their reduction buffer: 2 x (threads / 32) x 32 doubles of the LDS)
+    b.fin_blocks = static_cast<int>(ceil_div(g_wg_fin.C, 32));
+    b.fin_psum = g_wg_fin.psum;
+    b.fin_psq = g_wg_fin.psq;
+    b.fin_P = g_wg_fin.P;
+    b.fin_C = g_wg_fin.C;
+    b.fin_M = g_wg_fin.M;
+    b.fin_gamma = g_wg_fin.gamma;
+    b.fin_mean = g_wg_fin.mean;
+    b.fin_invstd = g_wg_fin.invstd;
+    b.fin_ws = g_wg_fin.ws;
+    g_wg_fin = FinReq{};
+  } else {
+    b.fin_blocks = 0;
+  }
   if (store && !(b.slab && !b.cnt)) {     // accumulating epilogues: the slot must start at zero
     if (hipMemset2DAsync(a.dw, (size_t)a.ld_dw * 4, 0, (size_t)a.Cout * 4, (size_t)R, st) != hipSuccess)
       return MDTF_EUNSUPPORTED;
   }
-  hipLaunchKernelGGL((conv_wgrad_v2<BM, BN, STAGES, NW, PIPE>), dim3(a.mtiles * a.ntiles * splits), dim3(64 * NW), lds,
-                     st, b);
+  hipLaunchKernelGGL((conv_wgrad_v2<BM, BN, STAGES, NW, PIPE>), dim3(a.mtiles * a.ntiles * splits + b.fin_blocks),
+                     dim3(64 * NW), lds, st, b);
   MDTF_LAUNCH_CHECK();
   if (b.slab && !b.cnt) {
     if (g_slab_stream && g_slab_stream != st) {
@@ -2677,6 +2776,16 @@ MDTF_EXPORT int mdtf_conv_dgrad_v2(const void* dy, const void* w, void* dx, int 
       hipLaunchKernelGGL(dgrad_zero_classes<false>, dim3(blocks), dim3(256), 0, st, a, C8);
     MDTF_LAUNCH_CHECK();
   }
+  return 0;
+}
+
+// The next v2 weight-gradient launch also runs the backward finalize of a BatchNorm (see fin_bwd_block): psum / psq
+// [P][C] partial statistics (re-zeroed), gamma (or null), mean, invstd [C], M rows; ws [5][C] receives k1 | k2 | k3 |
+// dgamma | dbeta.  The request is consumed by that launch.
+MDTF_EXPORT int mdtf_set_wgrad_fin(const float* psum, const float* psq, int P, const float* gamma, const float* mean,
+                                   const float* invstd, float* ws, long long M, int C) {
+  if (C < 0 || (C > 0 && (!psum || !psq || !mean || !invstd || !ws || P <= 0 || M <= 0))) return MDTF_EINVAL;
+  g_wg_fin = FinReq{psum, psq, gamma, mean, invstd, ws, P, C, M};
   return 0;
 }
 

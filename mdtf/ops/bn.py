@@ -29,6 +29,11 @@ FUSED_BWD = [0]      # backward passes that took their statistics from the dgrad
 # statistics instead of in the BN's backward (after the conv's weight gradient).  Measured -3 % in the captured
 # ResNet-50 step (the 45 fork / join pairs cost more than the finalize latency they hide, profiles/ab_r5.md): off.
 EARLY_FIN = os.environ.get("MDTF_BN_EARLY_FIN", "0") == "1"
+# MDTF_BN_WG_FIN=1 (default): the backward finalize runs as extra workgroups of the conv's weight-gradient launch that
+# follows the data gradient completing the statistics (csrc/conv_igemm.hip fin_bwd_block) -- same stream, no launch
+# and no fork of its own; the BN backward then runs only its input-gradient pass (mdtf_bn_dx_ws).
+WG_FIN = os.environ.get("MDTF_BN_WG_FIN", "1") == "1"
+WG_FIN_USED = [0]    # backward passes whose finalize rode on a weight-gradient launch (tests)
 EARLY_USED = [0]     # backward passes that used an early finalize (tests)
 _FIN_SIDE = {}
 
@@ -129,7 +134,10 @@ class _BNTrain(torch.autograd.Function):
             if EARLY_FIN and x.is_cuda and not N.deterministic():
                 def fin(sbuf, g=g, mean=mean, invstd=invstd, M=M, C=C):
                     return _early_finalize(sbuf, g, mean, invstd, M, C)
-            ctx.out_sink.stat_req = (x, mask, fin)
+            # the weight-gradient launch that follows the completing data gradient may run this BN's finalize
+            # (ops.conv _Conv.backward): the arguments it needs
+            wgf = (g, mean, invstd, M, C) if (WG_FIN and x.is_cuda and not N.deterministic()) else None
+            ctx.out_sink.stat_req = (x, mask, fin, wgf)
         return y
 
     @staticmethod
@@ -145,7 +153,8 @@ class _BNTrain(torch.autograd.Function):
             if early is not None and (pstats is None or dy is not None):
                 # finalized early from statistics that turned out incomplete: wait for it (it re-zeroed the
                 # partial rows) and drop its workspace -- nothing reached the slots
-                torch.cuda.current_stream(x.device).wait_event(early[1])
+                if early[1] is not None:
+                    torch.cuda.current_stream(x.device).wait_event(early[1])
                 early = None
             if pstats is not None and dy is not None:
                 # part of dy came through plain autograd: the epilogue statistics are incomplete
@@ -158,7 +167,7 @@ class _BNTrain(torch.autograd.Function):
         if BWD_TRACE is not None:
             BWD_TRACE.append((tuple(x.shape), ctx.has_res, why))
         if dy is None:
-            if early is not None:                        # join the side stream (captures must not end forked)
+            if early is not None and early[1] is not None:   # join the side stream (captures must not end forked)
                 torch.cuda.current_stream(x.device).wait_event(early[1])
             return (None,) * 10
         dy = dy.contiguous()
@@ -188,13 +197,16 @@ class _BNTrain(torch.autograd.Function):
         if pstats is not None and early is not None:
             from . import conv as _conv
             ws, ev = early
-            torch.cuda.current_stream(x.device).wait_event(ev)
+            if ev is not None:                           # side-stream early finalize (EARLY_FIN)
+                torch.cuda.current_stream(x.device).wait_event(ev)
+                EARLY_USED[0] += 1
+            else:                                        # rode on the conv's weight-gradient launch (WG_FIN)
+                WG_FIN_USED[0] += 1
             N.check(N.fn("mdtf_bn_dx_ws")(N.ptr(dy), N.ptr(x), N.ptr(mask if ctx.relu else None), N.ptr(dx),
                                           N.ptr(dres), M, C, N.ptr(ws), N.ptr(dgamma), N.ptr(dbeta), int(ctx.relu),
                                           accum, N.stream_ptr()), "bn_dx_ws")
             _conv.bwd_stats_release(pstats, True)        # the early finalize re-zeroed it
             FUSED_BWD[0] += 1
-            EARLY_USED[0] += 1
         elif pstats is not None:
             from . import conv as _conv
             ws = torch.empty(3 * C, dtype=torch.float32, device=x.device)

@@ -28,6 +28,7 @@ N.register("mdtf_conv_dgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.P, N.P, 
 N.register("mdtf_conv_wgrad_v2", [N.P, N.P, N.P] + [N.I] * 18 + [N.P, N.I, N.P])
 N.register("mdtf_set_slab_stream", [N.P])
 N.register("mdtf_set_wgrad_store", [N.I])
+N.register("mdtf_set_wgrad_fin", [N.P, N.P, N.I, N.P, N.P, N.P, N.P, N.L, N.I])
 
 # split-K weight gradients: per-split partial slabs + one reduction pass (plain stores) instead of fp32
 # atomics into DW.  Measured on MI355X (scripts/gpu.sh envab): +0.4 % BERT-base (dense GEMM weight
@@ -657,11 +658,13 @@ def pp_dgrad(dy, w, x_shape, pads, dil, tile, out=None, accumulate=False, bn_sta
     return dx
 
 
-def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=1, stages=2, store=False):
+def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=1, stages=2, store=False, fin=None):
     """fp32 HWIO weight gradient; accumulates into ``out`` when given (must be zeroed or a grad slot).  ``store``:
     the Variable whose grad slot ``out`` is -- when the launch reduces split-K slabs (v2 kernels), it claims the slot
     as the step's first writer and overwrites it (V.claim_store); the atomics epilogues accumulate (a claimed slot
-    would need a zeroing launch of its own, which costs more than the fill that covers it)."""
+    would need a zeroing launch of its own, which costs more than the fill that covers it).  ``fin``: (activation
+    sink, statistics buffer, gamma, mean, invstd, M, C) of the BatchNorm whose backward finalize this launch runs
+    in extra workgroups (v2 kernels; its result goes to the sink's ``early`` for ops.bn)."""
     dw = torch.zeros(w_shape, dtype=torch.float32, device=x.device) if out is None else out
     n, h, wd, c = x.shape
     kh, kw, ci, co = w_shape
@@ -680,6 +683,11 @@ def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=
                 V.note_accumulate(var)
         if store:
             N.fn("mdtf_set_wgrad_store")(1)
+        if fin is not None:
+            xs, sbuf, g, mean, invstd, M, C = fin
+            fws = torch.empty(5 * C, dtype=torch.float32, device=x.device)
+            N.check(N.fn("mdtf_set_wgrad_fin")(N.ptr(sbuf[0]), N.ptr(sbuf[1]), int(sbuf.shape[1]), N.ptr(g),
+                                               N.ptr(mean), N.ptr(invstd), N.ptr(fws), int(M), int(C)), "wgrad_fin")
         try:
             with slab_side(slab if out is not None else None), wgrad_tickets(slab):
                 N.check(N.fn("mdtf_conv_wgrad_v2")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1],
@@ -689,6 +697,10 @@ def mdtf_wgrad(x, dy, w_shape, stride, pads, dil, bm, bn, splits, out=None, ver=
         finally:
             if store:
                 N.fn("mdtf_set_wgrad_store")(0)
+            if fin is not None:
+                N.fn("mdtf_set_wgrad_fin")(None, None, 0, None, None, None, None, 0, 0)   # (consumed or cancelled)
+        if fin is not None:
+            xs.early = (fws, None)
         return dw
     N.check(N.fn("mdtf_conv_wgrad")(N.ptr(x), N.ptr(dy), N.ptr(dw), n, h, wd, c, dy.shape[1], dy.shape[2], co, kh,
                                     kw, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1], bm, bn, int(splits),
@@ -806,10 +818,16 @@ def bwd_stats_acquire(device, C, slots):
 
 def _early_finalize(xs, sbuf):
     """The BN whose output gradient this data gradient just completed may finalize its backward statistics now, on
-    a side stream beside this conv's weight gradient (``ops.bn`` EARLY_FIN), instead of after it."""
+    a side stream beside this conv's weight gradient (``ops.bn`` EARLY_FIN), instead of after it.  Returns the
+    arguments of a finalize that can ride on this conv's weight-gradient launch instead (``ops.bn`` WG_FIN) or
+    None."""
     req = xs.stat_req
     if req is not None and len(req) > 2 and req[2] is not None:
         xs.early = req[2](sbuf)
+        return None
+    if req is not None and len(req) > 3 and req[3] is not None:
+        return (xs, sbuf) + tuple(req[3])
+    return None
 
 
 def bwd_stats_release(buf, zeroed):
@@ -886,6 +904,7 @@ class _Conv(torch.autograd.Function):
         stride, pads, dil = ctx.args
         dy = dy.contiguous()
         need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        fin_job = None        # a BN backward finalize this conv's weight-gradient launch may run (ops.bn WG_FIN)
         dx = dw = None
         cd = choose("dgrad", x.shape, w.shape, stride, pads, dil) if need_dx else None
         cw = choose("wgrad", x.shape, w.shape, stride, pads, dil) if need_dw else None
@@ -927,7 +946,7 @@ class _Conv(torch.autograd.Function):
             xs.written(ws_dual(dy, w, pc, x.shape, bn_stats=bst))
             if bst is not None:
                 xs.stats = sbuf
-                _early_finalize(xs, sbuf)
+                fin_job = _early_finalize(xs, sbuf)
             DUAL_FUSED[0] += 1
             need_dx = False
         if need_dx and cd[0] == "winograd":
@@ -946,7 +965,7 @@ class _Conv(torch.autograd.Function):
                                     acc_src=pend))
                 if bst is not None:
                     xs.stats = sbuf
-                    _early_finalize(xs, sbuf)
+                    fin_job = _early_finalize(xs, sbuf)
             else:
                 dx = ws_dgrad(dy, w, x.shape, pads, dil, tile)
         elif need_dx and cd[0] == "pp":
@@ -962,7 +981,7 @@ class _Conv(torch.autograd.Function):
                                     acc_src=pend))
                 if bst is not None:
                     xs.stats = sbuf
-                    _early_finalize(xs, sbuf)
+                    fin_job = _early_finalize(xs, sbuf)
             else:
                 dx = pp_dgrad(dy, w, x.shape, pads, dil, cd[1])
         elif need_dx and not lib_dx:
@@ -978,7 +997,7 @@ class _Conv(torch.autograd.Function):
                                       accumulate=acc, bn_stats=bst, acc_src=pend))
                 if bst is not None:
                     xs.stats = sbuf
-                    _early_finalize(xs, sbuf)
+                    fin_job = _early_finalize(xs, sbuf)
                 dx = None
             else:
                 dx = mdtf_dgrad(dy, w, x.shape, stride, pads, dil, cd[1], cd[2], cd[4], cd[5])
@@ -1013,7 +1032,9 @@ class _Conv(torch.autograd.Function):
                     if cw[4] not in (2, 3):
                         V.note_accumulate(sink)
                     mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], out=sink.grad, ver=cw[4],
-                               stages=cw[5], store=sink if cw[4] in (2, 3) else False)
+                               stages=cw[5], store=sink if cw[4] in (2, 3) else False,
+                               fin=fin_job if cw[4] in (2, 3) else None)
+                    fin_job = None
                 dw = V.grad_marker(w)
             else:
                 dw = mdtf_wgrad(x, dy, w.shape, stride, pads, dil, cw[1], cw[2], cw[3], ver=cw[4], stages=cw[5])

@@ -2468,6 +2468,28 @@ def test_tied_decoder_padded_vocab_matches_fp32():
     assert not wv.grad_padded[Vn:].any() and not bv.grad_padded[Vn:].any()
 
 
+def test_bn_backward_finalize_on_wgrad_launch_matches_inline(monkeypatch):
+    """The BN backward finalize run by extra workgroups of the conv's weight-gradient launch (MDTF_BN_WG_FIN, the
+    default: csrc/conv_igemm.hip fin_bwd_block) == the finalize launch inside the BN backward: same loss and the
+    same gradients on a two-stage ResNet (up to the order of fp32 atomics); the fused path must actually run."""
+    from mdtf.ops import bn
+    torch.manual_seed(10)
+    x = torch.randn(8, 64, 64, 3)
+    y = torch.randint(0, 16, (8,))
+    monkeypatch.setattr(bn, "EARLY_FIN", False)
+    monkeypatch.setattr(bn, "WG_FIN", True)
+    n0 = bn.WG_FIN_USED[0]
+    lf, gf = _one_step(DEV, torch.bfloat16, x, y, blocks=[1, 1], grads=True)
+    assert bn.WG_FIN_USED[0] > n0
+    monkeypatch.setattr(bn, "WG_FIN", False)
+    n1 = bn.WG_FIN_USED[0]
+    li, gi = _one_step(DEV, torch.bfloat16, x, y, blocks=[1, 1], grads=True)
+    assert bn.WG_FIN_USED[0] == n1
+    assert lf == li
+    for k in gi:
+        assert _rel(gf[k], gi[k]) < 1e-4, (k, _rel(gf[k], gi[k]))
+
+
 def test_bn_backward_early_finalize_matches_inline(monkeypatch):
     """The BN backward finalize issued early on a side stream (MDTF_BN_EARLY_FIN=1: right after the data gradient
     that completes its statistics, beside the conv weight gradient) == the finalize inside the BN backward:
@@ -2477,6 +2499,7 @@ def test_bn_backward_early_finalize_matches_inline(monkeypatch):
     torch.manual_seed(9)
     x = torch.randn(8, 64, 64, 3)
     y = torch.randint(0, 16, (8,))
+    monkeypatch.setattr(bn, "WG_FIN", False)          # inline = the finalize launch inside the BN backward
     monkeypatch.setattr(bn, "EARLY_FIN", True)
     n0 = bn.EARLY_USED[0]
     le, ge = _one_step(DEV, torch.bfloat16, x, y, blocks=[1, 1], grads=True)
