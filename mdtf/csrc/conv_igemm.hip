@@ -104,9 +104,9 @@ struct ConvArgs {
   // v2 fwd / dgrad: first GEMM row of this launch (a tile-count tail split runs the last rows as a second launch
   // with smaller tiles, launch_fd_v2); rows [m_base, M)
   long long m_base;
-  // wgrad v2: fin_blocks extra workgroups (the last blocks of the grid) run the backward finalize of the BatchNorm
+  // wgrad v2: fin_blocks extra workgroups (the first blocks of the grid, or the last) run the backward finalize of the BatchNorm
   // whose output gradient the conv's data gradient just completed (fin_*; see fin_bwd_block)
-  int fin_blocks;
+  int fin_blocks, fin_first;
   const float* fin_psum;
   const float* fin_psq;
   int fin_P, fin_C;
@@ -1849,15 +1849,19 @@ __global__ void __launch_bounds__(64 * NW, (wgrad_min_waves<BM, BN, STAGES, NW>(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int tiles_mn = a.mtiles * a.ntiles;
-  const int nwg = static_cast<int>(gridDim.x) - a.fin_blocks;     // the GEMM's workgroups (then the finalize's)
-  if (static_cast<int>(blockIdx.x) >= nwg) {
+  // the finalize's workgroups last (default) or first (MDTF_BN_WG_FIN_FIRST=1: dispatched with the first round;
+  // measured neutral), the GEMM's in the rest
+  const int nwg = static_cast<int>(gridDim.x) - a.fin_blocks;
+  const int fb = a.fin_first ? static_cast<int>(blockIdx.x) : static_cast<int>(blockIdx.x) - nwg;
+  if (fb >= 0 && fb < a.fin_blocks) {
     fin_bwd_block(const_cast<float*>(a.fin_psum), const_cast<float*>(a.fin_psq), a.fin_P, a.fin_C, a.fin_M,
-                  a.fin_gamma, a.fin_mean, a.fin_invstd, a.fin_ws, static_cast<int>(blockIdx.x) - nwg, smem_raw);
+                  a.fin_gamma, a.fin_mean, a.fin_invstd, a.fin_ws, fb, smem_raw);
     return;
   }
+  const int gb = a.fin_first ? static_cast<int>(blockIdx.x) - a.fin_blocks : static_cast<int>(blockIdx.x);
   // consecutive blocks run on different XCDs (round robin); with wg_xcd the tiles of one pixel split
   // (which read the same DY rows / X pixels) are consecutive in the remapped order, i.e. on one XCD's L2
-  const int lb = a.wg_xcd ? xcd_remap(blockIdx.x, nwg) : blockIdx.x;
+  const int lb = a.wg_xcd ? xcd_remap(gb, nwg) : gb;
   const int tile = lb % tiles_mn;
   const int split = lb / tiles_mn;
   const int mt = tile / a.ntiles, nt = tile % a.ntiles;
@@ -2385,9 +2389,15 @@ int launch_wgrad_v2(ConvArgs& a, int splits, hipStream_t st) {
     b.fin_mean = g_wg_fin.mean;
     b.fin_invstd = g_wg_fin.invstd;
     b.fin_ws = g_wg_fin.ws;
+    static const int first = [] {      // measured neutral (r6w): 12973 vs 12972 img/s
+      const char* e = getenv("MDTF_BN_WG_FIN_FIRST");
+      return (e && e[0] == '1') ? 1 : 0;
+    }();
+    b.fin_first = first;
     g_wg_fin = FinReq{};
   } else {
     b.fin_blocks = 0;
+    b.fin_first = 0;
   }
   if (store && !(b.slab && !b.cnt)) {     // accumulating epilogues: the slot must start at zero
     if (hipMemset2DAsync(a.dw, (size_t)a.ld_dw * 4, 0, (size_t)a.Cout * 4, (size_t)R, st) != hipSuccess)
