@@ -643,6 +643,27 @@ MDTF_EXPORT int mdtf_bn_fwd_stats(const void* x, const void* res, void* y, uint8
   return 0;
 }
 
+// The finalize of mdtf_bn_fwd_stats alone: mean / invstd, the moving statistics and scale / shift (ws[0, C) /
+// ws[C, 2C)) for a consumer that applies them itself (the 1x1 conv's operand, mdtf_conv_ws_bna); partials re-zeroed.
+MDTF_EXPORT int mdtf_bn_fwd_coeffs(long long M, int C, const float* gamma, const float* beta, float* mmean,
+                                   float* mvar, float decay, float eps, float* mean, float* invstd, const float* psum,
+                                   const float* psq, int P, float* ws, hipStream_t st) {
+  if (C % 8) return MDTF_EINVAL;
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3(ceil_div(C, kFinCh)), dim3(kFinCh * kFinGroups), 0, st, psum, psq, P, M,
+                     C, gamma, beta, mmean, mvar, decay, eps, mean, invstd, ws, ws + C, 1);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
+// The apply of mdtf_bn_fwd_stats alone, from the coefficients mdtf_bn_fwd_coeffs wrote (ss = scale[C], shift[C]).
+MDTF_EXPORT int mdtf_bn_apply_ss(const void* x, void* y, uint8_t* mask, long long M, int C, const float* ss, int relu,
+                                 hipStream_t st) {
+  if (C % 8) return MDTF_EINVAL;
+  launch_apply(x, nullptr, y, mask, M * C / 8, C, ss, ss + C, relu, st);
+  MDTF_LAUNCH_CHECK();
+  return 0;
+}
+
 // Training forward of relu(BN(x) + BN2(r)) when both convs emitted their statistics partials: both finalizes,
 // then one apply pass.  mean/invstd and mean2/invstd2 are saved for the two backward passes.
 MDTF_EXPORT int mdtf_bn_fwd_dual(const void* x, const void* r, void* y, uint8_t* mask, long long M, int C,

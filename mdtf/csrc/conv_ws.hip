@@ -40,6 +40,7 @@ extern template int dispatch_ws<1>(WsArgs&, int, int, int, int, int, hipStream_t
 extern template int dispatch_ws<2>(WsArgs&, int, int, int, int, int, hipStream_t);
 extern template int dispatch_ws<3>(WsArgs&, int, int, int, int, int, hipStream_t);
 extern template int dispatch_ws<4>(WsArgs&, int, int, int, int, int, hipStream_t);
+extern template int dispatch_ws<5>(WsArgs&, int, int, int, int, int, hipStream_t);
 template int dispatch_ws_dual<0>(WsArgs&, int, int, int, hipStream_t);
 template int dispatch_ws_dual<3>(WsArgs&, int, int, int, hipStream_t);
 }  // namespace ws
@@ -87,7 +88,7 @@ int conv_ws_impl(const void* src, const void* wgt, void* out, int N, int H, int 
                  int Ncol, int KH, int KW, int SH, int SW, int PH, int PW, int DH, int DW, int wmode, int tile,
                  int grid_cap, float* ssum, float* ssq, int sslots, const void* bx, const void* bmask, float* bsum,
                  float* bsq, int bslots, int accumulate, const void* acc_src, const void* acc_mask,
-                 hipStream_t st) {
+                 hipStream_t st, const float* bn_ss = nullptr, void* bn_y = nullptr, void* bn_mask = nullptr) {
   WsArgs a{};
   a.cs = cs;
   a.src = (const bf16_t*)src;
@@ -120,6 +121,13 @@ int conv_ws_impl(const void* src, const void* wgt, void* out, int N, int H, int 
   a.epf = ws_epf();
   const bool stats = ssum != nullptr, bstat = bsum != nullptr;
   if (stats && bstat) return MDTF_EINVAL;
+  if (bn_ss) {                           // BN + ReLU applied to the operand (epilogue mode 5)
+    if (!stats || accumulate || !a.direct || wmode != 0 || !bn_y || !bn_mask || a.K > 128) return MDTF_EINVAL;
+    a.bn_ss = bn_ss;
+    a.bn_y = (bf16_t*)bn_y;
+    a.bn_mask = (uint8_t*)bn_mask;
+    return dispatch_ws<5>(a, tp, nw, cg, d, grid_cap, st);
+  }
   if (stats) return accumulate ? MDTF_EINVAL : dispatch_ws<1>(a, tp, nw, cg, d, grid_cap, st);
   if (bstat) return accumulate ? dispatch_ws<4>(a, tp, nw, cg, d, grid_cap, st)
                                : dispatch_ws<3>(a, tp, nw, cg, d, grid_cap, st);
@@ -134,6 +142,16 @@ MDTF_EXPORT int mdtf_conv_ws(const void* src, const void* wgt, void* out, int N,
                              const void* acc_src, const void* acc_mask, hipStream_t st) {
   return conv_ws_impl(src, wgt, out, N, H, W, C, C, OH, OW, Ncol, KH, KW, SH, SW, PH, PW, DH, DW, wmode, tile,
                       grid_cap, ssum, ssq, sslots, bx, bmask, bsum, bsq, bslots, accumulate, acc_src, acc_mask, st);
+}
+
+// 1x1 / stride-1 forward (with forward BN statistics) whose operand is a = relu(x * scale + shift), the output of a
+// training BatchNorm + ReLU applied on the fly: ss = scale[C] then shift[C] (the BN's finalize), a and its ReLU
+// mask (1 bit per element, as mdtf_bn_fwd_stats writes them) are written once for the backward.  C <= 128.
+MDTF_EXPORT int mdtf_conv_ws_bna(const void* x, const void* wgt, void* out, int N, int H, int W, int C, int Ncol,
+                                 int tile, int grid_cap, float* ssum, float* ssq, int sslots, const float* ss,
+                                 void* a_out, void* mask, hipStream_t st) {
+  return conv_ws_impl(x, wgt, out, N, H, W, C, C, H, W, Ncol, 1, 1, 1, 1, 0, 0, 1, 1, 0, tile, grid_cap, ssum, ssq,
+                      sslots, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, nullptr, st, ss, a_out, mask);
 }
 
 // Fused fan-out data gradient of a block input x that feeds a 1x1 / stride-1 convolution (gradient dy1

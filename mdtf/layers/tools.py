@@ -174,27 +174,28 @@ def bias(bias_shape):
 
 
 def conv_bn(layer_name, x, out_channels, kernel_size=3, stride=1, relu=True, residual=None, training=True,
-            bn_decay=0.9, bn_epsilon=1e-5, zero_gamma=False, padding=None, defer=False, pool=None):
+            bn_decay=0.9, bn_epsilon=1e-5, zero_gamma=False, padding=None, defer=False, pool=None, on_consumer=False):
     """conv (no bias) → BN (→ +residual) (→ ReLU), ResNet v1.5 building unit.
 
     Stride>1 convs use TF-official "fixed padding" (symmetric ``(k-1)//2``).  ``defer``: the BN may be
     returned unapplied (``ops.bn.DeferredBN``) for the residual BN that adds it to apply (GPU training).
     ``pool = (ksize, stride, padding)``: a max pool after the ReLU (fused with the BN on the GPU).
+    ``on_consumer``: the output's only reader is a 1x1 conv, which may apply the BN + ReLU itself (GPU training).
     """
     variables = conv_bn_variables(layer_name, x, out_channels, kernel_size, zero_gamma=zero_gamma)
     return conv_bn_apply(x, variables, kernel_size, stride, relu, residual, training, bn_decay, bn_epsilon, padding,
-                         defer, pool)
+                         defer, pool, on_consumer)
 
 
 def conv_bn_apply(x, variables, kernel_size=3, stride=1, relu=True, residual=None, training=True, bn_decay=0.9,
-                  bn_epsilon=1e-5, padding=None, defer=False, pool=None):
+                  bn_epsilon=1e-5, padding=None, defer=False, pool=None, on_consumer=False):
     """:func:`conv_bn` on variables already made by :func:`conv_bn_variables`."""
     k = kernel_size
     if padding is None:
         padding = "SAME" if stride == 1 else ((k - 1) // 2, (k - 1) // 2)
     w, gamma, beta, mm, mv = variables
     return ops.conv_bn(x, w, gamma, beta, mm, mv, stride, padding, training, bn_decay, bn_epsilon, relu, residual,
-                       defer=defer, pool=pool)
+                       defer=defer, pool=pool, on_consumer=on_consumer)
 
 
 def conv_bn_variables(layer_name, x, out_channels, kernel_size=3, zero_gamma=False, **unused):

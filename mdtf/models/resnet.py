@@ -57,7 +57,8 @@ class ResNet(Model):
                 # (ops.actsink, one fused pass over the block input's gradient)
                 sc_vars = tools.conv_bn_variables("shortcut", x, 4 * filters, 1, **kw)
             y = tools.conv_bn("conv1", x, filters, 1, 1, relu=True, **kw)
-            y = tools.conv_bn("conv2", y, filters, 3, stride, relu=True, **kw)
+            # (conv3 is its output's only reader: it may apply this BN + ReLU to its operand, ops.bn ON_CONSUMER)
+            y = tools.conv_bn("conv2", y, filters, 3, stride, relu=True, on_consumer=True, **kw)
             if proj and PROJ_LATE:
                 shortcut = tools.conv_bn_apply(x, sc_vars, 1, stride, relu=False, defer=True, **kw)
             elif not proj:

@@ -22,6 +22,8 @@ N.register("mdtf_maxpool_bn_bwd", [N.P] * 4 + [N.I] * 12 + [N.P] * 8 + [N.P])
 N.register("mdtf_bn_bwd_dual", [N.P] * 6 + [N.L, N.I] + [N.P] * 7 + [N.I] + [N.P] * 6 + [N.P])
 N.register("mdtf_bn_bwd_finalize_ws", [N.L, N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P, N.P])
 N.register("mdtf_bn_dx_ws", [N.P, N.P, N.P, N.P, N.P, N.L, N.I, N.P, N.P, N.P, N.I, N.I, N.P])
+N.register("mdtf_bn_fwd_coeffs", [N.L, N.I, N.P, N.P, N.P, N.P, N.F, N.F, N.P, N.P, N.P, N.P, N.I, N.P, N.P])
+N.register("mdtf_bn_apply_ss", [N.P, N.P, N.P, N.L, N.I, N.P, N.I, N.P])
 
 
 FUSED_BWD = [0]      # backward passes that took their statistics from the dgrad epilogue (tests)
@@ -63,6 +65,41 @@ def _early_finalize(sbuf, g, mean, invstd, M, C):
     return ws, ev
 # projection-shortcut BNs applied inside the residual BN's pass (MDTF_DEFER_SHORTCUT_BN=0: separate apply)
 DEFER_SHORTCUT = os.environ.get("MDTF_DEFER_SHORTCUT_BN", "1") != "0"
+# MDTF_BN_ON_CONSUMER=1: a BN + ReLU whose only consumer is a 1x1 / stride-1 conv on the weight-stationary kernel
+# with K <= 128 (ResNet's conv2 -> BN -> ReLU -> conv3 in stages 1 and 2) runs its finalize only; the conv applies
+# scale / shift / ReLU to its operand as it loads it and writes the BN output and ReLU mask for the backward
+# (csrc/conv_ws.hip mdtf_conv_ws_bna): the apply pass's read of x and the conv's re-read of its output are gone.
+# Any other consumer gets the separate apply first (take_pending / apply_pending).
+ON_CONSUMER = os.environ.get("MDTF_BN_ON_CONSUMER", "0") == "1"
+_PENDING = {}        # data_ptr of an unwritten BN output -> (y, x, scale|shift [2C], mask)
+ON_CONSUMER_USED = [0]   # BN outputs applied by their consumer conv (tests)
+
+
+def take_pending(y):
+    """The pending apply of BN output ``y`` (removed), or None."""
+    if not _PENDING:
+        return None
+    ent = _PENDING.get(y.data_ptr())
+    if ent is None or ent[0].shape != y.shape or ent[0].dtype != y.dtype:
+        return None
+    del _PENDING[y.data_ptr()]
+    return ent
+
+
+def apply_pending(ent):
+    """Run a pending BN + ReLU apply as its own pass (the consumer could not fuse it)."""
+    y, x, ss, mask = ent
+    C = x.shape[-1]
+    N.check(N.fn("mdtf_bn_apply_ss")(N.ptr(x), N.ptr(y), N.ptr(mask), x.numel() // C, C, N.ptr(ss), 1,
+                                     N.stream_ptr()), "bn_apply_ss")
+
+
+def materialize(y):
+    """Make sure BN output ``y`` is written (a consumer that reads it as a plain tensor)."""
+    ent = take_pending(y)
+    if ent is not None:
+        apply_pending(ent)
+    return y
 
 
 def _check(x):
@@ -87,7 +124,7 @@ DUAL_BWD = [0]       # one-pass dual backward launches (tests)
 
 class _BNTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, mm, mv, decay, eps, relu, stats):
+    def forward(ctx, x, gamma, beta, residual, mm, mv, decay, eps, relu, stats, on_consumer=False):
         from . import actsink
         ctx.set_materialize_grads(False)
         ctx.res_sink = actsink.sink_of(residual)       # residual fan-out: write dres into the producer's sink
@@ -103,7 +140,17 @@ class _BNTrain(torch.autograd.Function):
         mask = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device) if relu else None
         g, b = _f32(gamma), _f32(beta)
         res = residual.contiguous() if residual is not None else None
-        if stats is not None:
+        if stats is not None and on_consumer and relu and res is None:
+            # finalize only: the consumer conv applies scale / shift / ReLU to its operand and writes y and mask
+            psum, psq, P = stats
+            ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+            N.check(N.fn("mdtf_bn_fwd_coeffs")(M, C, N.ptr(g), N.ptr(b), N.ptr(mm), N.ptr(mv), float(decay),
+                                               float(eps), N.ptr(mean), N.ptr(invstd), N.ptr(psum), N.ptr(psq),
+                                               int(P), N.ptr(ws), N.stream_ptr()), "bn_fwd_coeffs")
+            from . import conv as _conv
+            _conv.stats_consumed(x.device)
+            _PENDING[y.data_ptr()] = (y, x, ws, mask)
+        elif stats is not None:
             # Σx / Σx² already produced by the conv epilogue: finalize + apply only
             psum, psq, P = stats
             ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
@@ -169,7 +216,7 @@ class _BNTrain(torch.autograd.Function):
         if dy is None:
             if early is not None and early[1] is not None:   # join the side stream (captures must not end forked)
                 torch.cuda.current_stream(x.device).wait_event(early[1])
-            return (None,) * 10
+            return (None,) * 11
         dy = dy.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
@@ -230,7 +277,7 @@ class _BNTrain(torch.autograd.Function):
         gamma, beta = ctx.like
         rg = (V.grad_marker(gamma) if sg is not None else dgamma) if ctx.has_gamma else None
         rb = (V.grad_marker(beta) if sb is not None else dbeta) if ctx.has_beta else None
-        return (dx, rg, rb, dres, None, None, None, None, None, None)
+        return (dx, rg, rb, dres, None, None, None, None, None, None, None)
 
 
 class DeferredBN(object):
@@ -420,7 +467,11 @@ def bn_relu_maxpool_nhwc(x, gamma, beta, moving_mean, moving_var, decay, epsilon
     return _BNReluMaxPool.apply(x, gamma, beta, moving_mean, moving_var, decay, epsilon, stats, geo)
 
 
-def batch_norm_nhwc(x, gamma, beta, moving_mean, moving_var, training, decay, epsilon, relu, residual, stats=None):
+def batch_norm_nhwc(x, gamma, beta, moving_mean, moving_var, training, decay, epsilon, relu, residual, stats=None,
+                    on_consumer=False):
+    """``on_consumer`` (training, ReLU, no residual, conv-epilogue statistics): the output may be left unwritten
+    for the 1x1 conv consuming it to apply (``ON_CONSUMER``); every other reader must go through
+    :func:`materialize`."""
     _check(x)
     if isinstance(residual, DeferredBN):
         d = residual
@@ -431,7 +482,10 @@ def batch_norm_nhwc(x, gamma, beta, moving_mean, moving_var, training, decay, ep
     if residual is not None and residual.dtype != x.dtype:
         residual = residual.to(x.dtype)
     if training:
-        return _BNTrain.apply(x, gamma, beta, residual, moving_mean, moving_var, decay, epsilon, bool(relu), stats)
+        oc = bool(on_consumer and ON_CONSUMER and relu and residual is None and stats is not None
+                  and not N.deterministic())
+        return _BNTrain.apply(x, gamma, beta, residual, moving_mean, moving_var, decay, epsilon, bool(relu), stats,
+                              oc)
     x = x.contiguous()
     C = x.shape[-1]
     M = x.numel() // C

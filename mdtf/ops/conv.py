@@ -551,6 +551,31 @@ def ws_fwd(x, wt, kh, kw, out_hw, stride, pads, dil, tile, stats=None, grid_cap=
     return y
 
 
+N.register("mdtf_conv_ws_bna", [N.P, N.P, N.P] + [N.I] * 7 + [N.P, N.P, N.I, N.P, N.P, N.P, N.P])
+
+
+def bna_ok(ch, x_shape, w_shape, stride, pads, dil):
+    """The forward of this conv can apply a pending BN + ReLU to its operand (``ops.bn`` ON_CONSUMER): the
+    weight-stationary kernel on a 1x1 / stride-1 / unpadded conv with 64, 96 or 128 input channels."""
+    kh, kw, ci, co = w_shape
+    return (ch[0] == "ws" and kh == 1 and kw == 1 and tuple(stride) == (1, 1) and tuple(pads) == (0, 0, 0, 0)
+            and tuple(dil) == (1, 1) and ci in (64, 96, 128) and ws_depth_ok(ci, ch[1][3] if len(ch[1]) > 3 else 4))
+
+
+def ws_fwd_bna(x, wt, tile, stats, pend):
+    """1x1 forward on the weight-stationary kernel whose operand is relu(x * scale + shift) of the pending BN
+    ``pend = (a, x, scale|shift, mask)``: writes the BN output a and its mask as it goes (mdtf_conv_ws_bna)."""
+    a, xin, ss, mask = pend
+    n, h, wd, c = xin.shape
+    co = wt.shape[0]
+    y = torch.empty((n, h, wd, co), dtype=xin.dtype, device=xin.device)
+    s_sum, s_sq = stats
+    N.check(N.fn("mdtf_conv_ws_bna")(N.ptr(xin), N.ptr(wt), N.ptr(y), n, h, wd, c, co, _ws_code(*tile), 0,
+                                     N.ptr(s_sum), N.ptr(s_sq), s_sum.shape[0], N.ptr(ss), N.ptr(a), N.ptr(mask),
+                                     N.stream_ptr()), "conv_ws_bna")
+    return y
+
+
 def ws_dgrad(dy, w, x_shape, pads, dil, tile, out=None, accumulate=False, bn_stats=None, grid_cap=0, acc_src=None):
     """DX of a stride-1 conv on the weight-stationary kernel (the filter used flipped, HWIO as is).
     ``bn_stats = (x, relu_mask or None, psum, psq, slots)`` and ``acc_src`` as in :func:`mdtf_dgrad`."""
@@ -845,9 +870,14 @@ class _Conv(torch.autograd.Function):
         ctx.x_sink = actsink.sink_of(x)       # fanned-out input: dgrad accumulates into the producer's sink
         if ctx.x_sink is not None:
             ctx.x_sink.register()
+        from . import bn as _bn
+        pend = _bn.take_pending(x)             # x: a BN output its producer left for this conv to apply
         x = x.contiguous()
         w = w.contiguous()
         ch = choose("fwd", x.shape, w.shape, stride, pads, dil)
+        if pend is not None and not (want_stats and bna_ok(ch, x.shape, w.shape, stride, pads, dil)):
+            _bn.apply_pending(pend)
+            pend = None
         stats = None
         # want_stats 2: a private zeroed partial buffer (statistics consumed later than the next conv, e.g. a
         # deferred shortcut BN), else the persistent per-device one
@@ -878,7 +908,11 @@ class _Conv(torch.autograd.Function):
             if want_stats:
                 buf = sbuf(w.shape[3], x.device, STAT_SLOTS)
                 stats = (buf[0], buf[1])
-            y = ws_fwd(x, transpose_filter(w), w.shape[0], w.shape[1], out_hw, stride, pads, dil, ch[1], stats)
+            if pend is not None:
+                y = ws_fwd_bna(x, transpose_filter(w), ch[1], stats, pend)
+                _bn.ON_CONSUMER_USED[0] += 1
+            else:
+                y = ws_fwd(x, transpose_filter(w), w.shape[0], w.shape[1], out_hw, stride, pads, dil, ch[1], stats)
         elif ch[0] == "winograd":
             y = winograd.winograd_fwd(x, w, out_hw, pads)
         else:

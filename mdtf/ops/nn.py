@@ -232,7 +232,7 @@ def batch_norm(x, gamma, beta, moving_mean, moving_var, training=True, decay=0.9
 
 
 def conv_bn(x, w, gamma, beta, moving_mean, moving_var, strides=1, padding="SAME", training=True, decay=0.9,
-            epsilon=1e-5, relu=True, residual=None, defer=False, pool=None):
+            epsilon=1e-5, relu=True, residual=None, defer=False, pool=None, on_consumer=False):
     """conv2d (no bias) -> batch_norm (+residual) (+ReLU).
 
     On the GPU the conv epilogue emits the per-channel Σy/Σy² partials, so the
@@ -241,6 +241,8 @@ def conv_bn(x, w, gamma, beta, moving_mean, moving_var, strides=1, padding="SAME
     the residual BN consuming it applies in its own pass; elsewhere the normalised tensor as usual.
     ``pool = (ksize, stride, padding)``: a max pool follows (the ResNet stem); on the GPU BN + ReLU + pool run
     as one pass (``bn.bn_relu_maxpool_nhwc``).
+    ``on_consumer``: the output feeds only a 1x1 conv that may apply the BN + ReLU to its operand on the GPU
+    (``bn.ON_CONSUMER``).
     """
     n, h, wd, c = x.shape
     kh, kw, ci, co = w.shape
@@ -259,7 +261,7 @@ def conv_bn(x, w, gamma, beta, moving_mean, moving_var, strides=1, padding="SAME
             return bn.bn_relu_maxpool_nhwc(y, gamma, beta, moving_mean, moving_var, decay, epsilon, stats,
                                            (poh, pow_, pkh, pkw, psh, psw, ppt, ppl))
         y = bn.batch_norm_nhwc(y, gamma, beta, moving_mean, moving_var, True, decay, epsilon, relu, residual,
-                               stats=stats)
+                               stats=stats, on_consumer=on_consumer and pool is None)
         return y if pool is None else max_pool(y, pool[0], pool[1], pool[2])
     y = conv2d(x, w, strides, (pt, pb, pl, pr))
     y = batch_norm(y, gamma, beta, moving_mean, moving_var, training, decay, epsilon, relu, residual)

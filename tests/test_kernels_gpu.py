@@ -2511,3 +2511,60 @@ def test_bn_backward_early_finalize_matches_inline(monkeypatch):
     assert le == li
     for k in gi:
         assert _rel(ge[k], gi[k]) < 1e-4, (k, _rel(ge[k], gi[k]))
+
+
+def test_bn_on_consumer_conv_matches_separate_apply(monkeypatch):
+    """A BN + ReLU applied by the 1x1 conv consuming it (MDTF_BN_ON_CONSUMER: finalize only, the weight-stationary
+    kernel's operand loads apply scale / shift / ReLU and write the BN output, csrc/conv_ws.hip
+    mdtf_conv_ws_bna) == the separate apply pass: the BN output bitwise, the conv + BN output up to the order of the
+    statistics atomics, both against an fp32 PyTorch reference; stage-1 and stage-2 conv3 shapes."""
+    from mdtf.ops import bn
+    torch.manual_seed(11)
+    for hw, c in ((56, 64), (28, 128)):
+        x = torch.randn(2, hw, hw, c, device=DEV).bfloat16()
+        w2 = (torch.randn(3, 3, c, c, device=DEV) * (1.0 / (3 * c ** 0.5))).bfloat16()
+        w3 = (torch.randn(1, 1, c, 4 * c, device=DEV) * (1.0 / c ** 0.5)).bfloat16()
+        g = torch.rand(c, device=DEV) + 0.5
+        b = torch.randn(c, device=DEV) * 0.2
+        g3, b3 = torch.ones(4 * c, device=DEV), torch.zeros(4 * c, device=DEV)
+
+        def run(on):
+            monkeypatch.setattr(bn, "ON_CONSUMER", on)
+            n0 = bn.ON_CONSUMER_USED[0]
+            a = ops.conv_bn(x, w2, g, b, torch.zeros(c, device=DEV), torch.ones(c, device=DEV), 1, "SAME", True, 0.9,
+                            1e-5, True, None, on_consumer=True)
+            z = ops.conv_bn(a, w3, g3, b3, torch.zeros(4 * c, device=DEV), torch.ones(4 * c, device=DEV), 1, "SAME",
+                            True, 0.9, 1e-5, False, None)
+            torch.cuda.synchronize()
+            return a.float().clone(), z.float().clone(), bn.ON_CONSUMER_USED[0] - n0
+
+        a1, z1, used1 = run(True)
+        a0, z0, used0 = run(False)
+        assert used1 == 1 and used0 == 0, (hw, used1, used0)
+        assert torch.equal(a1, a0), (hw, (a1 - a0).abs().max().item())
+        assert _rel(z1, z0) < 1e-3, (hw, _rel(z1, z0))
+        # fp32 reference of the pair
+        xf = x.float().permute(0, 3, 1, 2)
+        h = torch.nn.functional.conv2d(xf, w2.float().permute(3, 2, 0, 1), padding=1)
+        mu, var = h.mean((0, 2, 3), keepdim=True), h.var((0, 2, 3), unbiased=False, keepdim=True)
+        ar = torch.relu((h - mu) / torch.sqrt(var + 1e-5) * g.view(1, -1, 1, 1) + b.view(1, -1, 1, 1))
+        assert _rel(a1, ar.permute(0, 2, 3, 1)) < 2e-2, (hw, _rel(a1, ar.permute(0, 2, 3, 1)))
+
+
+def test_bn_on_consumer_resnet_step_matches(monkeypatch):
+    """A two-stage ResNet step at 224 x 224 (stage-1 / stage-2 conv3 on the weight-stationary kernel) with the
+    conv2 BN + ReLU applied by conv3 == the separate apply pass: the loss and every gradient (the backward reads
+    the BN output and ReLU mask the fused kernel wrote)."""
+    from mdtf.ops import bn
+    torch.manual_seed(12)
+    x = torch.randn(2, 224, 224, 3)
+    y = torch.randint(0, 16, (2,))
+    monkeypatch.setattr(bn, "ON_CONSUMER", True)
+    n0 = bn.ON_CONSUMER_USED[0]
+    l1, g1 = _one_step(DEV, torch.bfloat16, x, y, blocks=[1, 1], grads=True)
+    assert bn.ON_CONSUMER_USED[0] - n0 >= 2                # stage-1 and stage-2 conv3 (per forward the step runs)
+    monkeypatch.setattr(bn, "ON_CONSUMER", False)
+    l0, g0 = _one_step(DEV, torch.bfloat16, x, y, blocks=[1, 1], grads=True)
+    assert abs(l1 - l0) <= 1e-3 * abs(l0), (l1, l0)
+    for k in g0:
+        assert _rel(g1[k], g0[k]) < 2e-3, (k, _rel(g1[k], g0[k]))
