@@ -2516,8 +2516,8 @@ def test_bn_backward_early_finalize_matches_inline(monkeypatch):
 def test_bn_on_consumer_conv_matches_separate_apply(monkeypatch):
     """A BN + ReLU applied by the 1x1 conv consuming it (MDTF_BN_ON_CONSUMER: finalize only, the weight-stationary
     kernel's operand loads apply scale / shift / ReLU and write the BN output, csrc/conv_ws.hip
-    mdtf_conv_ws_bna) == the separate apply pass: the BN output bitwise, the conv + BN output up to the order of the
-    statistics atomics, both against an fp32 PyTorch reference; stage-1 and stage-2 conv3 shapes."""
+    mdtf_conv_ws_bna) == the separate apply pass: the BN output and the conv + BN output up to the order of the
+    statistics atomics, and the BN output against an fp32 PyTorch reference; stage-1 and stage-2 conv3 shapes."""
     from mdtf.ops import bn
     torch.manual_seed(11)
     for hw, c in ((56, 64), (28, 128)):
@@ -2541,7 +2541,9 @@ def test_bn_on_consumer_conv_matches_separate_apply(monkeypatch):
         a1, z1, used1 = run(True)
         a0, z0, used0 = run(False)
         assert used1 == 1 and used0 == 0, (hw, used1, used0)
-        assert torch.equal(a1, a0), (hw, (a1 - a0).abs().max().item())
+        # (not bitwise: the conv2 statistics are fp32 atomics, their order -- and the last bit of scale / shift --
+        # differs run to run)
+        assert _rel(a1, a0) < 1e-4, (hw, _rel(a1, a0))
         assert _rel(z1, z0) < 1e-3, (hw, _rel(z1, z0))
         # fp32 reference of the pair
         xf = x.float().permute(0, 3, 1, 2)
@@ -2565,6 +2567,8 @@ def test_bn_on_consumer_resnet_step_matches(monkeypatch):
     assert bn.ON_CONSUMER_USED[0] - n0 >= 2                # stage-1 and stage-2 conv3 (per forward the step runs)
     monkeypatch.setattr(bn, "ON_CONSUMER", False)
     l0, g0 = _one_step(DEV, torch.bfloat16, x, y, blocks=[1, 1], grads=True)
+    _, g0b = _one_step(DEV, torch.bfloat16, x, y, blocks=[1, 1], grads=True)     # the run-to-run noise floor
     assert abs(l1 - l0) <= 1e-3 * abs(l0), (l1, l0)
-    for k in g0:
-        assert _rel(g1[k], g0[k]) < 2e-3, (k, _rel(g1[k], g0[k]))
+    errs = {k: (_rel(g1[k], g0[k]), _rel(g0b[k], g0[k])) for k in g0}
+    bad = {k: e for k, e in errs.items() if e[0] > max(1e-3, 4 * e[1])}
+    assert not bad, bad
