@@ -1140,9 +1140,10 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   if (bstat) {
     static_assert(NT % (BN / 8) == 0, "one channel chunk per thread");
     __syncthreads();                           // the C tile copy-out is done with the LDS
-    // [16][NT + 8] floats: the per-k rows are written lane-contiguously and the +8 row pad puts the
-    // reads of 8 channels x 8 threads on 64 distinct banks (a [NT][16] layout was 16-way conflicted)
-    constexpr int LDR = NT + 8;
+    // [16][NT + 4] floats: the per-k rows are written lane-contiguously; the reads (ds_read_b32: two 32-lane groups,
+    // bank = dword mod 32) of lanes (k = lane & 7, c8 = lane >> 3) hit dword 4k + c8 mod 32 -- distinct within a
+    // group (an NT + 8 pad put k and k + 4 on one bank: 2-way on every read)
+    constexpr int LDR = NT + 4;
     float* red = reinterpret_cast<float*>(smem_raw);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
