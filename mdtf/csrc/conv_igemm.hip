@@ -107,6 +107,8 @@ struct ConvArgs {
   // wgrad v2: fin_blocks extra workgroups (the first blocks of the grid, or the last) run the backward finalize of the BatchNorm
   // whose output gradient the conv's data gradient just completed (fin_*; see fin_bwd_block)
   int fin_blocks, fin_first;
+  // v2 forward / data gradient, BN = 128: the copy-out's bank-aligned lane order (copyout_rc; MDTF_FD_COREMAP=0: row-major)
+  int co_remap;
   const float* fin_psum;
   const float* fin_psq;
   int fin_P, fin_C;
@@ -674,6 +676,24 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(ConvArgs a) {
 // taps that reach DY is fixed and the DY offsets are affine again, so each
 // class is a dense implicit GEMM over only its own taps (no zero-tap waste).
 // ============================================================================
+// Copy-out element idx (= tid + k * NT) of a BM x BN C tile staged in LDS -> (row, 16-B chunk).  ds_read_b128 serves
+// a wave in four 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same + 32): for BN = 128 each group
+// gets one whole 256-B row of the tile (all 64 banks once).  The row-major order (lanes 0-15 row r, 16-31 row r + 1)
+// gave every group parts of two rows whose 272-B pitch overlaps 4 banks: 2-way on every copy-out read.  Each 64-lane
+// block still covers the same 4 rows, so only the lanes' assignment within them changes.
+template <int BN>
+__device__ __forceinline__ void copyout_rc(int idx, int& row, int& c8, bool remap) {
+  if (BN == 128 && remap) {
+    const int l = idx & 31, hh = (idx >> 5) & 1;
+    const bool ga = l < 4 || (l >= 12 && l < 16) || (l >= 20 && l < 28);
+    c8 = ga ? (l < 4 ? l : (l < 16 ? l - 8 : l - 12)) : (l < 12 ? l - 4 : (l < 20 ? l - 8 : l - 16));
+    row = ((idx >> 6) << 2) + 2 * hh + (ga ? 0 : 1);
+  } else {
+    row = idx / (BN / 8);
+    c8 = idx - row * (BN / 8);
+  }
+}
+
 template <int BM, int BN, int MODE, bool STATS, int STAGES, int NW>
 __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   // NW = 4 waves (2x2) or 8 waves (one 256-row block per CU: 2 waves per SIMD, half the
@@ -821,7 +841,8 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
 #pragma unroll
     for (int it = 0; it < PITER; ++it) {
       const int idx = tid + it * 64 * NW;
-      const int row = idx / (BN / 8), c8 = idx - row * (BN / 8);
+      int row, c8;
+      copyout_rc<BN>(idx, row, c8, a.co_remap != 0);
       const long long m = m0 + row;
       const int n = n0 + c8 * 8;
       prepf[it] = (m < a.M && n < a.Ncol) ? *reinterpret_cast<const uint4*>(a.pre_out + m * a.Ncol + n)
@@ -1047,7 +1068,8 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
 #pragma unroll
   for (int it = 0; it < PF; ++it) {
     const int idx = tid + (g0 + it) * NT;
-    const int row = idx / (BN / 8), c8 = idx - row * (BN / 8);
+    int row, c8;
+    copyout_rc<BN>(idx, row, c8, a.co_remap != 0);
     const long long m = m0 + row;
     const int n = n0 + c8 * 8;
     off[it] = -1;
@@ -1076,7 +1098,8 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
   for (int it = 0; it < PF; ++it) {
     if (off[it] < 0) continue;
     const int idx = tid + (g0 + it) * NT;
-    const int row = idx / (BN / 8), c8 = idx - row * (BN / 8);
+    int row, c8;
+    copyout_rc<BN>(idx, row, c8, a.co_remap != 0);
     uint4 v = *reinterpret_cast<const uint4*>(smem_raw + row * LDC + c8 * 16);
     if ((row >> 3) & 1) v = make_uint4(v.z, v.w, v.x, v.y);
     bf16_t* dst = a.out + off[it];
@@ -1145,10 +1168,18 @@ __global__ void __launch_bounds__(64 * NW) conv_fd_v2(ConvArgs a) {
     // group (an NT + 8 pad put k and k + 4 on one bank: 2-way on every read)
     constexpr int LDR = NT + 4;
     float* red = reinterpret_cast<float*>(smem_raw);
+    // this thread's slot: slot % (BN / 8) == its chunk c8 (the reads below walk t2 = c8 + j BN / 8); with the
+    // BN = 128 copy-out remap the chunk is not tid % 16: slot = (wave, row within the wave's 4, c8)
+    int slot = tid;
+    if (BN == 128 && a.co_remap) {
+      int r0_, c0_;
+      copyout_rc<BN>(tid, r0_, c0_, true);
+      slot = (tid & ~63) | ((r0_ & 3) << 4) | c0_;
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      red[k * LDR + tid] = bs0[k];
-      red[(8 + k) * LDR + tid] = bs1[k];
+      red[k * LDR + slot] = bs0[k];
+      red[(8 + k) * LDR + slot] = bs1[k];
     }
     __syncthreads();
     for (int nl = tid; nl < BN; nl += NT) {
@@ -1753,6 +1784,13 @@ int launch_fd_v2(ConvArgs& a, hipStream_t st) {
   if (MODE <= 2 && STAGES >= 2 && conv_persist_mode() && a.K >= 64) {
     const int rc = launch_fd_p<BM, BN, MODE, STATS, STAGES, NW>(a, st);
     if (rc != MDTF_EUNSUPPORTED) return rc;
+  }
+  {
+    static const int remap = [] {
+      const char* e = getenv("MDTF_FD_COREMAP");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
+    a.co_remap = remap;
   }
   hipLaunchKernelGGL((conv_fd_v2<BM, BN, MODE, STATS, STAGES, NW>), dim3((unsigned)nblk), dim3(NT), lds, st, a);
   MDTF_LAUNCH_CHECK();
