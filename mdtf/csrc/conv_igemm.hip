@@ -107,7 +107,8 @@ struct ConvArgs {
   // wgrad v2: fin_blocks extra workgroups (the first blocks of the grid, or the last) run the backward finalize of the BatchNorm
   // whose output gradient the conv's data gradient just completed (fin_*; see fin_bwd_block)
   int fin_blocks, fin_first;
-  // v2 forward / data gradient, BN = 128: the copy-out's bank-aligned lane order (copyout_rc; MDTF_FD_COREMAP=0: row-major)
+  // v2 forward / data gradient, BN = 128: the copy-out's bank-aligned lane order (copyout_rc; MDTF_FD_COREMAP=1; default
+  // row-major)
   int co_remap;
   const float* fin_psum;
   const float* fin_psq;
@@ -1786,9 +1787,11 @@ int launch_fd_v2(ConvArgs& a, hipStream_t st) {
     if (rc != MDTF_EUNSUPPORTED) return rc;
   }
   {
+    // measured -0.65 % in the ResNet-50 step (13080 -> 12992 img/s, profiles/ab_r6.md) despite the conflict-free
+    // reads: off unless MDTF_FD_COREMAP=1
     static const int remap = [] {
       const char* e = getenv("MDTF_FD_COREMAP");
-      return (e && e[0] == '0') ? 0 : 1;
+      return (e && e[0] == '1') ? 1 : 0;
     }();
     a.co_remap = remap;
   }
