@@ -174,10 +174,15 @@ WG_SK = os.environ.get("MDTF_WG_SK", "0") == "1"
 # with MALL-resident operands 2 and 3 stages tie): MDTF_WG_STAGES=3 vs 2, alternating: 6485 / 6530 vs 6378 / 6420 seq/s
 # (FFN-out 3072 x 768: 256-row 3-stage 6368 / 6362 vs 128-row 2-stage 6356 / 6336 seq/s)
 # Round 6 (write-through slab publish + store-first slots): in-step re-tune moved the q|k|v and FFN-out shapes to
-# two 128-row workgroups per CU (bench/bert_wg_tune.py, profiles/bert_wg_tune_r6f.md: step 9.511 -> 9.402 ms)
-WG_TILES = {(768, 2304, 8192): (128, 2, 4), (768, 3072, 8192): (256, 3, 3), (3072, 768, 8192): (128, 2, 3),
+# two 128-row workgroups per CU (bench/bert_wg_tune.py, profiles/bert_wg_tune_r6f.md: step 9.511 -> 9.402 ms); the
+# final-tree re-tune moved the FFN-in shape too (bert_wg_tune_r6w.md; captured A/B 7049 vs 7024 seq/s, 6 of 6 pairs)
+WG_TILES = {(768, 2304, 8192): (128, 2, 4), (768, 3072, 8192): (128, 2, 3), (3072, 768, 8192): (128, 2, 3),
             (768, 768, 8192): (128, 2, 6), (1024, 3072, 8192): (256, 3, 2), (1024, 4096, 8192): (256, 3, 2),
             (4096, 1024, 8192): (256, 3, 2)}
+# MDTF_WG_TILES="M,N,K:bm,stages,splits;...": override entries (in-step A/B of a tuner's proposal)
+for _ent in filter(None, os.environ.get("MDTF_WG_TILES", "").split(";")):
+    _k, _v = _ent.split(":")
+    WG_TILES[tuple(int(t) for t in _k.split(","))] = tuple(int(t) for t in _v.split(","))
 _TICKETS = {}
 # MDTF_WG_STAGES: force the ring depth of the table entries (in-step A/B: the operands of the step are HBM-cold,
 # the graph-timed probe's are MALL-resident)
